@@ -1,0 +1,357 @@
+/*
+ * usv_hip.h -- C ABI of libusv_hip.so, the MI355X (gfx950) hot path of the
+ * USV CaptureXY environment + rl_games PPO trainer.
+ *
+ * The reference (loop-Z/omniisaacgymenvs_loop) is pure Python/PyTorch; it has
+ * no FFI.  Each entry point below replaces one reference call chain; the
+ * reference file:line it stands in for is cited next to it.  A maintainer binds
+ * these from Python with ctypes; the in-tree host package
+ * omniisaacgymenvs_loop_amd/_capi.py is exactly that binding.
+ *
+ * Conventions
+ *   - every pointer is a DEVICE pointer owned by the caller (torch tensors),
+ *     except `const usv_cfg_t*` / `const ppo_cfg_t*` which are host structs
+ *     passed by value into the kernels;
+ *   - every call is asynchronous on the given hipStream_t (passed as void*),
+ *     performs no allocation and no host synchronisation (graph-capturable);
+ *   - return value: 0 = launched, nonzero = argument error (the Python side
+ *     raises RuntimeError, mirroring the reference's exception-based errors,
+ *     e.g. tasks/USV_Virtual.py:91-95).
+ *   - env state is struct-of-arrays: field f of env e lives at f[e].
+ */
+#ifndef USV_HIP_H
+#define USV_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define USV_NOBS        33   /* obs dim: 3 + (5 + 5*3) + 2 + 8   (tasks/USV/USV_core.py:46) */
+#define USV_NOBST       16   /* obstacles per env                 (USV_capture_xy_static_obs.py:70) */
+#define USV_NCLOSE       5   /* closest obstacles in obs          (USV_core.py:33) */
+#define USV_GRID       150   /* potential-field grid              (USV_capture_xy_static_obs.py:30) */
+#define USV_GRID2    (USV_GRID * USV_GRID)
+#define USV_LUT_N     1000   /* thruster LUT points               (TEST yaml dynamics.thrusters) */
+#define USV_NSTAT       28   /* episode_sums keys                 (USV_Virtual.py:586-601) */
+#define USV_SPAWN_ITERS 20   /* obstacle rejection iterations     (static_obs.py:980) */
+/* Layout of the uniform draws of one reset slot (device [K][USV_NU_RESET]
+ * when injected; otherwise Philox4x32-10(key=seed, ctr={env, step_lo, step_hi,
+ * 0x100 + i/4})[i%4]).  Every torch.rand call of the reference reset path has
+ * one slot range here (tests/golden/make_golden.py records them by call site). */
+#define RU_MASS       0     /* MassDistributionDisturbances.randomize_masses:137 */
+#define RU_COM        1     /* _randomize_com:98-124 (3)                         */
+#define RU_KIZ        4     /* USVVirtual._sample_k_iz:164                        */
+#define RU_KDRAG      5     /* HydrodynamicsObject._sample_k_drag:129             */
+#define RU_THR        6     /* DynamicsFirstOrder.reset_thruster_randomization (2)*/
+#define RU_DRAG       8     /* HydrodynamicsObject.reset_coefficients (6 lin, 6 quad) */
+#define RU_SPAWN_R   20     /* CaptureXYTask.get_spawns:952                       */
+#define RU_SPAWN_TH  21     /* :953 */
+#define RU_YAW       22     /* :959 */
+#define RU_OBST      23     /* :977 (16 x 2) */
+#define RU_RESAMPLE  55     /* :1020, one 16x2 block per rejection iteration (20) */
+#define RU_VX       695     /* USVVirtual.reset_idx:1561 */
+#define RU_VY       696     /* :1564 */
+#define RU_GOAL     697     /* CaptureXYTask.get_goals:924 (2) */
+#define USV_NU_RESET 699
+/* Layout of the uniform draws of one env step (device [n][USV_NU_STEP] when
+ * injected; otherwise Philox(ctr={env, step_lo, step_hi, i/4})[i%4]).
+ * Only the draws of the LAST update_state of the step reach obs/reward
+ * (USV_Virtual.py:785-787 via post_physics_step -> get_observations:838). */
+#define SU_VX   0   /* NoisyObservations.add_noise_on_vel, column 0 */
+#define SU_VY   1   /* column 1 */
+#define SU_WZ   2   /* column 5 */
+#define SU_HEAD 3   /* add_noise_on_heading */
+#define SU_PX   4   /* add_noise_on_pos (2) */
+#define SU_ACT  6   /* NoisyActions.add_noise_on_act (2) */
+#define USV_NU_STEP 8
+
+/* episode_sums key order (dict insertion order of the reference) */
+enum usv_stat_key {
+  ST_TOTAL_REWARD = 0, ST_DISTANCE_REWARD, ST_ALIGNMENT_REWARD, ST_HEADING_IMPROVE_REWARD,
+  ST_POTENTIAL_SHAPING_REWARD, ST_SPEED_REWARD, ST_ANGULAR_REWARD, ST_TURN_HAZARD_PENALTY,
+  ST_GOAL_REWARD, ST_COLLISION_REWARD, ST_TIME_REWARD, ST_SUCCESS, ST_COLLISION,
+  ST_POSITION_ERROR, ST_BOUNDARY_PENALTY, ST_DANGER_MEAN, ST_DANGER_HI_RATE, ST_G_GATE_MEAN,
+  ST_G_SAFE_MEAN, ST_ANGULAR_VEL_PENALTY, ST_ANGULAR_VEL_VARIATION_PENALTY, ST_ENERGY_PENALTY,
+  ST_NORMED_LINEAR_VEL, ST_NORMED_ANGULAR_VEL, ST_CMD_NEG_RATE, ST_U_MEAN, ST_U_LOW_RATE, ST_U_SUM
+};
+
+/* penalty function kinds (the eval'd lambda strings of USV_task_rewards.py:429-438,
+ * TEST yaml :262-291, parsed host-side into one of these closed forms) */
+enum usv_pen_kind {
+  PEN_OFF = 0,
+  PEN_DEADZONE = 1,   /* -k * max(|x| - x0, 0) + c                      */
+  PEN_SUM = 2,        /* -k * sum(x) + c        (energy on u)            */
+  PEN_SUMSQ = 3,      /* -k * sum(x^2) + c                               */
+  PEN_NORM = 4,       /* -k * ||x|| + c         (linear velocity)        */
+  PEN_EXPABS = 5      /* k * (exp(x0 * |x|) - 1) + c                     */
+};
+
+/* All constants of the env step / reset path.  Built host-side from the task
+ * yaml (omniisaacgymenvs_loop_amd/tasks/usv_config.py). */
+typedef struct usv_cfg {
+  /* ---- integration (sim.dt, controlFrequencyInv, dynamics.*) ---- */
+  float dt;                 /* 0.02 */
+  int   substeps;           /* 10 */
+  float thr_alpha;          /* exp(-dt/tau), ThrusterDynamics.py:132 */
+  float thr_y;              /* thruster lateral lever arm (heron.usd) 0.37765 */
+  float izz0;               /* base_link Izz (heron.usd) 8.061 */
+  float lin_damp[3];        /* effective linear damping u, v, r (Hydrodynamics.py:185-192) */
+  float quad_damp[3];       /* quadratic damping + offset, u, v, r */
+  float scaling_damping;
+  int   use_drag_scale;     /* multiply damping by k_drag (Hydrodynamics.py:202) */
+  int   use_thr_mult;       /* apply thruster multiplier (ThrusterDynamics.py:200) */
+  int   thr_separate;       /* separate L/R multipliers */
+  /* ---- actions (USV_Virtual.py:1042-1101) ---- */
+  float clip_actions;       /* 1.0 */
+  int   affine_thrust;      /* u = 0.5(a+1) else clamp(a,0,1) */
+  int   act_noise_on;  float act_noise_min, act_noise_max;
+  /* ---- observation noise (USV_disturbances.py:533-601) ---- */
+  int   pos_noise_on;  float pos_noise_min, pos_noise_max;
+  int   vel_noise_on;  float vel_noise_min, vel_noise_max;
+  int   head_noise_on; float head_noise_min, head_noise_max;
+  /* ---- observation layout ---- */
+  int   obs_local;          /* observation_frame == "local" */
+  int   priv_dim;           /* 4 or 8 */
+  float clip_obs;           /* 12 */
+  int   masscom_base;       /* masscom_obs_source == "base" */
+  int   mass_relative;      /* mass_obs_mode == "relative" */
+  float base_mass;
+  int   com_scaled;         /* com_obs_mode == "scaled" */
+  float com_scale[3];       /* box_length, box_width, max(zero_height,1) */
+  float base_com[3];
+  int   priv_mode;          /* 0 raw, 1 centered, 2 minmax */
+  float priv_nominal;
+  int   priv_drag_on, priv_thr_on, priv_kiz_on;
+  float kdrag_min, kdrag_max, thr_min, thr_max, kiz_min, kiz_max;
+  /* ---- task (CaptureXYParameters, TEST yaml task_parameters) ---- */
+  float position_tolerance;
+  int   kill_after_n;
+  float kill_dist, boundary_cost, goal_reward, time_reward;
+  float collision_threshold;   /* 1.2 (static_obs.py:105) */
+  float obstacle_radius;       /* 0.5 */
+  int   max_episode_length;    /* 200 */
+  int   fixed_horizon_eval;
+  /* ---- CaptureXYReward (USV_task_rewards.py:20-80) ---- */
+  int   reward_mode;           /* 0 linear, 1 square, 2 exponential */
+  float position_scale, exp_coeff, align_la1, align_la2, align_la3;
+  /* ---- Penalties (USV_task_rewards.py:440-523) ---- */
+  int   pen_lin_kind;  float pen_lin_k,  pen_lin_x0,  pen_lin_c;
+  int   pen_ang_kind;  float pen_ang_k,  pen_ang_x0,  pen_ang_c;
+  int   pen_angv_kind; float pen_angv_k, pen_angv_x0, pen_angv_c;
+  int   pen_en_kind;   float pen_en_k,   pen_en_x0,   pen_en_c;
+  int   pen_actv_kind; float pen_actv_k, pen_actv_x0, pen_actv_c;
+  int   pen_use_u;           /* penalties_use_thrust_u */
+  /* ---- potential field (d_multi_gemini.py) ---- */
+  float map_size;            /* 30 */
+  int   field_iters;         /* 225 */
+  float influence_radius, eta, safe_radius, field_alpha;
+  /* ---- reset / domain randomisation ---- */
+  int   mass_dr_on;  float mass_min, mass_max;
+  int   com_mode;            /* 0 base, 1 xyz box, 2 legacy disk */
+  float com_disp[3];  float com_legacy_r;
+  int   couple_drag, couple_thr, couple_kiz;
+  int   indep_kdrag_on, kdrag_log;
+  int   indep_thr_on;  float thr_rand, left_rand, right_rand;
+  int   indep_kiz_on, kiz_log;
+  int   drag_rand_on; float lin_rand[3], quad_rand[3];
+  float spawn_rmin, spawn_rmax, goal_random_position;
+  float obst_box, min_dist_safe, min_obs_sep;
+  float init_vel;            /* 1.5 */
+  int   stats_on;            /* accumulate episode_sums */
+  int   pad_;
+} usv_cfg_t;
+
+/* Device buffers of the env (SoA).  All arrays have n entries unless noted. */
+typedef struct usv_bufs {
+  int n;
+  int pad0;
+  /* planar rigid-body state (local frame) */
+  float *px, *py, *yaw, *vx, *vy, *wz;
+  float *fl, *fr;                  /* thruster first-order lag state (ThrusterDynamics.py:133) */
+  /* per-episode parameters */
+  float *mass, *com_x, *com_y, *com_z, *k_drag, *thr_l, *thr_r, *k_iz, *mass_r;
+  float *lin_damp, *quad_damp;     /* [3][n] only when cfg.drag_rand_on, else NULL */
+  /* task */
+  float *tgt_x, *tgt_y;
+  float *obst;                     /* [16][2][n]  obstacle centres, local frame */
+  float *field;                    /* [n][150*150] potential field */
+  /* history */
+  float *prev_cmd;                 /* [2][n] raw policy command (obs 23:25) */
+  float *prev_dist, *prev_head, *prev_pot, *prev_wz;
+  int32_t *goal_cnt, *progress, *reset_buf;
+  uint8_t *just_reset;
+  int32_t *done_succ, *done_coll;
+  float *stats;                    /* [USV_NSTAT][n] episode sums */
+  /* outputs */
+  float *obs;                      /* [n][33] clamped observation */
+  float *rew;                      /* [n] */
+  int64_t *dones;                  /* [n] reset_buf copy as int64 (rl_games API) */
+  /* control block (device) */
+  int32_t *ctl;                    /* [16] see USV_CTL_* */
+  int32_t *reset_ids;              /* [n] compacted reset list */
+  float   *fscratch;               /* [16] float reductions (max_val, jmax) */
+  float   *extras;                 /* [USV_NSTAT] extras["episode"] (persistent) */
+  float   *extras_acc;             /* [USV_NSTAT] scratch sums */
+  float   *field_old_tgt;          /* [2][n] target used by the field of each reset slot */
+} usv_bufs_t;
+
+/* control words */
+#define USV_CTL_RESET_COUNT 0
+#define USV_CTL_POT_VALID   1   /* 0 => prev_potential is None (static_obs.py:448,773) */
+#define USV_CTL_PEN_VALID   2   /* 0 => Penalties.prev_state is None (USV_task_rewards.py:450) */
+#define USV_CTL_REW_VALID   3   /* 0 => CaptureXYReward.prev_position_error is None */
+#define USV_CTL_NAN_FLAG    4   /* device NaN probe (replaces USV_NAN_PROBE host syncs) */
+#define USV_CTL_ANY_INSIDE  5   /* potential field: any cell inside an obstacle in the batch */
+#define USV_CTL_N           16
+
+/* ------------------------------------------------------------------------ */
+/* Env entry points                                                          */
+/* ------------------------------------------------------------------------ */
+
+/* Build the 1000-point thruster LUT from the 21-point tables.
+ * Replaces DynamicsFirstOrder.interpolate_on_field_data, ThrusterDynamics.py:152-177.
+ * lut: device [2][USV_LUT_N]. */
+int usv_build_lut(const float *table_l21, const float *table_r21, int n_table,
+                  float *lut_dev, void *stream);
+
+/* Reset path, part 1: compact reset_buf into reset_ids/ctl[RESET_COUNT],
+ * reduce episode extras, sample domain randomisation, spawn + obstacle
+ * rejection sampling, initial velocities, new goals.
+ * Replaces USVVirtual.pre_physics_step:1045-1048 -> reset_idx:1502-1618
+ * (MassDistributionDisturbances.randomize_masses, _apply_mass_driven_coupling,
+ *  CaptureXYTask.reset/get_spawns/get_goals).
+ * u_inject: NULL => in-kernel Philox(seed, step); else device [n][USV_NU_RESET]
+ * uniforms per reset slot (parity tests). */
+int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed,
+              uint64_t step, const float *u_inject, void *stream);
+
+/* Reset path, part 2: per-reset-env potential field (occupancy/SDF,
+ * 8-neighbour wavefront cost-to-go, repulsion, batch-global normalisation).
+ * Replaces BatchedMapGPU.compute_occupancy_and_sdf / compute_cost_field_wavefront /
+ * compute_potential_field, tasks/USV/d_multi_gemini.py:66-271 (called from
+ * USV_capture_xy_static_obs.py:1054-1057). */
+int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream);
+
+/* One control step for all envs: action mapping, thruster LUT + lag,
+ * 10 substeps of 3-DoF hydrodynamics + semi-implicit Euler, state readback
+ * with observation noise, observation, reward, penalties, kills, stats.
+ * Replaces VecEnvRLGames.step (envs/vec_env_rlgames.py:120-217):
+ *   USVVirtual.pre_physics_step:1050-1101, apply_forces:1103-1133 + PhysX
+ *   World.step (x10), post_physics_step -> get_observations:837-986,
+ *   calculate_metrics:1628-1652, is_done:1223-1237, _process_data:82-112.
+ * actions: device [n][2]; action_bias: initial_action_bias if the global
+ * counter is below initial_action_bias_steps else 0 (USV_Virtual.py:1071-1077).
+ * u_inject: NULL => Philox, else device [n][USV_NU_STEP]. */
+int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions,
+                 const float *lut_dev, float action_bias, uint64_t seed,
+                 uint64_t step, const float *u_inject, void *stream);
+
+/* Planar force/moment model only (no integration), for parity with
+ * HydrodynamicsObject.ComputeHydrodynamicsEffects (Hydrodynamics.py:207-245)
+ * and the thruster lever arms.  out: [n][3] body X, Y, N. */
+int usv_forces(const usv_cfg_t *cfg, const usv_bufs_t *b, float *out, void *stream);
+
+/* ------------------------------------------------------------------------ */
+/* PPO entry points (rl_games a2c_continuous / a2c_common)                   */
+/* ------------------------------------------------------------------------ */
+
+#define PPO_NIN   33
+#define PPO_NH    128
+#define PPO_NA    2
+/* flat parameter order = model.parameters() order of the reference:
+ * sigma[2], W1[128][33], b1[128], W2[128][128], b2[128], Wv[1][128], bv[1],
+ * Wmu[2][128], bmu[2]  (network_builder.py:1480-1575)  => 21253 floats */
+#define PPO_NPARAM 21253
+#define PPO_OFF_SIGMA 0
+#define PPO_OFF_W1    2
+#define PPO_OFF_B1    (PPO_OFF_W1 + PPO_NH * PPO_NIN)
+#define PPO_OFF_W2    (PPO_OFF_B1 + PPO_NH)
+#define PPO_OFF_B2    (PPO_OFF_W2 + PPO_NH * PPO_NH)
+#define PPO_OFF_WV    (PPO_OFF_B2 + PPO_NH)
+#define PPO_OFF_BV    (PPO_OFF_WV + PPO_NH)
+#define PPO_OFF_WMU   (PPO_OFF_BV + 1)
+#define PPO_OFF_BMU   (PPO_OFF_WMU + PPO_NA * PPO_NH)
+
+typedef struct ppo_cfg {
+  int   horizon;            /* 16 */
+  int   n_envs;             /* num_actors per rank */
+  int   minibatch;          /* 8192 */
+  int   normalize_input, normalize_value, normalize_advantage;
+  float gamma, tau;         /* 0.99, 0.95 */
+  float e_clip;             /* 0.2 */
+  float critic_coef;        /* 0.5 */
+  float entropy_coef;       /* 0 */
+  float bounds_loss_coef;   /* 1e-4 */
+  int   clip_value;
+  int   truncate_grads;  float grad_norm;
+  float adam_b1, adam_b2, adam_eps, weight_decay;
+  int   lr_adaptive;  float kl_threshold, lr_min, lr_max;
+  float reward_scale, reward_shift;
+  float rms_eps;            /* 1e-5 */
+  int   pad_;
+} ppo_cfg_t;
+
+/* Rollout: obs RMS normalise (eval) -> MLP -> mu, value (denormalised),
+ * Normal sample, neglogp; writes rollout slot t of the env-major experience
+ * buffer. Replaces A2CBase.get_action_values (a2c_common.py:385-405) +
+ * ModelA2CContinuousLogStd.forward (models.py:366-401) +
+ * ExperienceBuffer.update_data (experience.py:392-398).
+ * params: [PPO_NPARAM]; obs_rms: double [2][33] (mean, var); val_rms double [2];
+ * buffers of the experience store are env-major [n][H][...].
+ * eps_inject: NULL => Philox normal draws, else device [n][2] N(0,1) draws. */
+int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
+                    const double *val_rms, const float *obs, int t,
+                    float *exp_obs, float *exp_act, float *exp_nlp, float *exp_val,
+                    float *exp_mu, float *exp_sigma, uint8_t *exp_done,
+                    const int64_t *dones_prev, float *actions_out,
+                    uint64_t seed, uint64_t step, const float *eps_inject, void *stream);
+
+/* Value of the last observation (A2CBase.get_values, a2c_common.py:407-430). */
+int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
+              const double *val_rms, const float *obs, float *values, void *stream);
+
+/* Store rewards of slot t shaped by DefaultRewardsShaper (tr_helpers.py:33-43)
+ * and accumulate the episode meters (a2c_common.py:738-759).
+ * meter: device [H][4] per-step (sum reward of done envs, sum shaped, sum length, count). */
+int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *dones, int t,
+                     float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len,
+                     float *meter, void *stream);
+
+/* GAE (A2CBase.discount_values a2c_common.py:525-540) + returns (:763) +
+ * value RMS train/normalise (prepare_dataset a2c_common.py:1257-1290) +
+ * advantage normalisation.  work: device scratch >= 64 doubles + 4*n*H floats. */
+int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
+                double *val_rms, const float *last_obs, const int64_t *last_dones,
+                const uint8_t *exp_done, float *exp_val, const float *exp_rew,
+                float *exp_ret, float *exp_adv, double *work, void *stream);
+
+/* One PPO minibatch: [obs RMS update (mini-epoch 0)], forward, losses,
+ * backward, [grad all-reduce happens between the two halves on multi-GPU],
+ * grad-norm clip, Adam, KL, adaptive LR, mu/sigma write-back.
+ * Replaces A2CAgent.calc_gradients (a2c_continuous.py:78-196),
+ * trancate_gradients_and_step (a2c_common.py:308-330),
+ * PPODataset.update_mu_sigma (datasets.py:25-29),
+ * AdaptiveScheduler.update (schedulers.py:26-32).
+ * Split in two so the flat gradient can be all-reduced in between:
+ *   ppo_minibatch_grad  -> grad[PPO_NPARAM] (+ kl sum in grad[PPO_NPARAM])
+ *   ppo_minibatch_apply -> clip + Adam + lr update.
+ * opt: device floats [0]=lr [1]=step [2..]=reserved; m, v: [PPO_NPARAM]. */
+int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rms,
+                       const double *val_rms, int update_obs_rms, int mb_index,
+                       const float *exp_obs, const float *exp_act, const float *exp_nlp,
+                       const float *exp_val, const float *exp_ret, const float *exp_adv,
+                       float *exp_mu, float *exp_sigma, float *grad, float *losses,
+                       float *partials, double *work, void *stream);
+int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m,
+                        float *adam_v, float *opt, float grad_scale, void *stream);
+
+/* library / device info */
+int usv_hip_version(void);
+int usv_hip_arch(char *buf, int len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* USV_HIP_H */

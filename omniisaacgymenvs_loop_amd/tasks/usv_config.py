@@ -1,0 +1,313 @@
+"""Task-yaml -> usv_cfg_t (the constant block every env kernel receives).
+
+Accepts the reference's task config dict unchanged (the keys of
+cfg/task/USV/IROS2024/USV_Virtual_CaptureXY_SysID-TEST.yaml and siblings) and
+resolves every flag the reference resolves at construction time:
+
+* USVVirtual.__init__ (tasks/USV_Virtual.py:295-648): action processing,
+  mass-driven coupling activation, privileged-tail encoding ranges;
+* HydrodynamicsObject / DynamicsFirstOrder constructors
+  (envs/USV/Hydrodynamics.py:6-117, envs/USV/ThrusterDynamics.py:33-110);
+* Penalties.__post_init__ (tasks/USV/USV_task_rewards.py:429-438): the
+  penalty lambdas are *strings eval'd* by the reference; here they are parsed
+  into a closed set of forms (usv_pen_kind) and anything else is rejected.
+"""
+from __future__ import annotations
+
+import math
+import re
+from typing import Any, Dict
+
+import numpy as np
+
+from .._abi import PEN, UsvCfg
+
+# heron.usd rigid-body constants (decoded offline)
+HERON_THRUSTER_Y = 0.37765
+HERON_THRUSTER_X = -0.5006
+HERON_IZZ = 8.061
+
+# CaptureXYParameters / CaptureXYReward defaults (USV_task_parameters.py:16-52,
+# USV_task_rewards.py:20-32)
+_TASK_DEFAULTS = dict(position_tolerance=0.1, kill_after_n_steps_in_tolerance=1, goal_random_position=0.0,
+                      max_spawn_dist=11.0, min_spawn_dist=0.5, kill_dist=20.0, boundary_cost=25.0,
+                      goal_reward=100.0, time_reward=-0.1)
+_REWARD_DEFAULTS = dict(reward_mode="exponential", position_scale=1.5, exponential_reward_coeff=0.25,
+                        align_la1=0.04, align_la2=-10.0, align_la3=-0.1)
+_PEN_DEFAULTS = dict(
+    penalize_linear_velocities=False, penalize_linear_velocities_fn="lambda x,step: -torch.norm(x, dim=-1)*c1 + c2",
+    penalize_linear_velocities_c1=0.01, penalize_linear_velocities_c2=0.0,
+    penalize_angular_velocities=False, penalize_angular_velocities_fn="lambda x,step : -torch.abs(x)*c1 + c2",
+    penalize_angular_velocities_c1=0.01, penalize_angular_velocities_c2=0.0,
+    penalize_angular_velocities_variation=False,
+    penalize_angular_velocities_variation_fn="lambda x,step: torch.exp(c1 * torch.abs(x)) - 1.0",
+    penalize_angular_velocities_variation_c1=-0.033,
+    penalize_energy=False, penalize_energy_fn="lambda x,step : -torch.sum(x**2)*c1 + c2",
+    penalize_energy_c1=0.01, penalize_energy_c2=0.0,
+    penalize_action_variation=False, penalize_action_variation_fn="lambda x,step: torch.exp(c1 * torch.abs(x)) - 1.0",
+    penalize_action_variation_c1=-0.033,
+)
+
+_NUM = r"([-+]?(?:\d+\.?\d*|\.\d+)(?:[eE][-+]?\d+)?|c1|c2)"
+
+
+def parse_penalty_fn(src: str, consts: Dict[str, float]):
+    """Map a reference penalty lambda string to (kind, k, x0, c).
+
+    The reference eval()s these strings (USV_task_rewards.py:432-438); only the
+    closed forms below are accepted, everything else raises ValueError.
+    """
+    s = re.sub(r"\s+", "", src)
+    body = s.split(":", 1)[1] if s.startswith("lambda") else s
+
+    def num(tok):
+        if tok in ("c1", "c2"):
+            return float(consts[tok])
+        return float(tok)
+
+    pats = [
+        # -torch.clamp(torch.abs(x)-X0,min=0.0)*K [+C]
+        (rf"^-torch\.clamp\(torch\.abs\(x\)-{_NUM},min=0(?:\.0)?\)\*{_NUM}(?:\+{_NUM})?$",
+         lambda m: (PEN["PEN_DEADZONE"], num(m[1]), num(m[0]), num(m[2]) if m[2] else 0.0)),
+        # -torch.abs(x)*K [+C]
+        (rf"^-torch\.abs\(x\)\*{_NUM}(?:\+{_NUM})?$",
+         lambda m: (PEN["PEN_DEADZONE"], num(m[0]), 0.0, num(m[1]) if m[1] else 0.0)),
+        # -torch.sum(x,dim=-1)*K [+C]
+        (rf"^-torch\.sum\(x(?:,dim=-1)?\)\*{_NUM}(?:\+{_NUM})?$",
+         lambda m: (PEN["PEN_SUM"], num(m[0]), 0.0, num(m[1]) if m[1] else 0.0)),
+        # -torch.sum(x**2[,dim=-1])*K [+C]
+        (rf"^-torch\.sum\(x\*\*2(?:,dim=-1)?\)\*{_NUM}(?:\+{_NUM})?$",
+         lambda m: (PEN["PEN_SUMSQ"], num(m[0]), 0.0, num(m[1]) if m[1] else 0.0)),
+        # -torch.norm(x,dim=-1)*K [+C]
+        (rf"^-torch\.norm\(x,dim=-1\)\*{_NUM}(?:\+{_NUM})?$",
+         lambda m: (PEN["PEN_NORM"], num(m[0]), 0.0, num(m[1]) if m[1] else 0.0)),
+        # (torch.exp(C1*torch.abs(x))-1.0)*K   or  torch.exp(C1*torch.abs(x))-1.0
+        (rf"^\(torch\.exp\({_NUM}\*torch\.abs\(x\)\)-1(?:\.0)?\)\*{_NUM}$",
+         lambda m: (PEN["PEN_EXPABS"], num(m[1]), num(m[0]), 0.0)),
+        (rf"^torch\.exp\({_NUM}\*torch\.abs\(x\)\)-1(?:\.0)?$",
+         lambda m: (PEN["PEN_EXPABS"], 1.0, num(m[0]), 0.0)),
+    ]
+    for pat, mk in pats:
+        m = re.match(pat, body)
+        if m:
+            return mk(m.groups())
+    raise ValueError(f"unsupported penalty function string: {src!r}")
+
+
+def _f32(x) -> float:
+    return float(np.float32(x))
+
+
+def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
+    """Resolve the task config into the kernel constant block."""
+    env = task_cfg["env"]
+    dyn = task_cfg["dynamics"]
+    dist = env["disturbances"]
+    c = UsvCfg()
+
+    # ---- integration ----
+    dt = float(task_cfg["sim"]["dt"])
+    c.dt = dt
+    c.substeps = int(env.get("controlFrequencyInv", 10))
+    tau = float(dyn["thrusters"]["timeConstant"])
+    # alpha = torch.exp(torch.tensor(-dt/tau)) in fp32 (ThrusterDynamics.py:132);
+    # -dt/tau is formed in double from the yaml values, then rounded once.
+    c.thr_alpha = float(np.exp(np.float32(-dt / tau), dtype=np.float32))
+    c.thr_y = HERON_THRUSTER_Y
+    c.izz0 = HERON_IZZ
+    hd = dyn["hydrodynamics"]
+    lin, quad = hd["linear_damping"], hd["quadratic_damping"]
+    fwd = hd["linear_damping_forward_speed"]
+    for k, dof in enumerate((0, 1, 5)):  # u, v, r
+        # lin + offset - (fwd + offset_fwd) (Hydrodynamics.py:185-192), in fp32
+        l = np.float32(lin[dof]) + np.float32(hd["offset_linear_damping"])
+        l = l - (np.float32(fwd[dof]) + np.float32(hd["offset_lin_forward_damping_speed"]))
+        c.lin_damp[k] = float(np.float32(l))
+        c.quad_damp[k] = float(np.float32(quad[dof]) + np.float32(hd["offset_nonlin_damping"]))
+    c.scaling_damping = hd["scaling_damping"]
+
+    # ---- domain randomisation / coupling flags (USV_Virtual.py:361-528) ----
+    mass = dist["mass"]
+    drag = dist.get("drag", {}) or {}
+    thr = dist.get("thruster", {}) or {}
+    inertia = dist.get("inertia", {}) or {}
+    coupling = ((dist.get("coupling", {}) or {}).get("mass_driven", {}) or {})
+    mass_dr = bool(mass.get("add_mass_disturbances", False))
+    coupled = bool(coupling.get("enabled", False)) and mass_dr
+    targets = coupling.get("targets", ["drag_scale", "thruster", "yaw_inertia"]) or []
+    if isinstance(targets, str):
+        targets = [targets]
+    c.couple_drag = int(coupled and "drag_scale" in targets)
+    c.couple_thr = int(coupled and "thruster" in targets)
+    c.couple_kiz = int(coupled and "yaw_inertia" in targets)
+    c.indep_kdrag_on = int(bool(drag.get("use_drag_scale_randomization", False)))
+    c.kdrag_log = int(str(drag.get("k_drag_sample_space", "linear")) == "log")
+    c.indep_thr_on = int(bool(thr.get("use_thruster_randomization", False)) or bool(c.couple_thr))
+    c.thr_separate = int(bool(thr.get("use_separate_randomization", False)) and not c.couple_thr)
+    c.thr_rand = float(thr.get("thruster_rand", 0.0))
+    c.left_rand = float(thr.get("left_rand", 0.0))
+    c.right_rand = float(thr.get("right_rand", 0.0))
+    c.indep_kiz_on = int(bool(inertia.get("use_yaw_inertia_randomization", False)))
+    c.kiz_log = int(str(inertia.get("k_Iz_sample_space", "linear")) == "log")
+    c.use_drag_scale = int(bool(c.indep_kdrag_on) or bool(c.couple_drag))
+    c.use_thr_mult = int(bool(c.indep_thr_on))
+    c.drag_rand_on = int(bool(drag.get("use_drag_randomization", False)))
+    for k, dof in enumerate((0, 1, 5)):
+        key = "uvwpqr"[dof]
+        c.lin_rand[k] = float(drag.get(f"{key}_linear_rand", 0.0)) * lin[dof]
+        c.quad_rand[k] = float(drag.get(f"{key}_quad_rand", 0.0)) * quad[dof]
+
+    c.mass_dr_on = int(mass_dr)
+    c.base_mass = float(mass.get("base_mass", mass.get("min_mass", 0.0)))
+    c.mass_min = float(mass.get("min_mass", c.base_mass))
+    c.mass_max = float(mass.get("max_mass", c.base_mass))
+    base_com = [float(v) for v in mass.get("base_com", [0.0, 0.0, 0.0])]
+    for a in range(3):
+        c.base_com[a] = base_com[a]
+    if mass.get("com_displacement_xyz", None) is not None:
+        c.com_mode = 1
+        for a in range(3):
+            c.com_disp[a] = float(mass["com_displacement_xyz"][a])
+    elif float(mass.get("CoM_max_displacement", 0.0) or 0.0) > 0.0:
+        c.com_mode = 2
+        c.com_legacy_r = float(mass["CoM_max_displacement"])
+    else:
+        c.com_mode = 0
+
+    # ---- actions ----
+    ap = env.get("action_processing", {}) or {}
+    c.clip_actions = float(env.get("clipActions", 1.0))
+    c.affine_thrust = int(bool(ap.get("use_affine_thrust_mapping", True)))
+    an = dist["actions"]
+    c.act_noise_on = int(bool(an["add_noise_on_act"]))
+    c.act_noise_min, c.act_noise_max = an["min_action_noise"], an["max_action_noise"]
+    on = dist["observations"]
+    c.pos_noise_on = int(bool(on["add_noise_on_pos"]))
+    c.pos_noise_min, c.pos_noise_max = on["position_noise_min"], on["position_noise_max"]
+    c.vel_noise_on = int(bool(on["add_noise_on_vel"]))
+    c.vel_noise_min, c.vel_noise_max = on["velocity_noise_min"], on["velocity_noise_max"]
+    c.head_noise_on = int(bool(on["add_noise_on_heading"]))
+    c.head_noise_min, c.head_noise_max = on["heading_noise_min"], on["heading_noise_max"]
+
+    # ---- observation ----
+    frame = env.get("observation_frame", "local")
+    if frame not in ("local", "global"):
+        raise ValueError(f"observation_frame must be local/global, got {frame}")
+    c.obs_local = int(frame == "local")
+    c.priv_dim = int(env.get("priv_dim", env.get("mass_dim", 4)))
+    if c.priv_dim not in (4, 8):
+        raise ValueError(f"Unsupported priv_dim/mass_dim={c.priv_dim}. Supported: 4 or 8.")
+    clip_obs = env.get("clipObservations", {"state": 12.0})
+    c.clip_obs = float(clip_obs["state"] if isinstance(clip_obs, dict) else clip_obs)
+    src = str(mass.get("masscom_obs_source", "sim"))
+    if src not in ("sim", "base"):
+        raise ValueError(f"mass.masscom_obs_source must be 'sim' or 'base', got {src}")
+    c.masscom_base = int(src == "base")
+    mom = mass.get("mass_obs_mode", "raw")
+    if mom not in ("raw", "relative"):
+        raise ValueError(f"Unknown mass_obs_mode: {mom}")
+    c.mass_relative = int(mom == "relative")
+    com_mode = mass.get("com_obs_mode", "raw")
+    if com_mode not in ("raw", "scaled"):
+        raise ValueError(f"Unknown com_obs_mode: {com_mode}")
+    c.com_scaled = int(com_mode == "scaled")
+    hs = dyn["hydrostatics"]
+    scale = mass.get("com_obs_scale", None)
+    if c.com_scaled and scale is None:
+        scale = [float(hs["box_length"]), float(hs["box_width"]), float(max(hs["heron_zero_height"], 1.0))]
+    if scale is not None:
+        for a in range(3):
+            c.com_scale[a] = float(scale[a])
+    pp = env.get("privileged_params", {}) or {}
+    mode = str(pp.get("mode", "raw"))
+    if mode not in ("raw", "centered", "minmax"):
+        raise ValueError(f"env.privileged_params.mode must be 'raw', 'centered' or 'minmax', got {mode}")
+    c.priv_mode = {"raw": 0, "centered": 1, "minmax": 2}[mode]
+    c.priv_nominal = float(pp.get("nominal", 1.0))
+    c.kdrag_min, c.kdrag_max = float(drag.get("k_drag_min", 1.0)), float(drag.get("k_drag_max", 1.0))
+    c.kiz_min, c.kiz_max = float(inertia.get("k_Iz_min", 1.0)), float(inertia.get("k_Iz_max", 1.0))
+    c.thr_min = 1.0 - c.thr_rand
+    c.thr_max = 1.0 if c.couple_thr else 1.0 + c.thr_rand
+    c.priv_drag_on = int(bool(drag.get("use_drag_scale_randomization", False)) or bool(c.couple_drag))
+    c.priv_thr_on = int(bool(thr.get("use_thruster_randomization", False)) or bool(c.couple_thr))
+    c.priv_kiz_on = int(bool(inertia.get("use_yaw_inertia_randomization", False)) or bool(c.couple_kiz))
+
+    # ---- task / reward ----
+    tp = dict(_TASK_DEFAULTS)
+    tp.update(env["task_parameters"])
+    if tp.get("name", "CaptureXY") != "CaptureXY":
+        raise ValueError("this kernel set implements the CaptureXY task")
+    c.position_tolerance = tp["position_tolerance"]
+    c.kill_after_n = int(tp["kill_after_n_steps_in_tolerance"])
+    c.kill_dist, c.boundary_cost = tp["kill_dist"], tp["boundary_cost"]
+    c.goal_reward, c.time_reward = tp["goal_reward"], tp["time_reward"]
+    c.goal_random_position = tp["goal_random_position"]
+    c.spawn_rmin, c.spawn_rmax = tp["min_spawn_dist"], tp["max_spawn_dist"]
+    rp = dict(_REWARD_DEFAULTS)
+    rp.update(env["reward_parameters"])
+    rm = rp["reward_mode"].lower()
+    if rm not in ("linear", "square", "exponential"):
+        raise ValueError("Linear, Square and Exponential are the only currently supported mode.")
+    c.reward_mode = {"linear": 0, "square": 1, "exponential": 2}[rm]
+    c.position_scale, c.exp_coeff = rp["position_scale"], rp["exponential_reward_coeff"]
+    c.align_la1, c.align_la2, c.align_la3 = rp["align_la1"], rp["align_la2"], rp["align_la3"]
+    c.collision_threshold = 1.2
+    c.obstacle_radius = 0.5
+    c.max_episode_length = int(env["maxEpisodeLength"])
+    c.fixed_horizon_eval = int(bool(env.get("fixed_horizon_eval", env.get("fixedHorizonEval", False))))
+
+    # ---- penalties ----
+    pen = dict(_PEN_DEFAULTS)
+    pen.update(env["penalties_parameters"])
+    for tag, key in (("lin", "linear_velocities"), ("ang", "angular_velocities"),
+                     ("angv", "angular_velocities_variation"), ("en", "energy"), ("actv", "action_variation")):
+        if bool(pen[f"penalize_{key}"]):
+            consts = {"c1": pen.get(f"penalize_{key}_c1", 0.0), "c2": pen.get(f"penalize_{key}_c2", 0.0)}
+            kind, k, x0, cc = parse_penalty_fn(pen[f"penalize_{key}_fn"], consts)
+        else:
+            kind, k, x0, cc = 0, 0.0, 0.0, 0.0
+        setattr(c, f"pen_{tag}_kind", kind)
+        setattr(c, f"pen_{tag}_k", k)
+        setattr(c, f"pen_{tag}_x0", x0)
+        setattr(c, f"pen_{tag}_c", cc)
+    if c.pen_lin_kind not in (0, PEN["PEN_NORM"]):
+        raise ValueError("linear-velocity penalty must be the norm form")
+    if c.pen_en_kind not in (0, PEN["PEN_SUM"], PEN["PEN_SUMSQ"]):
+        raise ValueError("energy penalty must be a sum form")
+    if c.pen_actv_kind != 0:
+        raise NotImplementedError("penalize_action_variation is not on the CaptureXY hot path")
+    c.pen_use_u = int(bool(ap.get("penalties_use_thrust_u", True)))
+
+    # ---- potential field (d_multi_gemini.py / static_obs.py:30-32) ----
+    c.map_size = 30.0
+    c.field_iters = int(150 * 1.5)
+    c.influence_radius, c.eta, c.safe_radius, c.field_alpha = 0.7, 20.0, 3.0, 0.5
+    # ---- spawn (static_obs.py:974-983) ----
+    c.obst_box, c.min_dist_safe, c.min_obs_sep = 12.0, 3.0, 2.5
+    c.init_vel = 1.5
+    c.stats_on = 1
+    if bool((env.get("scene_replay", {}) or {}).get("enabled", False)):
+        raise NotImplementedError("scene_replay (NPZ) is not supported yet; set env.scene_replay.enabled=False")
+    if bool(env.get("water_current", {}).get("use_water_current", False)):
+        raise NotImplementedError("water current is not on the CaptureXY hot path")
+    return c
+
+
+def action_bias_cfg(task_cfg: Dict[str, Any]):
+    ap = task_cfg["env"].get("action_processing", {}) or {}
+    return float(ap.get("initial_action_bias", 0.0)), int(ap.get("initial_action_bias_steps", 0))
+
+
+def thruster_tables(task_cfg: Dict[str, Any]):
+    it = task_cfg["dynamics"]["thrusters"]["interpolation"]
+    n = int(it["numberOfPointsForInterpolation"])
+    if n != 1000:
+        raise ValueError("numberOfPointsForInterpolation must be 1000")
+    return (np.asarray(it["interpolationPointsFromRealDataLeft"], np.float32),
+            np.asarray(it["interpolationPointsFromRealDataRight"], np.float32))
+
+
+def load_yaml(path: str) -> Dict[str, Any]:
+    import yaml
+    with open(path, "r", encoding="utf-8") as f:
+        return yaml.safe_load(f)

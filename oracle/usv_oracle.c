@@ -1,0 +1,868 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C, scalar, single-threaded restatement of the reference USV CaptureXY
+ * env path (loop-Z/omniisaacgymenvs_loop), written op-by-op after the PyTorch
+ * code it cites.  It is the parity checker for the HIP kernels and the
+ * `cpu_baseline` ("port") leg of bench.py.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline may load it; the product (libusv_hip.so) never
+ * links or calls it.
+ *
+ * Parity pinning: tests/golden/*.npz were produced by importing the reference
+ * Python in the build container (tests/golden/make_golden.py) and recording its
+ * outputs together with every torch.rand draw it consumed; tests/test_oracle_*.py
+ * replay those draws through this file.
+ *
+ * The rigid-body integrator has NO reference implementation (the reference
+ * calls PhysX through Isaac Sim, envs/vec_env_rlgames.py:154-171).  The 3-DoF
+ * semi-implicit Euler below is this build's own definition; the
+ * forces it integrates are pinned to the reference force model
+ * (Hydrodynamics.py:176-245, ThrusterDynamics.py:129-234).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "../include/usv_hip.h"
+#include "oracle_philox.h"
+
+#define OPI 3.14159265358979323846
+
+static inline float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+static inline float maxf_(float a, float b) { return a > b ? a : b; }
+static inline float minf_(float a, float b) { return a < b ? a : b; }
+/* torch.norm(v, dim=-1) of a 2-vector on CPU is sqrt(fma(y, y, x*x)) bit-for-bit
+ * (checked on 2M random pairs); sum-of-squares reductions ((e*e).sum(-1)) are
+ * plain x*x + y*y. */
+static inline float tnorm2(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
+
+/* ------------------------------------------------------------------------ */
+/* Philox streams (same mapping as the kernels)                              */
+/* ------------------------------------------------------------------------ */
+void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+  oracle_philox4x32_10(ctr, key, out);
+}
+
+static float philox_u(uint64_t seed, uint32_t env, uint64_t step, uint32_t site, int i) {
+  uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+  uint32_t ctr[4] = {env, (uint32_t)step, (uint32_t)(step >> 32), site + (uint32_t)(i >> 2)};
+  uint32_t out[4];
+  oracle_philox4x32_10(ctr, key, out);
+  return oracle_u01(out[i & 3]);
+}
+
+/* uniforms one env consumes in one step (layout SU_* in usv_hip.h) */
+void oracle_step_uniforms(uint64_t seed, uint64_t step, int n, float *u /*[n][USV_NU_STEP]*/) {
+  for (int e = 0; e < n; ++e)
+    for (int i = 0; i < USV_NU_STEP; ++i) u[(size_t)e * USV_NU_STEP + i] = philox_u(seed, (uint32_t)e, step, 0u, i);
+}
+
+/* uniforms of the reset slots (layout RU_* in usv_hip.h) */
+void oracle_reset_uniforms(uint64_t seed, uint64_t step, int k, const int32_t *ids, float *u /*[k][USV_NU_RESET]*/) {
+  for (int s = 0; s < k; ++s)
+    for (int i = 0; i < USV_NU_RESET; ++i)
+      u[(size_t)s * USV_NU_RESET + i] = philox_u(seed, (uint32_t)ids[s], step, 0x100u, i);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Thruster LUT: DynamicsFirstOrder.interpolate_on_field_data                */
+/* (ThrusterDynamics.py:152-177) = F.interpolate(mode="linear",               */
+/* align_corners=True) of the 21-point table onto 1000 points (fp32).         */
+/* ------------------------------------------------------------------------ */
+void oracle_lut(const float *table, int n_in, int n_out, float *lut) {
+  const float scale = (n_out > 1) ? (float)(n_in - 1) / (float)(n_out - 1) : 0.f;
+  for (int i = 0; i < n_out; ++i) {
+    const float src = scale * (float)i;
+    int i0 = (int)src;
+    if (i0 > n_in - 1) i0 = n_in - 1;
+    const int off = (i0 < n_in - 1) ? 1 : 0;
+    const float l1 = src - (float)i0;
+    const float l0 = 1.0f - l1;
+    lut[i] = fmaf(l0, table[i0], l1 * table[i0 + off]);   /* torch CPU build contracts to this FMA */
+  }
+}
+
+/* index used by DynamicsFirstOrder.get_cmd_interpolated (ThrusterDynamics.py:187-191) */
+static inline int lut_index(float cmd, int n) {
+  float t = (cmd + 1.0f) / 2.0f;
+  t = t * (float)(n - 1);
+  int idx = (int)rintf(t);        /* torch.round: half to even */
+  if (idx < 0) idx = 0;
+  if (idx > n - 1) idx = n - 1;
+  return idx;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Env state (SoA, host memory)                                             */
+/* ------------------------------------------------------------------------ */
+typedef struct oracle_env {
+  int n;
+  float *px, *py, *yaw, *vx, *vy, *wz, *fl, *fr;
+  float *mass, *com_x, *com_y, *com_z, *k_drag, *thr_l, *thr_r, *k_iz, *mass_r;
+  float *lin_damp, *quad_damp;      /* [3][n] or NULL */
+  float *tgt_x, *tgt_y;
+  float *obst;                      /* [16][2][n] */
+  float *field;                     /* [n][150*150] */
+  float *prev_cmd;                  /* [2][n] */
+  float *prev_dist, *prev_head, *prev_pot, *prev_wz;
+  int32_t *goal_cnt, *progress, *reset_buf;
+  uint8_t *just_reset;
+  int32_t *done_succ, *done_coll;
+  float *stats;                     /* [28][n] */
+  float *obs;                       /* [n][33] */
+  float *rew;
+  int32_t ctl[USV_CTL_N];
+  float extras[USV_NSTAT];
+  /* diagnostics of the last step (for parity tests) */
+  float *dbg;                       /* [n][16]: u_l, u_r, target_l, target_r, pot, danger, ... */
+  float *tmp;                       /* [n][8]: cmd[2], thrust[2], unit[2], target force[2] */
+  const float *grid_lin;            /* [150] potential-field cell centres, NULL => linspace formula */
+} oracle_env_t;
+
+/* ------------------------------------------------------------------------ */
+/* Forces: HydrodynamicsObject.ComputeDampingMatrix/ComputeHydrodynamicsEffects
+ * (Hydrodynamics.py:176-245) restricted to the planar DOFs u, v, r; thrusters
+ * at the heron.usd lever arms.                           */
+/* ------------------------------------------------------------------------ */
+static void planar_forces(const usv_cfg_t *c, const oracle_env_t *E, int e, float cy, float sy,
+                          float fl, float fr, float *X, float *Y, float *N) {
+  const float vx = E->vx[e], vy = E->vy[e], wz = E->wz[e];
+  /* getLocalLinearVelocities: R^T v  (Utils.py:8-12) */
+  const float u = cy * vx + sy * vy;
+  const float v = -sy * vx + cy * vy;
+  const float r = wz;
+  float lin[3], quad[3];
+  for (int k = 0; k < 3; ++k) {
+    lin[k] = E->lin_damp ? E->lin_damp[k * E->n + e] : c->lin_damp[k];
+    quad[k] = E->quad_damp ? E->quad_damp[k * E->n + e] : c->quad_damp[k];
+  }
+  const float vel[3] = {u, v, r};
+  float drag[3];
+  for (int k = 0; k < 3; ++k) {
+    float D = lin[k] + quad[k] * fabsf(vel[k]);           /* lin_damp + quad_damp (:185-196) */
+    D = D * c->scaling_damping;                            /* (:199) */
+    if (c->use_drag_scale) D = D * E->k_drag[e];           /* k_drag (:202-203) */
+    drag[k] = -D * vel[k];                                 /* (:243) */
+  }
+  const float comy = E->com_y[e];
+  *X = fl + fr + drag[0];
+  *Y = drag[1];
+  *N = -(c->thr_y - comy) * fl + (c->thr_y + comy) * fr + drag[2];
+}
+
+void oracle_forces(const usv_cfg_t *c, oracle_env_t *E, float *out /*[n][3]*/) {
+  for (int e = 0; e < E->n; ++e) {
+    const float cy = cosf(E->yaw[e]), sy = sinf(E->yaw[e]);
+    float X, Y, N;
+    planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], &X, &Y, &N);
+    out[e * 3 + 0] = X; out[e * 3 + 1] = Y; out[e * 3 + 2] = N;
+  }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Potential field: BatchedMapGPU (tasks/USV/d_multi_gemini.py:7-271)        */
+/* K envs, obstacles [K][16][2], targets [K][2] -> field [K][150][150]       */
+/* ------------------------------------------------------------------------ */
+static void grid_coords(float *lin /*150*/, float map_size) {
+  /* torch.linspace(-map/2 + cell/2, map/2 - cell/2, 150) (:18-20) */
+  const double cell_d = (double)map_size / USV_GRID;
+  const float start = (float)(-(double)map_size / 2 + cell_d / 2);
+  const float end = (float)((double)map_size / 2 - cell_d / 2);
+  const float step = (end - start) / (float)(USV_GRID - 1);
+  const int half = USV_GRID / 2;
+  for (int i = 0; i < USV_GRID; ++i)
+    lin[i] = (i < half) ? start + step * (float)i : end - step * (float)(USV_GRID - i - 1);
+}
+
+void oracle_grid_lin(float map_size, float *lin) { grid_coords(lin, map_size); }
+
+void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][16][2]*/,
+                            const float *tgt /*[K][2]*/, float *field /*[K][G2]*/,
+                            float *cost_out /*[K][G2] optional*/, const float *grid_lin) {
+  const int G = USV_GRID, G2 = USV_GRID2;
+  float lin[USV_GRID];
+  if (grid_lin) memcpy(lin, grid_lin, sizeof(lin));
+  else grid_coords(lin, c->map_size);
+  const float cell = (float)((double)c->map_size / G);
+  float *sdf = (float *)malloc(sizeof(float) * (size_t)K * G2);
+  uint8_t *freec = (uint8_t *)malloc((size_t)K * G2);
+  float *cost = (float *)malloc(sizeof(float) * (size_t)K * G2);
+  float *nxt = (float *)malloc(sizeof(float) * (size_t)G2);
+  /* compute_occupancy_and_sdf (:66-104) */
+  for (int k = 0; k < K; ++k) {
+    for (int i = 0; i < G; ++i)
+      for (int j = 0; j < G; ++j) {
+        const float gx = lin[j], gy = lin[i];
+        float m = INFINITY;
+        for (int o = 0; o < USV_NOBST; ++o) {
+          const float dx = gx - obst[(k * USV_NOBST + o) * 2 + 0];
+          const float dy = gy - obst[(k * USV_NOBST + o) * 2 + 1];
+          const float d = tnorm2(dx, dy);
+          if (d < m) m = d;
+        }
+        const float s = m - c->obstacle_radius;
+        sdf[(size_t)k * G2 + i * G + j] = s;
+        int occ = (s <= 0.f);
+        if (i == 0 || i == G - 1 || j == 0 || j == G - 1) occ = 1;
+        freec[(size_t)k * G2 + i * G + j] = (uint8_t)(occ ? 0 : 1);  /* is_free = occ < 0.5 (:162) */
+      }
+  }
+  /* compute_cost_field_wavefront (:135-192): Jacobi relaxation, fixed iterations */
+  const float diag = 1.414f;
+  for (int k = 0; k < K; ++k) {
+    float *C = cost + (size_t)k * G2;
+    const uint8_t *F = freec + (size_t)k * G2;
+    for (int q = 0; q < G2; ++q) C[q] = INFINITY;
+    const float half_map = (float)((double)c->map_size / 2);
+    const float tx = (tgt[k * 2 + 0] + half_map) / cell;
+    const float ty = (tgt[k * 2 + 1] + half_map) / cell;
+    long ix = (long)tx, iy = (long)ty;       /* .long() truncates */
+    if (ix < 0) ix = 0; if (ix > G - 1) ix = G - 1;
+    if (iy < 0) iy = 0; if (iy > G - 1) iy = G - 1;
+    C[iy * G + ix] = 0.f;
+    for (int it = 0; it < c->field_iters; ++it) {
+      int changed = 0;
+      for (int i = 0; i < G; ++i)
+        for (int j = 0; j < G; ++j) {
+          float m = C[i * G + j];
+          for (int di = -1; di <= 1; ++di)
+            for (int dj = -1; dj <= 1; ++dj) {
+              if (!di && !dj) continue;
+              const int ii = i + di, jj = j + dj;
+              if (ii < 0 || ii >= G || jj < 0 || jj >= G) continue;
+              const float cand = C[ii * G + jj] + ((di && dj) ? diag : 1.0f);
+              if (cand < m) m = cand;
+            }
+          const float nv = F[i * G + j] ? m : INFINITY;
+          if (nv != C[i * G + j]) changed = 1;
+          nxt[i * G + j] = nv;
+        }
+      memcpy(C, nxt, sizeof(float) * G2);
+      if (!changed) break;   /* a Jacobi fixed point stays fixed: exact early exit */
+    }
+  }
+  if (cost_out) memcpy(cost_out, cost, sizeof(float) * (size_t)K * G2);
+  /* compute_potential_field (:194-271) */
+  float max_val = -INFINITY;
+  int any_finite = 0;
+  for (size_t q = 0; q < (size_t)K * G2; ++q)
+    if (isfinite(cost[q])) { any_finite = 1; if (cost[q] > max_val) max_val = cost[q]; }
+  if (!any_finite) max_val = 100.0f;
+  const float inf_val = max_val * 1.5f;
+  float *J = (float *)malloc(sizeof(float) * (size_t)K * G2);
+  float jmax = -INFINITY;
+  int any_inside = 0;
+  const float inv_r = (float)(1.0 / (double)c->influence_radius);
+  for (int k = 0; k < K; ++k)
+    for (int q = 0; q < G2; ++q) {
+      const size_t p = (size_t)k * G2 + q;
+      const float cv = isinf(cost[p]) ? inf_val : cost[p];
+      const float dte = sdf[p] - c->obstacle_radius;
+      const float dist_goal = cv * cell;
+      const float rmask = clampf_(dist_goal / c->safe_radius, 0.f, 1.f);
+      float j = 0.f;
+      if (dte < c->influence_radius) {
+        const float d = maxf_(dte, 1e-3f);
+        const float t = 1.0f / d - inv_r;
+        j = c->eta * (t * t) * rmask;
+      }
+      J[p] = j;
+      if (j > jmax) jmax = j;
+      if (dte <= 0.f) any_inside = 1;
+    }
+  if (any_inside) {
+    const float high = (jmax > 1e-6f) ? jmax * 10.0f : 100.0f;
+    for (int k = 0; k < K; ++k)
+      for (int q = 0; q < G2; ++q) {
+        const size_t p = (size_t)k * G2 + q;
+        if (sdf[p] - c->obstacle_radius <= 0.f) J[p] = high;
+      }
+  }
+  for (int k = 0; k < K; ++k) {
+    float gmin = INFINITY, gmax = -INFINITY, jmn = INFINITY, jmx = -INFINITY;
+    for (int q = 0; q < G2; ++q) {
+      const size_t p = (size_t)k * G2 + q;
+      const float cv = isinf(cost[p]) ? inf_val : cost[p];
+      gmin = minf_(gmin, cv); gmax = maxf_(gmax, cv);
+      jmn = minf_(jmn, J[p]); jmx = maxf_(jmx, J[p]);
+    }
+    const float gden = (gmax - gmin) + 1e-6f;
+    const float jden = (jmx - jmn) + 1e-6f;
+    for (int q = 0; q < G2; ++q) {
+      const size_t p = (size_t)k * G2 + q;
+      const float cv = isinf(cost[p]) ? inf_val : cost[p];
+      const float gn = (cv - gmin) / gden;
+      const float jn = (J[p] - jmn) / jden;
+      field[p] = gn + c->field_alpha * jn;
+    }
+  }
+  free(sdf); free(freec); free(cost); free(nxt); free(J);
+}
+
+/* ------------------------------------------------------------------------ */
+/* grid_sample(field, 2*pos/map, bilinear, align_corners=False, border)      */
+/* (USV_capture_xy_static_obs.py:302-326)                                    */
+/* ------------------------------------------------------------------------ */
+static float sample_field(const float *F, float map_size, float x, float y) {
+  /* PyTorch CPU grid_sampler_2d, bilinear/border/align_corners=False
+   * (aten/src/ATen/native/cpu/GridSamplerKernel.cpp: ComputeLocation::unnormalize
+   * = (g + 1) * (size / 2) - 0.5, clip to [0, size-1]; weights from floor).
+   * The CPU build contracts the unnormalise and the corner sum into FMAs;
+   * this form reproduces torch's result bit-for-bit (tests/test_oracle_golden.py). */
+  const int G = USV_GRID;
+  const float gx = 2.0f * x / map_size, gy = 2.0f * y / map_size;
+  const float half = (float)G / 2.0f;
+  float ix = fmaf(gx + 1.f, half, -0.5f);
+  float iy = fmaf(gy + 1.f, half, -0.5f);
+  ix = minf_((float)(G - 1), maxf_(ix, 0.f));
+  iy = minf_((float)(G - 1), maxf_(iy, 0.f));
+  const float xw = floorf(ix), yn = floorf(iy);
+  const float w = ix - xw, e = 1.f - w;
+  const float nn = iy - yn, ss = 1.f - nn;
+  const float nw = ss * e, ne = ss * w, sw = nn * e, se = nn * w;
+  const int i0 = (int)xw, j0 = (int)yn, i1 = i0 + 1, j1 = j0 + 1;
+  const float v_nw = (i0 >= 0 && i0 < G && j0 >= 0 && j0 < G) ? F[j0 * G + i0] : 0.f;
+  const float v_ne = (i1 >= 0 && i1 < G && j0 >= 0 && j0 < G) ? F[j0 * G + i1] : 0.f;
+  const float v_sw = (i0 >= 0 && i0 < G && j1 >= 0 && j1 < G) ? F[j1 * G + i0] : 0.f;
+  const float v_se = (i1 >= 0 && i1 < G && j1 >= 0 && j1 < G) ? F[j1 * G + i1] : 0.f;
+  return fmaf(v_se, se, fmaf(v_sw, sw, fmaf(v_ne, ne, v_nw * nw)));
+}
+
+float oracle_sample_field(const float *F, float map_size, float x, float y) { return sample_field(F, map_size, x, y); }
+
+/* ------------------------------------------------------------------------ */
+/* Penalties.compute_penalty closed forms (USV_task_rewards.py:440-523)      */
+/* ------------------------------------------------------------------------ */
+static float pen_scalar(int kind, float k, float x0, float cc, float x) {
+  switch (kind) {
+    case PEN_DEADZONE: return -maxf_(fabsf(x) - x0, 0.f) * k + cc;
+    case PEN_EXPABS: return (expf(x0 * fabsf(x)) - 1.0f) * k + cc;
+    default: return 0.f;
+  }
+}
+
+/* priv-tail encoders (USV_Virtual.py:97-151) */
+static float enc_centered(float x, float xmin, float xmax, float nominal) {
+  double s = fabs((double)xmin - nominal);
+  if (fabs((double)xmax - nominal) > s) s = fabs((double)xmax - nominal);
+  if (1e-6 > s) s = 1e-6;
+  return clampf_((x - nominal) / (float)s, -1.f, 1.f);
+}
+static float enc_minmax(float x, float xmin, float xmax) {
+  if ((double)xmax - (double)xmin <= 1e-6) return 0.f;
+  const float z = (x - xmin) / (float)((double)xmax - (double)xmin);
+  return clampf_(2.0f * z - 1.0f, -1.f, 1.f);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reset path: USVVirtual.reset_idx (USV_Virtual.py:1502-1618)               */
+/* ids: compacted reset list (reset_buf.nonzero(), :1045); u: [k][NU_RESET]. */
+/* ------------------------------------------------------------------------ */
+void oracle_reset(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids, const float *U) {
+  const int n = E->n;
+  if (k <= 0) return;
+  float *obst_k = (float *)malloc(sizeof(float) * (size_t)k * USV_NOBST * 2);
+  float *tgt_k = (float *)malloc(sizeof(float) * (size_t)k * 2);
+  float *fld_k = (float *)malloc(sizeof(float) * (size_t)k * USV_GRID2);
+  /* extras: episode sums of the envs being reset, BEFORE they are cleared (:1591-1612);
+   * success/collision come from get_episode_outcomes (:1508-1514, static_obs.py:708-713) */
+  double acc[USV_NSTAT];
+  memset(acc, 0, sizeof(acc));
+  for (int s = 0; s < k; ++s) {
+    const int e = ids[s];
+    for (int q = 0; q < USV_NSTAT; ++q) {
+      float v = E->stats[q * n + e];
+      if (q == ST_SUCCESS) v = (float)E->done_succ[e];
+      if (q == ST_COLLISION) v = (float)E->done_coll[e];
+      acc[q] += v;
+    }
+  }
+  for (int q = 0; q < USV_NSTAT; ++q) {
+    float m = (float)(acc[q] / k);
+    if (q != ST_SUCCESS && q != ST_COLLISION) m = m / (float)c->max_episode_length;
+    E->extras[q] = isnan(m) ? 0.f : m;
+  }
+  E->ctl[USV_CTL_POT_VALID] = 0;  /* CaptureXYTask.reset: prev_potential = None (:773) */
+  for (int s = 0; s < k; ++s) {
+    const int e = ids[s];
+    const float *u = U + (size_t)s * USV_NU_RESET;
+    /* CaptureXYTask.reset (static_obs.py:767-778) */
+    E->goal_cnt[e] = 0; E->done_succ[e] = 0; E->done_coll[e] = 0;
+    E->just_reset[e] = 1;
+    /* MassDistributionDisturbances.randomize_masses (USV_disturbances.py:127-150) */
+    if (c->mass_dr_on) {
+      E->mass[e] = u[RU_MASS] * (float)((double)c->mass_max - (double)c->mass_min) + c->mass_min;
+    } else {
+      E->mass[e] = u[RU_MASS] * 0.0f + c->base_mass;
+    }
+    if (c->mass_dr_on && c->com_mode == 1) {         /* _randomize_com box (:98-103) */
+      float cm[3];
+      for (int a = 0; a < 3; ++a) cm[a] = c->base_com[a] + (u[RU_COM + a] * 2.0f - 1.0f) * c->com_disp[a];
+      E->com_x[e] = cm[0]; E->com_y[e] = cm[1]; E->com_z[e] = cm[2];
+    } else if (c->mass_dr_on && c->com_mode == 2 && c->com_legacy_r > 0.f) {  /* legacy disk (:112-124) */
+      const float r = u[RU_COM] * c->com_legacy_r;
+      const float th = u[RU_COM + 1] * (float)OPI * 2.0f;
+      E->com_x[e] = c->base_com[0] + cosf(th) * r;
+      E->com_y[e] = c->base_com[1] + sinf(th) * r;
+      E->com_z[e] = c->base_com[2];
+    } else {
+      E->com_x[e] = c->base_com[0]; E->com_y[e] = c->base_com[1]; E->com_z[e] = c->base_com[2];
+    }
+    /* independent yaw-inertia randomisation (USV_Virtual.py:193-240), skipped when coupled */
+    if (c->indep_kiz_on && !c->couple_kiz) {
+      const float uu = u[RU_KIZ];
+      E->k_iz[e] = c->kiz_log ? expf(logf(c->kiz_min) + uu * (logf(c->kiz_max) - logf(c->kiz_min)))
+                              : c->kiz_min + uu * (c->kiz_max - c->kiz_min);
+    }
+    /* HydrodynamicsObject.reset_coefficients (Hydrodynamics.py:136-174) */
+    if (c->drag_rand_on && E->lin_damp) {
+      for (int a = 0; a < 3; ++a) {
+        const int dof = (a == 2) ? 5 : a;  (void)dof;
+        E->lin_damp[a * n + e] = c->lin_damp[a] + (u[RU_DRAG + a] * 2.0f - 1.0f) * c->lin_rand[a];
+        E->quad_damp[a * n + e] = c->quad_damp[a] + (u[RU_DRAG + 6 + a] * 2.0f - 1.0f) * c->quad_rand[a];
+      }
+    }
+    if (c->indep_kdrag_on) {
+      const float uu = u[RU_KDRAG];
+      E->k_drag[e] = c->kdrag_log ? expf(logf(c->kdrag_min) + uu * (logf(c->kdrag_max) - logf(c->kdrag_min)))
+                                  : c->kdrag_min + uu * (c->kdrag_max - c->kdrag_min);
+    }
+    /* DynamicsFirstOrder.reset_thruster_randomization (ThrusterDynamics.py:112-127) */
+    if (c->indep_thr_on) {
+      if (c->thr_separate) {
+        E->thr_l[e] = u[RU_THR] * 2.0f * c->left_rand + (1.0f - c->left_rand);
+        E->thr_r[e] = u[RU_THR + 1] * 2.0f * c->right_rand + (1.0f - c->right_rand);
+      } else {
+        const float m = u[RU_THR] * 2.0f * c->thr_rand + (1.0f - c->thr_rand);
+        E->thr_l[e] = m; E->thr_r[e] = m;
+      }
+    }
+    /* _apply_mass_driven_coupling (USV_Virtual.py:988-1040) */
+    if (c->couple_drag || c->couple_thr || c->couple_kiz) {
+      const double denom = ((double)c->mass_max - (double)c->base_mass) > 1e-6 ? ((double)c->mass_max - (double)c->base_mass) : 1e-6;
+      float r = (E->mass[e] - c->base_mass) / (float)denom;
+      r = clampf_(r, 0.f, 1.f);
+      E->mass_r[e] = r;
+      if (c->couple_drag) E->k_drag[e] = c->kdrag_min + r * (float)((double)c->kdrag_max - (double)c->kdrag_min);
+      if (c->couple_thr) {
+        float s_thr = 1.0f - r * c->thr_rand;
+        s_thr = clampf_(s_thr, (float)(1.0 - (double)c->thr_rand), 1.0f);
+        E->thr_l[e] = s_thr; E->thr_r[e] = s_thr;
+      }
+      if (c->couple_kiz) E->k_iz[e] = c->kiz_min + r * (float)((double)c->kiz_max - (double)c->kiz_min);
+    }
+    /* CaptureXYTask.get_spawns (static_obs.py:936-1060).  The field and the
+     * obstacle box use the target of the PREVIOUS episode: get_goals runs later
+     * in set_targets (USV_Virtual.py:1618). */
+    const float rmin = c->spawn_rmin, rmax = c->spawn_rmax;
+    const float r = u[RU_SPAWN_R] * (rmax - rmin) + rmin;
+    const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
+    const float sx = r * cosf(th), sy = r * sinf(th);
+    const float yaw0 = u[RU_YAW] * (float)OPI;
+    /* quaternion (cos(yaw/2),0,0,sin(yaw/2)) -> yaw: identical in the planar state */
+    const float tx = E->tgt_x[e], ty = E->tgt_y[e];
+    float oc[USV_NOBST][2];
+    const float mn[2] = {tx - c->obst_box, ty - c->obst_box};
+    const float mx[2] = {tx + c->obst_box, ty + c->obst_box};
+    for (int o = 0; o < USV_NOBST; ++o)
+      for (int a = 0; a < 2; ++a) oc[o][a] = u[RU_OBST + o * 2 + a] * (mx[a] - mn[a]) + mn[a];
+    const float sep2 = c->min_obs_sep * c->min_obs_sep;
+    for (int it = 0; it < USV_SPAWN_ITERS; ++it) {
+      int inval[USV_NOBST], any = 0;
+      for (int o = 0; o < USV_NOBST; ++o) {
+        const float ds = tnorm2(oc[o][0] - sx, oc[o][1] - sy);
+        const float dt = tnorm2(oc[o][0] - tx, oc[o][1] - ty);
+        inval[o] = (ds < c->min_dist_safe) || (dt < c->min_dist_safe);
+      }
+      for (int j = 0; j < USV_NOBST; ++j)
+        for (int i = 0; i < j; ++i) {
+          const int vi = oc[i][0] < 900.f, vj = oc[j][0] < 900.f;
+          const float dx = oc[i][0] - oc[j][0], dy = oc[i][1] - oc[j][1];
+          if (vi && vj && (dx * dx + dy * dy) < sep2) inval[j] = 1;
+        }
+      for (int o = 0; o < USV_NOBST; ++o) any |= inval[o];
+      if (!any) break;
+      const float *rs = u + RU_RESAMPLE + it * USV_NOBST * 2;
+      for (int o = 0; o < USV_NOBST; ++o)
+        if (inval[o])
+          for (int a = 0; a < 2; ++a) oc[o][a] = rs[o * 2 + a] * (mx[a] - mn[a]) + mn[a];
+    }
+    {
+      int inval[USV_NOBST];
+      for (int o = 0; o < USV_NOBST; ++o) {
+        const float ds = tnorm2(oc[o][0] - sx, oc[o][1] - sy);
+        const float dt = tnorm2(oc[o][0] - tx, oc[o][1] - ty);
+        inval[o] = (ds < c->min_dist_safe) || (dt < c->min_dist_safe);
+      }
+      for (int j = 0; j < USV_NOBST; ++j)
+        for (int i = 0; i < j; ++i) {
+          const int vi = oc[i][0] < 900.f, vj = oc[j][0] < 900.f;
+          const float dx = oc[i][0] - oc[j][0], dy = oc[i][1] - oc[j][1];
+          if (vi && vj && (dx * dx + dy * dy) < sep2) inval[j] = 1;
+        }
+      for (int o = 0; o < USV_NOBST; ++o)
+        if (inval[o]) { oc[o][0] = 999.0f; oc[o][1] = 999.0f; }    /* limbo (:1042-1048) */
+    }
+    for (int o = 0; o < USV_NOBST; ++o) {
+      E->obst[(o * 2 + 0) * n + e] = oc[o][0];
+      E->obst[(o * 2 + 1) * n + e] = oc[o][1];
+      obst_k[(s * USV_NOBST + o) * 2 + 0] = oc[o][0];
+      obst_k[(s * USV_NOBST + o) * 2 + 1] = oc[o][1];
+    }
+    tgt_k[s * 2 + 0] = tx; tgt_k[s * 2 + 1] = ty;
+    /* pose and velocities (USV_Virtual.py:1541-1572) */
+    E->px[e] = sx; E->py[e] = sy; E->yaw[e] = yaw0;
+    E->vx[e] = u[RU_VX] * 3.0f - 1.5f;
+    E->vy[e] = u[RU_VY] * 3.0f - 1.5f;
+    E->wz[e] = 0.f;
+    /* bookkeeping (:1574-1579) */
+    E->reset_buf[e] = 0; E->progress[e] = 0;
+    E->prev_cmd[0 * n + e] = 0.f; E->prev_cmd[1 * n + e] = 0.f;
+    for (int q = 0; q < USV_NSTAT; ++q) E->stats[q * n + e] = 0.f;
+    E->stats[ST_SUCCESS * n + e] = 0.f; E->stats[ST_COLLISION * n + e] = 0.f;
+    /* set_targets -> get_goals (static_obs.py:913-930) */
+    const float g = c->goal_random_position;
+    E->tgt_x[e] = u[RU_GOAL + 0] * g * 2.0f - g;
+    E->tgt_y[e] = u[RU_GOAL + 1] * g * 2.0f - g;
+  }
+  /* potential field of the reset batch (static_obs.py:1054-1057) */
+  oracle_potential_field(c, k, obst_k, tgt_k, fld_k, NULL, E->grid_lin);
+  for (int s = 0; s < k; ++s)
+    memcpy(E->field + (size_t)ids[s] * USV_GRID2, fld_k + (size_t)s * USV_GRID2, sizeof(float) * USV_GRID2);
+  free(obst_k); free(tgt_k); free(fld_k);
+}
+
+void oracle_step_pre(const usv_cfg_t *c, oracle_env_t *E, const float *actions, const float *lut,
+                     float action_bias, const float *U);
+void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E);
+void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U);
+
+/* ------------------------------------------------------------------------ */
+/* One control step (VecEnvRLGames.step, envs/vec_env_rlgames.py:120-217)    */
+/* actions: [n][2] policy output; U: [n][NU_STEP] uniforms.                  */
+/* The reset part of pre_physics_step must be run first (oracle_reset).      */
+/* ------------------------------------------------------------------------ */
+void oracle_step(const usv_cfg_t *c, oracle_env_t *E, const float *actions, const float *lut /*[2][1000]*/,
+                 float action_bias, const float *U) {
+  oracle_step_pre(c, E, actions, lut, action_bias, U);
+  oracle_step_physics(c, E);
+  oracle_step_post(c, E, U);
+}
+
+void oracle_step_pre(const usv_cfg_t *c, oracle_env_t *E, const float *actions, const float *lut,
+                     float action_bias, const float *U) {
+  const int n = E->n;
+  for (int e = 0; e < n; ++e) {
+    const float *u = U + (size_t)e * USV_NU_STEP;
+    const int was_reset = E->just_reset[e];
+    float *dbg = E->dbg ? E->dbg + (size_t)e * 16 : NULL;
+    float *tmp = E->tmp + (size_t)e * 8;
+    /* ---- VecEnvRLGames.step: clamp actions (:136-140) ---- */
+    float cmd[2], thrust[2], uu[2], unit[2], tgt[2];
+    for (int a = 0; a < 2; ++a) cmd[a] = clampf_(actions[e * 2 + a], -c->clip_actions, c->clip_actions);
+    /* ---- USVVirtual.pre_physics_step (USV_Virtual.py:1050-1099) ---- */
+    for (int a = 0; a < 2; ++a) {
+      E->prev_cmd[a * n + e] = was_reset ? 0.f : cmd[a];                 /* :1064-1066 */
+      float t = cmd[a];
+      if (action_bias != 0.f) t = t + action_bias;                        /* :1071-1075 */
+      if (c->act_noise_on) t = t + (u[SU_ACT + a] * (float)((double)c->act_noise_max - (double)c->act_noise_min) + c->act_noise_min);
+      t = clampf_(t, -1.f, 1.f);                                          /* :1082 */
+      thrust[a] = t;
+      float v = c->affine_thrust ? 0.5f * (t + 1.0f) : clampf_(t, 0.f, 1.f);
+      v = clampf_(v, 0.f, 1.f);
+      unit[a] = v;                                                        /* thrust_cmds_unit :1095 */
+      uu[a] = was_reset ? 0.f : v;                                        /* :1097 */
+    }
+    /* set_target_force -> get_cmd_interpolated (ThrusterDynamics.py:179-219) */
+    for (int a = 0; a < 2; ++a) {
+      const int idx = lut_index(uu[a], USV_LUT_N);
+      float f = lut[a * USV_LUT_N + idx];
+      if (c->use_thr_mult) f = f * (a == 0 ? E->thr_l[e] : E->thr_r[e]);
+      tgt[a] = f;
+    }
+    if (dbg) { dbg[0] = uu[0]; dbg[1] = uu[1]; dbg[2] = tgt[0]; dbg[3] = tgt[1]; }
+    tmp[0] = cmd[0]; tmp[1] = cmd[1]; tmp[2] = thrust[0]; tmp[3] = thrust[1];
+    tmp[4] = unit[0]; tmp[5] = unit[1]; tmp[6] = tgt[0]; tmp[7] = tgt[1];
+  }
+}
+
+void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E) {
+  const float PI_F = (float)OPI, TWO_PI_F = (float)(2.0 * OPI);
+  for (int e = 0; e < E->n; ++e) {
+    const float *tmp = E->tmp + (size_t)e * 8;
+    const float tgt[2] = {tmp[6], tmp[7]};
+    /* ---- 10 physics substeps (:154-171): forces then integration ---- */
+    const float m = E->mass[e];
+    const float izz = c->izz0 * E->k_iz[e];
+    for (int s = 0; s < c->substeps; ++s) {
+      /* DynamicsFirstOrder.update (ThrusterDynamics.py:132-136) */
+      E->fl[e] = E->fl[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[0];
+      E->fr[e] = E->fr[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[1];
+      const float cy = cosf(E->yaw[e]), sy = sinf(E->yaw[e]);
+      float X, Y, N;
+      planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], &X, &Y, &N);
+      /* build's 3-DoF semi-implicit Euler (no reference: PhysX) */
+      const float ax = (cy * X - sy * Y) / m;
+      const float ay = (sy * X + cy * Y) / m;
+      const float aw = N / izz;
+      E->vx[e] = E->vx[e] + ax * c->dt;
+      E->vy[e] = E->vy[e] + ay * c->dt;
+      E->wz[e] = E->wz[e] + aw * c->dt;
+      E->px[e] = E->px[e] + E->vx[e] * c->dt;
+      E->py[e] = E->py[e] + E->vy[e] * c->dt;
+      float yw = E->yaw[e] + E->wz[e] * c->dt;
+      if (yw > PI_F) yw -= TWO_PI_F;
+      else if (yw <= -PI_F) yw += TWO_PI_F;
+      E->yaw[e] = yw;
+    }
+  }
+}
+
+void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
+  const int n = E->n;
+  const int any_reset_none = (E->ctl[USV_CTL_POT_VALID] == 0);
+  const int pen_valid = E->ctl[USV_CTL_PEN_VALID];
+  const int rew_valid = E->ctl[USV_CTL_REW_VALID];
+  const float PI_F = (float)OPI, TWO_PI_F = (float)(2.0 * OPI);
+  for (int e = 0; e < n; ++e) {
+    const float *u = U + (size_t)e * USV_NU_STEP;
+    const int was_reset = E->just_reset[e];
+    float *dbg = E->dbg ? E->dbg + (size_t)e * 16 : NULL;
+    const float *tmp = E->tmp + (size_t)e * 8;
+    const float cmd[2] = {tmp[0], tmp[1]}, thrust[2] = {tmp[2], tmp[3]}, unit[2] = {tmp[4], tmp[5]};
+    /* ---- post_physics_step (rl_task.py:283-303) ---- */
+    E->progress[e] += 1;
+    /* update_state (USV_Virtual.py:771-813) with the noise of the last call */
+    float px = E->px[e], py = E->py[e];
+    if (c->pos_noise_on) {
+      const float rng = (float)((double)c->pos_noise_max - (double)c->pos_noise_min);
+      px = px + (u[SU_PX] * rng + c->pos_noise_min);
+      py = py + (u[SU_PX + 1] * rng + c->pos_noise_min);
+    }
+    float vxn = E->vx[e], vyn = E->vy[e], wzn = E->wz[e];
+    if (c->vel_noise_on) {
+      const float rng = (float)((double)c->vel_noise_max - (double)c->vel_noise_min);
+      vxn = vxn + (u[SU_VX] * rng + c->vel_noise_min);
+      vyn = vyn + (u[SU_VY] * rng + c->vel_noise_min);
+      wzn = wzn + (u[SU_WZ] * rng + c->vel_noise_min);
+    }
+    float yawn = E->yaw[e];
+    if (c->head_noise_on) {
+      const float rng = (float)((double)c->head_noise_max - (double)c->head_noise_min);
+      yawn = yawn + (u[SU_HEAD] * rng + c->head_noise_min);
+    }
+    const float hc = cosf(yawn), hs = sinf(yawn);
+    /* ---- get_observations -> CaptureXYTask.get_state_observations (static_obs.py:193-299) ---- */
+    float obs[USV_NOBS];
+    memset(obs, 0, sizeof(obs));
+    const float ex = E->tgt_x[e] - px, ey = E->tgt_y[e] - py;
+    const float theta = atan2f(hs, hc);
+    const float beta = atan2f(ey, ex);
+    const float alpha = fmodf((beta - theta) + PI_F, TWO_PI_F) - PI_F;
+    const float herr = fabsf(alpha);
+    const float dist = sqrtf(ex * ex + ey * ey);       /* compute_reward :338 */
+    const float dist_n = tnorm2(ex, ey);                /* task_data[2] :224 */
+    float od[USV_NOBST], orx[USV_NOBST], ory[USV_NOBST];
+    float min_od = INFINITY;
+    for (int o = 0; o < USV_NOBST; ++o) {
+      orx[o] = E->obst[(o * 2 + 0) * n + e] - px;
+      ory[o] = E->obst[(o * 2 + 1) * n + e] - py;
+      od[o] = tnorm2(orx[o], ory[o]);
+      if (od[o] < min_od) min_od = od[o];
+    }
+    /* torch.topk(k=5, largest=False): ascending, ties keep lower index first */
+    int used[USV_NOBST] = {0}, sel[USV_NCLOSE];
+    for (int q = 0; q < USV_NCLOSE; ++q) {
+      int best = -1;
+      for (int o = 0; o < USV_NOBST; ++o)
+        if (!used[o] && (best < 0 || od[o] < od[best])) best = o;
+      used[best] = 1; sel[q] = best;
+    }
+    const float ct = cosf(theta), st = sinf(theta);
+    float task[5 + 3 * USV_NCLOSE];
+    memset(task, 0, sizeof(task));
+    task[0] = cosf(alpha); task[1] = sinf(alpha); task[2] = dist_n;
+    for (int q = 0; q < USV_NCLOSE; ++q) {
+      const int o = sel[q];
+      const float bx = orx[o] * ct + ory[o] * st;
+      const float by = -orx[o] * st + ory[o] * ct;
+      const float nf = sqrtf(bx * bx + by * by + 1e-6f);
+      task[5 + q * 3 + 0] = od[o] - c->obstacle_radius;
+      task[5 + q * 3 + 1] = -bx / nf;
+      task[5 + q * 3 + 2] = -by / nf;
+    }
+    /* Core.update_observation_tensor (USV_core.py:55-125) */
+    if (c->obs_local) {
+      obs[0] = hc * vxn + hs * vyn;
+      obs[1] = -hs * vxn + hc * vyn;
+    } else {
+      obs[0] = vxn; obs[1] = vyn;
+    }
+    obs[2] = wzn;
+    for (int q = 0; q < 5 + 3 * USV_NCLOSE; ++q) obs[3 + q] = task[q];
+    const int pa = USV_NOBS - c->priv_dim - 2;
+    obs[pa + 0] = E->prev_cmd[0 * n + e];
+    obs[pa + 1] = E->prev_cmd[1 * n + e];
+    /* privileged tail (USV_Virtual.py:840-976; MDD.get_masses USV_disturbances.py:153-194) */
+    {
+      float mass_o, com_o[3];
+      const float comv[3] = {E->com_x[e], E->com_y[e], E->com_z[e]};
+      if (c->masscom_base) {
+        mass_o = c->mass_relative ? 0.f : c->base_mass;
+        for (int a = 0; a < 3; ++a) com_o[a] = c->com_scaled ? c->base_com[a] / (c->com_scale[a] + 1e-6f) : c->base_com[a];
+      } else {
+        const float denom = (float)(fabs((double)c->base_mass) > 1e-6 ? fabs((double)c->base_mass) : 1e-6);
+        mass_o = c->mass_relative ? (E->mass[e] - c->base_mass) / denom : E->mass[e];
+        for (int a = 0; a < 3; ++a) com_o[a] = c->com_scaled ? comv[a] / (c->com_scale[a] + 1e-6f) : comv[a];
+      }
+      float *pt = obs + USV_NOBS - c->priv_dim;
+      pt[0] = mass_o; pt[1] = com_o[0]; pt[2] = com_o[1]; pt[3] = com_o[2];
+      if (c->priv_dim == 8) {
+        float kd, tl, tr, kz;
+        if (c->masscom_base) {
+          if (c->priv_mode == 2) {
+            kd = 0.5f * (c->kdrag_min + c->kdrag_max);
+            tl = tr = c->couple_thr ? (1.0f - 0.5f * c->thr_rand) : 1.0f;
+            kz = 0.5f * (c->kiz_min + c->kiz_max);
+          } else { kd = tl = tr = kz = 1.0f; }
+        } else {
+          kd = E->k_drag[e];
+          tl = E->thr_l[e]; tr = E->thr_r[e];
+          kz = E->k_iz[e];
+        }
+        if (c->priv_mode == 1) {
+          kd = enc_centered(kd, c->kdrag_min, c->kdrag_max, c->priv_nominal);
+          tl = enc_centered(tl, c->thr_min, c->thr_max, c->priv_nominal);
+          tr = enc_centered(tr, c->thr_min, c->thr_max, c->priv_nominal);
+          kz = enc_centered(kz, c->kiz_min, c->kiz_max, c->priv_nominal);
+        } else if (c->priv_mode == 2) {
+          kd = c->priv_drag_on ? enc_minmax(kd, c->kdrag_min, c->kdrag_max) : 0.f;
+          tl = c->priv_thr_on ? enc_minmax(tl, c->thr_min, c->thr_max) : 0.f;
+          tr = c->priv_thr_on ? enc_minmax(tr, c->thr_min, c->thr_max) : 0.f;
+          kz = c->priv_kiz_on ? enc_minmax(kz, c->kiz_min, c->kiz_max) : 0.f;
+        }
+        pt[4] = kd; pt[5] = tl; pt[6] = tr; pt[7] = kz;
+      }
+    }
+    /* ---- calculate_metrics -> CaptureXYTask.compute_reward (static_obs.py:335-657) ---- */
+    const float bover = maxf_(dist - c->kill_dist, 0.f);
+    const float bx_ = minf_(bover / 0.25f, 20.0f);
+    const float boundary_pen = -expm1f(bx_) * c->boundary_cost;
+    const int gir = dist < c->position_tolerance;
+    E->goal_cnt[e] = E->goal_cnt[e] * gir + gir;
+    /* CaptureXYReward.compute_reward (USV_task_rewards.py:44-80) */
+    const float prev_err = rew_valid ? E->prev_dist[e] : dist;
+    float dist_r;
+    if (c->reward_mode == 0) dist_r = c->position_scale * (prev_err - dist);
+    else if (c->reward_mode == 1) dist_r = c->position_scale * (prev_err * prev_err - dist * dist);
+    else dist_r = c->position_scale * (expf(-dist / c->exp_coeff) - expf(-prev_err / c->exp_coeff));
+    const float h2 = herr * herr;
+    float align_r = c->align_la1 * (expf(c->align_la2 * (h2 * h2)) + expf(c->align_la3 * h2));
+    if (was_reset) dist_r = 0.f;                                          /* :374 */
+    const float prev_dist = was_reset ? dist : (rew_valid ? E->prev_dist[e] : dist);  /* :361-380 */
+    const float pot = sample_field(E->field + (size_t)e * USV_GRID2, c->map_size, px, py);
+    const float pn = clampf_(pot, 0.f, 1.f);
+    const float xs = clampf_((pn - 0.6f) / (0.3f + 1e-6f), 0.f, 1.f);
+    const float danger = xs * xs * (3.0f - 2.0f * xs);
+    align_r = align_r * maxf_(0.3f, 1.0f - danger);
+    dist_r = dist_r * maxf_(0.6f, 1.0f - danger * 0.5f);
+    const float g = clampf_(cosf(herr), 0.f, 1.f);
+    dist_r = minf_(dist_r, 0.f) + g * maxf_(dist_r, 0.f);
+    float prev_h = (rew_valid && !was_reset) ? E->prev_head[e] : herr;
+    float hi = clampf_(prev_h - herr, -0.4f, 0.4f);
+    const float hi_r = hi * 0.05f;
+    E->prev_head[e] = herr;
+    const float prev_pot = (any_reset_none || was_reset) ? pot : E->prev_pot[e];
+    float praw = (prev_pot - pot) * 100.0f;
+    if (fabsf(praw) < 0.01f) praw = 0.f;
+    const float pa1 = 2.0f * tanhf(praw / (2.0f + 1e-6f));
+    const float gdx = ex / (dist + 1e-6f), gdy = ey / (dist + 1e-6f);
+    const float vtow = vxn * gdx + vyn * gdy;
+    const float vtp = maxf_(vtow, 0.f);
+    const float dd = prev_dist - dist;
+    const float ddp = maxf_(dd, 0.f);
+    const float gv = clampf_((vtp - 0.02f) / ((0.15f - 0.02f) + 1e-6f), 0.f, 1.f);
+    const float gd = clampf_(ddp / (0.01f + 1e-6f), 0.f, 1.f);
+    const float gprog = maxf_(gv, gd);
+    const float ggate = gprog * g;
+    const float ppos = maxf_(pa1, 0.f), pneg = minf_(pa1, 0.f);
+    const float gate_pos = (ppos < 0.5f) ? 1.0f : ggate;
+    const float shaping = gate_pos * ppos + pneg;
+    const int worsening = shaping < -0.05f;
+    const int turning = fabsf(wzn) > 0.2f;
+    const float vfwd = vxn * hc + vyn * hs;
+    const float sf = clampf_((fabsf(vfwd) - 0.15f) / ((0.60f - 0.15f) + 1e-6f), 0.f, 1.f);
+    const float turn_haz = (float)(worsening && turning) * (-10.0f) * (g * g) * sf;
+    E->prev_pot[e] = pot;
+    const float speed_r = (1.0f - expf(-vtp / (0.8f + 1e-6f))) * 0.05f;
+    float sgn = (alpha > 0.f) ? 1.f : ((alpha < 0.f) ? -1.f : 0.f);
+    const float tang = (herr > 1.0f) ? sgn * 1.0f : sgn * 0.2f;
+    const float dw = wzn - tang;
+    const float ang_r = expf(-(dw * dw) / 0.2f) * 0.03f;
+    float coll = 0.f;
+    for (int o = 0; o < USV_NOBST; ++o) coll += (float)(od[o] < c->collision_threshold) * (-10.0f) * 10.0f;
+    const float goal_r = ((float)E->goal_cnt[e] * c->goal_reward) * 5.0f;
+    E->prev_dist[e] = dist;
+    const float total = dist_r * 0.5f + align_r * 0.5f + shaping * 2.0f + turn_haz + goal_r + c->time_reward +
+                        coll + speed_r + ang_r + hi_r;
+    /* ---- Penalties.compute_penalty (USV_task_rewards.py:440-523) ---- */
+    const float pact0 = c->pen_use_u ? unit[0] : cmd[0];
+    const float pact1 = c->pen_use_u ? unit[1] : cmd[1];
+    float p_lin = 0.f, p_ang = 0.f, p_angv = 0.f, p_en = 0.f;
+    if (c->pen_lin_kind == PEN_NORM) p_lin = -tnorm2(vxn, vyn) * c->pen_lin_k + c->pen_lin_c;
+    if (c->pen_ang_kind) p_ang = pen_scalar(c->pen_ang_kind, c->pen_ang_k, c->pen_ang_x0, c->pen_ang_c, wzn);
+    if (c->pen_angv_kind) {
+      const float prev_w = pen_valid ? E->prev_wz[e] : wzn;
+      p_angv = pen_scalar(c->pen_angv_kind, c->pen_angv_k, c->pen_angv_x0, c->pen_angv_c, wzn - prev_w);
+    }
+    if (c->pen_en_kind == PEN_SUM) p_en = -(pact0 + pact1) * c->pen_en_k + c->pen_en_c;
+    else if (c->pen_en_kind == PEN_SUMSQ) p_en = -(pact0 * pact0 + pact1 * pact1) * c->pen_en_k + c->pen_en_c;
+    E->prev_wz[e] = wzn;
+    const float pens = p_lin + p_ang + p_angv + p_en;
+    E->rew[e] = total + pens;
+    /* ---- is_done -> CaptureXYTask.update_kills (static_obs.py:661-706) ---- */
+    const int dkill = dist > c->kill_dist;
+    const int ckill = min_od < c->collision_threshold;
+    const int skill = E->goal_cnt[e] >= c->kill_after_n;
+    const int die = dkill || ckill || skill;
+    if (die) { E->done_coll[e] = ckill; E->done_succ[e] = skill && !ckill; }
+    const int tout = E->progress[e] >= c->max_episode_length - 1;
+    E->reset_buf[e] = c->fixed_horizon_eval ? tout : (tout ? 1 : die);
+    /* ---- episode_sums (static_obs.py:720-765, Penalties.update_statistics, USV_Virtual.py:1187-1221) ---- */
+    if (c->stats_on) {
+      float *S = E->stats;
+#define ADDS(k, v) S[(k) * n + e] += (v)
+      ADDS(ST_TOTAL_REWARD, total); ADDS(ST_DISTANCE_REWARD, dist_r); ADDS(ST_ALIGNMENT_REWARD, align_r);
+      ADDS(ST_HEADING_IMPROVE_REWARD, hi_r); ADDS(ST_POTENTIAL_SHAPING_REWARD, shaping);
+      ADDS(ST_SPEED_REWARD, speed_r); ADDS(ST_ANGULAR_REWARD, ang_r); ADDS(ST_TURN_HAZARD_PENALTY, turn_haz);
+      ADDS(ST_GOAL_REWARD, goal_r); ADDS(ST_TIME_REWARD, c->time_reward); ADDS(ST_COLLISION_REWARD, coll);
+      ADDS(ST_DANGER_MEAN, danger); ADDS(ST_DANGER_HI_RATE, (float)(danger > 0.5f)); ADDS(ST_G_GATE_MEAN, gate_pos);
+      ADDS(ST_POSITION_ERROR, dist); ADDS(ST_BOUNDARY_PENALTY, boundary_pen);
+      if (c->pen_ang_kind) ADDS(ST_ANGULAR_VEL_PENALTY, p_ang);
+      if (c->pen_angv_kind) ADDS(ST_ANGULAR_VEL_VARIATION_PENALTY, p_angv);
+      if (c->pen_en_kind) ADDS(ST_ENERGY_PENALTY, p_en);
+      ADDS(ST_NORMED_LINEAR_VEL, tnorm2(vxn, vyn));
+      ADDS(ST_NORMED_ANGULAR_VEL, fabsf(wzn));
+      ADDS(ST_CMD_NEG_RATE, ((float)(thrust[0] < 0.f) + (float)(thrust[1] < 0.f)) / 2.0f);
+      ADDS(ST_U_MEAN, (unit[0] + unit[1]) / 2.0f);
+      ADDS(ST_U_LOW_RATE, ((float)(unit[0] < 0.05f) + (float)(unit[1] < 0.05f)) / 2.0f);
+      ADDS(ST_U_SUM, unit[0] + unit[1]);
+#undef ADDS
+    }
+    if (dbg) { dbg[4] = pot; dbg[5] = danger; dbg[6] = total; dbg[7] = pens; dbg[8] = shaping; dbg[9] = dist_r; dbg[10] = align_r; }
+    /* ---- _process_data: clamp obs (vec_env_rlgames.py:85-95) ---- */
+    for (int q = 0; q < USV_NOBS; ++q) E->obs[(size_t)e * USV_NOBS + q] = clampf_(obs[q], -c->clip_obs, c->clip_obs);
+    E->just_reset[e] = 0;
+  }
+  E->ctl[USV_CTL_POT_VALID] = 1;
+  E->ctl[USV_CTL_PEN_VALID] = 1;
+  E->ctl[USV_CTL_REW_VALID] = 1;
+}
+
+/* compaction: reset_buf.nonzero() (USV_Virtual.py:1045) */
+int oracle_compact(const oracle_env_t *E, int32_t *ids) {
+  int k = 0;
+  for (int e = 0; e < E->n; ++e)
+    if (E->reset_buf[e]) ids[k++] = e;
+  return k;
+}

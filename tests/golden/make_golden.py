@@ -1,0 +1,683 @@
+"""Generate the golden fixtures under tests/golden/ by importing the REFERENCE
+(loop-Z/omniisaacgymenvs_loop at /root/reference) in the build container.
+
+Run only where /root/reference exists:
+    python tests/golden/make_golden.py [--only NAME]
+
+Nothing here ships or runs on the GPU box; the committed .npz files are data
+(inputs + reference outputs).  The reference needs Isaac Sim / PhysX / gym /
+pytorch3d, none of which exist offline, so:
+  * top-level modules omni, pxr, carb, gym, ray, tensorboardX, wandb, hydra,
+    omegaconf, matplotlib are replaced by auto-stub modules;
+  * pytorch3d.transforms.quaternion_to_matrix is restated (real-first quaternion);
+  * PhysX is replaced by a fake Heron articulation view whose World.step()
+    integrates the reference-computed forces with this build's 3-DoF
+    semi-implicit Euler (the reference has no integrator of its own);
+  * every torch.rand / torch.rand_like call is recorded with its call site so
+    the oracle/kernels can replay the exact draws.
+Deviation (documented in DESIGN.md): right after reset_idx the fake view's
+fresh pose is pushed into the task's cached root_* tensors, so the first
+substep after a reset uses the new state (reference quirk App. C.1 is a PhysX
+artefact and is not reproduced).
+"""
+from __future__ import annotations
+
+import argparse
+import copy
+import importlib.abc
+import importlib.machinery
+import json
+import math
+import os
+import sys
+import types
+from unittest.mock import MagicMock
+
+import numpy as np
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# --------------------------------------------------------------------------
+# offline stubs
+# --------------------------------------------------------------------------
+_ROOTS = {"omni", "pxr", "carb", "ray", "tensorboardX", "gym", "wandb", "hydra", "omegaconf", "matplotlib"}
+
+
+class _Meta(type):
+    def __getattr__(cls, name):
+        return MagicMock()
+
+
+class _Mod(types.ModuleType):
+    def __getattr__(self, name):
+        if name.startswith("__"):
+            raise AttributeError(name)
+        if name[:1].isupper():
+            c = _Meta(name, (object,), {"__init__": lambda self, *a, **k: None})
+            setattr(self, name, c)
+            return c
+        m = MagicMock()
+        setattr(self, name, m)
+        return m
+
+
+class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
+    def find_spec(self, fullname, path, target=None):
+        if fullname.split(".")[0] in _ROOTS:
+            return importlib.machinery.ModuleSpec(fullname, self, is_package=True)
+        return None
+
+    def create_module(self, spec):
+        m = _Mod(spec.name)
+        m.__path__ = []
+        return m
+
+    def exec_module(self, module):
+        pass
+
+
+def install_stubs():
+    np.Inf = np.inf  # the reference predates NumPy 2
+    sys.meta_path.insert(0, _Finder())
+    import torch
+    p3d = types.ModuleType("pytorch3d")
+    tr = types.ModuleType("pytorch3d.transforms")
+
+    def quaternion_to_matrix(q):  # pytorch3d.transforms.quaternion_to_matrix restated
+        r, i, j, k = torch.unbind(q, -1)
+        two_s = 2.0 / (q * q).sum(-1)
+        o = torch.stack((
+            1 - two_s * (j * j + k * k), two_s * (i * j - k * r), two_s * (i * k + j * r),
+            two_s * (i * j + k * r), 1 - two_s * (i * i + k * k), two_s * (j * k - i * r),
+            two_s * (i * k - j * r), two_s * (j * k + i * r), 1 - two_s * (i * i + j * j)), -1)
+        return o.reshape(q.shape[:-1] + (3, 3))
+
+    tr.quaternion_to_matrix = quaternion_to_matrix
+    p3d.transforms = tr
+    sys.modules["pytorch3d"] = p3d
+    sys.modules["pytorch3d.transforms"] = tr
+    # gym.spaces must behave enough for Box/Dict construction
+    gym = sys.modules.get("gym") or __import__("gym")
+    spaces = types.ModuleType("gym.spaces")
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.low, self.high = np.asarray(low), np.asarray(high)
+            self.shape = self.low.shape if shape is None else shape
+            self.dtype = np.dtype(dtype)
+
+    class Dict:
+        def __init__(self, d):
+            self.spaces = d
+
+    spaces.Box, spaces.Dict = Box, Dict
+    spaces.Discrete = type("Discrete", (), {})
+    spaces.Tuple = type("Tuple", (), {})
+    sys.modules["gym.spaces"] = spaces
+    gym.spaces = spaces
+    sys.path.insert(0, REF)
+    sys.path.insert(0, os.path.join(REF, "rl_games"))
+
+
+# --------------------------------------------------------------------------
+# torch.rand recorder
+# --------------------------------------------------------------------------
+class RandRecorder:
+    def __init__(self, torch):
+        self.torch = torch
+        self.log = []
+        self._rand = torch.rand
+        self._rand_like = torch.rand_like
+
+    def __enter__(self):
+        torch = self.torch
+        rec = self
+
+        def rand(*a, **k):
+            t = rec._rand(*a, **k)
+            f = sys._getframe(1)
+            rec.log.append((f.f_code.co_name, f.f_lineno, os.path.basename(f.f_code.co_filename), t.detach().clone()))
+            return t
+
+        def rand_like(x, *a, **k):
+            t = rec._rand_like(x, *a, **k)
+            f = sys._getframe(1)
+            rec.log.append((f.f_code.co_name, f.f_lineno, os.path.basename(f.f_code.co_filename), t.detach().clone()))
+            return t
+
+        torch.rand = rand
+        torch.rand_like = rand_like
+        return self
+
+    def __exit__(self, *exc):
+        self.torch.rand = self._rand
+        self.torch.rand_like = self._rand_like
+
+    def take(self):
+        out, self.log = self.log, []
+        return out
+
+
+# --------------------------------------------------------------------------
+# fake Isaac Sim articulation view + world (planar, this build's integrator)
+# --------------------------------------------------------------------------
+HERON_Y = 0.37765
+HERON_IZZ = 8.061
+
+
+class _Body:
+    def __init__(self, owner, kind):
+        self.o, self.kind = owner, kind
+
+    def apply_forces_and_torques_at_pos(self, forces=None, torques=None, is_global=False, **kw):
+        assert not is_global
+        if self.kind == "base":
+            self.o.f_base = forces.detach().clone()
+            self.o.t_base = torques.detach().clone()
+        elif self.kind == "left":
+            self.o.f_left = forces.detach().clone()
+        else:
+            self.o.f_right = forces.detach().clone()
+
+    def set_masses(self, masses, indices=None):
+        self.o.mass[indices.long()] = masses.float()
+
+    def set_coms(self, coms, indices=None):
+        self.o.com[indices.long()] = coms.reshape(-1, 3).float()
+
+    def get_inertias(self, indices=None, clone=True):
+        if indices is None:
+            return self.o.inertia.clone()
+        return self.o.inertia[indices.long()].clone()
+
+    def set_inertias(self, values, indices=None):
+        self.o.inertia[indices.long()] = values.float()
+
+
+class FakeHeron:
+    """Planar stand-in for HeronView (robots/articulations/views/heron_view.py)."""
+
+    name = "heron"
+    num_dof = 2
+
+    def __init__(self, torch, n):
+        self.t = torch
+        self.n = n
+        z = lambda *s: torch.zeros(*s, dtype=torch.float32)
+        self.px, self.py, self.yaw = z(n), z(n), z(n)
+        self.vx, self.vy, self.wz = z(n), z(n), z(n)
+        self.pz = torch.full((n,), 0.5)
+        self.mass = torch.full((n,), 34.96)
+        self.com = z(n, 3)
+        self.inertia = z(n, 9)
+        self.inertia[:, 0], self.inertia[:, 4], self.inertia[:, 8] = 1.0, 2.0, HERON_IZZ
+        self.base = _Body(self, "base")
+        self.thruster_left = _Body(self, "left")
+        self.thruster_right = _Body(self, "right")
+        self.f_base = self.t_base = self.f_left = self.f_right = None
+
+    def quat(self):
+        t = self.t
+        q = t.zeros(self.n, 4)
+        q[:, 0] = t.cos(self.yaw * 0.5)
+        q[:, 3] = t.sin(self.yaw * 0.5)
+        return q
+
+    def get_world_poses(self, clone=True):
+        p = self.t.stack([self.px, self.py, self.pz], 1)
+        return p.clone(), self.quat()
+
+    def get_velocities(self, clone=True):
+        t = self.t
+        v = t.zeros(self.n, 6)
+        v[:, 0], v[:, 1], v[:, 5] = self.vx, self.vy, self.wz
+        return v
+
+    def get_joint_positions(self):
+        return self.t.zeros(self.n, 2)
+
+    def get_joint_velocities(self):
+        return self.t.zeros(self.n, 2)
+
+    def set_joint_positions(self, *a, **k):
+        pass
+
+    def set_joint_velocities(self, *a, **k):
+        pass
+
+    def set_world_poses(self, pos, rot, indices=None):
+        idx = indices.long()
+        self.px[idx] = pos[:, 0].float()
+        self.py[idx] = pos[:, 1].float()
+        self.pz[idx] = pos[:, 2].float()
+        w, z = rot[:, 0].float(), rot[:, 3].float()
+        self.yaw[idx] = 2.0 * self.t.atan2(z, w)
+
+    def set_velocities(self, vel, indices=None):
+        idx = indices.long()
+        self.vx[idx] = vel[:, 0].float()
+        self.vy[idx] = vel[:, 1].float()
+        self.wz[idx] = vel[:, 5].float()
+
+    def integrate(self, dt):
+        """This build's 3-DoF semi-implicit Euler, fp32."""
+        t = self.t
+        fl = self.f_left[:, 0]
+        fr = self.f_right[:, 0]
+        X = self.f_base[:, 0] + fl + fr
+        Y = self.f_base[:, 1]
+        comy = self.com[:, 1]
+        N = self.t_base[:, 2] + (-(HERON_Y - comy) * fl + (HERON_Y + comy) * fr)
+        c, s = t.cos(self.yaw), t.sin(self.yaw)
+        m = self.mass
+        izz = self.inertia[:, 8]
+        ax = (c * X - s * Y) / m
+        ay = (s * X + c * Y) / m
+        aw = N / izz
+        self.vx = self.vx + ax * dt
+        self.vy = self.vy + ay * dt
+        self.wz = self.wz + aw * dt
+        self.px = self.px + self.vx * dt
+        self.py = self.py + self.vy * dt
+        yw = self.yaw + self.wz * dt
+        pi = np.float32(math.pi)
+        yw = t.where(yw > pi, yw - np.float32(2 * math.pi), yw)
+        yw = t.where(yw <= -pi, yw + np.float32(2 * math.pi), yw)
+        self.yaw = yw
+
+
+class FakeWorld:
+    def __init__(self, heron, dt):
+        self.h, self.dt = heron, dt
+
+    def is_playing(self):
+        return True
+
+    def step(self, render=False):
+        self.h.integrate(self.dt)
+
+
+def load_task_cfg(variant: str):
+    import yaml
+    with open(os.path.join(REF, "omniisaacgymenvs/cfg/task/USV/IROS2024/USV_Virtual_CaptureXY_SysID-TEST.yaml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg["env"]["scene_replay"]["enabled"] = False
+    cfg["physics_engine"] = "physx"
+    if variant == "B":
+        # second parity variant: bias ends early, independent (non-coupled)
+        # randomisations, centered priv encoding, exponential reward, pos noise
+        env = cfg["env"]
+        env["action_processing"]["initial_action_bias_steps"] = 3
+        env["disturbances"]["coupling"]["mass_driven"]["enabled"] = False
+        env["disturbances"]["drag"]["use_drag_scale_randomization"] = True
+        env["disturbances"]["thruster"]["use_thruster_randomization"] = True
+        env["disturbances"]["thruster"]["use_separate_randomization"] = True
+        env["disturbances"]["thruster"]["left_rand"] = 0.3
+        env["disturbances"]["thruster"]["right_rand"] = 0.2
+        env["disturbances"]["observations"]["add_noise_on_pos"] = True
+        env["privileged_params"]["mode"] = "centered"
+        env["reward_parameters"]["reward_mode"] = "exponential"
+        env["task_parameters"]["goal_random_position"] = 0.0
+        env["maxEpisodeLength"] = 40
+    return cfg
+
+
+def build_usv(torch, n, variant):
+    from omniisaacgymenvs.tasks.base import rl_task
+    from omniisaacgymenvs.tasks import USV_Virtual as UV
+
+    def rl_init(self, name, env, offset=None):
+        self.test = False
+        self._device = "cpu"
+        self.randomize_actions = False
+        self.randomize_observations = False
+        self.clip_obs = self._cfg["task"]["env"].get("clipObservations", np.inf)
+        self.clip_actions = self._cfg["task"]["env"].get("clipActions", np.inf)
+        self.rl_device = "cpu"
+        self.control_frequency_inv = self._cfg["task"]["env"].get("controlFrequencyInv", 1)
+        self._env = env
+        self._num_agents = 1
+        self._num_states = 0
+        self.cleanup()
+
+    rl_task.RLTask.__init__ = rl_init
+    for prop, attr in (("num_envs", "_num_envs"), ("num_observations", "_num_observations"),
+                       ("num_actions", "_num_actions"), ("num_states", "_num_states"),
+                       ("num_agents", "_num_agents"), ("device", "_device")):
+        setattr(rl_task.RLTask, prop, property(lambda self, a=attr: getattr(self, a)))
+    task_cfg = load_task_cfg(variant)
+    task_cfg["env"]["numEnvs"] = n
+    sim_config = types.SimpleNamespace(config={"sim_device": "cpu", "test": False, "rl_device": "cpu",
+                                               "task": task_cfg},
+                                       task_config=task_cfg)
+    heron = FakeHeron(torch, n)
+    world = FakeWorld(heron, task_cfg["sim"]["dt"])
+    fake_env = types.SimpleNamespace(_world=world)
+    usv = UV.USVVirtual("USVVirtual", sim_config, fake_env)
+    usv._heron = heron
+    usv._env_pos = torch.zeros((n, 3))
+    usv.task._env = usv
+    usv.get_USV_dynamics()
+    usv._marker = None
+    usv._blue_markers = [None] * 16
+    return usv, heron, world, task_cfg
+
+
+def make_vecenv(torch, usv, world):
+    from omniisaacgymenvs.envs import vec_env_rlgames as VE
+    ve = VE.VecEnvRLGames.__new__(VE.VecEnvRLGames)
+    ve._task = usv
+    ve._world = world
+    ve._render = False
+    ve.sim_frame_count = 0
+    ve._loopz_first_step_trace_done = True
+    return ve
+
+
+# --------------------------------------------------------------------------
+# draw-site mapping into the kernel layouts (include/usv_hip.h RU_* / SU_*)
+# --------------------------------------------------------------------------
+RU = dict(MASS=0, COM=1, KIZ=4, KDRAG=5, THR=6, DRAG=8, SPAWN_R=20, SPAWN_TH=21, YAW=22, OBST=23,
+          RESAMPLE=55, VX=695, VY=696, GOAL=697)
+NU_RESET, NU_STEP = 699, 8
+
+
+def map_reset_draws(draws, k):
+    U = np.full((k, NU_RESET), np.nan, np.float32)
+    it = 0
+    vel = 0
+    spawn = 0
+    for fn, line, fname, t in draws:
+        a = t.numpy().astype(np.float32)
+        if fn == "randomize_masses":
+            U[:, RU["MASS"]] = a.reshape(k)
+        elif fn == "_randomize_com":
+            U[:, RU["COM"]:RU["COM"] + a.reshape(k, -1).shape[1]] = a.reshape(k, -1)
+        elif fn == "_sample_k_drag":
+            U[:, RU["KDRAG"]] = a.reshape(k)
+        elif fn == "_sample_k_iz":
+            U[:, RU["KIZ"]] = a.reshape(k)
+        elif fn == "reset_thruster_randomization":
+            col = RU["THR"] + (1 if (not np.isnan(U[0, RU["THR"]]) and fn == "reset_thruster_randomization") else 0)
+            U[:, col] = a.reshape(k)
+        elif fn == "reset_coefficients":
+            off = RU["DRAG"] if np.isnan(U[0, RU["DRAG"]]) else RU["DRAG"] + 6
+            U[:, off:off + 6] = a.reshape(k, 6)
+        elif fn == "get_spawns":
+            if a.ndim == 1:
+                U[:, [RU["SPAWN_R"], RU["SPAWN_TH"], RU["YAW"]][spawn]] = a
+                spawn += 1
+            elif a.shape[1:] == (16, 2) and np.isnan(U[0, RU["OBST"]]):
+                U[:, RU["OBST"]:RU["OBST"] + 32] = a.reshape(k, 32)
+            else:
+                U[:, RU["RESAMPLE"] + it * 32:RU["RESAMPLE"] + (it + 1) * 32] = a.reshape(k, 32)
+                it += 1
+        elif fn == "reset_idx":
+            U[:, [RU["VX"], RU["VY"]][vel]] = a.reshape(k)
+            vel += 1
+        elif fn == "get_goals":
+            U[:, RU["GOAL"]:RU["GOAL"] + 2] = a.reshape(k, 2)
+        else:
+            raise RuntimeError(f"unmapped reset draw site {fn}:{line} ({fname})")
+    return U
+
+
+def map_step_draws(draws, n):
+    U = np.zeros((n, NU_STEP), np.float32)
+    vel = [d for d in draws if d[0] == "add_noise_on_vel"]
+    head = [d for d in draws if d[0] == "add_noise_on_heading"]
+    pos = [d for d in draws if d[0] == "add_noise_on_pos"]
+    act = [d for d in draws if d[0] == "add_noise_on_act"]
+    if vel:
+        v = vel[-1][3].numpy()
+        U[:, 0], U[:, 1], U[:, 2] = v[:, 0], v[:, 1], v[:, 5]
+    if head:
+        U[:, 3] = head[-1][3].numpy()
+    if pos:
+        U[:, 4:6] = pos[-1][3].numpy()[:, :2]
+    if act:
+        U[:, 6:8] = act[-1][3].numpy()
+    other = [d for d in draws if d[0] not in ("add_noise_on_vel", "add_noise_on_heading", "add_noise_on_pos",
+                                             "add_noise_on_act")]
+    return U, other
+
+
+# --------------------------------------------------------------------------
+# fixtures
+# --------------------------------------------------------------------------
+def gen_lut(torch):
+    from omniisaacgymenvs.envs.USV.ThrusterDynamics import DynamicsFirstOrder
+    cfg = load_task_cfg("A")
+    th = cfg["dynamics"]["thrusters"]
+    tcfg = cfg["env"]["disturbances"]["thruster"]
+    res = {}
+    tables = {
+        "test": (th["interpolation"]["interpolationPointsFromRealDataLeft"],
+                 th["interpolation"]["interpolationPointsFromRealDataRight"]),
+        "sym": ([-40.0, -36.0, -32.0, -28.0, -24.0, -20.0, -16.0, -12.0, -8.0, -4.0, 0.0, 8.0, 16.0, 24.0, 32.0,
+                 40.0, 48.0, 56.0, 64.0, 72.0, 80.0],
+                [-3.8, -3.8, -3.6, -3.6, -1.6, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 4.0, 10.0, 15.0,
+                 21.0, 23.0, 22.0]),
+    }
+    for name, (tl, tr) in tables.items():
+        d = DynamicsFirstOrder(tcfg, 64, "cpu", th["timeConstant"], cfg["sim"]["dt"], 1000, tl, tr,
+                               [0.0] * 5, [0.0] * 5, -1.0, 1.0)
+        res[f"{name}_table_l"] = np.asarray(tl, np.float32)
+        res[f"{name}_table_r"] = np.asarray(tr, np.float32)
+        res[f"{name}_lut_l"] = d.y_linear_interp_left.numpy()
+        res[f"{name}_lut_r"] = d.y_linear_interp_right.numpy()
+        # index mapping + lag sequence
+        g = torch.Generator().manual_seed(3)
+        cmds = torch.rand((64, 2), generator=g) * 2 - 1
+        cmds[:4] = torch.tensor([[-1.0, 1.0], [0.0, 0.5], [1.0, -1.0], [0.001, 0.999]])
+        d.set_target_force(cmds)
+        res[f"{name}_cmds"] = cmds.numpy()
+        res[f"{name}_targets"] = d.thruster_forces_before_dynamics.numpy().copy()
+        lag = []
+        for _ in range(12):
+            out = d.update_forces()
+            lag.append(out[:, [0, 3]].numpy().copy())
+        res[f"{name}_lag"] = np.stack(lag)
+    np.savez_compressed(os.path.join(OUT, "lut.npz"), **res)
+
+
+def gen_forces(torch):
+    from omniisaacgymenvs.envs.USV.Hydrodynamics import HydrodynamicsObject
+    cfg = load_task_cfg("A")
+    hd = cfg["dynamics"]["hydrodynamics"]
+    n = 256
+    g = torch.Generator().manual_seed(5)
+    dcfg = dict(cfg["env"]["disturbances"]["drag"])
+    dcfg["use_drag_scale_randomization"] = True
+    h = HydrodynamicsObject(dcfg, n, "cpu", 1000, -9.81, hd["linear_damping"], hd["quadratic_damping"],
+                            hd["linear_damping_forward_speed"], hd["offset_linear_damping"],
+                            hd["offset_lin_forward_damping_speed"], hd["offset_nonlin_damping"],
+                            hd["scaling_damping"], 0.0, 1.0, 0.3, -10.0)
+    kd = 1.0 + 0.5 * torch.rand((n, 1), generator=g)
+    h.drag_scale[:, :] = kd
+    yaw = (torch.rand(n, generator=g) * 2 - 1) * math.pi
+    q = torch.zeros(n, 4)
+    q[:, 0] = torch.cos(yaw * 0.5)
+    q[:, 3] = torch.sin(yaw * 0.5)
+    vel = torch.zeros(n, 6)
+    vel[:, 0] = (torch.rand(n, generator=g) * 2 - 1) * 3
+    vel[:, 1] = (torch.rand(n, generator=g) * 2 - 1) * 3
+    vel[:, 5] = (torch.rand(n, generator=g) * 2 - 1) * 2
+    drag = h.ComputeHydrodynamicsEffects(0.01, q, vel, False, [0, 0, 0])
+    np.savez_compressed(os.path.join(OUT, "forces.npz"), yaw=yaw.numpy(), quat=q.numpy(), vel=vel.numpy(),
+                        k_drag=kd.numpy()[:, 0], drag=drag.numpy(),
+                        local_vel=h.local_velocities.numpy())
+
+
+def gen_field(torch):
+    from omniisaacgymenvs.tasks.USV.d_multi_gemini import BatchedMapGPU
+    res = {}
+    g = torch.Generator().manual_seed(11)
+    for name, k in (("b1", 1), ("b4", 4)):
+        obs = torch.rand((k, 16, 2), generator=g) * 24 - 12
+        if k == 4:
+            obs[1, 3] = torch.tensor([999.0, 999.0])      # limbo obstacle
+            obs[2, :6] = torch.tensor([[0.4, 0.0], [1.4, 0.0], [2.4, 0.0], [-1.0, 1.0], [-1.0, -1.0], [0.0, -1.2]])
+            obs[3] = torch.tensor([999.0, 999.0])          # empty map
+        tgt = torch.zeros((k, 2))
+        if k == 4:
+            tgt[1] = torch.tensor([2.3, -4.1])
+        m = BatchedMapGPU(k, 150, 30.0, 0.5, device="cpu")
+        occ, sdf = m.compute_occupancy_and_sdf(obs)
+        cost = m.compute_cost_field_wavefront(occ, tgt)
+        pot = m.compute_potential_field(cost, sdf)
+        # convergence check: one more Jacobi sweep must not change the field
+        m2 = BatchedMapGPU(k, 150, 30.0, 0.5, device="cpu")
+        res[f"{name}_obst"] = obs.numpy()
+        res[f"{name}_tgt"] = tgt.numpy()
+        res[f"{name}_cost"] = cost.numpy()
+        res[f"{name}_field"] = pot.numpy()
+        res["grid_lin"] = m.grid_coords[0, 0, :, 0].numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "field.npz"), **res)
+
+
+def policy_actions(rng, n, t):
+    """Deterministic, varied action sequences (forward runs, turns, idle)."""
+    a = np.zeros((n, 2), np.float32)
+    for e in range(n):
+        mode = e % 4
+        if mode == 0:
+            a[e] = [1.0, 1.0]
+        elif mode == 1:
+            a[e] = [1.0, 0.2 + 0.6 * math.sin(0.2 * t + e)]
+        elif mode == 2:
+            a[e] = rng.uniform(-1, 1, 2)
+        else:
+            a[e] = [0.6 + 0.4 * math.cos(0.3 * t), 1.0]
+    return a
+
+
+def gen_episode(torch, variant, n, steps, seed):
+    torch.manual_seed(seed)
+    usv, heron, world, task_cfg = build_usv(torch, n, variant)
+    ve = make_vecenv(torch, usv, world)
+    rec = RandRecorder(torch)
+    orig_reset_idx = type(usv).reset_idx
+
+    def reset_idx_refresh(self, env_ids):
+        orig_reset_idx(self, env_ids)
+        # push the fresh pose into the cached root_* state (see module doc)
+        self.root_pos, self.root_quats = self._heron.get_world_poses()
+        self.root_velocities = self._heron.get_velocities()
+
+    usv.reset_idx = types.MethodType(reset_idx_refresh, usv)
+    rng = np.random.default_rng(seed)
+    with rec:
+        usv.post_reset()
+        init_draws = rec.take()
+        init_tgt = usv.task._target_positions.numpy().copy()
+        usv.task.reset(torch.arange(n))   # flags only (reset via VecEnv.reset below)
+        rec.take()
+    data = {k: [] for k in ("actions", "obs", "rew", "reset", "progress", "px", "py", "yaw", "vx", "vy", "wz",
+                            "fl", "fr", "reset_mask", "u_step", "mass", "com", "k_drag", "thr_l", "thr_r",
+                            "k_iz", "obst", "tgt", "extras", "goal_cnt", "bias", "terms")}
+    reset_U = []
+    usv.task.just_had_been_reset = torch.arange(n)
+    with rec:
+        for t in range(steps):
+            reset_mask = usv.reset_buf.numpy().astype(bool).copy() if t > 0 else np.ones(n, bool)
+            if t == 0:
+                usv.reset()
+                act = np.zeros((n, 2), np.float32)
+            else:
+                act = policy_actions(rng, n, t)
+            bias_active = (usv._initial_action_bias_steps > 0 and
+                           usv._action_bias_step_count < usv._initial_action_bias_steps)
+            obs_dict, rew, resets, extras = ve.step(torch.from_numpy(act))
+            draws = rec.take()
+            reset_draws = [d for d in draws if d[0] not in ("add_noise_on_vel", "add_noise_on_heading",
+                                                             "add_noise_on_pos", "add_noise_on_act")]
+            Us, _ = map_step_draws(draws, n)
+            k = int(reset_mask.sum())
+            if k:
+                reset_U.append(map_reset_draws(reset_draws, k))
+            else:
+                assert not reset_draws, reset_draws
+            data["actions"].append(act)
+            data["bias"].append(np.float32(usv._initial_action_bias if bias_active else 0.0))
+            data["obs"].append(obs_dict["obs"]["state"].numpy().copy())
+            data["rew"].append(rew.numpy().copy())
+            data["reset"].append(resets.numpy().copy())
+            data["progress"].append(usv.progress_buf.numpy().copy())
+            data["reset_mask"].append(reset_mask)
+            data["u_step"].append(Us)
+            for key, val in (("px", heron.px), ("py", heron.py), ("yaw", heron.yaw), ("vx", heron.vx),
+                             ("vy", heron.vy), ("wz", heron.wz)):
+                data[key].append(val.numpy().copy())
+            cf = usv.thrusters_dynamics.current_forces.numpy().copy()
+            data["fl"].append(cf[:, 0])
+            data["fr"].append(cf[:, 1])
+            data["mass"].append(usv.MDD.platforms_mass[:, 0].numpy().copy())
+            data["com"].append(usv.MDD.platforms_CoM.numpy().copy())
+            data["k_drag"].append(usv.hydrodynamics.drag_scale[:, 0].numpy().copy())
+            td = usv.thrusters_dynamics
+            if td._use_separate_randomization:
+                data["thr_l"].append(td.thruster_left_multiplier[:, 0].numpy().copy())
+                data["thr_r"].append(td.thruster_right_multiplier[:, 0].numpy().copy())
+            else:
+                data["thr_l"].append(td.thruster_multiplier[:, 0].numpy().copy())
+                data["thr_r"].append(td.thruster_multiplier[:, 0].numpy().copy())
+            data["k_iz"].append(usv.k_Iz[:, 0].numpy().copy())
+            data["obst"].append(usv.task.xunlian_pos[:, :, :2].numpy().copy())
+            data["tgt"].append(usv.task._target_positions.numpy().copy())
+            data["goal_cnt"].append(usv.task._goal_reached.numpy().copy())
+            tk = usv.task
+            pen = usv._penalties
+            data["terms"].append(torch.stack([tk.distance_reward, tk.alignment_reward, tk.potential_shaping_reward,
+                                           tk._turn_hazard_penalty, tk._speed_reward, tk._angular_reward,
+                                           tk._heading_improve_reward, tk.collision_reward, tk._goal_reward,
+                                           tk._total_reward, pen.angular_vel_penalty,
+                                           pen.angular_vel_variation_penalty, pen.energy_penalty,
+                                           tk._danger_factor, tk.prev_potential], 1).numpy().astype(np.float32))
+            ex = extras.get("episode", {})
+            data["extras"].append(np.array([float(ex[k]) if k in ex else np.nan for k in STAT_NAMES], np.float32))
+    out = {k: np.stack(v) for k, v in data.items()}
+    out["reset_U"] = np.concatenate(reset_U, 0) if reset_U else np.zeros((0, NU_RESET), np.float32)
+    out["init_tgt"] = init_tgt
+    out["grid_lin"] = usv.task.gpu_map.grid_coords[0, 0, :, 0].numpy().copy()
+    out["config_json"] = np.frombuffer(json.dumps(task_cfg).encode(), dtype=np.uint8)
+    out["bias_steps"] = np.int64(usv._initial_action_bias_steps)
+    np.savez_compressed(os.path.join(OUT, f"episode_{variant}.npz"), **out)
+    print(f"episode_{variant}: resets per step", out["reset_mask"].sum(1).tolist())
+
+
+STAT_NAMES = [
+    "total_reward", "distance_reward", "alignment_reward", "heading_improve_reward",
+    "potential_shaping_reward", "speed_reward", "angular_reward", "turn_hazard_penalty",
+    "goal_reward", "collision_reward", "time_reward", "success", "collision",
+    "position_error", "boundary_penalty", "danger_mean", "danger_hi_rate", "g_gate_mean",
+    "g_safe_mean", "angular_vel_penalty", "angular_vel_variation_penalty", "energy_penalty",
+    "normed_linear_vel", "normed_angular_vel", "cmd_neg_rate", "u_mean", "u_low_rate", "u_sum",
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    install_stubs()
+    import torch
+    torch.set_num_threads(8)
+    jobs = {
+        "lut": lambda: gen_lut(torch),
+        "forces": lambda: gen_forces(torch),
+        "field": lambda: gen_field(torch),
+        "episodeA": lambda: gen_episode(torch, "A", 16, 64, 1234),
+        "episodeB": lambda: gen_episode(torch, "B", 12, 56, 99),
+    }
+    for name, fn in jobs.items():
+        if args.only and name not in args.only.split(","):
+            continue
+        print("generating", name)
+        fn()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+"""The CPU oracle (oracle/usv_oracle.c) against the reference's own outputs.
+
+Golden vectors: tests/golden/*.npz, produced by tests/golden/make_golden.py,
+which imports the reference Python (loop-Z/omniisaacgymenvs_loop) in the build
+container and records every input, every torch.rand draw and every output.
+"""
+import json
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg, load_yaml, parse_penalty_fn, thruster_tables
+from omniisaacgymenvs_loop_amd._abi import PEN
+import os
+
+TEST_YAML = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "omniisaacgymenvs_loop_amd",
+                         "cfg", "task", "USV", "IROS2024", "USV_Virtual_CaptureXY_SysID-TEST.yaml")
+
+
+def _cfg_from(d):
+    return json.loads(bytes(d["config_json"]).decode())
+
+
+def test_philox_known_answers():
+    # Random123 philox4x32-10 KAT vectors (kat_vectors, Salmon et al. SC'11)
+    assert O.philox([0, 0, 0, 0], [0, 0]).tolist() == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert O.philox([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2).tolist() == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert O.philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]).tolist() == \
+        [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_lut_bit_exact(golden):
+    g = golden("lut.npz")
+    for name in ("test", "sym"):
+        lut = O.make_lut(g[f"{name}_table_l"], g[f"{name}_table_r"])
+        np.testing.assert_array_equal(lut[0], g[f"{name}_lut_l"])
+        np.testing.assert_array_equal(lut[1], g[f"{name}_lut_r"])
+
+
+def test_lut_index_and_lag(golden):
+    """get_cmd_interpolated index mapping + first-order lag (ThrusterDynamics.py:129-234)."""
+    g = golden("lut.npz")
+    cfg = build_usv_cfg(load_yaml(TEST_YAML))
+    for name in ("test", "sym"):
+        lut = O.make_lut(g[f"{name}_table_l"], g[f"{name}_table_r"])
+        cmds = g[f"{name}_cmds"]
+        idx = np.clip(np.rint(((cmds + np.float32(1)) / np.float32(2)) * np.float32(999)), 0, 999).astype(int)
+        tgt = np.stack([lut[0][idx[:, 0]], lut[1][idx[:, 1]]], 1)
+        np.testing.assert_array_equal(tgt, g[f"{name}_targets"])
+        a = np.float32(cfg.thr_alpha)
+        f = np.zeros_like(tgt)
+        for k in range(g[f"{name}_lag"].shape[0]):
+            f = f * a + (np.float32(1) - a) * tgt
+            np.testing.assert_array_equal(f, g[f"{name}_lag"][k])
+
+
+def test_planar_drag_matches_reference(golden):
+    """Surge/sway/yaw drag of HydrodynamicsObject.ComputeHydrodynamicsEffects."""
+    g = golden("forces.npz")
+    cfg = build_usv_cfg(load_yaml(TEST_YAML))
+    cfg.use_drag_scale = 1
+    n = len(g["yaw"])
+    E = O.OracleEnv(cfg, n, np.zeros((2, 1000), np.float32))
+    E.yaw[:] = g["yaw"]
+    E.vx[:], E.vy[:], E.wz[:] = g["vel"][:, 0], g["vel"][:, 1], g["vel"][:, 5]
+    E.k_drag[:] = g["k_drag"]
+    E.fl[:] = 0
+    E.fr[:] = 0
+    F = E.forces()
+    ref = g["drag"][:, [0, 1, 5]]
+    # the reference rotates with a quaternion-derived matrix, the oracle with cos/sin(yaw)
+    np.testing.assert_allclose(F, ref, rtol=2e-5, atol=2e-5)
+
+
+def test_potential_field_bit_exact(golden):
+    g = golden("field.npz")
+    cfg = build_usv_cfg(load_yaml(TEST_YAML))
+    for name in ("b1", "b4"):
+        field, cost = O.potential_field(cfg, g[f"{name}_obst"], g[f"{name}_tgt"], want_cost=True, lin=g["grid_lin"])
+        rc = g[f"{name}_cost"].reshape(cost.shape)
+        np.testing.assert_array_equal(cost, rc)
+        np.testing.assert_array_equal(field, g[f"{name}_field"].reshape(field.shape))
+
+
+def test_grid_lin_formula_close(golden):
+    """Kernels default to the symmetric linspace formula (the CUDA kernel's);
+    the CPU-vectorised torch.linspace that made the fixtures differs by <=1 ulp."""
+    g = golden("field.npz")
+    np.testing.assert_allclose(O.grid_lin(30.0), g["grid_lin"], rtol=0, atol=2e-6)
+
+
+def _replay(d, post_only):
+    cfg_d = _cfg_from(d)
+    cfg = build_usv_cfg(cfg_d)
+    lut = O.make_lut(*thruster_tables(cfg_d))
+    T, n = d["obs"].shape[:2]
+    E = O.OracleEnv(cfg, n, lut)
+    E.set_grid_lin(d["grid_lin"])
+    E.tgt_x[:] = d["init_tgt"][:, 0]
+    E.tgt_y[:] = d["init_tgt"][:, 1]
+    ru = 0
+    out = []
+    for t in range(T):
+        ids = E.compact()
+        np.testing.assert_array_equal(ids, np.nonzero(d["reset_mask"][t])[0])
+        if len(ids):
+            E.reset(ids, d["reset_U"][ru:ru + len(ids)])
+            ru += len(ids)
+            ex = d["extras"][t]
+            np.testing.assert_allclose(E.extras, ex, rtol=1e-5, atol=1e-6)
+        E.step_pre(d["actions"][t], float(d["bias"][t]), d["u_step"][t])
+        E.step_physics()
+        if post_only:
+            for k in ("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr"):
+                getattr(E, k)[:] = d[k][t]
+        E.step_post(d["u_step"][t])
+        out.append((E.obs.copy(), E.rew.copy(), E.reset_buf.copy(), E.mass.copy(), E.k_drag.copy(), E.thr_l.copy(),
+                    E.thr_r.copy(), E.k_iz.copy(), E.obst.copy(), E.progress.copy(), E.goal_cnt.copy()))
+    return out
+
+
+@pytest.mark.parametrize("variant", ["A", "B"])
+def test_episode_post_physics(golden, variant):
+    """obs / reward / done / DR / spawns given the reference's post-integration state."""
+    d = golden(f"episode_{variant}.npz")
+    for t, (obs, rew, rb, mass, kd, tl, tr, kiz, obst, prog, gc) in enumerate(_replay(d, post_only=True)):
+        np.testing.assert_allclose(obs, d["obs"][t], rtol=2e-6, atol=2e-6, err_msg=f"obs step {t}")
+        np.testing.assert_allclose(rew, d["rew"][t], rtol=5e-6, atol=5e-6, err_msg=f"rew step {t}")
+        np.testing.assert_array_equal(rb, d["reset"][t])
+        np.testing.assert_array_equal(prog, d["progress"][t])
+        np.testing.assert_array_equal(gc, d["goal_cnt"][t])
+        np.testing.assert_allclose(mass, d["mass"][t], rtol=1e-6)
+        np.testing.assert_allclose(kd, d["k_drag"][t], rtol=1e-6)
+        np.testing.assert_allclose(tl, d["thr_l"][t], rtol=1e-6)
+        np.testing.assert_allclose(tr, d["thr_r"][t], rtol=1e-6)
+        np.testing.assert_allclose(kiz, d["k_iz"][t], rtol=1e-6)
+        np.testing.assert_array_equal(obst.transpose(2, 0, 1), d["obst"][t])
+
+
+@pytest.mark.parametrize("variant", ["A", "B"])
+def test_episode_end_to_end(golden, variant):
+    """Full replay incl. this build's integrator; the reference's potential-shaping
+    term amplifies ~1e-7 state differences by 100, hence the reward tolerance."""
+    d = golden(f"episode_{variant}.npz")
+    for t, (obs, rew, rb, *_rest) in enumerate(_replay(d, post_only=False)):
+        np.testing.assert_allclose(obs, d["obs"][t], rtol=2e-5, atol=2e-5, err_msg=f"obs step {t}")
+        np.testing.assert_allclose(rew, d["rew"][t], rtol=1e-4, atol=1e-4, err_msg=f"rew step {t}")
+        np.testing.assert_array_equal(rb, d["reset"][t])
+
+
+def test_penalty_parser():
+    c = {"c1": 0.3, "c2": 0.1}
+    assert parse_penalty_fn("lambda x,step: -torch.clamp(torch.abs(x) - 0.4, min=0.0) * 0.02", c) == \
+        (PEN["PEN_DEADZONE"], 0.02, 0.4, 0.0)
+    assert parse_penalty_fn("lambda x,step : -torch.sum(x, dim=-1) * 0.005", c) == (PEN["PEN_SUM"], 0.005, 0.0, 0.0)
+    assert parse_penalty_fn("lambda x,step : -torch.abs(x)*c1 + c2", c) == (PEN["PEN_DEADZONE"], 0.3, 0.0, 0.1)
+    assert parse_penalty_fn("lambda x,step: -torch.norm(x, dim=-1)*0.01", c) == (PEN["PEN_NORM"], 0.01, 0.0, 0.0)
+    assert parse_penalty_fn("lambda x,step: (torch.exp(-0.033 * torch.abs(x)) - 1.0) * 0.2", c)[0] == \
+        PEN["PEN_EXPABS"]
+    with pytest.raises(ValueError):
+        parse_penalty_fn("lambda x,step: torch.sin(x)", c)
+
+
+def test_packaged_yaml_matches_fixture_config(golden):
+    """The packaged TEST yaml resolves to the same kernel constants as the
+    reference yaml recorded in the fixture."""
+    ref = build_usv_cfg(_cfg_from(golden("episode_A.npz")))
+    mine = build_usv_cfg(load_yaml(TEST_YAML))
+    for name, _ in ref._fields_:
+        a, b = getattr(ref, name), getattr(mine, name)
+        if hasattr(a, "__len__"):
+            assert list(a) == list(b), name
+        else:
+            assert a == b, name
