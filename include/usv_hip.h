@@ -194,7 +194,9 @@ typedef struct usv_bufs {
   float   *fscratch;               /* [16] float reductions (max_val, jmax) */
   float   *extras;                 /* [USV_NSTAT] extras["episode"] (persistent) */
   float   *extras_acc;             /* [USV_NSTAT] scratch sums */
-  float   *field_old_tgt;          /* [2][n] target used by the field of each reset slot */
+  float   *field_old_tgt;          /* [2][n] target used by the field of each reset env */
+  float   *slot_stats;             /* [n][8] per-reset-slot field statistics (scratch) */
+  const float *grid_lin;           /* [150] cell centres of the field grid */
 } usv_bufs_t;
 
 /* control words */
@@ -204,6 +206,7 @@ typedef struct usv_bufs {
 #define USV_CTL_REW_VALID   3   /* 0 => CaptureXYReward.prev_position_error is None */
 #define USV_CTL_NAN_FLAG    4   /* device NaN probe (replaces USV_NAN_PROBE host syncs) */
 #define USV_CTL_ANY_INSIDE  5   /* potential field: any cell inside an obstacle in the batch */
+#define USV_CTL_ANY_FINITE  6   /* potential field: any finite cost in the batch */
 #define USV_CTL_N           16
 
 /* ------------------------------------------------------------------------ */
@@ -347,9 +350,10 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m,
                         float *adam_v, float *opt, float grad_scale, void *stream);
 
-/* library / device info */
+/* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad */
+int ppo_partials_floats(int minibatch);
+/* library version */
 int usv_hip_version(void);
-int usv_hip_arch(char *buf, int len);
 
 #ifdef __cplusplus
 }

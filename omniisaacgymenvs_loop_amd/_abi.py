@@ -50,6 +50,8 @@ def _struct_fields(txt: str, name: str, defines: dict):
     fields = []
     for decl in body.split(";"):
         decl = decl.strip()
+        if decl.startswith("const "):
+            decl = decl[len("const "):]
         if not decl:
             continue
         tm = re.match(r"(\w+)\s+(.*)", decl, flags=re.S)

@@ -1,0 +1,98 @@
+"""ctypes binding of libusv_hip.so (include/usv_hip.h) -- the product path.
+
+This module is exactly the FFI a reference maintainer would add:
+every entry point takes raw device pointers, sizes and a hipStream_t.  It fails
+loudly when the library is missing: there is no CPU fallback anywhere in the
+product package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import torch  # noqa: F401  -- load torch's HIP runtime first; the .so binds to it (same SONAME)
+
+from ._abi import PpoCfg, UsvBufs, UsvCfg
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+LIB_DIR = os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libusv_hip.so")
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("usv_env.hip", "usv_field.hip", "ppo.hip")]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", "usv_device.h"), os.path.join(ROOT, "include", "usv_hip.h")]
+
+HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
+               # no implicit FMA contraction: the arithmetic follows the reference op by op
+               "-ffp-contract=off"]
+
+_lib = None
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile the HIP kernels for gfx950 into lib/libusv_hip.so (in-tree)."""
+    os.makedirs(LIB_DIR, exist_ok=True)
+    if not force and os.path.exists(LIB_PATH):
+        lib_m = os.path.getmtime(LIB_PATH)
+        if all(os.path.getmtime(d) <= lib_m for d in DEPS):
+            return LIB_PATH
+    cmd = ["hipcc"] + HIPCC_FLAGS + ["-o", LIB_PATH] + SOURCES
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.check_call(cmd)
+    return LIB_PATH
+
+
+def _declare(lib):
+    P, I, U64, F = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_float
+    sig = {
+        "usv_build_lut": [P, P, I, P, P],
+        "usv_reset": [P, P, U64, U64, P, P],
+        "usv_potential_field": [P, P, P],
+        "usv_env_step": [P, P, P, P, F, U64, U64, P, P],
+        "usv_forces": [P, P, P, P],
+        "ppo_policy_step": [P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, U64, U64, P, P],
+        "ppo_value": [P, P, P, P, P, P, P],
+        "ppo_store_reward": [P, P, P, I, P, P, P, P, P, P],
+        "ppo_prepare": [P, P, P, P, P, P, P, P, P, P, P, P, P],
+        "ppo_minibatch_grad": [P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
+        "ppo_minibatch_apply": [P, P, P, P, P, P, F, P],
+        "ppo_partials_floats": [I],
+        "usv_hip_version": [],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    return lib
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                               f"g.build()'` (hipcc --offload-arch=gfx950)")
+        _lib = _declare(ctypes.CDLL(LIB_PATH))
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with status {rc}")
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def byref(s):
+    return ctypes.byref(s)
+
+
+__all__ = ["build", "lib", "call", "ptr", "stream_ptr", "byref", "UsvCfg", "UsvBufs", "PpoCfg", "LIB_PATH"]

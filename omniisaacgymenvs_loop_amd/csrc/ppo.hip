@@ -1,0 +1,759 @@
+// rl_games PPO hot path (a2c_continuous, actor_critic_mlp_dict 33-128-128-{2,1},
+// continuous_a2c_logstd) for MI355X (gfx950), fp32 end to end.
+//
+// Replaces (rl_games/rl_games/...):
+//   common/a2c_common.py:385-430,670-774   get_action_values/get_values, play_steps
+//   common/a2c_common.py:525-540,1257-1332 discount_values (GAE), prepare_dataset
+//   algos_torch/a2c_continuous.py:78-217    calc_gradients, bound_loss
+//   common/common_losses.py:6-48            actor_loss, critic_loss
+//   common/a2c_common.py:308-330,1200-1235  trancate_gradients_and_step, adaptive LR
+//   algos_torch/running_mean_std.py:44-139  RunningMeanStd (fp64 stats)
+//   algos_torch/torch_ext.py:27-36          policy_kl
+//   common/datasets.py:25-29                update_mu_sigma
+//
+// Block forward/backward: 256 threads own 64 rows of the minibatch; thread
+// (j = tid % 128, rg = tid / 128) computes hidden unit j for 32 rows, with the
+// row activations broadcast from LDS and the weight rows streamed from L2.
+// Weight gradients are per-block partial sums (deterministic), reduced by
+// k_reduce_partials; clip + Adam + LR schedule run in one workgroup.
+#include "usv_device.h"
+
+namespace {
+
+constexpr int NIN = PPO_NIN, NH = PPO_NH, NA = PPO_NA;
+constexpr int XP = 36;          // padded obs row in LDS
+constexpr int RB = 64;          // rows per block
+constexpr int TB = 256;         // threads per block
+constexpr int RG = 32;          // rows per thread (RB / 2)
+constexpr int NPART = PPO_NPARAM + 8;   // partial row: params (+ transposed blocks) + loss sums
+constexpr float kLog2Pi = 1.8378770664093453f;  // 0.5*log(2*pi)*2 (models.py:400)
+
+// partial-row layout (W1 and W2 stored transposed for coalesced stores)
+constexpr int P_SIGMA = 0;
+constexpr int P_W1T = 2;                          // [33][128]
+constexpr int P_B1 = P_W1T + NIN * NH;
+constexpr int P_W2T = P_B1 + NH;                  // [128 k][128 j]
+constexpr int P_B2 = P_W2T + NH * NH;
+constexpr int P_WV = P_B2 + NH;
+constexpr int P_BV = P_WV + NH;
+constexpr int P_WMU = P_BV + 1;                   // [2][128] (same as params)
+constexpr int P_BMU = P_WMU + NA * NH;
+constexpr int P_LOSS = PPO_NPARAM;                // a, c, entropy, b, kl sums
+
+__device__ __forceinline__ int partial_to_param(int p) {
+  if (p >= P_W1T && p < P_B1) {
+    const int q = p - P_W1T, k = q / NH, j = q % NH;
+    return PPO_OFF_W1 + j * NIN + k;
+  }
+  if (p >= P_W2T && p < P_B2) {
+    const int q = p - P_W2T, k = q / NH, j = q % NH;
+    return PPO_OFF_W2 + j * NH + k;
+  }
+  return p;  // all other sections share the parameter layout
+}
+
+__device__ __forceinline__ float rms_norm(float x, double mean, double var, float eps) {
+  // RunningMeanStd.forward (running_mean_std.py:113-118): fp32 math on fp64 stats
+  const float y = (x - (float)mean) / sqrtf((float)var + eps);
+  return clampt(y, -5.0f, 5.0f);
+}
+
+struct FwdSmem {
+  float x[RB * XP];       // normalised obs
+  float h1[RB * NH];      // tanh layer 1 (later dz1)
+  float h2[RB * NH];      // tanh layer 2 (later dz2)
+  float out[RB * 4];      // mu0, mu1, value, (spare)
+};
+
+// Forward of RB rows already staged (normalised) in s.x; rows >= nrows are 0.
+__device__ void block_forward(const float *__restrict__ P, FwdSmem &s) {
+  const int tid = threadIdx.x;
+  const int j = tid % NH, r0 = (tid / NH) * RG;
+  // ---- layer 1: h1 = tanh(W1 x + b1) ----
+  {
+    float acc[RG];
+    const float bj = P[PPO_OFF_B1 + j];
+#pragma unroll
+    for (int r = 0; r < RG; ++r) acc[r] = 0.f;
+    const float *w = P + PPO_OFF_W1 + j * NIN;
+    for (int k = 0; k < NIN; ++k) {
+      const float wk = w[k];
+#pragma unroll
+      for (int r = 0; r < RG; ++r) acc[r] = fmaf(wk, s.x[(r0 + r) * XP + k], acc[r]);
+    }
+#pragma unroll
+    for (int r = 0; r < RG; ++r) s.h1[(r0 + r) * NH + j] = tanhf(acc[r] + bj);
+  }
+  __syncthreads();
+  // ---- layer 2: h2 = tanh(W2 h1 + b2) ----
+  {
+    float acc[RG];
+    const float bj = P[PPO_OFF_B2 + j];
+#pragma unroll
+    for (int r = 0; r < RG; ++r) acc[r] = 0.f;
+    const float4 *w = reinterpret_cast<const float4 *>(P + PPO_OFF_W2 + j * NH);
+    for (int k4 = 0; k4 < NH / 4; ++k4) {
+      const float4 wk = w[k4];
+#pragma unroll
+      for (int r = 0; r < RG; ++r) {
+        const float4 hv = *reinterpret_cast<const float4 *>(&s.h1[(r0 + r) * NH + 4 * k4]);
+        acc[r] = fmaf(wk.x, hv.x, acc[r]);
+        acc[r] = fmaf(wk.y, hv.y, acc[r]);
+        acc[r] = fmaf(wk.z, hv.z, acc[r]);
+        acc[r] = fmaf(wk.w, hv.w, acc[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RG; ++r) s.h2[(r0 + r) * NH + j] = tanhf(acc[r] + bj);
+  }
+  __syncthreads();
+  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (4 threads per row) ----
+  {
+    const int r = tid / 4, part = tid % 4;   // 64 rows x 4 lanes
+    float a0 = 0.f, a1 = 0.f, av = 0.f;
+    for (int k = part * 32; k < part * 32 + 32; ++k) {
+      const float h = s.h2[r * NH + k];
+      a0 = fmaf(P[PPO_OFF_WMU + k], h, a0);
+      a1 = fmaf(P[PPO_OFF_WMU + NH + k], h, a1);
+      av = fmaf(P[PPO_OFF_WV + k], h, av);
+    }
+    a0 += __shfl_xor(a0, 1, 64); a0 += __shfl_xor(a0, 2, 64);
+    a1 += __shfl_xor(a1, 1, 64); a1 += __shfl_xor(a1, 2, 64);
+    av += __shfl_xor(av, 1, 64); av += __shfl_xor(av, 2, 64);
+    if (part == 0) {
+      s.out[r * 4 + 0] = a0 + P[PPO_OFF_BMU];
+      s.out[r * 4 + 1] = a1 + P[PPO_OFF_BMU + 1];
+      s.out[r * 4 + 2] = av + P[PPO_OFF_BV];
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void stage_obs(const float *__restrict__ obs, int row0, int nrows, const double *obs_rms,
+                                          bool normalize, float eps, FwdSmem &s) {
+  for (int i = threadIdx.x; i < RB * XP; i += TB) {
+    const int r = i / XP, k = i % XP;
+    float v = 0.f;
+    if (r < nrows && k < NIN) {
+      v = obs[(size_t)(row0 + r) * NIN + k];
+      if (normalize) v = rms_norm(v, obs_rms[k], obs_rms[NIN + k], eps);
+    }
+    s.x[i] = v;
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------ rollout
+__global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__restrict__ P,
+                                                    const double *__restrict__ obs_rms,
+                                                    const double *__restrict__ val_rms, const float *__restrict__ obs,
+                                                    int t, float *exp_obs, float *exp_act, float *exp_nlp,
+                                                    float *exp_val, float *exp_mu, float *exp_sigma, uint8_t *exp_done,
+                                                    const int64_t *__restrict__ dones_prev, float *actions_out,
+                                                    uint64_t seed, uint64_t step, const float *eps_inject) {
+  __shared__ FwdSmem s;
+  const int n = c.n_envs, H = c.horizon;
+  const int row0 = blockIdx.x * RB;
+  const int nrows = min(RB, n - row0);
+  // raw obs into the experience buffer (row = env*H + t, swap_and_flatten01 layout)
+  for (int i = threadIdx.x; i < nrows * NIN; i += TB) {
+    const int r = i / NIN, k = i % NIN;
+    exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = obs[(size_t)(row0 + r) * NIN + k];
+  }
+  stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  block_forward(P, s);
+  const int r = threadIdx.x;
+  if (r < nrows) {
+    const int e = row0 + r;
+    const size_t slot = (size_t)e * H + t;
+    const float mu0 = s.out[r * 4], mu1 = s.out[r * 4 + 1], v = s.out[r * 4 + 2];
+    const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
+    const float sg0 = expf(ls0), sg1 = expf(ls1);
+    float z0, z1;
+    if (eps_inject) {
+      z0 = eps_inject[2 * e];
+      z1 = eps_inject[2 * e + 1];
+    } else {  // Normal.sample via Box-Muller on Philox(site 0x200)
+      float u[4];
+      philox_u4(seed, (uint32_t)e, step, 0x200u, u);
+      const float rr0 = sqrtf(-2.0f * logf(1.0f - u[0])), rr1 = sqrtf(-2.0f * logf(1.0f - u[2]));
+      z0 = rr0 * cosf(USV_2PI_F * u[1]);
+      z1 = rr1 * cosf(USV_2PI_F * u[3]);
+    }
+    const float a0 = mu0 + sg0 * z0, a1 = mu1 + sg1 * z1;
+    const float q0 = (a0 - mu0) / sg0, q1 = (a1 - mu1) / sg1;
+    const float nlp = 0.5f * (q0 * q0 + q1 * q1) + kLog2Pi + (ls0 + ls1);
+    float vd = v;
+    if (c.normalize_value) {  // denorm_value (running_mean_std.py:113-115)
+      vd = clampt(v, -5.0f, 5.0f);
+      vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
+    }
+    exp_act[slot * 2] = a0; exp_act[slot * 2 + 1] = a1;
+    exp_mu[slot * 2] = mu0; exp_mu[slot * 2 + 1] = mu1;
+    exp_sigma[slot * 2] = sg0; exp_sigma[slot * 2 + 1] = sg1;
+    exp_nlp[slot] = nlp;
+    exp_val[slot] = vd;
+    exp_done[slot] = (uint8_t)(dones_prev[e] != 0);
+    // preprocess_actions: clamp(-1,1) then rescale to [low, high] = identity (a2c_common.py:1134-1144)
+    actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
+    actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
+  }
+}
+
+__global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,
+                                              const double *val_rms, const float *__restrict__ obs, float *values) {
+  __shared__ FwdSmem s;
+  const int n = c.n_envs;
+  const int row0 = blockIdx.x * RB;
+  const int nrows = min(RB, n - row0);
+  stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  block_forward(P, s);
+  const int r = threadIdx.x;
+  if (r < nrows) {
+    float vd = s.out[r * 4 + 2];
+    if (c.normalize_value) {
+      vd = clampt(vd, -5.0f, 5.0f);
+      vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
+    }
+    values[row0 + r] = vd;
+  }
+}
+
+// rewards_shaper + episode meters (a2c_common.py:721-759, tr_helpers.py:33-43)
+__global__ void k_store_reward(ppo_cfg_t c, const float *__restrict__ rew, const int64_t *__restrict__ dones, int t,
+                               float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len, float *meter) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = c.n_envs;
+  float s_rew = 0.f, s_shaped = 0.f, s_len = 0.f, s_cnt = 0.f;
+  if (e < n) {
+    const float r = rew[e];
+    const float shaped = (r + c.reward_shift) * c.reward_scale;
+    exp_rew[(size_t)e * c.horizon + t] = shaped;
+    const float cr = cur_rew[e] + r, cs = cur_shaped[e] + shaped, cl = cur_len[e] + 1.0f;
+    const bool d = dones[e] != 0;
+    if (d) { s_rew = cr; s_shaped = cs; s_len = cl; s_cnt = 1.f; }
+    const float nd = 1.0f - (float)d;
+    cur_rew[e] = cr * nd;
+    cur_shaped[e] = cs * nd;
+    cur_len[e] = cl * nd;
+  }
+  s_rew = wave_sum(s_rew); s_shaped = wave_sum(s_shaped); s_len = wave_sum(s_len); s_cnt = wave_sum(s_cnt);
+  if ((threadIdx.x & 63) == 0 && s_cnt > 0.f) {
+    atomicAdd(&meter[t * 4 + 0], s_rew);
+    atomicAdd(&meter[t * 4 + 1], s_shaped);
+    atomicAdd(&meter[t * 4 + 2], s_len);
+    atomicAdd(&meter[t * 4 + 3], s_cnt);
+  }
+}
+
+// ---------------------------------------------------------- GAE + stats ---
+// work (doubles): [0..5] sums (v, v^2, ret, ret^2, adv, adv^2) accumulated
+// per block into work[8 + 8*blk ...]; finalize in k_prepare_finalize.
+__global__ __launch_bounds__(TB) void k_gae(ppo_cfg_t c, const float *__restrict__ last_val,
+                                            const int64_t *__restrict__ last_dones, const uint8_t *__restrict__ done,
+                                            const float *__restrict__ val, const float *__restrict__ rew, float *ret,
+                                            float *adv, double *work) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int H = c.horizon;
+  double sv = 0, sv2 = 0, sr = 0, sr2 = 0, sa = 0, sa2 = 0;
+  if (e < c.n_envs) {
+    const size_t base = (size_t)e * H;
+    float lastgaelam = 0.f;
+    for (int t = H - 1; t >= 0; --t) {
+      float nnt, nv;
+      if (t == H - 1) {
+        nnt = 1.0f - (float)(last_dones[e] != 0);
+        nv = last_val[e];
+      } else {
+        nnt = 1.0f - (float)done[base + t + 1];
+        nv = val[base + t + 1];
+      }
+      const float v = val[base + t];
+      const float delta = rew[base + t] + c.gamma * nv * nnt - v;
+      lastgaelam = delta + c.gamma * c.tau * nnt * lastgaelam;
+      const float R = lastgaelam + v;          // returns = advs + values (:763)
+      const float A = R - v;                   // prepare_dataset :1269
+      ret[base + t] = R;
+      adv[base + t] = A;
+      sv += v; sv2 += (double)v * v; sr += R; sr2 += (double)R * R; sa += A; sa2 += (double)A * A;
+    }
+  }
+  __shared__ double red[6][TB / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  double vals[6] = {sv, sv2, sr, sr2, sa, sa2};
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    double x = vals[q];
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+    if (lane == 0) red[q][wid] = x;
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    double x = 0;
+    for (int w = 0; w < TB / 64; ++w) x += red[threadIdx.x][w];
+    work[8 + (size_t)blockIdx.x * 8 + threadIdx.x] = x;
+  }
+}
+
+__device__ __forceinline__ void rms_merge(double *rm, int len, const double *bmean, const double *bvar, double bcount) {
+  // _update_mean_var_count_from_moments (running_mean_std.py:29-39); count at rm[2*len]
+  const double count = rm[2 * len];
+  const double tot = count + bcount;
+  for (int k = 0; k < len; ++k) {
+    const double delta = bmean[k] - rm[k];
+    const double new_mean = rm[k] + delta * bcount / tot;
+    const double m_a = rm[len + k] * count;
+    const double m_b = bvar[k] * bcount;
+    const double M2 = m_a + m_b + delta * delta * count * bcount / tot;
+    rm[k] = new_mean;
+    rm[len + k] = M2 / tot;
+  }
+  rm[2 * len] = tot;
+}
+
+__global__ void k_prepare_finalize(ppo_cfg_t c, double *val_rms, double *work, int nblk) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double s[6] = {0, 0, 0, 0, 0, 0};
+  for (int b = 0; b < nblk; ++b)
+    for (int q = 0; q < 6; ++q) s[q] += work[8 + (size_t)b * 8 + q];
+  const double B = (double)c.n_envs * c.horizon;
+  const double mv = s[0] / B, vv = (s[1] - B * mv * mv) / (B - 1.0);
+  const double mr = s[2] / B, vr = (s[3] - B * mr * mr) / (B - 1.0);
+  const double ma = s[4] / B, va = (s[5] - B * ma * ma) / (B - 1.0);
+  // value_mean_std.train(); values = vms(values); returns = vms(returns) (:1271-1275)
+  double stats_v[2] = {0.0, 1.0}, stats_r[2] = {0.0, 1.0};
+  if (c.normalize_value) {
+    rms_merge(val_rms, 1, &mv, &vv, B);
+    stats_v[0] = val_rms[0]; stats_v[1] = val_rms[1];
+    rms_merge(val_rms, 1, &mr, &vr, B);
+    stats_r[0] = val_rms[0]; stats_r[1] = val_rms[1];
+  }
+  work[0] = stats_v[0]; work[1] = stats_v[1];
+  work[2] = stats_r[0]; work[3] = stats_r[1];
+  work[4] = ma;
+  work[5] = sqrt(va > 0 ? va : 0.0);
+}
+
+__global__ void k_prepare_apply(ppo_cfg_t c, const double *work, float *val, float *ret, float *adv) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t B = (size_t)c.n_envs * c.horizon;
+  if (i >= B) return;
+  if (c.normalize_value) {
+    val[i] = rms_norm(val[i], work[0], work[1], c.rms_eps);
+    ret[i] = rms_norm(ret[i], work[2], work[3], c.rms_eps);
+  }
+  if (c.normalize_advantage) {
+    // (adv - adv.mean()) / (adv.std() + 1e-8)  (:1287)
+    adv[i] = (adv[i] - (float)work[4]) / ((float)work[5] + 1e-8f);
+  }
+}
+
+// ------------------------------------------------------- obs RMS (mb) -----
+__global__ __launch_bounds__(TB) void k_obs_stats(ppo_cfg_t c, const float *__restrict__ obs, int row0, int rows,
+                                                  double *part) {
+  // each block sums a chunk of rows for all 33 columns (fp64)
+  __shared__ double acc[2][NIN][TB / NIN + 1];
+  const int col = threadIdx.x % NIN, lane_r = threadIdx.x / NIN;   // 7 row-lanes x 33 cols
+  const int nl = TB / NIN;
+  double s = 0, s2 = 0;
+  if (lane_r < nl) {
+    const int chunk = (rows + gridDim.x - 1) / gridDim.x;
+    const int a = blockIdx.x * chunk, bnd = min(rows, a + chunk);
+    for (int r = a + lane_r; r < bnd; r += nl) {
+      const double x = obs[(size_t)(row0 + r) * NIN + col];
+      s += x; s2 += x * x;
+    }
+    acc[0][col][lane_r] = s;
+    acc[1][col][lane_r] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x < NIN) {
+    double t = 0, t2 = 0;
+    for (int l = 0; l < nl; ++l) { t += acc[0][threadIdx.x][l]; t2 += acc[1][threadIdx.x][l]; }
+    part[(size_t)blockIdx.x * 2 * NIN + threadIdx.x] = t;
+    part[(size_t)blockIdx.x * 2 * NIN + NIN + threadIdx.x] = t2;
+  }
+}
+
+__global__ void k_obs_rms_update(double *obs_rms, const double *part, int nblk, int rows) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double mean[NIN], var[NIN];
+  for (int k = 0; k < NIN; ++k) {
+    double s = 0, s2 = 0;
+    for (int b = 0; b < nblk; ++b) { s += part[(size_t)b * 2 * NIN + k]; s2 += part[(size_t)b * 2 * NIN + NIN + k]; }
+    mean[k] = s / rows;
+    var[k] = (s2 - rows * mean[k] * mean[k]) / (rows - 1.0);
+  }
+  rms_merge(obs_rms, NIN, mean, var, (double)rows);
+}
+
+// ------------------------------------------------------ minibatch grad ----
+struct GradSmem {
+  FwdSmem f;
+  float g[RB * 4];        // dmu0, dmu1, dv, dnlp per row
+};
+
+__global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
+                                                const double *__restrict__ obs_rms, int row0,
+                                                const float *__restrict__ e_obs, const float *__restrict__ e_act,
+                                                const float *__restrict__ e_nlp, const float *__restrict__ e_val,
+                                                const float *__restrict__ e_ret, const float *__restrict__ e_adv,
+                                                float *e_mu, float *e_sigma, float *partials) {
+  __shared__ GradSmem s;
+  const int tid = threadIdx.x;
+  const int rb0 = row0 + blockIdx.x * RB;             // global row of this block
+  const float invB = 1.0f / (float)c.minibatch;
+  stage_obs(e_obs, rb0, RB, obs_rms, c.normalize_input != 0, c.rms_eps, s.f);
+  block_forward(P, s.f);
+  float *part = partials + (size_t)blockIdx.x * NPART;
+  // ---- per-row losses and output gradients ----
+  float la = 0.f, lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f, gs0 = 0.f, gs1 = 0.f;
+  if (tid < RB) {
+    const int r = tid;
+    const size_t row = (size_t)rb0 + r;
+    const float mu0 = s.f.out[r * 4], mu1 = s.f.out[r * 4 + 1], v = s.f.out[r * 4 + 2];
+    const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
+    const float sg0 = expf(ls0), sg1 = expf(ls1);
+    const float x0 = e_act[row * 2], x1 = e_act[row * 2 + 1];
+    const float z0 = (x0 - mu0) / sg0, z1 = (x1 - mu1) / sg1;
+    const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
+    const float A = e_adv[row];
+    // actor_loss (common_losses.py:36-46)
+    const float ratio = expf(e_nlp[row] - nlp);
+    const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
+    const float rc = clampt(ratio, lo, hi);
+    const float s1 = -(A * ratio), s2 = -(A * rc);
+    const float a_loss = fmaxf(s1, s2);
+    const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+    const float g1 = -A, g2 = -A * inr;                // d(-A r)/dr, d(-A clip(r))/dr
+    const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
+    const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
+    // critic_loss (common_losses.py:10-19)
+    const float vo = e_val[row], R = e_ret[row];
+    float dv;
+    float c_loss;
+    if (c.clip_value) {
+      const float dvr = v - vo;
+      const float dvc = clampt(dvr, -c.e_clip, c.e_clip);
+      const float vc = vo + dvc;
+      const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+      c_loss = fmaxf(l1, l2);
+      const float d1 = 2.f * (v - R);
+      const float d2 = 2.f * (vc - R) * ((dvr >= -c.e_clip && dvr <= c.e_clip) ? 1.f : 0.f);
+      dv = (l1 > l2) ? d1 : ((l1 < l2) ? d2 : 0.5f * (d1 + d2));
+    } else {
+      c_loss = (R - v) * (R - v);
+      dv = 2.f * (v - R);
+    }
+    dv *= 0.5f * c.critic_coef * invB;
+    // bound_loss (a2c_continuous.py:209-217)
+    const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
+    const float bh1 = fmaxf(mu1 - 1.1f, 0.f), bl1 = fminf(mu1 + 1.1f, 0.f);
+    const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
+    const float bc = c.bounds_loss_coef * invB;
+    const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
+    const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
+    // d nlp / d logstd = 1 - z^2 (through sigma = exp(logstd) and the sum of logstd)
+    gs0 = dnlp * (1.f - z0 * z0);
+    gs1 = dnlp * (1.f - z1 * z1);
+    const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
+    // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
+    const float om0 = e_mu[row * 2], om1 = e_mu[row * 2 + 1];
+    const float os0 = e_sigma[row * 2], os1 = e_sigma[row * 2 + 1];
+    const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
+    const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
+    e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
+    e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
+    la = a_loss; lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
+    s.g[r * 4 + 0] = dmu0;
+    s.g[r * 4 + 1] = dmu1;
+    s.g[r * 4 + 2] = dv;
+    s.g[r * 4 + 3] = dnlp;
+  }
+  // block sums of losses and the sigma gradient (rows live in wave 0)
+  if (tid < 64) {
+    la = wave_sum(la); lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
+    gs0 = wave_sum(gs0); gs1 = wave_sum(gs1);
+    if (tid == 0) {
+      part[P_LOSS + 0] = la; part[P_LOSS + 1] = lc; part[P_LOSS + 2] = le; part[P_LOSS + 3] = lb;
+      part[P_LOSS + 4] = lkl;
+      part[P_SIGMA] = gs0; part[P_SIGMA + 1] = gs1;
+    }
+  }
+  __syncthreads();
+  const int j = tid % NH, rg = tid / NH, r0 = rg * RG;
+  // ---- heads' grads (need h2) and dz2 = (dmu Wmu + dv Wv) * (1 - h2^2) ----
+  {
+    const float wm0 = P[PPO_OFF_WMU + j], wm1 = P[PPO_OFF_WMU + NH + j], wv = P[PPO_OFF_WV + j];
+    float gw0 = 0.f, gw1 = 0.f, gwv = 0.f;
+    float dz[RG];
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      const int rr = r0 + r;
+      const float h = s.f.h2[rr * NH + j];
+      const float d0 = s.g[rr * 4], d1 = s.g[rr * 4 + 1], dvv = s.g[rr * 4 + 2];
+      gw0 = fmaf(d0, h, gw0); gw1 = fmaf(d1, h, gw1); gwv = fmaf(dvv, h, gwv);
+      const float dh = d0 * wm0 + d1 * wm1 + dvv * wv;
+      dz[r] = dh * (1.f - h * h);
+    }
+    __syncthreads();   // every thread has read h2
+#pragma unroll
+    for (int r = 0; r < RG; ++r) s.f.h2[(r0 + r) * NH + j] = dz[r];   // h2 := dz2
+    // two row groups -> combine through LDS (out[] is free now)
+    __shared__ float hg[2][3][NH];
+    hg[rg][0][j] = gw0; hg[rg][1][j] = gw1; hg[rg][2][j] = gwv;
+    __syncthreads();
+    if (rg == 0) {
+      part[P_WMU + j] = hg[0][0][j] + hg[1][0][j];
+      part[P_WMU + NH + j] = hg[0][1][j] + hg[1][1][j];
+      part[P_WV + j] = hg[0][2][j] + hg[1][2][j];
+    }
+    if (tid < 3) {
+      float sacc = 0.f;
+      for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + tid];
+      if (tid < 2) part[P_BMU + tid] = sacc;
+      else part[P_BV] = sacc;
+    }
+  }
+  __syncthreads();
+  // ---- dW2^T[k][j] = sum_r dz2[r][j] h1[r][k]; thread (j, k-half) ----
+  {
+    const int kh = rg;   // k in [kh*64, kh*64+64)
+    float acc[64];
+#pragma unroll
+    for (int q = 0; q < 64; ++q) acc[q] = 0.f;
+    float db = 0.f;
+    for (int r = 0; r < RB; ++r) {
+      const float d = s.f.h2[r * NH + j];
+      db += d;
+#pragma unroll
+      for (int q4 = 0; q4 < 16; ++q4) {
+        const float4 hv = *reinterpret_cast<const float4 *>(&s.f.h1[r * NH + kh * 64 + 4 * q4]);
+        acc[4 * q4 + 0] = fmaf(d, hv.x, acc[4 * q4 + 0]);
+        acc[4 * q4 + 1] = fmaf(d, hv.y, acc[4 * q4 + 1]);
+        acc[4 * q4 + 2] = fmaf(d, hv.z, acc[4 * q4 + 2]);
+        acc[4 * q4 + 3] = fmaf(d, hv.w, acc[4 * q4 + 3]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 64; ++q) part[P_W2T + (kh * 64 + q) * NH + j] = acc[q];
+    if (kh == 0) part[P_B2 + j] = db;
+  }
+  // ---- dh1[r][k] = sum_j dz2[r][j] W2[j][k]; dz1 = dh1 (1 - h1^2); thread (k, rows) ----
+  {
+    const int k = j;
+    float acc[RG];
+#pragma unroll
+    for (int r = 0; r < RG; ++r) acc[r] = 0.f;
+    for (int jj4 = 0; jj4 < NH / 4; ++jj4) {
+      const float w0 = P[PPO_OFF_W2 + (4 * jj4 + 0) * NH + k];
+      const float w1 = P[PPO_OFF_W2 + (4 * jj4 + 1) * NH + k];
+      const float w2 = P[PPO_OFF_W2 + (4 * jj4 + 2) * NH + k];
+      const float w3 = P[PPO_OFF_W2 + (4 * jj4 + 3) * NH + k];
+#pragma unroll
+      for (int r = 0; r < RG; ++r) {
+        const float4 d = *reinterpret_cast<const float4 *>(&s.f.h2[(r0 + r) * NH + 4 * jj4]);
+        acc[r] = fmaf(d.x, w0, acc[r]);
+        acc[r] = fmaf(d.y, w1, acc[r]);
+        acc[r] = fmaf(d.z, w2, acc[r]);
+        acc[r] = fmaf(d.w, w3, acc[r]);
+      }
+    }
+    __syncthreads();   // dW2 used h1: all reads done before overwrite
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      const float h = s.f.h1[(r0 + r) * NH + k];
+      s.f.h1[(r0 + r) * NH + k] = acc[r] * (1.f - h * h);   // h1 := dz1
+    }
+  }
+  __syncthreads();
+  // ---- dW1^T[k][j] = sum_r dz1[r][j] x[r][k]; db1 ----
+  {
+    // 33 columns split over the two row groups: rg 0 -> k 0..16, rg 1 -> k 17..32
+    const int k0 = rg ? 17 : 0, k1 = rg ? NIN : 17;
+    float acc[17];
+#pragma unroll
+    for (int q = 0; q < 17; ++q) acc[q] = 0.f;
+    float db = 0.f;
+    for (int r = 0; r < RB; ++r) {
+      const float d = s.f.h1[r * NH + j];
+      db += d;
+#pragma unroll
+      for (int q = 0; q < 17; ++q)
+        if (k0 + q < k1) acc[q] = fmaf(d, s.f.x[r * XP + k0 + q], acc[q]);
+    }
+#pragma unroll
+    for (int q = 0; q < 17; ++q)
+      if (k0 + q < k1) part[P_W1T + (k0 + q) * NH + j] = acc[q];
+    if (rg == 0) part[P_B1 + j] = db;
+  }
+}
+
+// sum the per-block partials (fixed order => deterministic) into grad[]
+__global__ void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad, float *losses,
+                                  float inv_b) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= NPART) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partials[(size_t)b * NPART + p];
+  if (p < PPO_NPARAM) grad[partial_to_param(p)] = s;
+  else if (p < PPO_NPARAM + 5) {
+    const int q = p - PPO_NPARAM;
+    if (q == 4) grad[PPO_NPARAM] = s * inv_b;      // kl mean rides with the gradient (all-reduce)
+    if (losses) losses[q] = s * inv_b;
+  }
+}
+
+// clip_grad_norm_ + Adam + AdaptiveScheduler, one workgroup
+__global__ __launch_bounds__(1024) void k_apply(ppo_cfg_t c, float *P, const float *__restrict__ grad_in,
+                                                float *m, float *v, float *opt, float grad_scale) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x;
+  float ss = 0.f;
+  for (int i = tid; i < PPO_NPARAM; i += 1024) {
+    const float g = grad_in[i] * grad_scale;
+    ss += g * g;
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  float tot = 0.f;
+  for (int w = 0; w < 16; ++w) tot += red[w];
+  const float total_norm = sqrtf(tot);
+  float coef = 1.0f;
+  if (c.truncate_grads) {
+    coef = c.grad_norm / (total_norm + 1e-6f);
+    coef = fminf(coef, 1.0f);
+  }
+  const float lr = opt[0];
+  const float step = opt[1] + 1.0f;
+  // torch.optim.Adam forms the bias corrections in Python doubles
+  const double bc1 = 1.0 - pow((double)c.adam_b1, (double)step);
+  const double bc2 = 1.0 - pow((double)c.adam_b2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  for (int i = tid; i < PPO_NPARAM; i += 1024) {
+    float g = grad_in[i] * grad_scale * coef;
+    if (c.weight_decay != 0.f) g = g + c.weight_decay * P[i];
+    float mi = m[i], vi = v[i];
+    mi = mi + (1.0f - c.adam_b1) * (g - mi);          // exp_avg.lerp_(grad, 1 - beta1)
+    vi = vi * c.adam_b2 + (1.0f - c.adam_b2) * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    const float denom = sqrtf(vi) / bc2s + c.adam_eps;
+    P[i] = P[i] - step_size * (mi / denom);
+    m[i] = mi;
+    v[i] = vi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    opt[1] = step;
+    opt[3] = total_norm;
+    // AdaptiveScheduler.update on this minibatch's KL (schedulers.py:26-32)
+    if (c.lr_adaptive) {
+      const float kl = grad_in[PPO_NPARAM] * grad_scale;
+      float nl = lr;
+      if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
+      if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
+      opt[0] = nl;
+      opt[2] = kl;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, const double *val_rms,
+                    const float *obs, int t, float *exp_obs, float *exp_act, float *exp_nlp, float *exp_val,
+                    float *exp_mu, float *exp_sigma, uint8_t *exp_done, const int64_t *dones_prev,
+                    float *actions_out, uint64_t seed, uint64_t step, const float *eps_inject, void *stream) {
+  if (!cfg || !params || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
+  const int grid = (cfg->n_envs + RB - 1) / RB;
+  hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
+                     obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
+                     actions_out, seed, step, eps_inject);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, const double *val_rms,
+              const float *obs, float *values, void *stream) {
+  if (!cfg || !params || !obs || !values || cfg->n_envs <= 0) return 1;
+  const int grid = (cfg->n_envs + RB - 1) / RB;
+  hipLaunchKernelGGL(k_value, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
+                     values);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *dones, int t, float *exp_rew,
+                     float *cur_rew, float *cur_shaped, float *cur_len, float *meter, void *stream) {
+  if (!cfg || !rew || !dones || cfg->n_envs <= 0) return 1;
+  hipLaunchKernelGGL(k_store_reward, dim3((cfg->n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream, *cfg, rew,
+                     dones, t, exp_rew, cur_rew, cur_shaped, cur_len, meter);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, double *val_rms,
+                const float *last_obs, const int64_t *last_dones, const uint8_t *exp_done, float *exp_val,
+                const float *exp_rew, float *exp_ret, float *exp_adv, double *work, void *stream) {
+  if (!cfg || !params || !work || cfg->n_envs <= 0) return 1;
+  hipStream_t s = (hipStream_t)stream;
+  // last values (get_values :407-430) into work-adjacent scratch: reuse exp_ret's tail? use a dedicated slice
+  float *last_val = reinterpret_cast<float *>(work + 8 + 8 * 4096);
+  if (ppo_value(cfg, params, obs_rms, val_rms, last_obs, last_val, stream)) return 2;
+  const int nblk = (cfg->n_envs + TB - 1) / TB;
+  if (nblk > 4096) return 3;
+  hipLaunchKernelGGL(k_gae, dim3(nblk), dim3(TB), 0, s, *cfg, last_val, last_dones, exp_done, exp_val, exp_rew,
+                     exp_ret, exp_adv, work);
+  USV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_prepare_finalize, dim3(1), dim3(64), 0, s, *cfg, val_rms, work, nblk);
+  USV_CHECK_LAUNCH();
+  const size_t B = (size_t)cfg->n_envs * cfg->horizon;
+  hipLaunchKernelGGL(k_prepare_apply, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *cfg, work, exp_val,
+                     exp_ret, exp_adv);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rms, const double *val_rms,
+                       int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+                       const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
+                       float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
+                       void *stream) {
+  (void)val_rms;
+  if (!cfg || !params || !grad || !partials || !work) return 1;
+  if (cfg->minibatch % RB != 0) return 2;
+  hipStream_t s = (hipStream_t)stream;
+  const int row0 = mb_index * cfg->minibatch;
+  if (update_obs_rms && cfg->normalize_input) {
+    // RunningMeanStd.train on the minibatch obs (mini-epoch 0 only, a2c_common.py:1243-1244)
+    const int nb = 64;
+    hipLaunchKernelGGL(k_obs_stats, dim3(nb), dim3(TB), 0, s, *cfg, exp_obs, row0, cfg->minibatch, work);
+    USV_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_obs_rms_update, dim3(1), dim3(64), 0, s, obs_rms, work, nb, cfg->minibatch);
+    USV_CHECK_LAUNCH();
+  }
+  const int nblk = cfg->minibatch / RB;
+  hipLaunchKernelGGL(k_mb_grad, dim3(nblk), dim3(TB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
+                     exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials);
+  USV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_partials, dim3((NPART + 255) / 256), dim3(256), 0, s, partials, nblk, grad, losses,
+                     1.0f / (float)cfg->minibatch);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m, float *adam_v, float *opt,
+                        float grad_scale, void *stream) {
+  if (!cfg || !params || !grad || !adam_m || !adam_v || !opt) return 1;
+  hipLaunchKernelGGL(k_apply, dim3(1), dim3(1024), 0, (hipStream_t)stream, *cfg, params, grad, adam_m, adam_v, opt,
+                     grad_scale);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_partials_floats(int minibatch) { return (minibatch / RB) * NPART; }
+
+}  // extern "C"

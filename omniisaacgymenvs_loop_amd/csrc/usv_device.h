@@ -1,0 +1,73 @@
+// Device-side helpers shared by the env and PPO kernels (gfx950 / CDNA4).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/usv_hip.h"
+
+#define USV_PI_F 3.14159265358979323846f
+#define USV_2PI_F 6.28318530717958647692f
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (counter-based RNG; Salmon et al. SC'11).  Every in-kernel
+// draw is Philox(key = seed, ctr = {env, step_lo, step_hi, site + i/4})[i%4],
+// so a draw depends only on (seed, env, step, site, i): no RNG state in HBM.
+// ---------------------------------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+__device__ __forceinline__ float u01(uint32_t x) { return (float)(x >> 8) * (1.0f / 16777216.0f); }
+
+// 4 uniforms of block `blk` of a (seed, env, step, site) stream
+__device__ __forceinline__ void philox_u4(uint64_t seed, uint32_t env, uint64_t step, uint32_t site_blk,
+                                          float out[4]) {
+  const u32x4 r = philox4x32_10(u32x4{env, (uint32_t)step, (uint32_t)(step >> 32), site_blk}, (uint32_t)seed,
+                                (uint32_t)(seed >> 32));
+  out[0] = u01(r.x); out[1] = u01(r.y); out[2] = u01(r.z); out[3] = u01(r.w);
+}
+
+__device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
+// torch's clamp/max/min propagate NaN differently from fminf/fmaxf; inputs here are finite.
+__device__ __forceinline__ float maxf(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float minf(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float clampt(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+// torch.norm(v, dim=-1) of a 2-vector == sqrt(fma(y, y, x*x)) (PyTorch CPU reduction)
+__device__ __forceinline__ float tnorm2(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+// float atomic max for non-negative-or-any floats via int ordering
+__device__ __forceinline__ void atomic_max_f32(float *addr, float v) {
+  if (v >= 0.f) atomicMax((int *)addr, __float_as_int(v));
+  else atomicMin((unsigned int *)addr, __float_as_uint(v));
+}
+
+#define USV_CHECK_LAUNCH()                                   \
+  do {                                                       \
+    hipError_t _e = hipGetLastError();                       \
+    if (_e != hipSuccess) return 100 + (int)_e;              \
+  } while (0)

@@ -1,0 +1,76 @@
+"""VecEnvRLGames: the omniisaacgymenvs env wrapper contract rl_games drives.
+
+Reference: omniisaacgymenvs/envs/vec_env_rlgames.py:82-230.  step(actions)
+returns ({"obs": {"state": [N,33]}, "states": [N,0]}, rew [N] fp32,
+resets [N] int64, extras); reset() flags every env and runs one zero-action
+step.  The 10 physics substeps, the reset path and the observation / reward /
+done computation are one fused sequence of HIP kernels on the current stream
+(no host synchronisation inside a step).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, Optional
+
+import torch
+
+
+class VecEnvRLGames:
+    def __init__(self, headless: bool = True, sim_device: int = 0, enable_livestream: bool = False,
+                 enable_viewport: bool = False, **_: Any):
+        self._headless = headless
+        self._sim_device = sim_device
+        self._render = not headless
+        self._task = None
+        self._world = None
+        self.sim_frame_count = 0
+
+    # omni.isaac.gym VecEnvBase.set_task
+    def set_task(self, task, backend: str = "torch", sim_params: Optional[dict] = None, init_sim: bool = True) -> None:
+        self._task = task
+        self._world = task._world
+        self._num_envs = task.num_envs
+        self.num_envs = task.num_envs
+        self.num_states = task.num_states
+        self.state_space = task.state_space
+        self.observation_space = task.observation_space
+        self.action_space = task.action_space
+
+    # ------------------------------------------------------------------ API
+    def step(self, actions: torch.Tensor):
+        t = self._task
+        a = actions
+        if a.device != torch.device(t.device):
+            a = a.to(t.device)
+        # clamp to clipActions happens inside the step kernel (vec_env_rlgames.py:136-140)
+        obs, rew, dones = t.env_step(a)
+        self.sim_frame_count += t.control_frequency_inv
+        obs_dict = {"obs": {"state": obs}, "states": t.get_states()}
+        return obs_dict, rew, dones, t.extras
+
+    def reset(self):
+        """Resets the task and applies zero actions to recompute observations (:219-230)."""
+        self._task.reset()
+        actions = torch.zeros((self.num_envs, self._task.num_actions), device=self._task.rl_device)
+        obs_dict, _, _, _ = self.step(actions)
+        return obs_dict
+
+    def get_number_of_agents(self) -> int:
+        return 1
+
+    def get_env_info(self) -> Dict[str, Any]:
+        info = {"action_space": self.action_space, "observation_space": self.observation_space}
+        if self.num_states > 0:
+            info["state_space"] = self.state_space
+        return info
+
+    def set_train_info(self, env_frames, *args, **kwargs):
+        pass
+
+    def get_env_state(self):
+        return None
+
+    def set_env_state(self, env_state):
+        pass
+
+    def close(self):
+        pass

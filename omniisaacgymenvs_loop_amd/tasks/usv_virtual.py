@@ -1,0 +1,233 @@
+"""USVVirtual: the CaptureXY task state on the GPU, stepped by libusv_hip.so.
+
+Mirrors the task object the reference's VecEnvRLGames drives
+(omniisaacgymenvs/tasks/USV_Virtual.py:56-1726 + tasks/base/rl_task.py):
+same names for the buffers rl_games and the env wrapper touch (obs_buf,
+rew_buf, reset_buf, progress_buf, extras, num_envs, num_observations,
+num_actions, num_states, clip_obs, clip_actions, observation_space,
+action_space, reset(), update_state(), get_states()), but every per-env
+quantity is a struct-of-arrays device tensor and one control step is four
+kernel launches (reset, potential field, step) with no host synchronisation.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+
+from .. import _capi
+from .._abi import DEFINES, STAT_NAMES, UsvBufs
+from ..utils.spaces import Box, DictSpace
+from .usv_config import action_bias_cfg, build_usv_cfg, thruster_tables
+
+NOBS = DEFINES["USV_NOBS"]
+NOBST = DEFINES["USV_NOBST"]
+GRID2 = DEFINES["USV_GRID"] ** 2
+NSTAT = DEFINES["USV_NSTAT"]
+NU_RESET = DEFINES["USV_NU_RESET"]
+NU_STEP = DEFINES["USV_NU_STEP"]
+CTL_N = DEFINES["USV_CTL_N"]
+
+
+class _World:
+    """Stand-in for omni.isaac.core World: physics runs inside the step kernel."""
+
+    def is_playing(self) -> bool:
+        return True
+
+    def step(self, render: bool = False) -> None:
+        return None
+
+
+class USVVirtual:
+    """CaptureXY task (USV_capture_xy_static_obs.CaptureXYTask glue) on MI355X."""
+
+    def __init__(self, task_cfg: Dict[str, Any], num_envs: Optional[int] = None, device: str = "cuda:0",
+                 seed: int = 42, rl_device: Optional[str] = None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("USVVirtual needs a ROCm GPU (MI355X); there is no CPU path")
+        self._task_cfg = task_cfg
+        self._num_envs = int(num_envs if num_envs is not None else task_cfg["env"]["numEnvs"])
+        self._device = device
+        self.device = device
+        self.rl_device = rl_device or device
+        self.cfg = build_usv_cfg(task_cfg)
+        self._max_episode_length = int(task_cfg["env"]["maxEpisodeLength"])
+        self._num_observations = NOBS
+        self._num_actions = 2
+        self._num_states = 0
+        self._num_agents = 1
+        self.clip_obs = task_cfg["env"].get("clipObservations", {"state": 12.0})
+        self.clip_actions = task_cfg["env"].get("clipActions", 1.0)
+        self.control_frequency_inv = int(task_cfg["env"].get("controlFrequencyInv", 10))
+        self.randomize_actions = False
+        self.randomize_observations = False
+        self.observation_space = DictSpace({"state": Box(-np.inf, np.inf, (NOBS,))})
+        self.action_space = Box(np.array([-1.0, -1.0], np.float32), np.array([1.0, 1.0], np.float32))
+        self.state_space = Box(-np.inf, np.inf, (0,))
+        self._initial_action_bias, self._initial_action_bias_steps = action_bias_cfg(task_cfg)
+        self._action_bias_step_count = 0
+        self.seed = int(seed)
+        self._step_index = 0
+        self.step = 0.0                     # USVVirtual.step (+= 1/horizon per metrics call)
+        self._horizon = int(task_cfg["env"].get("horizon_length", 16))
+        self.grid_lin: Optional[torch.Tensor] = None
+        self._alloc()
+        self._env = self
+        self._world = _World()
+
+    # ------------------------------------------------------------------ buffers
+    def _alloc(self):
+        n, dev = self._num_envs, self._device
+        f32 = dict(device=dev, dtype=torch.float32)
+        i32 = dict(device=dev, dtype=torch.int32)
+        Z = lambda *s, **k: torch.zeros(*s, **k)
+        self.state = Z((8, n), **f32)                  # px py yaw vx vy wz fl fr
+        self.params = Z((9, n), **f32)                 # mass com_x com_y com_z k_drag thr_l thr_r k_iz mass_r
+        self.params[0] = self.cfg.base_mass
+        self.params[4:8] = 1.0
+        self.damp = Z((2, 3, n), **f32) if self.cfg.drag_rand_on else None
+        if self.damp is not None:
+            for a in range(3):
+                self.damp[0, a] = self.cfg.lin_damp[a]
+                self.damp[1, a] = self.cfg.quad_damp[a]
+        self.tgt = Z((2, n), **f32)
+        self.obst = Z((NOBST * 2, n), **f32)
+        self.field = Z((n, GRID2), **f32)
+        self.prev_cmd = Z((2, n), **f32)
+        self.hist = Z((4, n), **f32)                   # prev_dist prev_head prev_pot prev_wz
+        self.ibuf = Z((5, n), **i32)                   # goal_cnt progress reset_buf done_succ done_coll
+        self.ibuf[2] = 1                               # RLTask.cleanup: reset_buf = ones
+        self.just_reset = torch.ones(n, device=dev, dtype=torch.uint8)
+        self.stats = Z((NSTAT, n), **f32)
+        self.obs_buf_t = Z((n, NOBS), **f32)
+        self.rew_buf = Z(n, **f32)
+        self.dones = Z(n, device=dev, dtype=torch.int64)
+        self.ctl = Z(CTL_N, **i32)
+        self.reset_ids = Z(n, **i32)
+        self.fscratch = Z(16, **f32)
+        self.extras_buf = Z(NSTAT, **f32)
+        self.extras_acc = Z(NSTAT, **f32)
+        self.field_old_tgt = Z((2, n), **f32)
+        self.slot_stats = Z((n, 8), **f32)
+        self.lut = Z((2, 1000), **f32)
+        tl, tr = thruster_tables(self._task_cfg)
+        self._tables = torch.tensor(np.stack([tl, tr]), **f32)
+        _capi.call("usv_build_lut", _capi.ptr(self._tables[0]), _capi.ptr(self._tables[1]), int(len(tl)),
+                   _capi.ptr(self.lut), _capi.stream_ptr())
+        self._bufs = self._make_bufs()
+        self.extras: Dict[str, Any] = {}
+
+    def _make_bufs(self) -> UsvBufs:
+        b = UsvBufs()
+        b.n = self._num_envs
+        p = _capi.ptr
+        for i, k in enumerate(("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr")):
+            setattr(b, k, p(self.state[i]))
+        for i, k in enumerate(("mass", "com_x", "com_y", "com_z", "k_drag", "thr_l", "thr_r", "k_iz", "mass_r")):
+            setattr(b, k, p(self.params[i]))
+        b.lin_damp = p(self.damp[0]) if self.damp is not None else None
+        b.quad_damp = p(self.damp[1]) if self.damp is not None else None
+        b.tgt_x, b.tgt_y = p(self.tgt[0]), p(self.tgt[1])
+        b.obst = p(self.obst)
+        b.field = p(self.field)
+        b.prev_cmd = p(self.prev_cmd)
+        b.prev_dist, b.prev_head, b.prev_pot, b.prev_wz = (p(self.hist[i]) for i in range(4))
+        b.goal_cnt, b.progress, b.reset_buf, b.done_succ, b.done_coll = (p(self.ibuf[i]) for i in range(5))
+        b.just_reset = p(self.just_reset)
+        b.stats = p(self.stats)
+        b.obs, b.rew, b.dones = p(self.obs_buf_t), p(self.rew_buf), p(self.dones)
+        b.ctl, b.reset_ids, b.fscratch = p(self.ctl), p(self.reset_ids), p(self.fscratch)
+        b.extras, b.extras_acc = p(self.extras_buf), p(self.extras_acc)
+        b.field_old_tgt = p(self.field_old_tgt)
+        b.slot_stats = p(self.slot_stats)
+        b.grid_lin = p(self.grid_lin) if self.grid_lin is not None else None
+        return b
+
+    def set_grid_lin(self, lin: torch.Tensor) -> None:
+        """Override the field grid's cell centres (parity tests vs CPU fixtures)."""
+        self.grid_lin = lin.to(self._device, torch.float32).contiguous()
+        self._bufs = self._make_bufs()
+
+    # ------------------------------------------------------------ RLTask API
+    @property
+    def num_envs(self) -> int:
+        return self._num_envs
+
+    @property
+    def num_observations(self) -> int:
+        return self._num_observations
+
+    @property
+    def num_actions(self) -> int:
+        return self._num_actions
+
+    @property
+    def num_states(self) -> int:
+        return self._num_states
+
+    @property
+    def num_agents(self) -> int:
+        return self._num_agents
+
+    @property
+    def reset_buf(self) -> torch.Tensor:
+        return self.ibuf[2]
+
+    @property
+    def progress_buf(self) -> torch.Tensor:
+        return self.ibuf[1]
+
+    @property
+    def obs_buf(self) -> Dict[str, torch.Tensor]:
+        return {"state": self.obs_buf_t}
+
+    def reset(self) -> None:
+        """RLTask.reset: flag every env for reset (rl_task.py:268-270)."""
+        self.ibuf[2].fill_(1)
+
+    def update_state(self) -> None:
+        """Physics state lives in the SoA buffers; nothing to read back."""
+        return None
+
+    def get_states(self) -> torch.Tensor:
+        return torch.zeros((self._num_envs, 0), device=self._device)
+
+    def get_extras(self) -> Dict[str, Any]:
+        return self.extras
+
+    # -------------------------------------------------------------- stepping
+    def current_action_bias(self) -> float:
+        if self._initial_action_bias_steps > 0 and self._action_bias_step_count < self._initial_action_bias_steps:
+            return float(self._initial_action_bias)
+        return 0.0
+
+    def env_step(self, actions: torch.Tensor, u_step: Optional[torch.Tensor] = None,
+                 u_reset: Optional[torch.Tensor] = None):
+        """pre_physics_step + 10 substeps + post_physics_step (USV_Virtual.py:1042-1652).
+
+        Returns the device tensors (obs [n,33], rew [n], dones int64 [n])."""
+        if actions.dtype != torch.float32 or not actions.is_contiguous():
+            actions = actions.to(torch.float32).contiguous()
+        s = _capi.stream_ptr()
+        cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
+        bias = self.current_action_bias()
+        self._action_bias_step_count += 1
+        k = self._step_index
+        _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
+        _capi.call("usv_potential_field", cfg, b, s)
+        _capi.call("usv_env_step", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias), self.seed,
+                   k, _capi.ptr(u_step), s)
+        self._step_index += 1
+        self.step += 1.0 / self._horizon
+        if k == 0 or "episode" not in self.extras:
+            # extras["episode"]: 0-d views of the device buffer written at every reset (USV_Virtual.py:1591-1612)
+            self.extras = {"episode": {name: self.extras_buf[i] for i, name in enumerate(STAT_NAMES)}}
+        return self.obs_buf_t, self.rew_buf, self.dones
+
+    def forces(self) -> torch.Tensor:
+        out = torch.empty((self._num_envs, 3), device=self._device, dtype=torch.float32)
+        _capi.call("usv_forces", _capi.byref(self.cfg), _capi.byref(self._bufs), _capi.ptr(out), _capi.stream_ptr())
+        return out
