@@ -648,6 +648,127 @@ def gen_episode(torch, variant, n, steps, seed):
     print(f"episode_{variant}: resets per step", out["reset_mask"].sum(1).tolist())
 
 
+class ScriptedVecEnv:
+    """Plays back fixed obs/rewards/dones; exposes what A2CBase.__init__ touches."""
+
+    def __init__(self, torch, n, horizon, seed):
+        g = torch.Generator().manual_seed(seed)
+        self.t = torch
+        self.n = n
+        self.obs = [torch.randn((n, 33), generator=g) * 2.0 for _ in range(horizon + 1)]
+        self.rew = [torch.randn((n,), generator=g) * 3.0 for _ in range(horizon)]
+        self.dones = [(torch.rand((n,), generator=g) < 0.08).long() for _ in range(horizon)]
+        self.k = 0
+        self.actions_seen = []
+        self.env = types.SimpleNamespace(_world=types.SimpleNamespace(step=lambda render=False: None),
+                                         _task=types.SimpleNamespace(update_state=lambda: None))
+
+    def reset(self):
+        self.k = 0
+        return {"obs": {"state": self.obs[0].clone()}, "states": self.t.zeros((self.n, 0))}
+
+    def step(self, actions):
+        self.actions_seen.append(actions.clone())
+        k = self.k
+        self.k += 1
+        return ({"obs": {"state": self.obs[k + 1].clone()}, "states": self.t.zeros((self.n, 0))},
+                self.rew[k].clone(), self.dones[k].clone(), {})
+
+    def set_train_info(self, *a, **k):
+        pass
+
+    def get_env_state(self):
+        return None
+
+
+def gen_ppo(torch, n=32, horizon=16, minibatch=128, seed=5):
+    import yaml
+    from rl_games.algos_torch import a2c_continuous
+    from rl_games.common.algo_observer import DefaultAlgoObserver
+    from rl_games.common import tr_helpers
+    with open(os.path.join(REF, "omniisaacgymenvs/cfg/train/USV/USV_PPOcontinuous_MLP.yaml")) as f:
+        params = yaml.safe_load(f)["params"]
+    cfg = params["config"]
+    cfg.update(dict(name="golden", full_experiment_name="golden", device="cpu", device_name="cpu", num_actors=n,
+                    minibatch_size=minibatch, max_epochs=10, train_dir="/tmp/golden_runs", print_stats=False))
+    cfg["reward_shaper"] = tr_helpers.DefaultRewardsShaper(**cfg["reward_shaper"])
+    cfg["features"] = {"observer": DefaultAlgoObserver()}
+    spaces = sys.modules["gym.spaces"]
+    env_info = {"action_space": spaces.Box(np.array([-1.0, -1.0], np.float32), np.array([1.0, 1.0], np.float32)),
+                "observation_space": spaces.Dict({"state": spaces.Box(np.ones(33) * -np.inf, np.ones(33) * np.inf)})}
+    env_info["observation_space"].spaces["state"].shape = (33,)
+    cfg["env_info"] = env_info
+    venv = ScriptedVecEnv(torch, n, horizon, seed)
+    cfg["vec_env"] = venv
+    params["seed"] = seed
+    torch.manual_seed(seed)
+    agent = a2c_continuous.A2CAgent("run", params)
+    init_state = {k: v.detach().clone().numpy() for k, v in agent.model.state_dict().items()}
+    agent.init_tensors()
+    agent.obs = agent.env_reset()
+    torch.manual_seed(seed + 1)
+    recorded = {"losses": [], "kl": [], "lr": [], "mu_after": []}
+    orig_train_ac = agent.train_actor_critic
+
+    def train_ac(input_dict):
+        res = orig_train_ac(input_dict)
+        a_loss, c_loss, entropy, kl, last_lr, lr_mul, cmu, csigma, b_loss = res
+        recorded["losses"].append([float(a_loss), float(c_loss), float(entropy), float(b_loss)])
+        recorded["kl"].append(float(kl))
+        return res
+
+    agent.train_actor_critic = train_ac
+    orig_update_lr = agent.update_lr
+
+    def update_lr(lr):
+        recorded["lr"].append(float(lr))
+        return orig_update_lr(lr)
+
+    agent.update_lr = update_lr
+    exp_snap = {}
+    orig_prepare = agent.prepare_dataset
+
+    def prepare(batch_dict):
+        for k, v in batch_dict.items():
+            if hasattr(v, "numpy"):
+                exp_snap["batch_" + k] = v.detach().clone().numpy()
+        orig_prepare(batch_dict)
+        for k, v in agent.dataset.values_dict.items():
+            if hasattr(v, "numpy"):
+                exp_snap["ds_" + k] = v.detach().clone().numpy()
+            elif isinstance(v, dict):
+                for kk, vv in v.items():
+                    exp_snap[f"ds_{k}_{kk}"] = vv.detach().clone().numpy()
+
+    agent.prepare_dataset = prepare
+    agent.train_epoch()
+    out = {f"init_{k.replace('.', '__')}": v for k, v in init_state.items()}
+    out.update({f"final_{k.replace('.', '__')}": v.detach().clone().numpy() for k, v in agent.model.state_dict().items()})
+    eb = agent.experience_buffer.tensor_dict
+    for k in ("actions", "neglogpacs", "values", "mus", "sigmas", "dones", "rewards"):
+        out["exp_" + k] = eb[k].detach().clone().numpy()
+    out["exp_obses"] = eb["obses"]["state"].detach().clone().numpy() if isinstance(eb["obses"], dict) else \
+        eb["obses"].detach().clone().numpy()
+    out["env_obs"] = np.stack([o.numpy() for o in venv.obs])
+    out["env_rew"] = np.stack([r.numpy() for r in venv.rew])
+    out["env_dones"] = np.stack([d.numpy() for d in venv.dones])
+    out["env_actions"] = np.stack([a.numpy() for a in venv.actions_seen])
+    out.update(exp_snap)
+    out["losses"] = np.asarray(recorded["losses"], np.float64)
+    out["kl"] = np.asarray(recorded["kl"], np.float64)
+    out["lr_seq"] = np.asarray(recorded["lr"], np.float64)
+    opt = agent.optimizer.state_dict()
+    for i in range(9):
+        out[f"adam_m_{i}"] = opt["state"][i]["exp_avg"].numpy()
+        out[f"adam_v_{i}"] = opt["state"][i]["exp_avg_sq"].numpy()
+        out[f"adam_step_{i}"] = np.float64(opt["state"][i]["step"])
+    out["hyper"] = np.array([n, horizon, minibatch, agent.mini_epochs_num], np.int64)
+    out["game_rewards_mean"] = agent.game_rewards.get_mean()
+    out["game_rewards_size"] = np.int64(agent.game_rewards.current_size)
+    np.savez_compressed(os.path.join(OUT, "ppo_epoch.npz"), **out)
+    print("ppo: lr", recorded["lr"][:6], "... kl", recorded["kl"][:4])
+
+
 STAT_NAMES = [
     "total_reward", "distance_reward", "alignment_reward", "heading_improve_reward",
     "potential_shaping_reward", "speed_reward", "angular_reward", "turn_hazard_penalty",
@@ -671,6 +792,7 @@ def main():
         "field": lambda: gen_field(torch),
         "episodeA": lambda: gen_episode(torch, "A", 16, 64, 1234),
         "episodeB": lambda: gen_episode(torch, "B", 12, 56, 99),
+        "ppo": lambda: gen_ppo(torch),
     }
     for name, fn in jobs.items():
         if args.only and name not in args.only.split(","):
