@@ -1,0 +1,431 @@
+"""A2CAgent: rl_games continuous PPO (a2c_continuous + ContinuousA2CBase + A2CBase)
+with every per-sample operation in HIP kernels (csrc/ppo.hip).
+
+Reference: rl_games/rl_games/algos_torch/a2c_continuous.py:14-217 and
+rl_games/rl_games/common/a2c_common.py:65-1486.  Same constructor
+(`A2CAgent(base_name, params)`), same config keys (train yaml `params.config`),
+same train() / train_epoch() / play_steps() / prepare_dataset() structure, same
+checkpoint dict.  Differences by design:
+  * the experience buffer is env-major on the device (the layout
+    swap_and_flatten01 produces), written in place by the rollout kernel;
+  * the episode meters are accumulated on the device per step and replayed
+    into AverageMeter semantics once per epoch (one host sync per epoch,
+    instead of per-step .item() calls);
+  * the KL and the adaptive learning rate stay on the device;
+  * multi-GPU: one process per GPU, flat-gradient all-reduce (+ KL in the same
+    buffer) between the gradient and the Adam kernels.
+"""
+from __future__ import annotations
+
+import copy
+import os
+import time
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .. import _capi
+from .._abi import DEFINES, PpoCfg
+from . import checkpoint as ckpt
+from . import vecenv
+
+NIN, NH, NA = DEFINES["PPO_NIN"], DEFINES["PPO_NH"], DEFINES["PPO_NA"]
+NPARAM = DEFINES["PPO_NPARAM"]
+
+
+class AverageMeter:
+    """torch_ext.AverageMeter (torch_ext.py:281-307) fed with (mean, size) pairs."""
+
+    def __init__(self, max_size: int = 100):
+        self.max_size = max_size
+        self.current_size = 0
+        self.mean = 0.0
+
+    def update_stats(self, new_mean: float, size: int) -> None:
+        if size == 0:
+            return
+        size = int(np.clip(size, 0, self.max_size))
+        old_size = min(self.max_size - size, self.current_size)
+        size_sum = old_size + size
+        self.current_size = size_sum
+        self.mean = (self.mean * old_size + new_mean * size) / size_sum
+
+    def clear(self):
+        self.current_size = 0
+        self.mean = 0.0
+
+    def get_mean(self) -> float:
+        return self.mean
+
+    def __len__(self):
+        return self.current_size
+
+
+class DefaultAlgoObserver:
+    """rl_games.common.algo_observer.AlgoObserver hooks (algo_observer.py:6-26)."""
+
+    def before_init(self, base_name, config, experiment_name):
+        pass
+
+    def after_init(self, algo):
+        self.algo = algo
+
+    def process_infos(self, infos, done_indices):
+        pass
+
+    def after_steps(self):
+        pass
+
+    def after_clear_stats(self):
+        pass
+
+    def after_print_stats(self, frame, epoch_num, total_time):
+        pass
+
+
+def default_linear_init(seed: int) -> torch.Tensor:
+    """PyTorch nn.Linear default init in the reference's construction order
+    (actor_mlp 33->128, 128->128, value 128->1, mu 128->2), biases zeroed,
+    sigma = const 0 (network_builder.py:1520-1575)."""
+    g = torch.Generator().manual_seed(int(seed))
+    parts = {"sigma": torch.zeros(NA)}
+
+    def lin(i, o):
+        bound = 1.0 / np.sqrt(i)   # kaiming_uniform(a=sqrt(5)) == U(-1/sqrt(fan_in), 1/sqrt(fan_in))
+        w = (torch.rand((o, i), generator=g) * 2 - 1) * bound
+        torch.rand((o,), generator=g)   # bias draw (then zeroed by the builder)
+        return w, torch.zeros(o)
+
+    W1, b1 = lin(NIN, NH)
+    W2, b2 = lin(NH, NH)
+    Wv, bv = lin(NH, 1)
+    Wmu, bmu = lin(NH, NA)
+    flat = torch.cat([parts["sigma"], W1.reshape(-1), b1, W2.reshape(-1), b2, Wv.reshape(-1), bv,
+                      Wmu.reshape(-1), bmu]).float()
+    assert flat.numel() == NPARAM
+    return flat
+
+
+class A2CAgent:
+    def __init__(self, base_name: str, params: Dict[str, Any]):
+        self.config = config = params["config"]
+        self.name = base_name
+        self.params = params
+        self.seed = int(params.get("seed", 42))
+        self.experiment_name = config.get("full_experiment_name") or config["name"]
+        self.algo_observer = config.get("features", {}).get("observer") or DefaultAlgoObserver()
+        self.algo_observer.before_init(base_name, config, self.experiment_name)
+        # ---- distributed (a2c_common.py:87-101): one process per GPU ----
+        self.multi_gpu = bool(config.get("multi_gpu", False))
+        self.rank, self.rank_size = 0, 1
+        if self.multi_gpu:
+            self.rank = int(os.getenv("LOCAL_RANK", "0"))
+            self.rank_size = int(os.getenv("WORLD_SIZE", "1"))
+            if not dist.is_initialized():
+                dist.init_process_group("nccl", rank=int(os.getenv("RANK", self.rank)), world_size=self.rank_size)
+            config["device"] = f"cuda:{self.rank}"
+        self.ppo_device = config.get("device", "cuda:0")
+        torch.cuda.set_device(torch.device(self.ppo_device))
+        self.num_actors = int(config["num_actors"])
+        self.env_name = config.get("env_name", "rlgpu")
+        self.vec_env = config.get("vec_env", None)
+        if self.vec_env is None:
+            self.vec_env = vecenv.create_vec_env(self.env_name, self.num_actors, **config.get("env_config", {}))
+        self.env_info = config.get("env_info") or self.vec_env.get_env_info()
+        # "sim-system need run few step before reset by rlgames" (a2c_common.py:123-127)
+        inner = getattr(self.vec_env, "env", None)
+        if inner is not None and hasattr(inner, "_world") and hasattr(inner, "_task"):
+            for _ in range(5):
+                inner._world.step(render=False)
+                inner._task.update_state()
+        obs_space = self.env_info["observation_space"]
+        obs_shape = obs_space.spaces["state"].shape if hasattr(obs_space, "spaces") else obs_space.shape
+        if tuple(obs_shape) != (NIN,):
+            raise ValueError(f"observation 'state' must be ({NIN},), got {obs_shape}")
+        self.actions_num = self.env_info["action_space"].shape[0]
+        if self.actions_num != NA:
+            raise ValueError(f"action space must have {NA} dims")
+        self.horizon_length = int(config["horizon_length"])
+        self.batch_size = self.horizon_length * self.num_actors
+        self.minibatch_size = int(config.get("minibatch_size", self.num_actors * config.get("minibatch_size_per_env", 0)))
+        assert self.batch_size % self.minibatch_size == 0, "batch_size % minibatch_size != 0 (a2c_common.py:240)"
+        if self.minibatch_size % 64 != 0:
+            raise ValueError("minibatch_size must be a multiple of 64 (kernel row block)")
+        self.num_minibatches = self.batch_size // self.minibatch_size
+        self.mini_epochs_num = int(config["mini_epochs"])
+        self.max_epochs = int(config.get("max_epochs", -1))
+        self.max_frames = int(config.get("max_frames", -1))
+        self.save_freq = int(config.get("save_frequency", 0))
+        self.save_best_after = int(config.get("save_best_after", 100))
+        self.print_stats = bool(config.get("print_stats", True)) and self.rank == 0
+        self.games_to_track = int(config.get("games_to_track", 100))
+        self.score_to_win = float(config.get("score_to_win", float("inf")))
+        self.normalize_input = bool(config.get("normalize_input", False))
+        self.normalize_value = bool(config.get("normalize_value", False))
+        self.normalize_advantage = bool(config.get("normalize_advantage", True))
+        self.last_lr = float(config["learning_rate"])
+        self.is_adaptive_lr = config.get("lr_schedule") == "adaptive"
+        if config.get("lr_schedule") not in (None, "adaptive", "None"):
+            raise NotImplementedError(f"lr_schedule {config.get('lr_schedule')} is not on the USV hot path")
+        if str(config.get("schedule_type", "legacy")) != "legacy":
+            raise NotImplementedError("only the legacy (per-minibatch) KL schedule is implemented")
+        rs = config.get("reward_shaper", {}) or {}
+        if not isinstance(rs, dict):
+            rs = {"scale_value": getattr(rs, "scale_value", 1.0), "shift_value": getattr(rs, "shift_value", 0.0)}
+        self.cfg = c = PpoCfg()
+        c.horizon, c.n_envs, c.minibatch = self.horizon_length, self.num_actors, self.minibatch_size
+        c.normalize_input, c.normalize_value = int(self.normalize_input), int(self.normalize_value)
+        c.normalize_advantage = int(self.normalize_advantage)
+        c.gamma, c.tau = float(config["gamma"]), float(config["tau"])
+        c.e_clip, c.critic_coef = float(config["e_clip"]), float(config["critic_coef"])
+        c.entropy_coef = float(config["entropy_coef"])
+        c.bounds_loss_coef = float(config.get("bounds_loss_coef", 0.0) or 0.0)
+        c.clip_value = int(bool(config.get("clip_value", False)))
+        c.truncate_grads, c.grad_norm = int(bool(config.get("truncate_grads", False))), float(config["grad_norm"])
+        c.adam_b1, c.adam_b2, c.adam_eps = 0.9, 0.999, 1e-8
+        c.weight_decay = float(config.get("weight_decay", 0.0))
+        c.lr_adaptive = int(self.is_adaptive_lr)
+        c.kl_threshold = float(config.get("kl_threshold", 0.008))
+        c.lr_min, c.lr_max = 1e-6, 1e-2
+        c.reward_scale = float(rs.get("scale_value", 1.0))
+        c.reward_shift = float(rs.get("shift_value", 0.0))
+        c.rms_eps = 1e-5
+        if c.entropy_coef != 0.0:
+            raise NotImplementedError("entropy_coef != 0 (gradient of the entropy bonus) is not implemented")
+        self._alloc()
+        self.frame = 0
+        self.epoch_num = 0
+        self.mean_rewards = self.last_mean_rewards = -100500
+        self.game_rewards = AverageMeter(self.games_to_track)
+        self.game_shaped_rewards = AverageMeter(self.games_to_track)
+        self.game_lengths = AverageMeter(self.games_to_track)
+        self.train_dir = config.get("train_dir", "runs")
+        self.experiment_dir = os.path.join(self.train_dir, self.experiment_name)
+        self.nn_dir = os.path.join(self.experiment_dir, "nn")
+        self.obs = None
+        self._step_counter = 0
+        self.algo_observer.after_init(self)
+
+    # ------------------------------------------------------------ buffers
+    def _alloc(self):
+        dev = self.ppo_device
+        f32, f64 = dict(device=dev, dtype=torch.float32), dict(device=dev, dtype=torch.float64)
+        N, H = self.num_actors, self.horizon_length
+        self.model_params = default_linear_init(self.seed).to(dev)
+        if self.multi_gpu:
+            dist.broadcast(self.model_params, 0)     # a2c_common.py:1354 (initial weights from rank 0)
+        self.adam_m = torch.zeros(NPARAM, **f32)
+        self.adam_v = torch.zeros(NPARAM, **f32)
+        self.opt = torch.zeros(8, **f32)
+        self.opt[0] = self.last_lr
+        self.obs_rms = torch.zeros(2 * NIN + 1, **f64)
+        self.obs_rms[NIN:2 * NIN] = 1.0
+        self.obs_rms[2 * NIN] = 1.0
+        self.val_rms = torch.tensor([0.0, 1.0, 1.0], **f64)
+        self.grad = torch.zeros(NPARAM + 8, **f32)
+        self.losses = torch.zeros(8, **f32)
+        self.partials = torch.zeros(_capi.lib().ppo_partials_floats(self.minibatch_size), **f32)
+        self.work = torch.zeros(8 + 8 * 4096 + N // 2 + 64, **f64)
+        B = N * H
+        self.exp_obs = torch.zeros((B, NIN), **f32)
+        self.exp_act = torch.zeros((B, NA), **f32)
+        self.exp_nlp = torch.zeros(B, **f32)
+        self.exp_val = torch.zeros(B, **f32)
+        self.exp_ret = torch.zeros(B, **f32)
+        self.exp_adv = torch.zeros(B, **f32)
+        self.exp_rew = torch.zeros(B, **f32)
+        self.exp_mu = torch.zeros((B, NA), **f32)
+        self.exp_sigma = torch.zeros((B, NA), **f32)
+        self.exp_done = torch.zeros(B, device=dev, dtype=torch.uint8)
+        self.actions = torch.zeros((N, NA), **f32)
+        self.dones = torch.ones(N, device=dev, dtype=torch.int64)
+        self.cur_rew = torch.zeros(N, **f32)
+        self.cur_shaped = torch.zeros(N, **f32)
+        self.cur_len = torch.zeros(N, **f32)
+        self.meter = torch.zeros((H, 4), **f32)
+        self.kls = torch.zeros(self.mini_epochs_num * self.num_minibatches, **f32)
+        self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 4), **f32)
+
+    # ------------------------------------------------------------- rollout
+    def env_reset(self):
+        obs = self.vec_env.reset()
+        return obs
+
+    def play_steps(self) -> Dict[str, Any]:
+        """A2CBase.play_steps (a2c_common.py:670-774): H x (policy kernel, env kernels, reward kernel)."""
+        c = _capi
+        cfg = c.byref(self.cfg)
+        s = c.stream_ptr()
+        self.meter.zero_()
+        step_time = 0.0
+        for n in range(self.horizon_length):
+            obs = self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"]
+            c.call("ppo_policy_step", cfg, c.ptr(self.model_params), c.ptr(self.obs_rms), c.ptr(self.val_rms),
+                   c.ptr(obs), n, c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp),
+                   c.ptr(self.exp_val), c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.exp_done),
+                   c.ptr(self.dones), c.ptr(self.actions), self.seed + 7919 * self.rank, self._step_counter,
+                   None, s)
+            t0 = time.time()
+            self.obs, rewards, self.dones, infos = self.vec_env.step(self.actions)
+            step_time += time.time() - t0
+            c.call("ppo_store_reward", cfg, c.ptr(rewards), c.ptr(self.dones), n, c.ptr(self.exp_rew),
+                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter), s)
+            self.algo_observer.process_infos(infos, None)
+            self._step_counter += 1
+        return {"played_frames": self.batch_size, "step_time": step_time}
+
+    def prepare_dataset(self) -> None:
+        """GAE + returns + value RMS + advantage normalisation (a2c_common.py:525-540, 1257-1332)."""
+        c = _capi
+        obs = self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"]
+        c.call("ppo_prepare", c.byref(self.cfg), c.ptr(self.model_params), c.ptr(self.obs_rms),
+               c.ptr(self.val_rms), c.ptr(obs), c.ptr(self.dones), c.ptr(self.exp_done), c.ptr(self.exp_val),
+               c.ptr(self.exp_rew), c.ptr(self.exp_ret), c.ptr(self.exp_adv), c.ptr(self.work), c.stream_ptr())
+
+    def _allreduce_grad(self) -> float:
+        """trancate_gradients_and_step multi-GPU branch (a2c_common.py:309-323): flat SUM / world,
+        with the minibatch KL in the same buffer (a2c_common.py:1218-1222)."""
+        if not self.multi_gpu or self.rank_size == 1:
+            return 1.0
+        dist.all_reduce(self.grad[:NPARAM + 1], op=dist.ReduceOp.SUM)
+        return 1.0 / self.rank_size
+
+    def update_epoch_minibatches(self) -> None:
+        c = _capi
+        cfg = c.byref(self.cfg)
+        s = c.stream_ptr()
+        k = 0
+        for mini_ep in range(self.mini_epochs_num):
+            for i in range(self.num_minibatches):
+                c.call("ppo_minibatch_grad", cfg, c.ptr(self.model_params), c.ptr(self.obs_rms),
+                       c.ptr(self.val_rms), int(mini_ep == 0), i, c.ptr(self.exp_obs), c.ptr(self.exp_act),
+                       c.ptr(self.exp_nlp), c.ptr(self.exp_val), c.ptr(self.exp_ret), c.ptr(self.exp_adv),
+                       c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.grad), c.ptr(self.losses),
+                       c.ptr(self.partials), c.ptr(self.work), s)
+                scale = self._allreduce_grad()
+                c.call("ppo_minibatch_apply", cfg, c.ptr(self.model_params), c.ptr(self.grad), c.ptr(self.adam_m),
+                       c.ptr(self.adam_v), c.ptr(self.opt), float(scale), s)
+                self.kls[k:k + 1].copy_(self.opt[2:3])
+                self.loss_log[k].copy_(self.losses[:4])
+                k += 1
+
+    def train_epoch(self):
+        """ContinuousA2CBase.train_epoch (a2c_common.py:1152-1255)."""
+        self.vec_env.set_train_info(self.frame, self)
+        play_time_start = time.time()
+        batch = self.play_steps()
+        play_time_end = time.time()
+        self.curr_frames = batch["played_frames"]
+        self.prepare_dataset()
+        self.algo_observer.after_steps()
+        self.update_epoch_minibatches()
+        torch.cuda.current_stream().synchronize()
+        update_time_end = time.time()
+        self._replay_meters()
+        self.last_lr = float(self.opt[0].item())
+        return (batch["step_time"], play_time_end - play_time_start, update_time_end - play_time_end,
+                update_time_end - play_time_start)
+
+    def _replay_meters(self):
+        m = self.meter.cpu().numpy()
+        for t in range(m.shape[0]):
+            cnt = int(round(m[t, 3]))
+            if cnt > 0:
+                self.game_rewards.update_stats(m[t, 0] / cnt, cnt)
+                self.game_shaped_rewards.update_stats(m[t, 1] / cnt, cnt)
+                self.game_lengths.update_stats(m[t, 2] / cnt, cnt)
+
+    def init_tensors(self):
+        pass
+
+    def train(self):
+        """ContinuousA2CBase.train (a2c_common.py:1334-1486) minus TensorBoard."""
+        self.init_tensors()
+        self.last_mean_rewards = -100500
+        start_time = time.time()
+        total_time = 0.0
+        self.obs = self.env_reset()
+        self.curr_frames = self.batch_size
+        while True:
+            epoch_num = self.update_epoch()
+            step_time, play_time, update_time, sum_time = self.train_epoch()
+            total_time += sum_time
+            frame = self.frame // self.rank_size
+            curr_frames = self.curr_frames * self.rank_size if self.multi_gpu else self.curr_frames
+            self.frame += curr_frames
+            should_exit = False
+            if self.rank == 0:
+                if self.print_stats:
+                    fps_step = curr_frames / max(step_time, 1e-9)
+                    fps_si = curr_frames / max(play_time, 1e-9)
+                    fps_total = curr_frames / max(sum_time, 1e-9)
+                    print(f"fps step: {fps_step:.0f} fps step and policy inference: {fps_si:.0f} fps total: "
+                          f"{fps_total:.0f} epoch: {epoch_num}/{self.max_epochs} frames: {self.frame}")
+                if self.game_rewards.current_size > 0:
+                    mean_rewards = self.game_rewards.get_mean()
+                    self.mean_rewards = mean_rewards
+                    checkpoint_name = self.config["name"] + "_ep_" + str(epoch_num) + "_rew_" + str(mean_rewards)
+                    if self.save_freq > 0 and epoch_num % self.save_freq == 0:
+                        self.save(os.path.join(self.nn_dir, "last_" + checkpoint_name))
+                    if mean_rewards > self.last_mean_rewards and epoch_num >= self.save_best_after:
+                        print("saving next best rewards: ", mean_rewards)
+                        self.last_mean_rewards = mean_rewards
+                        self.save(os.path.join(self.nn_dir, self.config["name"]))
+                        if self.last_mean_rewards > self.score_to_win:
+                            print("Maximum reward achieved. Network won!")
+                            should_exit = True
+                if epoch_num >= self.max_epochs and self.max_epochs != -1:
+                    mean_rewards = self.game_rewards.get_mean() if self.game_rewards.current_size else -np.inf
+                    self.save(os.path.join(self.nn_dir, "last_" + self.config["name"] + "_ep_" + str(epoch_num) +
+                                           "_rew_" + str(mean_rewards)))
+                    print("MAX EPOCHS NUM!")
+                    should_exit = True
+                if self.frame >= self.max_frames and self.max_frames != -1:
+                    should_exit = True
+            if self.multi_gpu:
+                t = torch.tensor([float(should_exit)], device=self.ppo_device)
+                dist.broadcast(t, 0)
+                should_exit = bool(t.item())
+            if should_exit:
+                return self.last_mean_rewards, epoch_num
+
+    def update_epoch(self):
+        self.epoch_num += 1
+        return self.epoch_num
+
+    # ----------------------------------------------------------- checkpoints
+    def get_full_state_weights(self) -> Dict[str, Any]:
+        step = float(self.opt[1].item())
+        return {"model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms),
+                "epoch": self.epoch_num,
+                "optimizer": ckpt.optimizer_state_dict(self.adam_m, self.adam_v, step, float(self.opt[0].item()),
+                                                       self.cfg.weight_decay),
+                "frame": self.frame,
+                "last_mean_rewards": self.last_mean_rewards,
+                "env_state": self.vec_env.get_env_state() if self.vec_env is not None else None}
+
+    def set_full_state_weights(self, weights: Dict[str, Any]) -> None:
+        ckpt.load_model_state_dict(weights["model"], self.model_params, self.obs_rms, self.val_rms)
+        self.epoch_num = int(weights["epoch"])
+        step, lr = ckpt.load_optimizer_state_dict(weights["optimizer"], self.adam_m, self.adam_v)
+        self.opt[1] = step
+        self.opt[0] = lr
+        self.last_lr = lr
+        self.frame = int(weights.get("frame", 0))
+        self.last_mean_rewards = weights.get("last_mean_rewards", -100500)
+        if self.vec_env is not None:
+            self.vec_env.set_env_state(weights.get("env_state", None))
+
+    def save(self, fn: str) -> None:
+        ckpt.save_checkpoint(fn, self.get_full_state_weights())
+
+    def restore(self, fn: str) -> None:
+        self.set_full_state_weights(ckpt.load_checkpoint(fn))
+
+    def get_weights(self):
+        return {"model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms)}
+
+    def set_weights(self, weights):
+        ckpt.load_model_state_dict(weights["model"], self.model_params, self.obs_rms, self.val_rms)

@@ -1,0 +1,143 @@
+"""rl_games checkpoint layout (a2c_common.py:590-621, torch_ext.py:54-84).
+
+{'model': state_dict, 'epoch', 'optimizer', 'frame', 'last_mean_rewards',
+ 'env_state'} with the ModelA2CContinuousLogStd state_dict keys; the flat
+device parameter vector maps onto them in model.parameters() order.
+"""
+from __future__ import annotations
+
+import os
+import time
+from collections import OrderedDict
+from typing import Any, Dict
+
+import numpy as np
+import torch
+
+from .._abi import DEFINES
+
+NIN, NH, NA = DEFINES["PPO_NIN"], DEFINES["PPO_NH"], DEFINES["PPO_NA"]
+# (state_dict key, shape) in model.parameters() order (network_builder.py:1480-1575)
+PARAM_LAYOUT = [
+    ("a2c_network.sigma", (NA,)),
+    ("a2c_network.actor_mlp.0.weight", (NH, NIN)),
+    ("a2c_network.actor_mlp.0.bias", (NH,)),
+    ("a2c_network.actor_mlp.2.weight", (NH, NH)),
+    ("a2c_network.actor_mlp.2.bias", (NH,)),
+    ("a2c_network.value.weight", (1, NH)),
+    ("a2c_network.value.bias", (1,)),
+    ("a2c_network.mu.weight", (NA, NH)),
+    ("a2c_network.mu.bias", (NA,)),
+]
+NPARAM = sum(int(np.prod(s)) for _, s in PARAM_LAYOUT)
+assert NPARAM == DEFINES["PPO_NPARAM"]
+
+
+def split_flat(flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+    out, o = OrderedDict(), 0
+    for k, s in PARAM_LAYOUT:
+        m = int(np.prod(s))
+        out[k] = flat[o:o + m].view(*s)
+        o += m
+    return out
+
+
+def model_state_dict(params: torch.Tensor, obs_rms: torch.Tensor, val_rms: torch.Tensor) -> "OrderedDict":
+    """ModelA2CContinuousLogStd.state_dict() key order: value_mean_std, running_mean_std, a2c_network."""
+    sd = OrderedDict()
+    v = val_rms.detach().cpu()
+    o = obs_rms.detach().cpu()
+    sd["value_mean_std.running_mean"] = v[0:1].clone()
+    sd["value_mean_std.running_var"] = v[1:2].clone()
+    sd["value_mean_std.count"] = v[2].clone()
+    sd["running_mean_std.running_mean_std.state.running_mean"] = o[0:NIN].clone()
+    sd["running_mean_std.running_mean_std.state.running_var"] = o[NIN:2 * NIN].clone()
+    sd["running_mean_std.running_mean_std.state.count"] = o[2 * NIN].clone()
+    for k, t in split_flat(params.detach().cpu()).items():
+        sd[k] = t.clone()
+    return sd
+
+
+def load_model_state_dict(sd: Dict[str, torch.Tensor], params: torch.Tensor, obs_rms: torch.Tensor,
+                          val_rms: torch.Tensor) -> None:
+    for k, s in PARAM_LAYOUT:
+        if tuple(sd[k].shape) != tuple(s):
+            raise ValueError(f"checkpoint tensor {k} has shape {tuple(sd[k].shape)}, expected {s}")
+    flat = torch.cat([sd[k].reshape(-1).to(torch.float32) for k, _ in PARAM_LAYOUT])
+    params.copy_(flat.to(params.device))
+    o = torch.cat([sd["running_mean_std.running_mean_std.state.running_mean"].double(),
+                   sd["running_mean_std.running_mean_std.state.running_var"].double(),
+                   sd["running_mean_std.running_mean_std.state.count"].double().reshape(1)])
+    obs_rms[:o.numel()].copy_(o.to(obs_rms.device))
+    v = torch.cat([sd["value_mean_std.running_mean"].double(), sd["value_mean_std.running_var"].double(),
+                   sd["value_mean_std.count"].double().reshape(1)])
+    val_rms[:3].copy_(v.to(val_rms.device))
+
+
+def optimizer_state_dict(adam_m: torch.Tensor, adam_v: torch.Tensor, step: float, lr: float,
+                         weight_decay: float = 0.0) -> Dict[str, Any]:
+    """torch.optim.Adam.state_dict() layout (one param group, params 0..8)."""
+    m = split_flat(adam_m.detach().cpu())
+    v = split_flat(adam_v.detach().cpu())
+    state = {}
+    for i, (k, _) in enumerate(PARAM_LAYOUT):
+        state[i] = {"step": torch.tensor(float(step)), "exp_avg": m[k].clone(), "exp_avg_sq": v[k].clone()}
+    group = {"lr": float(lr), "betas": (0.9, 0.999), "eps": 1e-08, "weight_decay": float(weight_decay),
+             "amsgrad": False, "maximize": False, "foreach": None, "capturable": False, "differentiable": False,
+             "fused": None, "params": list(range(len(PARAM_LAYOUT)))}
+    return {"state": state, "param_groups": [group]}
+
+
+def load_optimizer_state_dict(osd: Dict[str, Any], adam_m: torch.Tensor, adam_v: torch.Tensor):
+    ms, vs, step = [], [], 0.0
+    for i, (k, s) in enumerate(PARAM_LAYOUT):
+        st = osd["state"].get(i)
+        if st is None:
+            ms.append(torch.zeros(int(np.prod(s))))
+            vs.append(torch.zeros(int(np.prod(s))))
+            continue
+        ms.append(st["exp_avg"].reshape(-1).float())
+        vs.append(st["exp_avg_sq"].reshape(-1).float())
+        step = float(st["step"])
+    adam_m.copy_(torch.cat(ms).to(adam_m.device))
+    adam_v.copy_(torch.cat(vs).to(adam_v.device))
+    return step, float(osd["param_groups"][0]["lr"])
+
+
+def safe_filesystem_op(func, *args, **kwargs):
+    """torch_ext.safe_filesystem_op: 5 attempts with exponential back-off (torch_ext.py:54-69)."""
+    for attempt in range(5):
+        try:
+            return func(*args, **kwargs)
+        except Exception as exc:  # noqa: BLE001 -- mirror the reference's retry-on-anything
+            print(f"Exception {exc} when trying to execute {func}; retrying in {2 ** attempt}s")
+            time.sleep(2 ** attempt)
+    raise RuntimeError(f"Could not execute {func}, give up after 5 attempts...")
+
+
+def save_checkpoint(filename: str, state: Dict[str, Any]) -> None:
+    print(f"=> saving checkpoint '{filename}.pth'")
+    d = os.path.dirname(filename)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    safe_filesystem_op(torch.save, state, filename + ".pth")
+
+
+def _allow_numpy_globals():
+    import codecs
+    allow = [np.dtype, codecs.encode]
+    try:
+        allow.append((np._core.multiarray.scalar, "numpy.core.multiarray.scalar"))
+    except AttributeError:  # numpy < 2
+        allow.append(np.core.multiarray.scalar)
+    for name in ("Float64DType", "Float32DType", "Int64DType"):
+        if hasattr(np, "dtypes") and hasattr(np.dtypes, name):
+            allow.append(getattr(np.dtypes, name))
+    torch.serialization.add_safe_globals(allow)
+
+
+def load_checkpoint(filename: str) -> Dict[str, Any]:
+    """Loads with weights_only=True (never unpickles arbitrary objects)."""
+    print(f"=> loading checkpoint '{filename}'")
+    _allow_numpy_globals()
+    return safe_filesystem_op(torch.load, filename, map_location="cpu", weights_only=True)

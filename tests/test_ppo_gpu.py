@@ -1,0 +1,199 @@
+"""HIP PPO kernels (via A2CAgent + the C ABI) vs the reference rl_games fixture
+(tests/golden/ppo_epoch.npz) and the numpy oracle (oracle/ppo_oracle.py)."""
+import copy
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import ppo_oracle as PO
+from tests.test_ppo_oracle import _params
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+class FakeVecEnv:
+    def __init__(self, n):
+        from omniisaacgymenvs_loop_amd.utils.spaces import Box, DictSpace
+        self.n = n
+        self.info = {"action_space": Box(np.array([-1, -1], np.float32), np.array([1, 1], np.float32)),
+                     "observation_space": DictSpace({"state": Box(-np.inf, np.inf, (33,))})}
+
+    def get_env_info(self):
+        return self.info
+
+    def set_train_info(self, *a, **k):
+        pass
+
+    def get_env_state(self):
+        return None
+
+    def set_env_state(self, s):
+        pass
+
+
+def _agent(n, minibatch, mini_epochs=8):
+    import yaml
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
+    with open(os.path.join(ROOT, "omniisaacgymenvs_loop_amd/cfg/train/USV/USV_PPOcontinuous_MLP.yaml")) as f:
+        params = yaml.safe_load(f)["params"]
+    params["config"].update(num_actors=n, minibatch_size=minibatch, mini_epochs=mini_epochs, device=DEV,
+                            vec_env=FakeVecEnv(n), train_dir="/tmp/ppo_gpu_runs")
+    return A2CAgent("run", params)
+
+
+def _flat_params(P):
+    return torch.tensor(PO.flatten(P), device=DEV)
+
+
+def _swap(a):  # [H, N, ...] -> [N*H, ...] (swap_and_flatten01)
+    return np.ascontiguousarray(np.swapaxes(a, 0, 1).reshape(a.shape[0] * a.shape[1], *a.shape[2:]))
+
+
+@pytest.fixture(scope="module")
+def ppo(golden):
+    return golden("ppo_epoch.npz")
+
+
+def test_policy_kernel_vs_reference_rollout(ppo):
+    from omniisaacgymenvs_loop_amd import _capi as c
+    H, N = ppo["exp_rewards"].shape[:2]
+    ag = _agent(N, 128)
+    ag.model_params.copy_(_flat_params(_params(ppo, "init")))
+    for t in range(H):
+        obs = torch.tensor(ppo["env_obs"][t], device=DEV)
+        eps = (ppo["exp_actions"][t] - ppo["exp_mus"][t]) / ppo["exp_sigmas"][t]
+        dones_prev = torch.tensor(ppo["exp_dones"][t].astype(np.int64), device=DEV)
+        c.call("ppo_policy_step", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
+               c.ptr(obs), t, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp), c.ptr(ag.exp_val),
+               c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.exp_done), c.ptr(dones_prev), c.ptr(ag.actions),
+               1, t, c.ptr(torch.tensor(eps, device=DEV)), c.stream_ptr())
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(ag.actions.cpu().numpy(), np.clip(ppo["exp_actions"][t], -1, 1), atol=2e-6)
+    rows = lambda x: x.cpu().numpy()
+    np.testing.assert_array_equal(rows(ag.exp_obs), _swap(ppo["exp_obses"]))
+    np.testing.assert_allclose(rows(ag.exp_mu), _swap(ppo["exp_mus"]), rtol=1e-5, atol=2e-6)
+    np.testing.assert_allclose(rows(ag.exp_sigma), _swap(ppo["exp_sigmas"]), rtol=1e-6)
+    np.testing.assert_allclose(rows(ag.exp_val), _swap(ppo["exp_values"])[:, 0], rtol=1e-5, atol=2e-6)
+    np.testing.assert_allclose(rows(ag.exp_nlp), _swap(ppo["exp_neglogpacs"]), rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(rows(ag.exp_done), _swap(ppo["exp_dones"]))
+
+
+def _load_rollout(ag, ppo):
+    H, N = ppo["exp_rewards"].shape[:2]
+    T = lambda a, **k: torch.tensor(np.ascontiguousarray(a), device=DEV, **k)
+    ag.exp_val.copy_(T(_swap(ppo["exp_values"])[:, 0]))
+    ag.exp_rew.copy_(T(_swap(ppo["exp_rewards"])[:, 0]))
+    ag.exp_done.copy_(T(_swap(ppo["exp_dones"])))
+    ag.obs = {"obs": {"state": T(ppo["env_obs"][H])}}
+    ag.dones = T(ppo["env_dones"][H - 1].astype(np.int64))
+
+
+def test_prepare_kernel_vs_reference(ppo):
+    H, N = ppo["exp_rewards"].shape[:2]
+    ag = _agent(N, 128)
+    ag.model_params.copy_(_flat_params(_params(ppo, "init")))
+    _load_rollout(ag, ppo)
+    ag.prepare_dataset()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(ag.exp_val.cpu().numpy(), ppo["ds_old_values"][:, 0], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(ag.exp_ret.cpu().numpy(), ppo["ds_returns"][:, 0], rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(ag.exp_adv.cpu().numpy(), ppo["ds_advantages"], rtol=1e-4, atol=2e-5)
+    vr = ag.val_rms.cpu().numpy()
+    np.testing.assert_allclose(vr[0], ppo["final_value_mean_std__running_mean"][0], rtol=1e-6)
+    np.testing.assert_allclose(vr[1], ppo["final_value_mean_std__running_var"][0], rtol=1e-6)
+    assert vr[2] == float(ppo["final_value_mean_std__count"])
+
+
+def test_minibatch_epoch_vs_reference(ppo):
+    """32 optimizer steps: per-minibatch KL / losses, adaptive LR, obs RMS and final weights."""
+    H, N = ppo["exp_rewards"].shape[:2]
+    ag = _agent(N, int(ppo["hyper"][2]))
+    ag.model_params.copy_(_flat_params(_params(ppo, "init")))
+    T = lambda a: torch.tensor(np.ascontiguousarray(a), device=DEV)
+    ag.exp_obs.copy_(T(ppo["ds_obs_state"]))
+    ag.exp_act.copy_(T(ppo["ds_actions"]))
+    ag.exp_nlp.copy_(T(ppo["ds_old_logp_actions"]))
+    ag.exp_val.copy_(T(ppo["ds_old_values"][:, 0]))
+    ag.exp_ret.copy_(T(ppo["ds_returns"][:, 0]))
+    ag.exp_adv.copy_(T(ppo["ds_advantages"]))
+    ag.exp_mu.copy_(T(ppo["batch_mus"]))
+    ag.exp_sigma.copy_(T(ppo["batch_sigmas"]))
+    ag.update_epoch_minibatches()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(ag.kls.cpu().numpy(), ppo["kl"], rtol=3e-3, atol=1e-7)
+    np.testing.assert_allclose(ag.loss_log.cpu().numpy(), ppo["losses"], rtol=3e-3, atol=1e-6)
+    np.testing.assert_allclose(float(ag.opt[0]), ppo["lr_seq"][-1], rtol=1e-6)
+    orms = ag.obs_rms.cpu().numpy()
+    np.testing.assert_allclose(orms[:33], ppo["final_running_mean_std__running_mean_std__state__running_mean"],
+                               rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(orms[33:66], ppo["final_running_mean_std__running_mean_std__state__running_var"],
+                               rtol=1e-6)
+    Pf = PO.unflatten(ag.model_params.cpu().numpy())
+    for k, v in _params(ppo, "final").items():
+        np.testing.assert_allclose(Pf[k], v, rtol=0, atol=5e-5, err_msg=k)
+
+
+def test_minibatch_gradient_vs_oracle_full_size():
+    """One 8192-row minibatch (BASELINE minibatch_size) vs the numpy oracle's gradient."""
+    N, H = 512, 16
+    ag = _agent(N, 8192, mini_epochs=1)
+    rng = np.random.default_rng(0)
+    B = N * H
+    obs = rng.normal(0, 2, (B, 33)).astype(np.float32)
+    act = rng.normal(0, 1, (B, 2)).astype(np.float32)
+    P = PO.unflatten(ag.model_params.cpu().numpy())
+    xn = PO.RMS.zeros(33)
+    xn.update(obs)
+    _, _, mu0, _ = PO.forward(P, xn.norm(obs))
+    sig0 = np.ones_like(mu0)
+    nlp0 = PO.neglogp(act, mu0, sig0, np.zeros_like(mu0)) + rng.normal(0, 0.05, B).astype(np.float32)
+    val = rng.normal(0, 1, B).astype(np.float32)
+    ret = (val + rng.normal(0, 0.5, B)).astype(np.float32)
+    adv = rng.normal(0, 1, B).astype(np.float32)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a), device=DEV)
+    for name, arr in (("exp_obs", obs), ("exp_act", act), ("exp_nlp", nlp0), ("exp_val", val), ("exp_ret", ret),
+                      ("exp_adv", adv), ("exp_mu", mu0 + 0.01), ("exp_sigma", sig0)):
+        getattr(ag, name).copy_(T(arr))
+    from omniisaacgymenvs_loop_amd import _capi as c
+    c.call("ppo_minibatch_grad", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms), 1,
+           0, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp), c.ptr(ag.exp_val), c.ptr(ag.exp_ret),
+           c.ptr(ag.exp_adv), c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.grad), c.ptr(ag.losses),
+           c.ptr(ag.partials), c.ptr(ag.work), c.stream_ptr())
+    torch.cuda.synchronize()
+    orms = PO.RMS.zeros(33)
+    orms.update(obs)
+    np.testing.assert_allclose(ag.obs_rms.cpu().numpy()[:33], orms.mean, rtol=1e-6, atol=1e-9)
+    g_ref, losses, kl, _, _ = PO.minibatch_grad(P, orms.norm(obs), act, nlp0, val, ret, adv, mu0 + 0.01, sig0,
+                                                PO.PPOConfig(minibatch=8192))
+    g = ag.grad.cpu().numpy()[:PO.NPARAM]
+    scale = np.abs(g_ref).max()
+    np.testing.assert_allclose(g, g_ref, rtol=0, atol=2e-4 * scale)
+    np.testing.assert_allclose(ag.losses.cpu().numpy()[:4], losses, rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(float(ag.grad[PO.NPARAM]), kl, rtol=1e-3, atol=1e-8)
+
+
+def test_checkpoint_roundtrip(tmp_path):
+    from omniisaacgymenvs_loop_amd.rl_games import checkpoint as ck
+    ag = _agent(64, 128)
+    ag.model_params.add_(0.25)
+    ag.obs_rms[:33] = 3.0
+    ag.epoch_num, ag.frame = 7, 1024
+    ag.save(str(tmp_path / "ck"))
+    sd = torch.load(str(tmp_path / "ck.pth"), weights_only=True)
+    assert list(sd.keys()) == ["model", "epoch", "optimizer", "frame", "last_mean_rewards", "env_state"]
+    assert list(sd["model"].keys())[:6] == ["value_mean_std.running_mean", "value_mean_std.running_var",
+                                            "value_mean_std.count",
+                                            "running_mean_std.running_mean_std.state.running_mean",
+                                            "running_mean_std.running_mean_std.state.running_var",
+                                            "running_mean_std.running_mean_std.state.count"]
+    assert sd["model"]["a2c_network.actor_mlp.2.weight"].shape == (128, 128)
+    ag2 = _agent(64, 128)
+    ag2.restore(str(tmp_path / "ck.pth"))
+    assert torch.equal(ag2.model_params, ag.model_params)
+    assert torch.equal(ag2.obs_rms, ag.obs_rms)
+    assert ag2.epoch_num == 7 and ag2.frame == 1024
