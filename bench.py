@@ -1,0 +1,283 @@
+"""Benchmark: env-steps/s of rl_games PPO training on USV_Virtual_CaptureXY.
+
+One bench "step" = one rl_games train epoch: horizon_length=16 control steps of
+num_envs envs (each = reset path + 10 physics substeps + obs/reward/done, on the
+GPU) interleaved with the policy forward, then GAE + dataset preparation and
+8 mini-epochs of PPO minibatch updates (fwd + bwd + clip + Adam), i.e. the
+reference's "fps total" (rl_games a2c_common.py:46-60).  Workload:
+BASELINE.json configs[1] = USV_Virtual_CaptureXY num_envs=4096 PPO-MLP fp32 per
+GPU; with --gpus N each rank owns 4096 envs (weak scaling) and gradients are
+all-reduced over RCCL every minibatch.
+
+    python bench.py [--gpus N --steps K --warmup W --envs 4096]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env-steps/sec USV_CaptureXY at 1/2/4/8 MI355X; wall-clock to reward=30"
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+FP32_PEAK_TFS = 157.3          # MI355X fp32 vector / f32-MFMA peak (same table)
+# Algorithmic bytes of the fused env-step kernel per env-step:
+# SURVEY §8(d) fused figure (476 B: state, lag, DR params, target, obstacles,
+# reward history, 4 field texels, obs row, reward, done) + the episode_sums
+# read-modify-write the reference performs every step (25 x 8 B) - counted
+# exactly from k_env_step's loads/stores: 357 B read + 313 B written.
+ENV_STEP_BYTES = 670
+# PPO minibatch gradient kernel: forward (2*(33*128+128*128+128*3)) + backward
+# (2x the two hidden GEMMs + heads) = 6 x 21,120 + 2 x 384 flops per row.
+PPO_FLOPS_PER_ROW = 2 * (33 * 128 + 128 * 128 + 3 * 128) + 2 * (2 * 128 * 128 + 2 * 33 * 128 + 128 * 128 + 3 * 128)
+
+
+def _dist_setup(gpus):
+    import torch
+    import torch.distributed as dist
+    rank = int(os.getenv("RANK", "0"))
+    world = int(os.getenv("WORLD_SIZE", "1"))
+    local = int(os.getenv("LOCAL_RANK", "0"))
+    if world != gpus:
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    return rank, world, local
+
+
+def build(envs, local, world, seed):
+    from omniisaacgymenvs_loop_amd.envs.vec_env_rlgames import VecEnvRLGames
+    from omniisaacgymenvs_loop_amd.rl_games import vecenv
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
+    from omniisaacgymenvs_loop_amd.scripts.rlgames_train import build_config
+    from omniisaacgymenvs_loop_amd.utils.task_util import initialize_task
+    cfg = build_config({"num_envs": envs, "seed": seed, "multi_gpu": world > 1, "rl_device": f"cuda:{local}"})
+    cfg["train"]["params"]["config"]["train_dir"] = "/tmp/bench_runs"
+    env = VecEnvRLGames(headless=True)
+    task = initialize_task(cfg, env)
+    vecenv.register("RLGPU", lambda name, n, **kw: vecenv.RLGPUEnv(name, n, **kw))
+    vecenv.register_env("rlgpu", {"vecenv_type": "RLGPU", "env_creator": lambda **kw: env})
+    params = cfg["train"]["params"]
+    params["config"]["print_stats"] = False
+    agent = A2CAgent("run", params)
+    return env, task, agent
+
+
+class KernelTimer:
+    """HIP events around one C-ABI launch on torch's current stream (the launch stream)."""
+
+    def __init__(self):
+        self.pairs = []
+
+    def __call__(self, fn):
+        import torch
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        self.pairs.append((a, b))
+
+    def mean_ms(self):
+        if not self.pairs:
+            return float("nan")
+        return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
+
+
+def cpu_baseline(envs=256, budget_s=12.0):
+    """The oracle (C env restatement + numpy PPO) timed on one host core, on a
+    bounded sample of the same workload: repeated train epochs of envs x 16
+    control steps (incl. episode resets + potential fields) + 8 mini-epochs of
+    PPO on that epoch's batch, until ~budget_s of CPU time has been spent."""
+    import numpy as np
+    from threadpoolctl import threadpool_limits
+    from oracle import oracle as O
+    from oracle import ppo_oracle as PO
+    from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg, load_yaml, thruster_tables
+    yaml_path = os.path.join(ROOT, "omniisaacgymenvs_loop_amd/cfg/task/USV/IROS2024/USV_Virtual_CaptureXY_SysID-TEST.yaml")
+    task_cfg = load_yaml(yaml_path)
+    cfg = build_usv_cfg(task_cfg)
+    H = 16
+    sw = lambda x: np.ascontiguousarray(np.swapaxes(np.stack(x), 0, 1).reshape(envs * H, *np.stack(x).shape[2:]))
+    with threadpool_limits(1):
+        E = O.OracleEnv(cfg, envs, O.make_lut(*thruster_tables(task_cfg)))
+        rng = np.random.default_rng(0)
+        P = PO.unflatten(np.random.default_rng(1).uniform(-0.08, 0.08, PO.NPARAM).astype(np.float32))
+        orms, adam, lr = PO.RMS.zeros(33), PO.Adam.zeros(), 1e-4
+        E.full_step(np.zeros((envs, 2), np.float32), -0.6, 0, seed=1)     # initial reset of every env: untimed
+        obs = E.obs.copy()
+        step, epochs = 1, 0
+        t0 = time.perf_counter()
+        while epochs < 2 or time.perf_counter() - t0 < budget_s:
+            obs_buf, act_buf, nlp_buf, val_buf, mu_buf = [], [], [], [], []
+            for _ in range(H):
+                _, _, mu, v = PO.forward(P, orms.norm(obs).astype(np.float32))
+                a = (mu + rng.standard_normal(mu.shape).astype(np.float32)).astype(np.float32)
+                obs_buf.append(obs.copy()); act_buf.append(a); val_buf.append(v[:, 0]); mu_buf.append(mu)
+                nlp_buf.append(PO.neglogp(a, mu, np.ones_like(mu), np.zeros_like(mu)))
+                E.full_step(np.clip(a, -1, 1), -0.6, step, seed=1)
+                obs = E.obs.copy()
+                step += 1
+            ds = {"obs": sw(obs_buf), "actions": sw(act_buf), "old_logp": sw(nlp_buf), "old_values": sw(val_buf),
+                  "returns": sw(val_buf) + 0.1, "advantages": rng.standard_normal(envs * H).astype(np.float32),
+                  "mu": sw(mu_buf), "sigma": np.ones((envs * H, 2), np.float32)}
+            P, lr, _ = PO.train_epoch_update(P, adam, lr, orms, ds, PO.PPOConfig(minibatch=envs * H))
+            epochs += 1
+        dt = time.perf_counter() - t0
+    return {"value": epochs * envs * H / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{epochs} train epochs of {envs} envs x {H} steps (C oracle env incl. episode resets + "
+                      f"potential fields; initial reset untimed) + 8 mini-epochs numpy PPO per epoch; "
+                      f"1 thread; {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (BASELINE configs[1]: 4096)")
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--env-only-envs", type=int, default=131072,
+                    help="extra env-only throughput probe at the C5 per-GPU size (0 = skip)")
+    args = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    rank, world, local = _dist_setup(args.gpus)
+    env, task, agent = build(args.envs, local, world, args.seed + rank)
+    from omniisaacgymenvs_loop_amd import _capi
+
+    # live per-launch timing of the fused env-step kernel and the PPO gradient kernel
+    env_timer, ppo_timer = KernelTimer(), KernelTimer()
+    orig_call = _capi.call
+
+    def timed_call(name, *a):
+        if timing[0] and name == "usv_env_step":
+            env_timer(lambda: orig_call(name, *a))
+        elif timing[0] and name == "ppo_minibatch_grad":
+            ppo_timer(lambda: orig_call(name, *a))
+        else:
+            orig_call(name, *a)
+
+    timing = [False]
+    _capi.call = timed_call
+
+    agent.obs = agent.env_reset()
+    for _ in range(args.warmup):
+        agent.train_epoch()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    timing[0] = True
+    t0 = time.perf_counter()
+    step_t = play_t = 0.0
+    for _ in range(args.steps):
+        st, pt, ut, tt = agent.train_epoch()
+        step_t += st
+        play_t += pt
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timing[0] = False
+    t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    frames = world * args.envs * agent.horizon_length * args.steps
+    value = frames / elapsed
+
+    # env + inference only (play_steps) and env only (VecEnv.step with fixed actions), same sizes
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(max(2, args.steps // 4)):
+        agent.play_steps()
+    torch.cuda.synchronize()
+    play_fps = args.envs * agent.horizon_length * max(2, args.steps // 4) / (time.perf_counter() - t1)
+    acts = torch.zeros((args.envs, 2), device=f"cuda:{local}")
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    nenv = 64
+    for _ in range(nenv):
+        env.step(acts)
+    torch.cuda.synchronize()
+    env_fps = args.envs * nenv / (time.perf_counter() - t1)
+
+    env_ms = env_timer.mean_ms()
+    ppo_ms = ppo_timer.mean_ms()
+    achieved = ENV_STEP_BYTES * args.envs / (env_ms * 1e-3) / 1e9
+    ppo_tfs = PPO_FLOPS_PER_ROW * agent.minibatch_size / (ppo_ms * 1e-3) / 1e12
+    extra = {}
+    if args.env_only_envs and rank == 0 and world == 1:
+        # C5 per-GPU size: env-only throughput and the env-step kernel roofline at scale
+        from omniisaacgymenvs_loop_amd.tasks.usv_virtual import USVVirtual
+        big = USVVirtual(task._task_cfg, num_envs=args.env_only_envs, device=f"cuda:{local}", seed=5)
+        a = torch.rand((args.env_only_envs, 2), device=f"cuda:{local}") * 2 - 1
+        for _ in range(3):
+            big.env_step(a)
+        big_timer = KernelTimer()
+        timing_big = []
+
+        def big_call(name, *aa):
+            if name == "usv_env_step":
+                big_timer(lambda: orig_call(name, *aa))
+            else:
+                orig_call(name, *aa)
+
+        _capi.call = big_call
+        torch.cuda.synchronize()
+        tb = time.perf_counter()
+        nb = 32
+        for _ in range(nb):
+            big.env_step(a)
+        torch.cuda.synchronize()
+        tb = time.perf_counter() - tb
+        _capi.call = timed_call
+        bms = big_timer.mean_ms()
+        extra = {"env_only_envs": args.env_only_envs, "env_only_fps": args.env_only_envs * nb / tb,
+                 "env_step_kernel_ms": bms,
+                 "env_step_kernel_gbs": ENV_STEP_BYTES * args.env_only_envs / (bms * 1e-3) / 1e9}
+        del big
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init policy, "
+            "randomised spawns/obstacles/DR from the reset path)",
+            "config": {"workload": "USV_Virtual_CaptureXY num_envs=4096/GPU PPO-MLP fp32 (BASELINE configs[1])",
+                       "num_envs_per_gpu": args.envs, "horizon_length": agent.horizon_length,
+                       "minibatch_size": agent.minibatch_size, "mini_epochs": agent.mini_epochs_num,
+                       "parallelism": f"dp{world}"},
+            "fps_step_inference": play_fps, "fps_step_env_only": env_fps,
+            "roofline": {"bound": "hbm", "kernel": "k_env_step (fused 10-substep integrator + obs/reward/done)",
+                         "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": None, "bytes_per_env_step": ENV_STEP_BYTES, "launch_ms": env_ms,
+                         "envs_per_launch": args.envs},
+            "roofline_ppo": {"bound": "mfma", "kernel": "k_mb_grad (fp32 fwd+bwd, VALU)", "achieved": ppo_tfs,
+                             "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
+                             "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},
+            "extra": extra,
+        }
+        traffic_file = os.path.join(ROOT, "profiles", "env_step_traffic.json")
+        if os.path.exists(traffic_file):
+            with open(traffic_file) as f:
+                tr = json.load(f)
+            if tr.get("envs") == args.envs:
+                out["roofline"]["traffic"] = tr.get("bytes_per_launch")
+                out["roofline"]["traffic_source"] = tr.get("source")
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
