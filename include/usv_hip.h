@@ -195,7 +195,8 @@ typedef struct usv_bufs {
   float   *extras;                 /* [USV_NSTAT] extras["episode"] (persistent) */
   float   *extras_acc;             /* [USV_NSTAT] scratch sums */
   float   *field_old_tgt;          /* [2][n] target used by the field of each reset env */
-  float   *slot_stats;             /* [n][8] per-reset-slot field statistics (scratch) */
+  float   *slot_stats;             /* [n][16] per-reset-slot field statistics (scratch) */
+  float   *sdf;                    /* [n][150*150] per-reset-slot signed distance (scratch) */
   const float *grid_lin;           /* [150] cell centres of the field grid */
 } usv_bufs_t;
 
@@ -340,7 +341,12 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
  * Split in two so the flat gradient can be all-reduced in between:
  *   ppo_minibatch_grad  -> grad[PPO_NPARAM] (+ kl sum in grad[PPO_NPARAM])
  *   ppo_minibatch_apply -> clip + Adam + lr update.
- * opt: device floats [0]=lr [1]=step [2..]=reserved; m, v: [PPO_NPARAM]. */
+ * opt: device floats [0]=lr [1]=step [2]=last kl [3]=last grad norm [4..6]=reserved,
+ *      [7]=completion counter of the multi-workgroup Adam kernel (uint bits, keep 0);
+ * m, v: [PPO_NPARAM].  minibatch must be a multiple of 32 (workgroup row block).
+ * grad must be 16-byte aligned.  losses (nullable) receives the minibatch means
+ * (a_loss, c_loss, entropy, b_loss, kl) of this rank; kl_out (nullable) the KL
+ * the LR schedule used (after the all-reduce), as kls[] of the reference log. */
 int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rms,
                        const double *val_rms, int update_obs_rms, int mb_index,
                        const float *exp_obs, const float *exp_act, const float *exp_nlp,
@@ -348,7 +354,7 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        float *exp_mu, float *exp_sigma, float *grad, float *losses,
                        float *partials, double *work, void *stream);
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m,
-                        float *adam_v, float *opt, float grad_scale, void *stream);
+                        float *adam_v, float *opt, float grad_scale, float *kl_out, void *stream);
 
 /* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad */
 int ppo_partials_floats(int minibatch);

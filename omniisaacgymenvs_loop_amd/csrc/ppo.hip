@@ -11,46 +11,35 @@
 //   algos_torch/torch_ext.py:27-36          policy_kl
 //   common/datasets.py:25-29                update_mu_sigma
 //
-// Block forward/backward: 256 threads own 64 rows of the minibatch; thread
-// (j = tid % 128, rg = tid / 128) computes hidden unit j for 32 rows, with the
-// row activations broadcast from LDS and the weight rows streamed from L2.
-// Weight gradients are per-block partial sums (deterministic), reduced by
-// k_reduce_partials; clip + Adam + LR schedule run in one workgroup.
+// Block forward/backward (RB = 32 rows per 256-thread workgroup, 4 waves):
+// every 32x128 / 128x128 product runs on the f32 matrix cores
+// (v_mfma_f32_32x32x2_f32, an exact k-ordered fmaf chain, so the layer
+// outputs equal a sequential fmaf loop over k).  The weights are staged once
+// per workgroup into LDS (W2 with a 130-float row stride: conflict-free
+// operand reads for both the W2 and W2^T access patterns the forward and the
+// backward need), activations never leave LDS, and each workgroup writes one
+// deterministic partial gradient (param layout) that k_reduce_partials sums
+// in a fixed order.  clip + Adam + the adaptive LR run in k_apply.
 #include "usv_device.h"
 
 namespace {
 
 constexpr int NIN = PPO_NIN, NH = PPO_NH, NA = PPO_NA;
-constexpr int XP = 36;          // padded obs row in LDS
-constexpr int RB = 64;          // rows per block
-constexpr int TB = 256;         // threads per block
-constexpr int RG = 32;          // rows per thread (RB / 2)
-constexpr int NPART = PPO_NPARAM + 8;   // partial row: params (+ transposed blocks) + loss sums
+constexpr int RB = 32;          // rows per block
+constexpr int TB = 256;         // threads per block (4 waves; wave w owns output columns 32w..32w+31)
+constexpr int XS = 36;          // row stride of x / W1 in LDS (k 33..35 zero)
+constexpr int HS = 130;         // row stride of h1 / h2 / W2 in LDS
+constexpr int NPART = PPO_NPARAM + 8;   // partial row: params + loss sums
+constexpr int P_LOSS = PPO_NPARAM;      // a, c, entropy, b, kl sums
 constexpr float kLog2Pi = 1.8378770664093453f;  // 0.5*log(2*pi)*2 (models.py:400)
 
-// partial-row layout (W1 and W2 stored transposed for coalesced stores)
-constexpr int P_SIGMA = 0;
-constexpr int P_W1T = 2;                          // [33][128]
-constexpr int P_B1 = P_W1T + NIN * NH;
-constexpr int P_W2T = P_B1 + NH;                  // [128 k][128 j]
-constexpr int P_B2 = P_W2T + NH * NH;
-constexpr int P_WV = P_B2 + NH;
-constexpr int P_BV = P_WV + NH;
-constexpr int P_WMU = P_BV + 1;                   // [2][128] (same as params)
-constexpr int P_BMU = P_WMU + NA * NH;
-constexpr int P_LOSS = PPO_NPARAM;                // a, c, entropy, b, kl sums
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__device__ __forceinline__ int partial_to_param(int p) {
-  if (p >= P_W1T && p < P_B1) {
-    const int q = p - P_W1T, k = q / NH, j = q % NH;
-    return PPO_OFF_W1 + j * NIN + k;
-  }
-  if (p >= P_W2T && p < P_B2) {
-    const int q = p - P_W2T, k = q / NH, j = q % NH;
-    return PPO_OFF_W2 + j * NH + k;
-  }
-  return p;  // all other sections share the parameter layout
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
+// C/D layout of a 32x32 tile: lane l holds column l&31, rows (r&3) + 8(r>>2) + 4(l>>5), r = 0..15
+__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
 __device__ __forceinline__ float rms_norm(float x, double mean, double var, float eps) {
   // RunningMeanStd.forward (running_mean_std.py:113-118): fp32 math on fp64 stats
@@ -58,87 +47,114 @@ __device__ __forceinline__ float rms_norm(float x, double mean, double var, floa
   return clampt(y, -5.0f, 5.0f);
 }
 
-struct FwdSmem {
-  float x[RB * XP];       // normalised obs
-  float h1[RB * NH];      // tanh layer 1 (later dz1)
-  float h2[RB * NH];      // tanh layer 2 (later dz2)
-  float out[RB * 4];      // mu0, mu1, value, (spare)
+constexpr int TAIL = PPO_NPARAM - PPO_OFF_B2;     // b2, Wv, bv, Wmu, bmu (contiguous)
+constexpr int T_B2 = 0, T_WV = NH, T_BV = 2 * NH, T_WMU = 2 * NH + 1, T_BMU = 4 * NH + 1;
+
+struct MlpSmem {
+  float w2[NH * HS];      // W2[j][k]
+  float w1[NH * XS];      // W1[j][k], k 33..35 = 0
+  float x[RB * XS];       // normalised obs (later unchanged: dW1 operand)
+  float h1[RB * HS];      // tanh layer 1 (later dz1)
+  float h2[RB * HS];      // tanh layer 2 (later dz2)
+  float out[RB * 4];      // mu0, mu1, value
+  float g[RB * 4];        // dmu0, dmu1, dv, dnlp per row
+  float hg[2][4][NH];     // head-gradient / bias half sums
+  float b1[NH];
+  float tail[TAIL + 1];   // params from b2 on (T_* offsets)
 };
 
-// Forward of RB rows already staged (normalised) in s.x; rows >= nrows are 0.
-__device__ void block_forward(const float *__restrict__ P, FwdSmem &s) {
+// every load is issued before the first LDS store (the trip counts are compile-time)
+__device__ __forceinline__ void stage_weights(const float *__restrict__ P, MlpSmem &s) {
   const int tid = threadIdx.x;
-  const int j = tid % NH, r0 = (tid / NH) * RG;
-  // ---- layer 1: h1 = tanh(W1 x + b1) ----
-  {
-    float acc[RG];
-    const float bj = P[PPO_OFF_B1 + j];
+  constexpr int NW2 = NH * NH / 2 / TB, NW1 = NH * XS / TB, NTL = (TAIL + TB - 1) / TB;
+  static_assert(NH * NH / 2 % TB == 0 && NH * XS % TB == 0, "staging trip counts");
+  const float2 *W2 = reinterpret_cast<const float2 *>(P + PPO_OFF_W2);   // PPO_OFF_W2 is even
+  float2 w2r[NW2];
+  float w1r[NW1], tlr[NTL];
 #pragma unroll
-    for (int r = 0; r < RG; ++r) acc[r] = 0.f;
-    const float *w = P + PPO_OFF_W1 + j * NIN;
-    for (int k = 0; k < NIN; ++k) {
-      const float wk = w[k];
+  for (int u = 0; u < NW2; ++u) w2r[u] = W2[tid + u * TB];
 #pragma unroll
-      for (int r = 0; r < RG; ++r) acc[r] = fmaf(wk, s.x[(r0 + r) * XP + k], acc[r]);
-    }
-#pragma unroll
-    for (int r = 0; r < RG; ++r) s.h1[(r0 + r) * NH + j] = tanhf(acc[r] + bj);
+  for (int u = 0; u < NW1; ++u) {
+    const int i = tid + u * TB, j = i / XS, k = i % XS;
+    w1r[u] = k < NIN ? P[PPO_OFF_W1 + j * NIN + k] : 0.f;
   }
-  __syncthreads();
-  // ---- layer 2: h2 = tanh(W2 h1 + b2) ----
-  {
-    float acc[RG];
-    const float bj = P[PPO_OFF_B2 + j];
 #pragma unroll
-    for (int r = 0; r < RG; ++r) acc[r] = 0.f;
-    const float4 *w = reinterpret_cast<const float4 *>(P + PPO_OFF_W2 + j * NH);
-    for (int k4 = 0; k4 < NH / 4; ++k4) {
-      const float4 wk = w[k4];
+  for (int u = 0; u < NTL; ++u) tlr[u] = (tid + u * TB < TAIL) ? P[PPO_OFF_B2 + tid + u * TB] : 0.f;
+  const float b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
 #pragma unroll
-      for (int r = 0; r < RG; ++r) {
-        const float4 hv = *reinterpret_cast<const float4 *>(&s.h1[(r0 + r) * NH + 4 * k4]);
-        acc[r] = fmaf(wk.x, hv.x, acc[r]);
-        acc[r] = fmaf(wk.y, hv.y, acc[r]);
-        acc[r] = fmaf(wk.z, hv.z, acc[r]);
-        acc[r] = fmaf(wk.w, hv.w, acc[r]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < RG; ++r) s.h2[(r0 + r) * NH + j] = tanhf(acc[r] + bj);
+  for (int u = 0; u < NW2; ++u) {
+    const int i = tid + u * TB, j = i / (NH / 2), k2 = i % (NH / 2);
+    *reinterpret_cast<float2 *>(&s.w2[j * HS + 2 * k2]) = w2r[u];
   }
-  __syncthreads();
-  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (4 threads per row) ----
-  {
-    const int r = tid / 4, part = tid % 4;   // 64 rows x 4 lanes
-    float a0 = 0.f, a1 = 0.f, av = 0.f;
-    for (int k = part * 32; k < part * 32 + 32; ++k) {
-      const float h = s.h2[r * NH + k];
-      a0 = fmaf(P[PPO_OFF_WMU + k], h, a0);
-      a1 = fmaf(P[PPO_OFF_WMU + NH + k], h, a1);
-      av = fmaf(P[PPO_OFF_WV + k], h, av);
-    }
-    a0 += __shfl_xor(a0, 1, 64); a0 += __shfl_xor(a0, 2, 64);
-    a1 += __shfl_xor(a1, 1, 64); a1 += __shfl_xor(a1, 2, 64);
-    av += __shfl_xor(av, 1, 64); av += __shfl_xor(av, 2, 64);
-    if (part == 0) {
-      s.out[r * 4 + 0] = a0 + P[PPO_OFF_BMU];
-      s.out[r * 4 + 1] = a1 + P[PPO_OFF_BMU + 1];
-      s.out[r * 4 + 2] = av + P[PPO_OFF_BV];
-    }
-  }
-  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < NW1; ++u) s.w1[tid + u * TB] = w1r[u];
+#pragma unroll
+  for (int u = 0; u < NTL; ++u)
+    if (tid + u * TB < TAIL) s.tail[tid + u * TB] = tlr[u];
+  if (tid < NH) s.b1[tid] = b1r;
 }
 
 __device__ __forceinline__ void stage_obs(const float *__restrict__ obs, int row0, int nrows, const double *obs_rms,
-                                          bool normalize, float eps, FwdSmem &s) {
-  for (int i = threadIdx.x; i < RB * XP; i += TB) {
-    const int r = i / XP, k = i % XP;
+                                          bool normalize, float eps, MlpSmem &s) {
+  for (int i = threadIdx.x; i < RB * XS; i += TB) {
+    const int r = i / XS, k = i % XS;
     float v = 0.f;
     if (r < nrows && k < NIN) {
       v = obs[(size_t)(row0 + r) * NIN + k];
       if (normalize) v = rms_norm(v, obs_rms[k], obs_rms[NIN + k], eps);
     }
     s.x[i] = v;
+  }
+}
+
+// Forward of the RB rows staged in s.x (weights staged); leaves h1, h2, out.
+__device__ void block_forward(const float *__restrict__ P, MlpSmem &s) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
+  // ---- layer 1: h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero) ----
+  {
+    f32x16 acc = {};
+#pragma unroll
+    for (int st = 0; st < 17; ++st) {
+      const int k = 2 * st + h;
+      acc = mfma32(s.x[i * XS + k], s.w1[(n0 + i) * XS + k], acc);
+    }
+    const float bj = s.b1[n0 + i];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = tanhf(acc[r] + bj);
+  }
+  __syncthreads();
+  // ---- layer 2: h2 = tanh(h1 W2^T + b2) ----
+  {
+    f32x16 acc = {};
+#pragma unroll 16
+    for (int st = 0; st < NH / 2; ++st) {
+      const int k = 2 * st + h;
+      acc = mfma32(s.h1[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
+    }
+    const float bj = s.tail[T_B2 + n0 + i];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = tanhf(acc[r] + bj);
+  }
+  __syncthreads();
+  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (4 threads per row) ----
+  if (tid < RB * 4) {
+    const int r = tid / 4, part = tid % 4;
+    float a0 = 0.f, a1 = 0.f, av = 0.f;
+    for (int k = part * 32; k < part * 32 + 32; ++k) {
+      const float hv = s.h2[r * HS + k];
+      a0 = fmaf(s.tail[T_WMU + k], hv, a0);
+      a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
+      av = fmaf(s.tail[T_WV + k], hv, av);
+    }
+    a0 += __shfl_xor(a0, 1, 64); a0 += __shfl_xor(a0, 2, 64);
+    a1 += __shfl_xor(a1, 1, 64); a1 += __shfl_xor(a1, 2, 64);
+    av += __shfl_xor(av, 1, 64); av += __shfl_xor(av, 2, 64);
+    if (part == 0) {
+      s.out[r * 4 + 0] = a0 + s.tail[T_BMU];
+      s.out[r * 4 + 1] = a1 + s.tail[T_BMU + 1];
+      s.out[r * 4 + 2] = av + s.tail[T_BV];
+    }
   }
   __syncthreads();
 }
@@ -151,7 +167,7 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
                                                     float *exp_val, float *exp_mu, float *exp_sigma, uint8_t *exp_done,
                                                     const int64_t *__restrict__ dones_prev, float *actions_out,
                                                     uint64_t seed, uint64_t step, const float *eps_inject) {
-  __shared__ FwdSmem s;
+  __shared__ MlpSmem s;
   const int n = c.n_envs, H = c.horizon;
   const int row0 = blockIdx.x * RB;
   const int nrows = min(RB, n - row0);
@@ -160,7 +176,9 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
     const int r = i / NIN, k = i % NIN;
     exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = obs[(size_t)(row0 + r) * NIN + k];
   }
+  stage_weights(P, s);
   stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  __syncthreads();
   block_forward(P, s);
   const int r = threadIdx.x;
   if (r < nrows) {
@@ -202,11 +220,13 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
 
 __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,
                                               const double *val_rms, const float *__restrict__ obs, float *values) {
-  __shared__ FwdSmem s;
+  __shared__ MlpSmem s;
   const int n = c.n_envs;
   const int row0 = blockIdx.x * RB;
   const int nrows = min(RB, n - row0);
+  stage_weights(P, s);
   stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  __syncthreads();
   block_forward(P, s);
   const int r = threadIdx.x;
   if (r < nrows) {
@@ -349,11 +369,16 @@ __global__ void k_prepare_apply(ppo_cfg_t c, const double *work, float *val, flo
 }
 
 // ------------------------------------------------------- obs RMS (mb) -----
+// RunningMeanStd.train on the minibatch obs (running_mean_std.py:29-39, 84-111):
+// each workgroup sums a chunk of rows for all 33 columns (fp64) into
+// part[blk][66]; the last workgroup to finish (counter *cnt) folds the
+// partials in block order and merges them into the running statistics.
 __global__ __launch_bounds__(TB) void k_obs_stats(ppo_cfg_t c, const float *__restrict__ obs, int row0, int rows,
-                                                  double *part) {
-  // each block sums a chunk of rows for all 33 columns (fp64)
+                                                  double *part, double *obs_rms, unsigned *cnt) {
   __shared__ double acc[2][NIN][TB / NIN + 1];
-  const int col = threadIdx.x % NIN, lane_r = threadIdx.x / NIN;   // 7 row-lanes x 33 cols
+  __shared__ bool last;
+  const int tid = threadIdx.x;
+  const int col = tid % NIN, lane_r = tid / NIN;   // 7 row-lanes x 33 cols
   const int nl = TB / NIN;
   double s = 0, s2 = 0;
   if (lane_r < nl) {
@@ -367,259 +392,273 @@ __global__ __launch_bounds__(TB) void k_obs_stats(ppo_cfg_t c, const float *__re
     acc[1][col][lane_r] = s2;
   }
   __syncthreads();
-  if (threadIdx.x < NIN) {
+  if (tid < NIN) {
     double t = 0, t2 = 0;
-    for (int l = 0; l < nl; ++l) { t += acc[0][threadIdx.x][l]; t2 += acc[1][threadIdx.x][l]; }
-    part[(size_t)blockIdx.x * 2 * NIN + threadIdx.x] = t;
-    part[(size_t)blockIdx.x * 2 * NIN + NIN + threadIdx.x] = t2;
+    for (int l = 0; l < nl; ++l) { t += acc[0][tid][l]; t2 += acc[1][tid][l]; }
+    part[(size_t)blockIdx.x * 2 * NIN + tid] = t;
+    part[(size_t)blockIdx.x * 2 * NIN + NIN + tid] = t2;
   }
-}
-
-__global__ void k_obs_rms_update(double *obs_rms, const double *part, int nblk, int rows) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double mean[NIN], var[NIN];
-  for (int k = 0; k < NIN; ++k) {
-    double s = 0, s2 = 0;
-    for (int b = 0; b < nblk; ++b) { s += part[(size_t)b * 2 * NIN + k]; s2 += part[(size_t)b * 2 * NIN + NIN + k]; }
-    mean[k] = s / rows;
-    var[k] = (s2 - rows * mean[k] * mean[k]) / (rows - 1.0);
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    last = atomicAdd(cnt, 1u) == gridDim.x - 1;
+    __threadfence();
   }
-  rms_merge(obs_rms, NIN, mean, var, (double)rows);
+  __syncthreads();
+  if (!last) return;
+  const double count = obs_rms[2 * NIN];
+  if (tid < NIN) {
+    const int k = tid;
+    double sa = 0, sb = 0;
+#pragma unroll 8
+    for (int bb = 0; bb < (int)gridDim.x; ++bb) {
+      sa += part[(size_t)bb * 2 * NIN + k];
+      sb += part[(size_t)bb * 2 * NIN + NIN + k];
+    }
+    const double bmean = sa / rows;
+    const double bvar = (sb - rows * bmean * bmean) / (rows - 1.0);
+    const double tot = count + (double)rows;
+    const double delta = bmean - obs_rms[k];
+    const double M2 = obs_rms[NIN + k] * count + bvar * rows + delta * delta * count * rows / tot;
+    obs_rms[k] = obs_rms[k] + delta * rows / tot;
+    obs_rms[NIN + k] = M2 / tot;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    obs_rms[2 * NIN] = count + (double)rows;
+    *cnt = 0u;
+  }
 }
 
 // ------------------------------------------------------ minibatch grad ----
-struct GradSmem {
-  FwdSmem f;
-  float g[RB * 4];        // dmu0, dmu1, dv, dnlp per row
-};
-
 __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
                                                 const double *__restrict__ obs_rms, int row0,
                                                 const float *__restrict__ e_obs, const float *__restrict__ e_act,
                                                 const float *__restrict__ e_nlp, const float *__restrict__ e_val,
                                                 const float *__restrict__ e_ret, const float *__restrict__ e_adv,
                                                 float *e_mu, float *e_sigma, float *partials) {
-  __shared__ GradSmem s;
-  const int tid = threadIdx.x;
+  __shared__ MlpSmem s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 31, h = lane >> 5;
   const int rb0 = row0 + blockIdx.x * RB;             // global row of this block
   const float invB = 1.0f / (float)c.minibatch;
-  stage_obs(e_obs, rb0, RB, obs_rms, c.normalize_input != 0, c.rms_eps, s.f);
-  block_forward(P, s.f);
+  stage_weights(P, s);
+  stage_obs(e_obs, rb0, RB, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  __syncthreads();
+  block_forward(P, s);
   float *part = partials + (size_t)blockIdx.x * NPART;
-  // ---- per-row losses and output gradients ----
-  float la = 0.f, lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f, gs0 = 0.f, gs1 = 0.f;
-  if (tid < RB) {
-    const int r = tid;
-    const size_t row = (size_t)rb0 + r;
-    const float mu0 = s.f.out[r * 4], mu1 = s.f.out[r * 4 + 1], v = s.f.out[r * 4 + 2];
-    const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
-    const float sg0 = expf(ls0), sg1 = expf(ls1);
-    const float x0 = e_act[row * 2], x1 = e_act[row * 2 + 1];
-    const float z0 = (x0 - mu0) / sg0, z1 = (x1 - mu1) / sg1;
-    const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
-    const float A = e_adv[row];
-    // actor_loss (common_losses.py:36-46)
-    const float ratio = expf(e_nlp[row] - nlp);
-    const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
-    const float rc = clampt(ratio, lo, hi);
-    const float s1 = -(A * ratio), s2 = -(A * rc);
-    const float a_loss = fmaxf(s1, s2);
-    const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-    const float g1 = -A, g2 = -A * inr;                // d(-A r)/dr, d(-A clip(r))/dr
-    const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
-    const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
-    // critic_loss (common_losses.py:10-19)
-    const float vo = e_val[row], R = e_ret[row];
-    float dv;
-    float c_loss;
-    if (c.clip_value) {
-      const float dvr = v - vo;
-      const float dvc = clampt(dvr, -c.e_clip, c.e_clip);
-      const float vc = vo + dvc;
-      const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
-      c_loss = fmaxf(l1, l2);
-      const float d1 = 2.f * (v - R);
-      const float d2 = 2.f * (vc - R) * ((dvr >= -c.e_clip && dvr <= c.e_clip) ? 1.f : 0.f);
-      dv = (l1 > l2) ? d1 : ((l1 < l2) ? d2 : 0.5f * (d1 + d2));
-    } else {
-      c_loss = (R - v) * (R - v);
-      dv = 2.f * (v - R);
-    }
-    dv *= 0.5f * c.critic_coef * invB;
-    // bound_loss (a2c_continuous.py:209-217)
-    const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
-    const float bh1 = fmaxf(mu1 - 1.1f, 0.f), bl1 = fminf(mu1 + 1.1f, 0.f);
-    const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
-    const float bc = c.bounds_loss_coef * invB;
-    const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
-    const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
-    // d nlp / d logstd = 1 - z^2 (through sigma = exp(logstd) and the sum of logstd)
-    gs0 = dnlp * (1.f - z0 * z0);
-    gs1 = dnlp * (1.f - z1 * z1);
-    const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
-    // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
-    const float om0 = e_mu[row * 2], om1 = e_mu[row * 2 + 1];
-    const float os0 = e_sigma[row * 2], os1 = e_sigma[row * 2 + 1];
-    const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
-    const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
-    e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
-    e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
-    la = a_loss; lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
-    s.g[r * 4 + 0] = dmu0;
-    s.g[r * 4 + 1] = dmu1;
-    s.g[r * 4 + 2] = dv;
-    s.g[r * 4 + 3] = dnlp;
-  }
-  // block sums of losses and the sigma gradient (rows live in wave 0)
+  // ---- per-row losses and output gradients (wave 0, lanes < RB) ----
   if (tid < 64) {
+    float la = 0.f, lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f, gs0 = 0.f, gs1 = 0.f;
+    if (tid < RB) {
+      const int r = tid;
+      const size_t row = (size_t)rb0 + r;
+      const float mu0 = s.out[r * 4], mu1 = s.out[r * 4 + 1], v = s.out[r * 4 + 2];
+      const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
+      const float sg0 = expf(ls0), sg1 = expf(ls1);
+      const float x0 = e_act[row * 2], x1 = e_act[row * 2 + 1];
+      const float z0 = (x0 - mu0) / sg0, z1 = (x1 - mu1) / sg1;
+      const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
+      const float A = e_adv[row];
+      // actor_loss (common_losses.py:36-46)
+      const float ratio = expf(e_nlp[row] - nlp);
+      const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
+      const float rc = clampt(ratio, lo, hi);
+      const float s1 = -(A * ratio), s2 = -(A * rc);
+      const float a_loss = fmaxf(s1, s2);
+      const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+      const float g1 = -A, g2 = -A * inr;                // d(-A r)/dr, d(-A clip(r))/dr
+      const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
+      const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
+      // critic_loss (common_losses.py:10-19)
+      const float vo = e_val[row], R = e_ret[row];
+      float dv, c_loss;
+      if (c.clip_value) {
+        const float dvr = v - vo;
+        const float dvc = clampt(dvr, -c.e_clip, c.e_clip);
+        const float vc = vo + dvc;
+        const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+        c_loss = fmaxf(l1, l2);
+        const float d1 = 2.f * (v - R);
+        const float d2 = 2.f * (vc - R) * ((dvr >= -c.e_clip && dvr <= c.e_clip) ? 1.f : 0.f);
+        dv = (l1 > l2) ? d1 : ((l1 < l2) ? d2 : 0.5f * (d1 + d2));
+      } else {
+        c_loss = (R - v) * (R - v);
+        dv = 2.f * (v - R);
+      }
+      dv *= 0.5f * c.critic_coef * invB;
+      // bound_loss (a2c_continuous.py:209-217)
+      const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
+      const float bh1 = fmaxf(mu1 - 1.1f, 0.f), bl1 = fminf(mu1 + 1.1f, 0.f);
+      const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
+      const float bc = c.bounds_loss_coef * invB;
+      const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
+      const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
+      // d nlp / d logstd = 1 - z^2 (through sigma = exp(logstd) and the sum of logstd)
+      gs0 = dnlp * (1.f - z0 * z0);
+      gs1 = dnlp * (1.f - z1 * z1);
+      const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
+      // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
+      const float om0 = e_mu[row * 2], om1 = e_mu[row * 2 + 1];
+      const float os0 = e_sigma[row * 2], os1 = e_sigma[row * 2 + 1];
+      const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
+      const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
+      e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
+      e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
+      la = a_loss; lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
+      s.g[r * 4 + 0] = dmu0;
+      s.g[r * 4 + 1] = dmu1;
+      s.g[r * 4 + 2] = dv;
+      s.g[r * 4 + 3] = dnlp;
+    }
     la = wave_sum(la); lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
     gs0 = wave_sum(gs0); gs1 = wave_sum(gs1);
     if (tid == 0) {
       part[P_LOSS + 0] = la; part[P_LOSS + 1] = lc; part[P_LOSS + 2] = le; part[P_LOSS + 3] = lb;
       part[P_LOSS + 4] = lkl;
-      part[P_SIGMA] = gs0; part[P_SIGMA + 1] = gs1;
+      part[PPO_OFF_SIGMA] = gs0; part[PPO_OFF_SIGMA + 1] = gs1;
     }
   }
   __syncthreads();
-  const int j = tid % NH, rg = tid / NH, r0 = rg * RG;
-  // ---- heads' grads (need h2) and dz2 = (dmu Wmu + dv Wv) * (1 - h2^2) ----
+  // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 ----
   {
-    const float wm0 = P[PPO_OFF_WMU + j], wm1 = P[PPO_OFF_WMU + NH + j], wv = P[PPO_OFF_WV + j];
-    float gw0 = 0.f, gw1 = 0.f, gwv = 0.f;
-    float dz[RG];
+    const int j = tid & (NH - 1), half = tid >> 7;     // rows 16*half .. 16*half+15
+    const float wm0 = s.tail[T_WMU + j], wm1 = s.tail[T_WMU + NH + j], wv = s.tail[T_WV + j];
+    float gw0 = 0.f, gw1 = 0.f, gwv = 0.f, db = 0.f;
 #pragma unroll
-    for (int r = 0; r < RG; ++r) {
-      const int rr = r0 + r;
-      const float h = s.f.h2[rr * NH + j];
+    for (int q = 0; q < RB / 2; ++q) {
+      const int rr = half * (RB / 2) + q;
+      const float hv = s.h2[rr * HS + j];
       const float d0 = s.g[rr * 4], d1 = s.g[rr * 4 + 1], dvv = s.g[rr * 4 + 2];
-      gw0 = fmaf(d0, h, gw0); gw1 = fmaf(d1, h, gw1); gwv = fmaf(dvv, h, gwv);
-      const float dh = d0 * wm0 + d1 * wm1 + dvv * wv;
-      dz[r] = dh * (1.f - h * h);
+      gw0 = fmaf(d0, hv, gw0); gw1 = fmaf(d1, hv, gw1); gwv = fmaf(dvv, hv, gwv);
+      const float dz = (d0 * wm0 + d1 * wm1 + dvv * wv) * (1.f - hv * hv);
+      s.h2[rr * HS + j] = dz;
+      db += dz;
     }
-    __syncthreads();   // every thread has read h2
-#pragma unroll
-    for (int r = 0; r < RG; ++r) s.f.h2[(r0 + r) * NH + j] = dz[r];   // h2 := dz2
-    // two row groups -> combine through LDS (out[] is free now)
-    __shared__ float hg[2][3][NH];
-    hg[rg][0][j] = gw0; hg[rg][1][j] = gw1; hg[rg][2][j] = gwv;
-    __syncthreads();
-    if (rg == 0) {
-      part[P_WMU + j] = hg[0][0][j] + hg[1][0][j];
-      part[P_WMU + NH + j] = hg[0][1][j] + hg[1][1][j];
-      part[P_WV + j] = hg[0][2][j] + hg[1][2][j];
-    }
-    if (tid < 3) {
-      float sacc = 0.f;
-      for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + tid];
-      if (tid < 2) part[P_BMU + tid] = sacc;
-      else part[P_BV] = sacc;
-    }
+    s.hg[half][0][j] = gw0; s.hg[half][1][j] = gw1; s.hg[half][2][j] = gwv; s.hg[half][3][j] = db;
   }
   __syncthreads();
-  // ---- dW2^T[k][j] = sum_r dz2[r][j] h1[r][k]; thread (j, k-half) ----
-  {
-    const int kh = rg;   // k in [kh*64, kh*64+64)
-    float acc[64];
-#pragma unroll
-    for (int q = 0; q < 64; ++q) acc[q] = 0.f;
-    float db = 0.f;
-    for (int r = 0; r < RB; ++r) {
-      const float d = s.f.h2[r * NH + j];
-      db += d;
-#pragma unroll
-      for (int q4 = 0; q4 < 16; ++q4) {
-        const float4 hv = *reinterpret_cast<const float4 *>(&s.f.h1[r * NH + kh * 64 + 4 * q4]);
-        acc[4 * q4 + 0] = fmaf(d, hv.x, acc[4 * q4 + 0]);
-        acc[4 * q4 + 1] = fmaf(d, hv.y, acc[4 * q4 + 1]);
-        acc[4 * q4 + 2] = fmaf(d, hv.z, acc[4 * q4 + 2]);
-        acc[4 * q4 + 3] = fmaf(d, hv.w, acc[4 * q4 + 3]);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 64; ++q) part[P_W2T + (kh * 64 + q) * NH + j] = acc[q];
-    if (kh == 0) part[P_B2 + j] = db;
+  if (tid < NH) {
+    const int j = tid;
+    part[PPO_OFF_WMU + j] = s.hg[0][0][j] + s.hg[1][0][j];
+    part[PPO_OFF_WMU + NH + j] = s.hg[0][1][j] + s.hg[1][1][j];
+    part[PPO_OFF_WV + j] = s.hg[0][2][j] + s.hg[1][2][j];
+    part[PPO_OFF_B2 + j] = s.hg[0][3][j] + s.hg[1][3][j];
+  } else if (tid < NH + 3) {
+    const int q = tid - NH;
+    float sacc = 0.f;
+    for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
+    part[q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV] = sacc;
   }
-  // ---- dh1[r][k] = sum_j dz2[r][j] W2[j][k]; dz1 = dh1 (1 - h1^2); thread (k, rows) ----
+  // ---- dW2[j][k] = sum_r dz2[r][j] h1[r][k]: wave w owns rows j in [32w, 32w+32), 4 k tiles ----
   {
-    const int k = j;
-    float acc[RG];
+    f32x16 acc[4] = {};
+#pragma unroll 4
+    for (int st = 0; st < RB / 2; ++st) {
+      const int r = st + (RB / 2) * h;
+      const float a = s.h2[r * HS + 32 * w + i];
 #pragma unroll
-    for (int r = 0; r < RG; ++r) acc[r] = 0.f;
-    for (int jj4 = 0; jj4 < NH / 4; ++jj4) {
-      const float w0 = P[PPO_OFF_W2 + (4 * jj4 + 0) * NH + k];
-      const float w1 = P[PPO_OFF_W2 + (4 * jj4 + 1) * NH + k];
-      const float w2 = P[PPO_OFF_W2 + (4 * jj4 + 2) * NH + k];
-      const float w3 = P[PPO_OFF_W2 + (4 * jj4 + 3) * NH + k];
-#pragma unroll
-      for (int r = 0; r < RG; ++r) {
-        const float4 d = *reinterpret_cast<const float4 *>(&s.f.h2[(r0 + r) * NH + 4 * jj4]);
-        acc[r] = fmaf(d.x, w0, acc[r]);
-        acc[r] = fmaf(d.y, w1, acc[r]);
-        acc[r] = fmaf(d.z, w2, acc[r]);
-        acc[r] = fmaf(d.w, w3, acc[r]);
-      }
+      for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma32(a, s.h1[r * HS + 32 * kt + i], acc[kt]);
     }
-    __syncthreads();   // dW2 used h1: all reads done before overwrite
 #pragma unroll
-    for (int r = 0; r < RG; ++r) {
-      const float h = s.f.h1[(r0 + r) * NH + k];
-      s.f.h1[(r0 + r) * NH + k] = acc[r] * (1.f - h * h);   // h1 := dz1
-    }
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) part[PPO_OFF_W2 + (32 * w + crow(q, h)) * NH + 32 * kt + i] = acc[kt][q];
+  }
+  // ---- dh1[r][k] = sum_j dz2[r][j] W2[j][k]: wave w owns columns k in [32w, 32w+32) ----
+  f32x16 dh = {};
+#pragma unroll 16
+  for (int st = 0; st < NH / 2; ++st) {
+    const int j = 2 * st + h;
+    dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + 32 * w + i], dh);
+  }
+  __syncthreads();   // every read of h1 (dW2 operand) is done
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int idx = crow(q, h) * HS + 32 * w + i;
+    const float hv = s.h1[idx];
+    s.h1[idx] = dh[q] * (1.f - hv * hv);   // h1 := dz1
   }
   __syncthreads();
-  // ---- dW1^T[k][j] = sum_r dz1[r][j] x[r][k]; db1 ----
+  // ---- dW1[j][k] = sum_r dz1[r][j] x[r][k] (k < 32 on the matrix cores), db1 ----
   {
-    // 33 columns split over the two row groups: rg 0 -> k 0..16, rg 1 -> k 17..32
-    const int k0 = rg ? 17 : 0, k1 = rg ? NIN : 17;
-    float acc[17];
+    f32x16 acc = {};
 #pragma unroll
-    for (int q = 0; q < 17; ++q) acc[q] = 0.f;
-    float db = 0.f;
-    for (int r = 0; r < RB; ++r) {
-      const float d = s.f.h1[r * NH + j];
-      db += d;
-#pragma unroll
-      for (int q = 0; q < 17; ++q)
-        if (k0 + q < k1) acc[q] = fmaf(d, s.f.x[r * XP + k0 + q], acc[q]);
+    for (int st = 0; st < RB / 2; ++st) {
+      const int r = st + (RB / 2) * h;
+      acc = mfma32(s.h1[r * HS + 32 * w + i], s.x[r * XS + i], acc);
     }
 #pragma unroll
-    for (int q = 0; q < 17; ++q)
-      if (k0 + q < k1) part[P_W1T + (k0 + q) * NH + j] = acc[q];
-    if (rg == 0) part[P_B1 + j] = db;
+    for (int q = 0; q < 16; ++q) part[PPO_OFF_W1 + (32 * w + crow(q, h)) * NIN + i] = acc[q];
+  }
+  if (tid < NH) {
+    const int j = tid;
+    float a = 0.f;
+    for (int r = 0; r < RB; ++r) a = fmaf(s.h1[r * HS + j], s.x[r * XS + NIN - 1], a);
+    part[PPO_OFF_W1 + j * NIN + NIN - 1] = a;
+  } else {
+    const int j = tid - NH;
+    float a = 0.f;
+    for (int r = 0; r < RB; ++r) a += s.h1[r * HS + j];
+    part[PPO_OFF_B1 + j] = a;
   }
 }
 
-// sum the per-block partials (fixed order => deterministic) into grad[]
-__global__ void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad, float *losses,
-                                  float inv_b) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= NPART) return;
-  float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partials[(size_t)b * NPART + p];
-  if (p < PPO_NPARAM) grad[partial_to_param(p)] = s;
-  else if (p < PPO_NPARAM + 5) {
-    const int q = p - PPO_NPARAM;
-    if (q == 4) grad[PPO_NPARAM] = s * inv_b;      // kl mean rides with the gradient (all-reduce)
-    if (losses) losses[q] = s * inv_b;
+// sum the per-block partials (fixed order => deterministic) into grad[]:
+// 64 params x 4 block-strided groups per workgroup, combined in LDS.
+__global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
+                                                         float *losses, float inv_b) {
+  __shared__ float red[4][64];
+  const int cidx = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int p = blockIdx.x * 64 + cidx;
+  float acc = 0.f;
+  if (p < PPO_NPARAM + 5) {
+#pragma unroll 8
+    for (int b = g; b < nblk; b += 4) acc += partials[(size_t)b * NPART + p];
+  }
+  red[g][cidx] = acc;
+  __syncthreads();
+  if (g == 0 && p < PPO_NPARAM + 5) {
+    const float sum = ((red[0][cidx] + red[1][cidx]) + red[2][cidx]) + red[3][cidx];
+    if (p < PPO_NPARAM) grad[p] = sum;
+    else {
+      const int q = p - PPO_NPARAM;
+      if (q == 4) grad[PPO_NPARAM] = sum * inv_b;      // kl mean rides with the gradient (all-reduce)
+      if (losses) losses[q] = sum * inv_b;
+    }
   }
 }
 
-// clip_grad_norm_ + Adam + AdaptiveScheduler, one workgroup
-__global__ __launch_bounds__(1024) void k_apply(ppo_cfg_t c, float *P, const float *__restrict__ grad_in,
-                                                float *m, float *v, float *opt, float grad_scale) {
-  __shared__ float red[16];
+// clip_grad_norm_ + Adam + AdaptiveScheduler.  Every workgroup forms the same
+// total norm (same order), updates its 256 parameters; the last workgroup to
+// finish (completion counter in opt[7]) advances step / lr / kl / norm.
+constexpr int AP_TB = 256;
+__global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const float *__restrict__ grad_in,
+                                                 float *m, float *v, float *opt, float grad_scale, float *kl_out) {
+  __shared__ float red[AP_TB / 64];
+  __shared__ bool last;
   const int tid = threadIdx.x;
+  // total norm: every load issued up front (16-byte aligned gradient, checked on the host)
+  constexpr int N4 = PPO_NPARAM / 4, U = (N4 + AP_TB - 1) / AP_TB;
+  const float4 *g4 = reinterpret_cast<const float4 *>(grad_in);
+  float4 gv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) gv[u] = (tid + u * AP_TB < N4) ? g4[tid + u * AP_TB] : make_float4(0.f, 0.f, 0.f, 0.f);
   float ss = 0.f;
-  for (int i = tid; i < PPO_NPARAM; i += 1024) {
-    const float g = grad_in[i] * grad_scale;
-    ss += g * g;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float x = gv[u].x * grad_scale, y = gv[u].y * grad_scale;
+    const float z = gv[u].z * grad_scale, w = gv[u].w * grad_scale;
+    ss = fmaf(x, x, ss); ss = fmaf(y, y, ss); ss = fmaf(z, z, ss); ss = fmaf(w, w, ss);
+  }
+  for (int q = 4 * N4 + tid; q < PPO_NPARAM; q += AP_TB) {
+    const float g = grad_in[q] * grad_scale;
+    ss = fmaf(g, g, ss);
   }
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
-  float tot = 0.f;
-  for (int w = 0; w < 16; ++w) tot += red[w];
-  const float total_norm = sqrtf(tot);
+  const float total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
   float coef = 1.0f;
   if (c.truncate_grads) {
     coef = c.grad_norm / (total_norm + 1e-6f);
@@ -632,19 +671,26 @@ __global__ __launch_bounds__(1024) void k_apply(ppo_cfg_t c, float *P, const flo
   const double bc2 = 1.0 - pow((double)c.adam_b2, (double)step);
   const float step_size = (float)((double)lr / bc1);
   const float bc2s = (float)sqrt(bc2);
-  for (int i = tid; i < PPO_NPARAM; i += 1024) {
-    float g = grad_in[i] * grad_scale * coef;
-    if (c.weight_decay != 0.f) g = g + c.weight_decay * P[i];
-    float mi = m[i], vi = v[i];
+  const int q = blockIdx.x * AP_TB + tid;
+  if (q < PPO_NPARAM) {
+    float g = grad_in[q] * grad_scale * coef;
+    if (c.weight_decay != 0.f) g = g + c.weight_decay * P[q];
+    float mi = m[q], vi = v[q];
     mi = mi + (1.0f - c.adam_b1) * (g - mi);          // exp_avg.lerp_(grad, 1 - beta1)
     vi = vi * c.adam_b2 + (1.0f - c.adam_b2) * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
     const float denom = sqrtf(vi) / bc2s + c.adam_eps;
-    P[i] = P[i] - step_size * (mi / denom);
-    m[i] = mi;
-    v[i] = vi;
+    P[q] = P[q] - step_size * (mi / denom);
+    m[q] = mi;
+    v[q] = vi;
   }
   __syncthreads();
   if (tid == 0) {
+    __threadfence();
+    unsigned *cnt = reinterpret_cast<unsigned *>(opt + 7);
+    last = atomicAdd(cnt, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && tid == 0) {
     opt[1] = step;
     opt[3] = total_norm;
     // AdaptiveScheduler.update on this minibatch's KL (schedulers.py:26-32)
@@ -655,7 +701,10 @@ __global__ __launch_bounds__(1024) void k_apply(ppo_cfg_t c, float *P, const flo
       if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
       opt[0] = nl;
       opt[2] = kl;
+      if (kl_out) *kl_out = kl;
     }
+    __threadfence();
+    atomicExch(reinterpret_cast<unsigned *>(opt + 7), 0u);
   }
 }
 
@@ -728,28 +777,29 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
   hipStream_t s = (hipStream_t)stream;
   const int row0 = mb_index * cfg->minibatch;
   if (update_obs_rms && cfg->normalize_input) {
-    // RunningMeanStd.train on the minibatch obs (mini-epoch 0 only, a2c_common.py:1243-1244)
+    // RunningMeanStd.train on the minibatch obs (mini-epoch 0 only, a2c_common.py:1243-1244);
+    // partials at work[8..], completion counter in the bits of work[7]
     const int nb = 64;
-    hipLaunchKernelGGL(k_obs_stats, dim3(nb), dim3(TB), 0, s, *cfg, exp_obs, row0, cfg->minibatch, work);
-    USV_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_obs_rms_update, dim3(1), dim3(64), 0, s, obs_rms, work, nb, cfg->minibatch);
+    hipLaunchKernelGGL(k_obs_stats, dim3(nb), dim3(TB), 0, s, *cfg, exp_obs, row0, cfg->minibatch, work + 8, obs_rms,
+                       reinterpret_cast<unsigned *>(work + 7));
     USV_CHECK_LAUNCH();
   }
   const int nblk = cfg->minibatch / RB;
   hipLaunchKernelGGL(k_mb_grad, dim3(nblk), dim3(TB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
                      exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_reduce_partials, dim3((NPART + 255) / 256), dim3(256), 0, s, partials, nblk, grad, losses,
+  hipLaunchKernelGGL(k_reduce_partials, dim3((PPO_NPARAM + 5 + 63) / 64), dim3(256), 0, s, partials, nblk, grad, losses,
                      1.0f / (float)cfg->minibatch);
   USV_CHECK_LAUNCH();
   return 0;
 }
 
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m, float *adam_v, float *opt,
-                        float grad_scale, void *stream) {
+                        float grad_scale, float *kl_out, void *stream) {
   if (!cfg || !params || !grad || !adam_m || !adam_v || !opt) return 1;
-  hipLaunchKernelGGL(k_apply, dim3(1), dim3(1024), 0, (hipStream_t)stream, *cfg, params, grad, adam_m, adam_v, opt,
-                     grad_scale);
+  if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
+  hipLaunchKernelGGL(k_apply, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB), dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params,
+                     grad, adam_m, adam_v, opt, grad_scale, kl_out);
   USV_CHECK_LAUNCH();
   return 0;
 }

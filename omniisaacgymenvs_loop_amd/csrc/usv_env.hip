@@ -62,10 +62,25 @@ struct ResetRng {
 };
 
 // ------------------------------------------------------------------------
+// Per-step scratch reset (reset count, field maxima, extras sums): one tiny
+// kernel instead of four memset nodes.
+// ------------------------------------------------------------------------
+__global__ void k_step_begin(usv_bufs_t b) {
+  const int t = threadIdx.x;
+  if (t == 0) b.ctl[USV_CTL_RESET_COUNT] = 0;
+  if (t == 1) b.ctl[USV_CTL_ANY_INSIDE] = 0;
+  if (t == 2) b.ctl[USV_CTL_ANY_FINITE] = 0;
+  if (t < 4) b.fscratch[t] = 0.f;
+  if (t < USV_NSTAT) b.extras_acc[t] = 0.f;
+}
+
+// ------------------------------------------------------------------------
 // Reset path (USVVirtual.reset_idx, USV_Virtual.py:1502-1618).  One thread per
 // env; threads of envs with reset_buf==1 do the work.  The reset list is
 // compacted with a wave ballot + one atomic per wave (order is irrelevant:
 // draws are keyed by env id, the potential-field batch statistics are maxima).
+// Obstacle rejection sampling runs afterwards in k_reset_obst, 16 lanes per
+// reset env.
 // ------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uint64_t seed, uint64_t step,
                                                   const float *__restrict__ inj) {
@@ -80,20 +95,23 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   int base = 0;
   if (lane == leader) base = atomicAdd(&b.ctl[USV_CTL_RESET_COUNT], __popcll(mask));
   base = __shfl(base, leader, 64);
+  // ---- episode extras: sums of the envs being reset (:1591-1612), one atomic per wave ----
+  if (c.stats_on) {
+    for (int q = 0; q < USV_NSTAT; ++q) {
+      float v = 0.f;
+      if (active) {
+        v = b.stats[(size_t)q * n + e];
+        if (q == ST_SUCCESS) v = (float)b.done_succ[e];
+        if (q == ST_COLLISION) v = (float)b.done_coll[e];
+        b.stats[(size_t)q * n + e] = 0.f;
+      }
+      v = wave_sum(v);
+      if (lane == leader) atomicAdd(&b.extras_acc[q], v);
+    }
+  }
   if (!active) return;
   const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
   b.reset_ids[slot] = e;
-
-  // ---- episode extras: sums of the envs being reset (:1591-1612) ----
-  if (c.stats_on) {
-    for (int q = 0; q < USV_NSTAT; ++q) {
-      float v = b.stats[(size_t)q * n + e];
-      if (q == ST_SUCCESS) v = (float)b.done_succ[e];
-      if (q == ST_COLLISION) v = (float)b.done_coll[e];
-      atomicAdd(&b.extras_acc[q], v);
-      b.stats[(size_t)q * n + e] = 0.f;
-    }
-  }
   ResetRng U{inj, seed, step, (uint32_t)e};
   // ---- CaptureXYTask.reset (static_obs.py:767-778) ----
   b.goal_cnt[e] = 0;
@@ -166,52 +184,6 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   const float sx = r * cosf(th), sy = r * sinf(th);
   const float yaw0 = U(RU_YAW) * USV_PI_F;
   const float tx = b.tgt_x[e], ty = b.tgt_y[e];
-  const float mnx = tx - c.obst_box, mny = ty - c.obst_box;
-  const float dx_ = (tx + c.obst_box) - mnx, dy_ = (ty + c.obst_box) - mny;
-  float ox[USV_NOBST], oy[USV_NOBST];
-#pragma unroll
-  for (int o = 0; o < USV_NOBST; ++o) {
-    ox[o] = U(RU_OBST + 2 * o) * dx_ + mnx;
-    oy[o] = U(RU_OBST + 2 * o + 1) * dy_ + mny;
-  }
-  const float sep2 = c.min_obs_sep * c.min_obs_sep;
-  for (int it = 0; it <= USV_SPAWN_ITERS; ++it) {
-    uint32_t inval = 0;
-#pragma unroll
-    for (int o = 0; o < USV_NOBST; ++o) {
-      const float ds = tnorm2(ox[o] - sx, oy[o] - sy);
-      const float dt = tnorm2(ox[o] - tx, oy[o] - ty);
-      if ((ds < c.min_dist_safe) || (dt < c.min_dist_safe)) inval |= 1u << o;
-    }
-#pragma unroll
-    for (int j = 1; j < USV_NOBST; ++j) {
-      const bool vj = ox[j] < 900.f;
-#pragma unroll
-      for (int i = 0; i < j; ++i) {
-        const float ddx = ox[i] - ox[j], ddy = oy[i] - oy[j];
-        if (vj && (ox[i] < 900.f) && (ddx * ddx + ddy * ddy) < sep2) inval |= 1u << j;
-      }
-    }
-    if (inval == 0) break;
-    if (it == USV_SPAWN_ITERS) {  // leftovers to limbo (:1042-1048)
-#pragma unroll
-      for (int o = 0; o < USV_NOBST; ++o)
-        if (inval & (1u << o)) { ox[o] = 999.0f; oy[o] = 999.0f; }
-      break;
-    }
-    const int rb = RU_RESAMPLE + it * USV_NOBST * 2;
-#pragma unroll
-    for (int o = 0; o < USV_NOBST; ++o)
-      if (inval & (1u << o)) {
-        ox[o] = U(rb + 2 * o) * dx_ + mnx;
-        oy[o] = U(rb + 2 * o + 1) * dy_ + mny;
-      }
-  }
-#pragma unroll
-  for (int o = 0; o < USV_NOBST; ++o) {
-    b.obst[(size_t)(2 * o) * n + e] = ox[o];
-    b.obst[(size_t)(2 * o + 1) * n + e] = oy[o];
-  }
   b.field_old_tgt[e] = tx;
   b.field_old_tgt[n + e] = ty;
   // ---- pose / velocities / bookkeeping (USV_Virtual.py:1541-1579) ----
@@ -229,6 +201,65 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   const float g = c.goal_random_position;
   b.tgt_x[e] = U(RU_GOAL) * g * 2.0f - g;
   b.tgt_y[e] = U(RU_GOAL + 1) * g * 2.0f - g;
+}
+
+// ------------------------------------------------------------------------
+// Obstacle placement with rejection (CaptureXYTask.get_spawns obstacle part,
+// static_obs.py:968-1048): 16 lanes per reset env, lane o owns obstacle o.
+// Box around the previous-episode target; an obstacle is redrawn while it is
+// closer than min_dist_safe to the spawn or the target, or closer than
+// min_obs_sep to a lower-index obstacle; after USV_SPAWN_ITERS redraws the
+// leftovers go to limbo (999, 999).  Same uniforms as the per-env restatement
+// (reset slots RU_OBST + 2o, RU_RESAMPLE + 32 it + 2o (+1)).
+// ------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_reset_obst(usv_cfg_t c, usv_bufs_t b, uint64_t seed, uint64_t step,
+                                                       const float *__restrict__ inj) {
+  static_assert(USV_NOBST == 16, "one 16-lane group per env");
+  const int n = b.n;
+  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int lane = threadIdx.x & 63, o = lane & 15, gbase = lane & 48;
+  const int groups = gridDim.x * (kBlock / 16);
+  for (int slot = (blockIdx.x * kBlock + threadIdx.x) / 16; slot < count; slot += groups) {
+    const int e = b.reset_ids[slot];
+    auto U = [&](int i) -> float {
+      if (inj) return inj[(size_t)e * USV_NU_RESET + i];
+      float u4[4];
+      philox_u4(seed, (uint32_t)e, step, 0x100u + (uint32_t)(i >> 2), u4);
+      return u4[i & 3];
+    };
+    const float sx = b.px[e], sy = b.py[e];
+    const float tx = b.field_old_tgt[e], ty = b.field_old_tgt[n + e];
+    const float mnx = tx - c.obst_box, mny = ty - c.obst_box;
+    const float dx_ = (tx + c.obst_box) - mnx, dy_ = (ty + c.obst_box) - mny;
+    float ox = U(RU_OBST + 2 * o) * dx_ + mnx;
+    float oy = U(RU_OBST + 2 * o + 1) * dy_ + mny;
+    const float sep2 = c.min_obs_sep * c.min_obs_sep;
+    for (int it = 0; it <= USV_SPAWN_ITERS; ++it) {
+      const float ds = tnorm2(ox - sx, oy - sy);
+      const float dt = tnorm2(ox - tx, oy - ty);
+      bool bad = (ds < c.min_dist_safe) || (dt < c.min_dist_safe);
+      const bool vo = ox < 900.f;
+#pragma unroll
+      for (int i = 0; i < USV_NOBST - 1; ++i) {
+        const float xi = __shfl(ox, gbase + i, 64), yi = __shfl(oy, gbase + i, 64);
+        const float ddx = xi - ox, ddy = yi - oy;
+        if (i < o && vo && (xi < 900.f) && (ddx * ddx + ddy * ddy) < sep2) bad = true;
+      }
+      const uint32_t inval = (uint32_t)((__ballot(bad) >> gbase) & 0xFFFFull);
+      if (inval == 0) break;
+      if (it == USV_SPAWN_ITERS) {  // leftovers to limbo (:1042-1048)
+        if (bad) { ox = 999.0f; oy = 999.0f; }
+        break;
+      }
+      if (bad) {
+        const int rb = RU_RESAMPLE + it * USV_NOBST * 2;
+        ox = U(rb + 2 * o) * dx_ + mnx;
+        oy = U(rb + 2 * o + 1) * dy_ + mny;
+      }
+    }
+    b.obst[(size_t)(2 * o) * n + e] = ox;
+    b.obst[(size_t)(2 * o + 1) * n + e] = oy;
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -289,7 +320,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   const bool pot_none = ctl[USV_CTL_POT_VALID] == 0 || ctl[USV_CTL_RESET_COUNT] > 0;
   const bool pen_valid = ctl[USV_CTL_PEN_VALID] != 0;
   const bool rew_valid = ctl[USV_CTL_REW_VALID] != 0;
-  float obs[USV_NOBS];
+  // obs row staged straight into LDS (odd row stride: conflict-free), clamped on write
+  // (_process_data clamp, vec_env_rlgames.py:85-95)
+  float *obs = sobs + threadIdx.x * USV_NOBS;
+  const float clip = c.clip_obs;
+  auto put = [&](int q, float v) { obs[q] = clampt(v, -clip, clip); };
 #pragma unroll
   for (int q = 0; q < USV_NOBS; ++q) obs[q] = 0.f;
   if (e < n) {
@@ -431,28 +466,28 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       }
     }
     if (c.obs_local) {
-      obs[0] = hc * vxn + hs * vyn;
-      obs[1] = -hs * vxn + hc * vyn;
+      put(0, hc * vxn + hs * vyn);
+      put(1, -hs * vxn + hc * vyn);
     } else {
-      obs[0] = vxn;
-      obs[1] = vyn;
+      put(0, vxn);
+      put(1, vyn);
     }
-    obs[2] = wzn;
-    obs[3] = cosf(alpha);
-    obs[4] = sinf(alpha);
-    obs[5] = dist_n;
+    put(2, wzn);
+    put(3, cosf(alpha));
+    put(4, sinf(alpha));
+    put(5, dist_n);
 #pragma unroll
     for (int q = 0; q < USV_NCLOSE; ++q) {
       const float vbx = bx[q] * ct + by[q] * st;
       const float vby = -bx[q] * st + by[q] * ct;
       const float nf = sqrtf(vbx * vbx + vby * vby + 1e-6f);
-      obs[8 + 3 * q] = bd[q] - c.obstacle_radius;
-      obs[9 + 3 * q] = -vbx / nf;
-      obs[10 + 3 * q] = -vby / nf;
+      put(8 + 3 * q, bd[q] - c.obstacle_radius);
+      put(9 + 3 * q, -vbx / nf);
+      put(10 + 3 * q, -vby / nf);
     }
     const int pa = USV_NOBS - c.priv_dim - 2;
-    obs[pa] = prev_cmd0;
-    obs[pa + 1] = prev_cmd1;
+    put(pa, prev_cmd0);
+    put(pa + 1, prev_cmd1);
     b.prev_cmd[e] = prev_cmd0;
     b.prev_cmd[n + e] = prev_cmd1;
     // ---- privileged tail (USV_Virtual.py:840-976) ----
@@ -472,7 +507,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
         co2 = c.com_scaled ? cz / (c.com_scale[2] + 1e-6f) : cz;
       }
       const int pt = USV_NOBS - c.priv_dim;
-      obs[pt] = mass_o; obs[pt + 1] = co0; obs[pt + 2] = co1; obs[pt + 3] = co2;
+      put(pt, mass_o); put(pt + 1, co0); put(pt + 2, co1); put(pt + 3, co2);
       if (c.priv_dim == 8) {
         float kdv, tl, tr, kz;
         if (c.masscom_base) {
@@ -495,7 +530,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
           tr = c.priv_thr_on ? enc_minmax(tr, c.thr_min, c.thr_max) : 0.f;
           kz = c.priv_kiz_on ? enc_minmax(kz, c.kiz_min, c.kiz_max) : 0.f;
         }
-        obs[pt + 4] = kdv; obs[pt + 5] = tl; obs[pt + 6] = tr; obs[pt + 7] = kz;
+        put(pt + 4, kdv); put(pt + 5, tl); put(pt + 6, tr); put(pt + 7, kz);
       }
     }
     // ---- compute_reward (static_obs.py:335-657) ----
@@ -601,13 +636,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       ADDS(ST_U_SUM, unit0 + unit1);
 #undef ADDS
     }
-    // ---- _process_data clamp (vec_env_rlgames.py:85-95) ----
-#pragma unroll
-    for (int q = 0; q < USV_NOBS; ++q) obs[q] = clampt(obs[q], -c.clip_obs, c.clip_obs);
   }
   // ---- coalesced obs store: rows of 33 floats staged through LDS ----
-#pragma unroll
-  for (int q = 0; q < USV_NOBS; ++q) sobs[threadIdx.x * USV_NOBS + q] = obs[q];
   __syncthreads();
   const int row0 = blockIdx.x * kBlock;
   const int rows = min(kBlock, n - row0);
@@ -671,13 +701,16 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t
               void *stream) {
   if (!cfg || !b || b->n <= 0) return 1;
   hipStream_t s = (hipStream_t)stream;
-  // per-step scratch: reset count, field maxima, extras sums (a memset node under graph capture)
-  if (hipMemsetAsync(b->ctl + USV_CTL_RESET_COUNT, 0, sizeof(int32_t), s) != hipSuccess) return 2;
-  if (hipMemsetAsync(b->ctl + USV_CTL_ANY_INSIDE, 0, 2 * sizeof(int32_t), s) != hipSuccess) return 2;
-  if (hipMemsetAsync(b->fscratch, 0, 4 * sizeof(float), s) != hipSuccess) return 2;
-  if (hipMemsetAsync(b->extras_acc, 0, sizeof(float) * USV_NSTAT, s) != hipSuccess) return 2;
+  // per-step scratch: reset count, field maxima, extras sums
+  hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, s, *b);
+  USV_CHECK_LAUNCH();
   const int grid = (b->n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_reset, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, seed, step, u_inject);
+  USV_CHECK_LAUNCH();
+  // 16 lanes per reset env; the grid covers every env up to 2048 workgroups, then strides
+  const int grid_o = (int)(((size_t)b->n * 16 + kBlock - 1) / kBlock);
+  hipLaunchKernelGGL(k_reset_obst, dim3(grid_o < 2048 ? grid_o : 2048), dim3(kBlock), 0, s, *cfg, *b, seed, step,
+                     u_inject);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_extras_finalize, dim3(1), dim3(64), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();

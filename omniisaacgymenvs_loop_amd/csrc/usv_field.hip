@@ -7,27 +7,47 @@
 //   by clamp(dist_to_goal/3, 0, 1), batch-global max of finite costs and of J,
 //   per-env min/max normalisation, potential = g_norm + 0.5 J_norm.
 //
-// Pass B (k_field_wave): one 1024-thread workgroup per reset env keeps the whole
-// 150x150 fp32 cost grid LDS-resident (90 KB of the 160 KB LDS).  Each of 900
-// threads owns a 5x5 tile in registers and relaxes it with forward+backward
-// Gauss-Seidel sweeps over its tile against a halo read from LDS; one barrier
-// per iteration with a block-wide "changed" vote.  The reference runs 225
-// synchronous Jacobi sweeps; both iterate to the same (unique) fixed point --
-// every cell = min over paths of the fp32 path sums -- so the result is the
-// reference's bit-for-bit whenever its 225 sweeps have converged (they do: the
-// hop depth of a 150x150 grid with 16 r=0.5 m obstacles is < 120; checked on
-// the golden fixtures).  An occupied target cell is seeded exactly as the
-// reference's first Jacobi sweep does (its neighbours get 1 / 1.414).
-// Passes C/D re-derive SDF and J per cell (16 distances) instead of storing them.
+// k_field_wave (one 256-thread workgroup per reset env, persistent over the
+// device-side reset count):
+//   1. SDF + occupancy of the 150x150 grid (SDF to a per-slot HBM scratch, the
+//      cost grid initialised in LDS, 90 KB);
+//   2. cost-to-go: 225 threads each own a 10x10 tile in registers and relax it
+//      with a raster forward + backward chamfer sweep against a halo ring read
+//      from LDS; one barrier per iteration with a block-wide "changed" vote.
+//      The reference runs 225 synchronous Jacobi sweeps; both iterate to the
+//      same unique fixed point (every cell = min over paths of the fp32 path
+//      sums), so the result is the reference's bit for bit whenever its 225
+//      sweeps have converged (they do: the hop depth of a 150x150 grid with 16
+//      r = 0.5 m obstacles is < 120; checked on the golden fixtures).  An
+//      occupied target cell is seeded exactly as the reference's first Jacobi
+//      sweep does (its neighbours get 1 / 1.414);
+//   3. raw cost to the field buffer + per-env statistics, split by finite and
+//      infinite cost so that the batch constant inf_val (unknown until every
+//      env is done) enters only through one monotone scalar per batch.
+// k_field_batch (one workgroup): batch max of finite costs -> inf_val, the
+//   repulsion mask of infinite cells, batch J max, any-inside flag.
+// k_field_final (grid-stride over (slot, 2048-cell chunk)): normalisation.
 #include "usv_device.h"
 
 namespace {
 
 constexpr int G = USV_GRID;
-constexpr int T = 5;             // tile edge
-constexpr int NT = G / T;        // 30 tiles per edge
-constexpr int kWaveThreads = 1024;
+constexpr int G2 = USV_GRID2;
+constexpr int T = 10;            // tile edge
+constexpr int NT = G / T;        // 15 tiles per edge
+constexpr int GP = G + 2;        // LDS cost grid padded with an +inf ring (no halo bounds checks)
+constexpr int kWaveThreads = 256;
 constexpr int kMaxIters = 4096;  // safety cap (never reached)
+constexpr int kChunk = 2048;     // cells per k_field_final work item
+constexpr int kChunks = (G2 + kChunk - 1) / kChunk;
+
+// slot_stats layout (per reset slot)
+enum {
+  SS_GMIN_F = 0, SS_GMAX_F, SS_ANY_INF,        // finite-cost extrema, any infinite cell
+  SS_JMIN_F_NI, SS_JMAX_F_NI, SS_JMAX_F_ALL,   // J over finite cells: non-inside min/max, max of all
+  SS_JRMIN_I_NI, SS_JRMAX_I_NI, SS_JRMAX_I_ALL,  // eta (1/d - 1/r0)^2 over infinite cells (mask applied later)
+  SS_INSIDE, SS_ITERS
+};
 
 __device__ __forceinline__ float grid_coord(const float *lin, float map_size, int i) {
   if (lin) return lin[i];
@@ -48,12 +68,32 @@ __device__ __forceinline__ float min_dist(const float *so, float gx, float gy) {
   return sqrtf(m2);   // sqrt is monotone: sqrt(min) == min(sqrt), bit-exact
 }
 
+// +inf for an occupied cell, 0 for a free one (costs are >= 0: max(m, wall) keeps
+// free cells and pins occupied ones), from the tile's free bit mask without a
+// per-cell lane mask
+__device__ __forceinline__ float wall(const uint32_t *freem, int bit) {
+  const uint32_t f = (freem[bit >> 5] >> (bit & 31)) & 1u;
+  return __uint_as_float((f - 1u) & 0x7f800000u);
+}
+
+// eta (1/d - 1/r0)^2 before the goal mask, 0 outside the influence radius
+__device__ __forceinline__ float j_raw(const usv_cfg_t &c, float dte, float inv_r) {
+  if (!(dte < c.influence_radius)) return 0.f;
+  const float d = maxf(dte, 1e-3f);
+  const float t = 1.0f / d - inv_r;
+  return c.eta * (t * t);
+}
+__device__ __forceinline__ float goal_mask(const usv_cfg_t &c, float cv, float cell) {
+  return clampt((cv * cell) / c.safe_radius, 0.f, 1.f);
+}
+
 // ---------------------------------------------------------------- pass B ---
 __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) {
-  __shared__ float cost[G * G];
+  __shared__ float cost[GP * GP];
+  __shared__ uint8_t occ[G2];
   __shared__ float so[2 * USV_NOBST];
   __shared__ float slin[G];
-  __shared__ float red[16];
+  __shared__ float red[12][kWaveThreads / 64];
   const int n = b.n;
   const int count = b.ctl[USV_CTL_RESET_COUNT];
   const int tid = threadIdx.x;
@@ -63,6 +103,7 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
   const int r0 = tr * T, c0 = tc * T;
   const float cell = (float)((double)c.map_size / G);
   const float half_map = (float)((double)c.map_size / 2);
+  const float inv_r = (float)(1.0 / (double)c.influence_radius);
   for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
     const int e = b.reset_ids[slot];
     if (tid < 2 * USV_NOBST) so[tid] = b.obst[(size_t)tid * n + e];
@@ -73,56 +114,62 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
     int ix = (int)((tx + half_map) / cell), iy = (int)((ty + half_map) / cell);
     ix = min(max(ix, 0), G - 1);
     iy = min(max(iy, 0), G - 1);
-    // occupancy (compute_occupancy_and_sdf :66-104): free bits of the tile
-    uint32_t freem = 0;
-    bool tgt_free = true;
-    {
-      const float gx = slin[ix], gy = slin[iy];
-      tgt_free = !((min_dist(so, gx, gy) - c.obstacle_radius) <= 0.f) && ix > 0 && ix < G - 1 && iy > 0 &&
-                 iy < G - 1;
+    const bool tgt_free = !((min_dist(so, slin[ix], slin[iy]) - c.obstacle_radius) <= 0.f) && ix > 0 &&
+                          ix < G - 1 && iy > 0 && iy < G - 1;
+    for (int q = tid; q < 4 * GP; q += kWaveThreads) {   // the +inf ring
+      const int side = q / GP, k = q % GP;
+      const int idx = side == 0 ? k : side == 1 ? (GP - 1) * GP + k : side == 2 ? k * GP : k * GP + GP - 1;
+      cost[idx] = INFINITY;
     }
-    float v[T][T];
+    // ---- 1. occupancy / SDF (compute_occupancy_and_sdf :66-104) + initial cost ----
+    float *sdf_s = b.sdf + (size_t)slot * G2;
+    for (int q = tid; q < G2; q += kWaveThreads) {
+      const int r = q / G, cc = q % G;
+      const float sdf = min_dist(so, slin[cc], slin[r]) - c.obstacle_radius;
+      sdf_s[q] = sdf;
+      const bool border = r == 0 || r == G - 1 || cc == 0 || cc == G - 1;
+      const bool o = border || sdf <= 0.f;
+      occ[q] = o ? 1 : 0;
+      float init = INFINITY;
+      if (tgt_free) {
+        if (r == iy && cc == ix) init = 0.f;
+      } else if (!o) {
+        // reference's first synchronous sweep from an occupied target cell
+        const int di = r - iy, dj = cc - ix;
+        if (abs(di) <= 1 && abs(dj) <= 1 && (di || dj)) init = (di && dj) ? 1.414f : 1.0f;
+      }
+      cost[(r + 1) * GP + cc + 1] = init;
+    }
+    __syncthreads();
+    // ---- 2. cost-to-go: tiled chamfer sweeps until nothing changes ----
+    // h holds the tile (interior, persistent across iterations) and its halo
+    // ring (reloaded every iteration).  Updates only ever lower a value, so a
+    // cell changed iff its new value is below the old one; only the tile's
+    // edge cells are read by other threads, so only they go back to LDS.
+    float h[T + 2][T + 2];
+    uint32_t freem[4] = {0u, 0u, 0u, 0u};
     if (owner) {
 #pragma unroll
       for (int i = 0; i < T; ++i)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
-          const int r = r0 + i, cc = c0 + j;
-          const bool border = r == 0 || r == G - 1 || cc == 0 || cc == G - 1;
-          const bool occ = border || (min_dist(so, slin[cc], slin[r]) - c.obstacle_radius) <= 0.f;
-          if (!occ) freem |= 1u << (i * T + j);
-          float init = INFINITY;
-          if (tgt_free) {
-            if (r == iy && cc == ix) init = 0.f;
-          } else if (!occ) {
-            // reference's first synchronous sweep from an occupied target cell
-            const int di = r - iy, dj = cc - ix;
-            if (abs(di) <= 1 && abs(dj) <= 1 && (di || dj)) init = (di && dj) ? 1.414f : 1.0f;
-          }
-          v[i][j] = init;
-          cost[r * G + cc] = init;
+          const int q = (r0 + i) * G + c0 + j;
+          h[i + 1][j + 1] = cost[(r0 + i + 1) * GP + c0 + j + 1];
+          if (!occ[q]) freem[(i * T + j) >> 5] |= 1u << ((i * T + j) & 31);
         }
     }
-    __syncthreads();
     int it = 0;
     for (; it < kMaxIters; ++it) {
       int changed = 0;
       if (owner) {
-        // halo ring (7x7 minus the 5x5 interior); outside the grid = inf
-        float h[T + 2][T + 2];
 #pragma unroll
         for (int i = 0; i < T + 2; ++i)
 #pragma unroll
           for (int j = 0; j < T + 2; ++j) {
             if (i >= 1 && i <= T && j >= 1 && j <= T) continue;
-            const int r = r0 + i - 1, cc = c0 + j - 1;
-            h[i][j] = (r >= 0 && r < G && cc >= 0 && cc < G) ? cost[r * G + cc] : INFINITY;
+            h[i][j] = cost[(r0 + i) * GP + c0 + j];   // padded coordinates
           }
-#pragma unroll
-        for (int i = 0; i < T; ++i)
-#pragma unroll
-          for (int j = 0; j < T; ++j) h[i + 1][j + 1] = v[i][j];
-        // forward sweep (neighbours up/left), then backward sweep (down/right)
+        // forward raster sweep (up-left, up, up-right, left), then backward (mirror)
 #pragma unroll
         for (int i = 1; i <= T; ++i)
 #pragma unroll
@@ -132,8 +179,9 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
             m = fminf(m, h[i - 1][j] + 1.0f);
             m = fminf(m, h[i - 1][j + 1] + 1.414f);
             m = fminf(m, h[i][j - 1] + 1.0f);
-            m = fminf(m, h[i + 1][j - 1] + 1.414f);
-            h[i][j] = (freem >> ((i - 1) * T + (j - 1))) & 1u ? m : INFINITY;
+            const float nv = fmaxf(m, wall(freem, (i - 1) * T + (j - 1)));
+            changed |= nv < h[i][j];
+            h[i][j] = nv;
           }
 #pragma unroll
         for (int i = T; i >= 1; --i)
@@ -144,168 +192,181 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
             m = fminf(m, h[i + 1][j] + 1.0f);
             m = fminf(m, h[i + 1][j - 1] + 1.414f);
             m = fminf(m, h[i][j + 1] + 1.0f);
-            m = fminf(m, h[i - 1][j + 1] + 1.414f);
-            h[i][j] = (freem >> ((i - 1) * T + (j - 1))) & 1u ? m : INFINITY;
+            const float nv = fmaxf(m, wall(freem, (i - 1) * T + (j - 1)));
+            changed |= nv < h[i][j];
+            h[i][j] = nv;
           }
+        if (changed) {
 #pragma unroll
-        for (int i = 0; i < T; ++i)
+          for (int i = 1; i <= T; ++i)
 #pragma unroll
-          for (int j = 0; j < T; ++j) {
-            const float nv = h[i + 1][j + 1];
-            if (nv != v[i][j]) {
-              changed = 1;
-              v[i][j] = nv;
-              cost[(r0 + i) * G + (c0 + j)] = nv;
-            }
-          }
+            for (int j = 1; j <= T; ++j)
+              if (i == 1 || i == T || j == 1 || j == T) cost[(r0 + i) * GP + c0 + j] = h[i][j];
+        }
       }
       if (!__syncthreads_or(changed)) break;
     }
-    // write the G field (raw cost) in place, reduce the finite maximum
-    float fmax_ = -INFINITY;
-    for (int q = tid; q < G * G; q += kWaveThreads) {
-      const float x = cost[q];
-      b.field[(size_t)e * USV_GRID2 + q] = x;
-      if (isfinite(x)) fmax_ = fmaxf(fmax_, x);
+    if (owner) {
+#pragma unroll
+      for (int i = 1; i <= T; ++i)
+#pragma unroll
+        for (int j = 1; j <= T; ++j) cost[(r0 + i) * GP + c0 + j] = h[i][j];
     }
-    fmax_ = wave_max(fmax_);
-    if (lane == 0) red[wid] = fmax_;
     __syncthreads();
+    // ---- 3. raw cost out + per-env statistics (finite / infinite split) ----
+    float gmin = INFINITY, gmax = -INFINITY, jmin_f = INFINITY, jmax_f = -INFINITY, jall_f = 0.f;
+    float jrmin_i = INFINITY, jrmax_i = -INFINITY, jrall_i = 0.f;
+    int any_inf = 0, inside = 0;
+    float *Fe = b.field + (size_t)e * G2;
+    for (int q = tid; q < G2; q += kWaveThreads) {
+      const float g = cost[(q / G + 1) * GP + q % G + 1];
+      Fe[q] = g;
+      const float dte = sdf_s[q] - c.obstacle_radius;   // this thread's own phase-1 write
+      const bool ins = dte <= 0.f;
+      inside |= ins;
+      const float jr = j_raw(c, dte, inv_r);
+      if (isinf(g)) {
+        any_inf = 1;
+        jrall_i = fmaxf(jrall_i, jr);
+        if (!ins) { jrmin_i = fminf(jrmin_i, jr); jrmax_i = fmaxf(jrmax_i, jr); }
+      } else {
+        gmin = fminf(gmin, g);
+        gmax = fmaxf(gmax, g);
+        const float j = jr == 0.f && !(dte < c.influence_radius) ? 0.f : jr * goal_mask(c, g, cell);
+        jall_f = fmaxf(jall_f, j);
+        if (!ins) { jmin_f = fminf(jmin_f, j); jmax_f = fmaxf(jmax_f, j); }
+      }
+    }
+    float vals[10] = {wave_min(gmin), wave_max(gmax), 0.f, wave_min(jmin_f), wave_max(jmax_f), wave_max(jall_f),
+                      wave_min(jrmin_i), wave_max(jrmax_i), wave_max(jrall_i), 0.f};
+    if (lane == 0)
+      for (int k = 0; k < 10; ++k) red[k][wid] = vals[k];
+    const int has_inf = __syncthreads_or(any_inf);
+    const int has_inside = __syncthreads_or(inside);
     if (tid == 0) {
-      float m = -INFINITY;
-      for (int w = 0; w < kWaveThreads / 64; ++w) m = fmaxf(m, red[w]);
-      if (isfinite(m)) {
-        atomic_max_f32(&b.fscratch[0], m);
+      float a[10];
+      for (int k = 0; k < 10; ++k) a[k] = red[k][0];
+      for (int w = 1; w < kWaveThreads / 64; ++w) {
+        a[SS_GMIN_F] = fminf(a[SS_GMIN_F], red[SS_GMIN_F][w]);
+        a[SS_GMAX_F] = fmaxf(a[SS_GMAX_F], red[SS_GMAX_F][w]);
+        a[SS_JMIN_F_NI] = fminf(a[SS_JMIN_F_NI], red[SS_JMIN_F_NI][w]);
+        a[SS_JMAX_F_NI] = fmaxf(a[SS_JMAX_F_NI], red[SS_JMAX_F_NI][w]);
+        a[SS_JMAX_F_ALL] = fmaxf(a[SS_JMAX_F_ALL], red[SS_JMAX_F_ALL][w]);
+        a[SS_JRMIN_I_NI] = fminf(a[SS_JRMIN_I_NI], red[SS_JRMIN_I_NI][w]);
+        a[SS_JRMAX_I_NI] = fmaxf(a[SS_JRMAX_I_NI], red[SS_JRMAX_I_NI][w]);
+        a[SS_JRMAX_I_ALL] = fmaxf(a[SS_JRMAX_I_ALL], red[SS_JRMAX_I_ALL][w]);
+      }
+      float *st = b.slot_stats + (size_t)slot * 16;
+      for (int k = 0; k < 9; ++k) st[k] = a[k];
+      st[SS_ANY_INF] = has_inf ? 1.f : 0.f;
+      st[SS_INSIDE] = has_inside ? 1.f : 0.f;
+      st[SS_ITERS] = (float)it;   // iterations (diagnostic)
+      if (isfinite(a[SS_GMAX_F])) {
+        atomic_max_f32(&b.fscratch[0], a[SS_GMAX_F]);
         atomicOr(&b.ctl[USV_CTL_ANY_FINITE], 1);
       }
-      b.slot_stats[(size_t)slot * 8 + 7] = (float)it;   // iterations (diagnostic)
     }
     __syncthreads();
   }
 }
 
-// per-cell repulsion before the "inside" override (compute_potential_field :194-260)
-struct CellJ {
-  float cv, j;
-  bool inside;
+// batch constants given every slot's statistics
+struct BatchK {
+  float inf_val, mask_inf;
 };
-
-__device__ __forceinline__ CellJ cell_j(const usv_cfg_t &c, const float *so, const float *slin, float gval,
-                                        float inf_val, float cell, float inv_r, int q) {
-  const int r = q / G, cc = q % G;
-  const float sdf = min_dist(so, slin[cc], slin[r]) - c.obstacle_radius;
-  const float cv = isinf(gval) ? inf_val : gval;
-  const float dte = sdf - c.obstacle_radius;
-  const float rmask = clampt((cv * cell) / c.safe_radius, 0.f, 1.f);
-  float j = 0.f;
-  if (dte < c.influence_radius) {
-    const float d = maxf(dte, 1e-3f);
-    const float t = 1.0f / d - inv_r;
-    j = c.eta * (t * t) * rmask;
-  }
-  return CellJ{cv, j, dte <= 0.f};
-}
-
-// ---------------------------------------------------------------- pass C ---
-__global__ __launch_bounds__(kWaveThreads) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
-  __shared__ float so[2 * USV_NOBST];
-  __shared__ float slin[G];
-  __shared__ float red[5][16];
-  const int n = b.n;
-  const int count = b.ctl[USV_CTL_RESET_COUNT];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+__device__ __forceinline__ BatchK batch_k(const usv_cfg_t &c, const usv_bufs_t &b) {
   const float max_val = b.ctl[USV_CTL_ANY_FINITE] ? b.fscratch[0] : 100.0f;
   const float inf_val = max_val * 1.5f;
   const float cell = (float)((double)c.map_size / G);
-  const float inv_r = (float)(1.0 / (double)c.influence_radius);
-  for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
-    const int e = b.reset_ids[slot];
-    if (tid < 2 * USV_NOBST) so[tid] = b.obst[(size_t)tid * n + e];
-    if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
-    __syncthreads();
-    float gmin = INFINITY, gmax = -INFINITY, jmin = INFINITY, jmax_ni = -INFINITY, jmax_all = 0.f;
-    int inside = 0;
-    const float *Fe = b.field + (size_t)e * USV_GRID2;
-    for (int q = tid; q < G * G; q += kWaveThreads) {
-      const CellJ cj = cell_j(c, so, slin, Fe[q], inf_val, cell, inv_r, q);
-      gmin = fminf(gmin, cj.cv);
-      gmax = fmaxf(gmax, cj.cv);
-      jmax_all = fmaxf(jmax_all, cj.j);
-      if (cj.inside) inside = 1;
-      else { jmin = fminf(jmin, cj.j); jmax_ni = fmaxf(jmax_ni, cj.j); }
-    }
-    gmin = wave_min(gmin); gmax = wave_max(gmax); jmin = wave_min(jmin); jmax_ni = wave_max(jmax_ni);
-    jmax_all = wave_max(jmax_all);
-    if (lane == 0) {
-      red[0][wid] = gmin; red[1][wid] = gmax; red[2][wid] = jmin; red[3][wid] = jmax_ni; red[4][wid] = jmax_all;
-    }
-    const int has_inside = __syncthreads_or(inside);
-    if (tid == 0) {
-      float a0 = INFINITY, a1 = -INFINITY, a2 = INFINITY, a3 = -INFINITY, a4 = 0.f;
-      for (int w = 0; w < kWaveThreads / 64; ++w) {
-        a0 = fminf(a0, red[0][w]); a1 = fmaxf(a1, red[1][w]); a2 = fminf(a2, red[2][w]);
-        a3 = fmaxf(a3, red[3][w]); a4 = fmaxf(a4, red[4][w]);
-      }
-      float *st = b.slot_stats + (size_t)slot * 8;
-      st[0] = a0; st[1] = a1; st[2] = a2; st[3] = a3; st[4] = has_inside ? 1.f : 0.f;
-      atomic_max_f32(&b.fscratch[1], a4);          // J.max() over the batch (:257)
-      if (has_inside) atomicOr(&b.ctl[USV_CTL_ANY_INSIDE], 1);
-    }
-    __syncthreads();
+  return BatchK{inf_val, goal_mask(c, inf_val, cell)};
+}
+
+// ---------------------------------------------------------------- pass C ---
+__global__ __launch_bounds__(1024) void k_field_batch(usv_cfg_t c, usv_bufs_t b) {
+  __shared__ float red[16];
+  __shared__ int ins;
+  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int tid = threadIdx.x;
+  if (count <= 0) return;
+  const BatchK k = batch_k(c, b);
+  if (tid == 0) ins = 0;
+  __syncthreads();
+  float jm = 0.f;
+  int inside = 0;
+  for (int s = tid; s < count; s += 1024) {
+    const float *st = b.slot_stats + (size_t)s * 16;
+    jm = fmaxf(jm, st[SS_JMAX_F_ALL]);
+    if (st[SS_ANY_INF] != 0.f) jm = fmaxf(jm, st[SS_JRMAX_I_ALL] * k.mask_inf);   // monotone in the raw value
+    inside |= st[SS_INSIDE] != 0.f;
+  }
+  jm = wave_max(jm);
+  if ((tid & 63) == 0) red[tid >> 6] = jm;
+  if (inside) ins = 1;
+  __syncthreads();
+  if (tid == 0) {
+    float m = 0.f;
+    for (int w = 0; w < 16; ++w) m = fmaxf(m, red[w]);
+    b.fscratch[1] = m;                                   // J.max() over the batch (:257)
+    b.ctl[USV_CTL_ANY_INSIDE] = ins;
   }
 }
 
 // ---------------------------------------------------------------- pass D ---
-__global__ __launch_bounds__(kWaveThreads) void k_field_final(usv_cfg_t c, usv_bufs_t b) {
-  __shared__ float so[2 * USV_NOBST];
-  __shared__ float slin[G];
-  const int n = b.n;
+__global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) {
   const int count = b.ctl[USV_CTL_RESET_COUNT];
-  const int tid = threadIdx.x;
-  const float max_val = b.ctl[USV_CTL_ANY_FINITE] ? b.fscratch[0] : 100.0f;
-  const float inf_val = max_val * 1.5f;
+  const BatchK k = batch_k(c, b);
   const float cell = (float)((double)c.map_size / G);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
   const bool any_inside = b.ctl[USV_CTL_ANY_INSIDE] != 0;
   const float cur_max = b.fscratch[1];
   const float high = (cur_max > 1e-6f) ? cur_max * 10.0f : 100.0f;
-  for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
+  const int items = count * kChunks;
+  for (int w = blockIdx.x; w < items; w += gridDim.x) {
+    const int slot = w / kChunks, ch = w % kChunks;
     const int e = b.reset_ids[slot];
-    if (tid < 2 * USV_NOBST) so[tid] = b.obst[(size_t)tid * n + e];
-    if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
-    __syncthreads();
-    const float *st = b.slot_stats + (size_t)slot * 8;
-    const float gmin = st[0], gmax = st[1];
-    const bool has_inside = st[4] == 1.f;
-    float jmn = st[2], jmx = st[3];
+    const float *st = b.slot_stats + (size_t)slot * 16;
+    const bool has_inf = st[SS_ANY_INF] != 0.f;
+    const bool has_inside = st[SS_INSIDE] != 0.f;
+    const float gmin = has_inf ? fminf(st[SS_GMIN_F], k.inf_val) : st[SS_GMIN_F];
+    const float gmax = has_inf ? fmaxf(st[SS_GMAX_F], k.inf_val) : st[SS_GMAX_F];
+    float jmn = st[SS_JMIN_F_NI], jmx = st[SS_JMAX_F_NI];
+    if (isfinite(st[SS_JRMIN_I_NI])) {       // some infinite-cost, not-inside cell exists
+      jmn = fminf(jmn, st[SS_JRMIN_I_NI] * k.mask_inf);
+      jmx = fmaxf(jmx, st[SS_JRMAX_I_NI] * k.mask_inf);
+    }
     if (any_inside && has_inside) { jmn = fminf(jmn, high); jmx = fmaxf(jmx, high); }
     const float gden = (gmax - gmin) + 1e-6f;
     const float jden = (jmx - jmn) + 1e-6f;
-    float *Fe = b.field + (size_t)e * USV_GRID2;
-    for (int q = tid; q < G * G; q += kWaveThreads) {
-      const CellJ cj = cell_j(c, so, slin, Fe[q], inf_val, cell, inv_r, q);
-      const float jv = (any_inside && cj.inside) ? high : cj.j;
-      const float gn = (cj.cv - gmin) / gden;
+    float *Fe = b.field + (size_t)e * G2;
+    const float *sdf_s = b.sdf + (size_t)slot * G2;
+    const int q1 = min(G2, (ch + 1) * kChunk);
+    for (int q = ch * kChunk + threadIdx.x; q < q1; q += 256) {
+      const float g = Fe[q];
+      const float cv = isinf(g) ? k.inf_val : g;
+      const float dte = sdf_s[q] - c.obstacle_radius;
+      const float jr = j_raw(c, dte, inv_r);
+      const float j = (dte < c.influence_radius) ? jr * goal_mask(c, cv, cell) : 0.f;
+      const float jv = (any_inside && dte <= 0.f) ? high : j;
+      const float gn = (cv - gmin) / gden;
       const float jn = (jv - jmn) / jden;
       Fe[q] = gn + c.field_alpha * jn;
     }
-    __syncthreads();
   }
 }
 
 }  // namespace
 
 extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream) {
-  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field) return 1;
+  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field || !b->sdf) return 1;
   hipStream_t s = (hipStream_t)stream;
   // the reset count lives on the device: launch persistent grids, blocks loop over slots
-  const int grid_b = b->n < 256 ? b->n : 256;
-  const int grid_cd = b->n < 1024 ? b->n : 1024;
+  const int grid_b = b->n < 512 ? b->n : 512;
+  const int grid_d = b->n * kChunks < 4096 ? b->n * kChunks : 4096;
   hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_stats, dim3(grid_cd), dim3(kWaveThreads), 0, s, *cfg, *b);
+  hipLaunchKernelGGL(k_field_batch, dim3(1), dim3(1024), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_final, dim3(grid_cd), dim3(kWaveThreads), 0, s, *cfg, *b);
+  hipLaunchKernelGGL(k_field_final, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   return 0;
 }

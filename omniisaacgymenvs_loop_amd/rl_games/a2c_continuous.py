@@ -151,8 +151,8 @@ class A2CAgent:
         self.batch_size = self.horizon_length * self.num_actors
         self.minibatch_size = int(config.get("minibatch_size", self.num_actors * config.get("minibatch_size_per_env", 0)))
         assert self.batch_size % self.minibatch_size == 0, "batch_size % minibatch_size != 0 (a2c_common.py:240)"
-        if self.minibatch_size % 64 != 0:
-            raise ValueError("minibatch_size must be a multiple of 64 (kernel row block)")
+        if self.minibatch_size % 32 != 0:
+            raise ValueError("minibatch_size must be a multiple of 32 (kernel row block)")
         self.num_minibatches = self.batch_size // self.minibatch_size
         self.mini_epochs_num = int(config["mini_epochs"])
         self.max_epochs = int(config.get("max_epochs", -1))
@@ -246,7 +246,8 @@ class A2CAgent:
         self.cur_len = torch.zeros(N, **f32)
         self.meter = torch.zeros((H, 4), **f32)
         self.kls = torch.zeros(self.mini_epochs_num * self.num_minibatches, **f32)
-        self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 4), **f32)
+        # per minibatch: a_loss, c_loss, entropy, b_loss, kl (this rank), written by the reduce kernel
+        self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 8), **f32)
 
     # ------------------------------------------------------------- rollout
     def env_reset(self):
@@ -302,13 +303,11 @@ class A2CAgent:
                 c.call("ppo_minibatch_grad", cfg, c.ptr(self.model_params), c.ptr(self.obs_rms),
                        c.ptr(self.val_rms), int(mini_ep == 0), i, c.ptr(self.exp_obs), c.ptr(self.exp_act),
                        c.ptr(self.exp_nlp), c.ptr(self.exp_val), c.ptr(self.exp_ret), c.ptr(self.exp_adv),
-                       c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.grad), c.ptr(self.losses),
+                       c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.grad), c.ptr(self.loss_log[k]),
                        c.ptr(self.partials), c.ptr(self.work), s)
                 scale = self._allreduce_grad()
                 c.call("ppo_minibatch_apply", cfg, c.ptr(self.model_params), c.ptr(self.grad), c.ptr(self.adam_m),
-                       c.ptr(self.adam_v), c.ptr(self.opt), float(scale), s)
-                self.kls[k:k + 1].copy_(self.opt[2:3])
-                self.loss_log[k].copy_(self.losses[:4])
+                       c.ptr(self.adam_v), c.ptr(self.opt), float(scale), c.ptr(self.kls[k:k + 1]), s)
                 k += 1
 
     def train_epoch(self):

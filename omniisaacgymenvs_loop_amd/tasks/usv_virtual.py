@@ -111,7 +111,8 @@ class USVVirtual:
         self.extras_buf = Z(NSTAT, **f32)
         self.extras_acc = Z(NSTAT, **f32)
         self.field_old_tgt = Z((2, n), **f32)
-        self.slot_stats = Z((n, 8), **f32)
+        self.slot_stats = Z((n, 16), **f32)
+        self.sdf = torch.empty((n, GRID2), **f32)      # per-reset-slot SDF scratch of the field kernels
         self.lut = Z((2, 1000), **f32)
         tl, tr = thruster_tables(self._task_cfg)
         self._tables = torch.tensor(np.stack([tl, tr]), **f32)
@@ -143,6 +144,7 @@ class USVVirtual:
         b.extras, b.extras_acc = p(self.extras_buf), p(self.extras_acc)
         b.field_old_tgt = p(self.field_old_tgt)
         b.slot_stats = p(self.slot_stats)
+        b.sdf = p(self.sdf)
         b.grid_lin = p(self.grid_lin) if self.grid_lin is not None else None
         return b
 

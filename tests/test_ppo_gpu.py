@@ -126,7 +126,7 @@ def test_minibatch_epoch_vs_reference(ppo):
     ag.update_epoch_minibatches()
     torch.cuda.synchronize()
     np.testing.assert_allclose(ag.kls.cpu().numpy(), ppo["kl"], rtol=3e-3, atol=1e-7)
-    np.testing.assert_allclose(ag.loss_log.cpu().numpy(), ppo["losses"], rtol=3e-3, atol=1e-6)
+    np.testing.assert_allclose(ag.loss_log[:, :4].cpu().numpy(), ppo["losses"], rtol=3e-3, atol=1e-6)
     np.testing.assert_allclose(float(ag.opt[0]), ppo["lr_seq"][-1], rtol=1e-6)
     orms = ag.obs_rms.cpu().numpy()
     np.testing.assert_allclose(orms[:33], ppo["final_running_mean_std__running_mean_std__state__running_mean"],
