@@ -29,6 +29,7 @@ import torch.distributed as dist
 from .. import _capi
 from .._abi import DEFINES, PpoCfg
 from . import checkpoint as ckpt
+from . import dist_util
 from . import vecenv
 
 NIN, NH, NA = DEFINES["PPO_NIN"], DEFINES["PPO_NH"], DEFINES["PPO_NA"]
@@ -215,7 +216,7 @@ class A2CAgent:
         N, H = self.num_actors, self.horizon_length
         self.model_params = default_linear_init(self.seed).to(dev)
         if self.multi_gpu:
-            dist.broadcast(self.model_params, 0)     # a2c_common.py:1354 (initial weights from rank 0)
+            dist_util.broadcast_params(self.model_params, 0)   # a2c_common.py:1354 (initial weights from rank 0)
         self.adam_m = torch.zeros(NPARAM, **f32)
         self.adam_v = torch.zeros(NPARAM, **f32)
         self.opt = torch.zeros(8, **f32)
@@ -290,8 +291,7 @@ class A2CAgent:
         with the minibatch KL in the same buffer (a2c_common.py:1218-1222)."""
         if not self.multi_gpu or self.rank_size == 1:
             return 1.0
-        dist.all_reduce(self.grad[:NPARAM + 1], op=dist.ReduceOp.SUM)
-        return 1.0 / self.rank_size
+        return dist_util.allreduce_grad(self.grad[:NPARAM + 1])
 
     def update_epoch_minibatches(self) -> None:
         c = _capi
