@@ -195,10 +195,12 @@ typedef struct usv_bufs {
   float   *extras;                 /* [USV_NSTAT] extras["episode"] (persistent) */
   float   *extras_acc;             /* [USV_NSTAT] scratch sums */
   float   *field_old_tgt;          /* [2][n] target used by the field of each reset env */
-  float   *slot_stats;             /* [n][16] per-reset-slot field statistics (scratch) */
+  float   *slot_stats;             /* [n][USV_FIELD_SLOT_STATS] per-reset-slot field statistics (scratch) */
   float   *sdf;                    /* [n][150*150] per-reset-slot signed distance (scratch) */
   const float *grid_lin;           /* [150] cell centres of the field grid */
 } usv_bufs_t;
+
+#define USV_FIELD_SLOT_STATS 160   /* 16 + 12 per 2048-cell chunk (11 chunks) */
 
 /* control words */
 #define USV_CTL_RESET_COUNT 0

@@ -19,6 +19,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libusv_hip.so")
+# instrumented build (per-workgroup phase timestamps, tools/phase_probe.py); selected with USV_HIP_PROBE=1
+PROBE_LIB_PATH = os.path.join(LIB_DIR, "libusv_hip_probe.so")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("usv_env.hip", "usv_field.hip", "ppo.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "usv_device.h"), os.path.join(ROOT, "include", "usv_hip.h")]
 
@@ -29,18 +31,19 @@ HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
 _lib = None
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, probe: bool = False) -> str:
     """Compile the HIP kernels for gfx950 into lib/libusv_hip.so (in-tree)."""
     os.makedirs(LIB_DIR, exist_ok=True)
-    if not force and os.path.exists(LIB_PATH):
-        lib_m = os.path.getmtime(LIB_PATH)
+    out = PROBE_LIB_PATH if probe else LIB_PATH
+    if not force and os.path.exists(out):
+        lib_m = os.path.getmtime(out)
         if all(os.path.getmtime(d) <= lib_m for d in DEPS):
-            return LIB_PATH
-    cmd = ["hipcc"] + HIPCC_FLAGS + ["-o", LIB_PATH] + SOURCES
+            return out
+    cmd = ["hipcc"] + HIPCC_FLAGS + (["-DUSV_PHASE_PROBE"] if probe else []) + ["-o", out] + SOURCES
     if verbose:
         print(" ".join(cmd))
     subprocess.check_call(cmd)
-    return LIB_PATH
+    return out
 
 
 def _declare(lib):
@@ -70,10 +73,11 @@ def _declare(lib):
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+        path = PROBE_LIB_PATH if os.getenv("USV_HIP_PROBE") == "1" else LIB_PATH
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
                                f"g.build()'` (hipcc --offload-arch=gfx950)")
-        _lib = _declare(ctypes.CDLL(LIB_PATH))
+        _lib = _declare(ctypes.CDLL(path))
     return _lib
 
 

@@ -22,6 +22,8 @@
 // in a fixed order.  clip + Adam + the adaptive LR run in k_apply.
 #include "usv_device.h"
 
+USV_PROBE_DEFINE(ppo)
+
 namespace {
 
 constexpr int NIN = PPO_NIN, NH = PPO_NH, NA = PPO_NA;
@@ -442,10 +444,13 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
   const int i = lane & 31, h = lane >> 5;
   const int rb0 = row0 + blockIdx.x * RB;             // global row of this block
   const float invB = 1.0f / (float)c.minibatch;
+  USV_PHASE(ppo, 0);
   stage_weights(P, s);
   stage_obs(e_obs, rb0, RB, obs_rms, c.normalize_input != 0, c.rms_eps, s);
   __syncthreads();
+  USV_PHASE(ppo, 1);
   block_forward(P, s);
+  USV_PHASE(ppo, 2);
   float *part = partials + (size_t)blockIdx.x * NPART;
   // ---- per-row losses and output gradients (wave 0, lanes < RB) ----
   if (tid < 64) {
@@ -520,6 +525,7 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
     }
   }
   __syncthreads();
+  USV_PHASE(ppo, 3);
   // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 ----
   {
     const int j = tid & (NH - 1), half = tid >> 7;     // rows 16*half .. 16*half+15
@@ -550,6 +556,7 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
     for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
     part[q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV] = sacc;
   }
+  USV_PHASE(ppo, 4);
   // ---- dW2[j][k] = sum_r dz2[r][j] h1[r][k]: wave w owns rows j in [32w, 32w+32), 4 k tiles ----
   {
     f32x16 acc[4] = {};
@@ -565,6 +572,7 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
 #pragma unroll
       for (int q = 0; q < 16; ++q) part[PPO_OFF_W2 + (32 * w + crow(q, h)) * NH + 32 * kt + i] = acc[kt][q];
   }
+  USV_PHASE(ppo, 5);
   // ---- dh1[r][k] = sum_j dz2[r][j] W2[j][k]: wave w owns columns k in [32w, 32w+32) ----
   f32x16 dh = {};
 #pragma unroll 16
@@ -572,6 +580,7 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
     const int j = 2 * st + h;
     dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + 32 * w + i], dh);
   }
+  USV_PHASE(ppo, 6);
   __syncthreads();   // every read of h1 (dW2 operand) is done
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
@@ -580,6 +589,7 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
     s.h1[idx] = dh[q] * (1.f - hv * hv);   // h1 := dz1
   }
   __syncthreads();
+  USV_PHASE(ppo, 7);
   // ---- dW1[j][k] = sum_r dz1[r][j] x[r][k] (k < 32 on the matrix cores), db1 ----
   {
     f32x16 acc = {};
@@ -602,6 +612,7 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
     for (int r = 0; r < RB; ++r) a += s.h1[r * HS + j];
     part[PPO_OFF_B1 + j] = a;
   }
+  USV_PHASE(ppo, 8);
 }
 
 // sum the per-block partials (fixed order => deterministic) into grad[]:

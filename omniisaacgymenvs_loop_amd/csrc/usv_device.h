@@ -66,6 +66,24 @@ __device__ __forceinline__ void atomic_max_f32(float *addr, float v) {
   else atomicMin((unsigned int *)addr, __float_as_uint(v));
 }
 
+// Phase probe (instrumented build only, -DUSV_PHASE_PROBE): thread 0 of each of
+// the first 4096 workgroups stamps wall_clock64() (100 MHz) at phase k of the
+// last launch of an instrumented kernel; usv_probe_read_<tu>() copies it out.
+#ifdef USV_PHASE_PROBE
+#define USV_PROBE_DEFINE(tu)                                                           \
+  __device__ unsigned long long g_probe_##tu[4096][16];                                \
+  extern "C" int usv_probe_read_##tu(void *host_out) {                                 \
+    return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(g_probe_##tu), sizeof(g_probe_##tu)); \
+  }
+#define USV_PHASE(tu, k)                                                               \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_probe_##tu[blockIdx.x][k] = wall_clock64(); \
+  } while (0)
+#else
+#define USV_PROBE_DEFINE(tu)
+#define USV_PHASE(tu, k) ((void)0)
+#endif
+
 #define USV_CHECK_LAUNCH()                                   \
   do {                                                       \
     hipError_t _e = hipGetLastError();                       \

@@ -29,17 +29,19 @@
 // k_field_final (grid-stride over (slot, 2048-cell chunk)): normalisation.
 #include "usv_device.h"
 
+USV_PROBE_DEFINE(field)
+
 namespace {
 
 constexpr int G = USV_GRID;
 constexpr int G2 = USV_GRID2;
 constexpr int T = 10;            // tile edge
 constexpr int NT = G / T;        // 15 tiles per edge
-constexpr int GP = G + 2;        // LDS cost grid padded with an +inf ring (no halo bounds checks)
 constexpr int kWaveThreads = 256;
 constexpr int kMaxIters = 4096;  // safety cap (never reached)
 constexpr int kChunk = 2048;     // cells per k_field_final work item
 constexpr int kChunks = (G2 + kChunk - 1) / kChunk;
+constexpr int kSlotStride = USV_FIELD_SLOT_STATS;   // floats per reset slot: 16 final + 12 per chunk
 
 // slot_stats layout (per reset slot)
 enum {
@@ -88,9 +90,22 @@ __device__ __forceinline__ float goal_mask(const usv_cfg_t &c, float cv, float c
 }
 
 // ---------------------------------------------------------------- pass B ---
+// LDS: the SDF grid (90 KB, also the occupancy source), the four edge rows /
+// columns of every tile (the only cells other threads read; a ring of +inf
+// tiles around the 15x15 tile grid removes bounds checks), the per-row
+// obstacle dy table of the separable SDF, and each tile's last-changed
+// iteration (a tile is swept only while it or a neighbour still changes).
+constexpr int NTP = NT + 2;                     // padded tile grid edge
+constexpr uint32_t kInfBits = 0x7f800000u;      // +inf
+constexpr uint32_t kOcc = 0xFFFFFFFFu;          // occupied cell marker (a NaN above +inf in u32 order)
+enum { E_TOP = 0, E_BOT, E_LEFT, E_RIGHT };
+constexpr int kSegRows = 30;                    // SDF work unit: one column x 30 rows
+constexpr int kUnits = G * (G / kSegRows);
+
 __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) {
-  __shared__ float cost[GP * GP];
-  __shared__ uint8_t occ[G2];
+  __shared__ float sdf_l[G2];
+  __shared__ float edge[4][NTP * NTP][T];
+  __shared__ int lastc[NTP * NTP];
   __shared__ float so[2 * USV_NOBST];
   __shared__ float slin[G];
   __shared__ float red[12][kWaveThreads / 64];
@@ -98,175 +113,221 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
   const int count = b.ctl[USV_CTL_RESET_COUNT];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  const bool owner = tid < NT * NT;
-  const int tr = owner ? tid / NT : 0, tc = owner ? tid % NT : 0;
+  // tile of this thread; waves own compact quadrants of the tile grid (8x8,
+  // 8x7, 7x8, 7x7 tiles) so a wave idles as a whole while its region is ahead
+  // of / behind the front
+  const int quad = tid >> 6, qk = tid & 63;
+  const int qr = quad >> 1, qc = quad & 1;
+  const int qw = qc ? NT - 8 : 8, qh = qr ? NT - 8 : 8;
+  const bool tile_ok = qk < qw * qh;
+  const int tr = tile_ok ? qr * 8 + qk / qw : 0;
+  const int tc = tile_ok ? qc * 8 + qk % qw : 0;
   const int r0 = tr * T, c0 = tc * T;
+  const int tp = (tr + 1) * NTP + tc + 1;
   const float cell = (float)((double)c.map_size / G);
   const float half_map = (float)((double)c.map_size / 2);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
+  // the +inf ring of tiles (constant for the launch)
+  for (int q = tid; q < 4 * NTP * NTP * T; q += kWaveThreads) {
+    const int t = (q / T) % (NTP * NTP);
+    const int rr = t / NTP, cc = t % NTP;
+    if (rr == 0 || rr == NTP - 1 || cc == 0 || cc == NTP - 1) (&edge[0][0][0])[q] = INFINITY;
+  }
+  for (int q = tid; q < NTP * NTP; q += kWaveThreads) lastc[q] = -1000;
   for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
+    USV_PHASE(field, 0);
     const int e = b.reset_ids[slot];
     if (tid < 2 * USV_NOBST) so[tid] = b.obst[(size_t)tid * n + e];
     if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
     __syncthreads();
+#ifdef USV_PHASE_PROBE
+    if (tid == 0 && blockIdx.x < 4096) g_probe_field[blockIdx.x][12] = wall_clock64();
+#endif
+    // ---- 1. SDF (compute_occupancy_and_sdf :66-104), separable: one column x 30 rows per unit ----
+    float *sdf_s = b.sdf + (size_t)slot * G2;
+    float oy[USV_NOBST];
+#pragma unroll
+    for (int o = 0; o < USV_NOBST; ++o) oy[o] = so[2 * o + 1];
+    for (int u = tid; u < kUnits; u += kWaveThreads) {
+      const int cc = u % G, rs = (u / G) * kSegRows;
+      const float gx = slin[cc];
+      float dx2[USV_NOBST];
+#pragma unroll
+      for (int o = 0; o < USV_NOBST; ++o) {
+        const float dx = gx - so[2 * o];
+        dx2[o] = dx * dx;
+      }
+      // three rows at a time (independent chains), each a balanced min tree over
+      // the 16 obstacles; squared distances are >= 0: float order == u32 order
+      for (int r = rs; r < rs + kSegRows; r += 3) {
+        float sd[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float gy = slin[r + k];
+          uint32_t a[USV_NOBST];
+#pragma unroll
+          for (int o = 0; o < USV_NOBST; ++o) {
+            const float dy = gy - oy[o];
+            a[o] = __float_as_uint(fmaf(dy, dy, dx2[o]));
+          }
+#pragma unroll
+          for (int w = USV_NOBST / 2; w >= 1; w >>= 1)
+#pragma unroll
+            for (int o = 0; o < w; ++o) a[o] = min(a[o], a[o + w]);
+          sd[k] = sqrtf(__uint_as_float(a[0])) - c.obstacle_radius;   // sqrt(min) == min(sqrt), bit-exact
+        }
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          sdf_l[(r + k) * G + cc] = sd[k];
+          sdf_s[(r + k) * G + cc] = sd[k];
+        }
+      }
+    }
+    __syncthreads();
+    USV_PHASE(field, 1);
+#ifdef USV_PHASE_PROBE
+    if (tid == 0 && blockIdx.x < 4096) g_probe_field[blockIdx.x][13] = clock64();
+#endif
     // target cell (compute_cost_field_wavefront :148-154)
     const float tx = b.field_old_tgt[e], ty = b.field_old_tgt[n + e];
     int ix = (int)((tx + half_map) / cell), iy = (int)((ty + half_map) / cell);
     ix = min(max(ix, 0), G - 1);
     iy = min(max(iy, 0), G - 1);
-    const bool tgt_free = !((min_dist(so, slin[ix], slin[iy]) - c.obstacle_radius) <= 0.f) && ix > 0 &&
-                          ix < G - 1 && iy > 0 && iy < G - 1;
-    for (int q = tid; q < 4 * GP; q += kWaveThreads) {   // the +inf ring
-      const int side = q / GP, k = q % GP;
-      const int idx = side == 0 ? k : side == 1 ? (GP - 1) * GP + k : side == 2 ? k * GP : k * GP + GP - 1;
-      cost[idx] = INFINITY;
-    }
-    // ---- 1. occupancy / SDF (compute_occupancy_and_sdf :66-104) + initial cost ----
-    float *sdf_s = b.sdf + (size_t)slot * G2;
-    for (int q = tid; q < G2; q += kWaveThreads) {
-      const int r = q / G, cc = q % G;
-      const float sdf = min_dist(so, slin[cc], slin[r]) - c.obstacle_radius;
-      sdf_s[q] = sdf;
-      const bool border = r == 0 || r == G - 1 || cc == 0 || cc == G - 1;
-      const bool o = border || sdf <= 0.f;
-      occ[q] = o ? 1 : 0;
-      float init = INFINITY;
-      if (tgt_free) {
-        if (r == iy && cc == ix) init = 0.f;
-      } else if (!o) {
-        // reference's first synchronous sweep from an occupied target cell
-        const int di = r - iy, dj = cc - ix;
-        if (abs(di) <= 1 && abs(dj) <= 1 && (di || dj)) init = (di && dj) ? 1.414f : 1.0f;
-      }
-      cost[(r + 1) * GP + cc + 1] = init;
-    }
-    __syncthreads();
+    const bool tgt_free = !(sdf_l[iy * G + ix] <= 0.f) && ix > 0 && ix < G - 1 && iy > 0 && iy < G - 1;
     // ---- 2. cost-to-go: tiled chamfer sweeps until nothing changes ----
-    // h holds the tile (interior, persistent across iterations) and its halo
-    // ring (reloaded every iteration).  Updates only ever lower a value, so a
-    // cell changed iff its new value is below the old one; only the tile's
-    // edge cells are read by other threads, so only they go back to LDS.
+    // Costs are >= 0, so float order == unsigned order of the bit patterns:
+    // the relaxation runs on u32 min (no NaN canonicalisation).  An occupied
+    // cell holds 0xFFFFFFFF (a NaN): every neighbour's "NaN + w" compares above
+    // +inf and drops out of the min, and the cell keeps its own value by one
+    // max with its own sign bit.  Updates only ever lower a value.
     float h[T + 2][T + 2];
-    uint32_t freem[4] = {0u, 0u, 0u, 0u};
-    if (owner) {
+    if (tile_ok) {
 #pragma unroll
       for (int i = 0; i < T; ++i)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
-          const int q = (r0 + i) * G + c0 + j;
-          h[i + 1][j + 1] = cost[(r0 + i + 1) * GP + c0 + j + 1];
-          if (!occ[q]) freem[(i * T + j) >> 5] |= 1u << ((i * T + j) & 31);
+          const int r = r0 + i, cc = c0 + j;
+          const bool border = r == 0 || r == G - 1 || cc == 0 || cc == G - 1;
+          const bool o = border || sdf_l[r * G + cc] <= 0.f;
+          float init = INFINITY;
+          if (o) {
+            init = __uint_as_float(kOcc);
+          } else if (tgt_free) {
+            if (r == iy && cc == ix) init = 0.f;
+          } else {
+            // reference's first synchronous sweep from an occupied target cell
+            const int di = r - iy, dj = cc - ix;
+            if (abs(di) <= 1 && abs(dj) <= 1 && (di || dj)) init = (di && dj) ? 1.414f : 1.0f;
+          }
+          h[i + 1][j + 1] = init;
         }
+#pragma unroll
+      for (int k = 0; k < T; ++k) {
+        edge[E_TOP][tp][k] = h[1][k + 1];
+        edge[E_BOT][tp][k] = h[T][k + 1];
+        edge[E_LEFT][tp][k] = h[k + 1][1];
+        edge[E_RIGHT][tp][k] = h[k + 1][T];
+      }
+      lastc[tp] = 0;
     }
+    __syncthreads();
     int it = 0;
     for (; it < kMaxIters; ++it) {
       int changed = 0;
-      if (owner) {
+      bool dirty = false;
+      if (tile_ok) {
 #pragma unroll
-        for (int i = 0; i < T + 2; ++i)
+        for (int dr = -1; dr <= 1; ++dr)
 #pragma unroll
-          for (int j = 0; j < T + 2; ++j) {
-            if (i >= 1 && i <= T && j >= 1 && j <= T) continue;
-            h[i][j] = cost[(r0 + i) * GP + c0 + j];   // padded coordinates
+          for (int dc = -1; dc <= 1; ++dc) dirty |= lastc[tp + dr * NTP + dc] >= it - 1;
+      }
+      if (dirty) {
+#pragma unroll
+        for (int k = 0; k < T; ++k) {
+          h[0][k + 1] = edge[E_BOT][tp - NTP][k];
+          h[T + 1][k + 1] = edge[E_TOP][tp + NTP][k];
+          h[k + 1][0] = edge[E_RIGHT][tp - 1][k];
+          h[k + 1][T + 1] = edge[E_LEFT][tp + 1][k];
+        }
+        h[0][0] = edge[E_BOT][tp - NTP - 1][T - 1];
+        h[0][T + 1] = edge[E_BOT][tp - NTP + 1][0];
+        h[T + 1][0] = edge[E_TOP][tp + NTP - 1][T - 1];
+        h[T + 1][T + 1] = edge[E_TOP][tp + NTP + 1][0];
+        // forward raster sweep (up-left, up, up-right, left), then backward (mirror).
+        // Cell (i, j) of the forward sweep depends on (i, j-1) and row i-1 up to
+        // column j+1, so cells with equal 2i + j are independent: emitting the
+        // sweep level by level gives the scheduler 3-5 independent chains (a
+        // single wave's dependent VALU op costs ~7 cycles on gfx950, an
+        // independent one ~4).  Same updates in a dependency-respecting order
+        // (each cell still sees exactly the raster sweep's operands).
+#pragma unroll
+        for (int L = 0; L < 3 * T - 2; ++L)
+#pragma unroll
+          for (int i = 1; i <= T; ++i) {
+            const int j = L - 2 * (i - 1) + 1;
+            if (j < 1 || j > T) continue;
+            const uint32_t hb = __float_as_uint(h[i][j]);
+            uint32_t m = min(hb, __float_as_uint(h[i - 1][j - 1] + 1.414f));
+            m = min(m, __float_as_uint(h[i - 1][j] + 1.0f));
+            m = min(m, __float_as_uint(h[i - 1][j + 1] + 1.414f));
+            m = min(m, __float_as_uint(h[i][j - 1] + 1.0f));
+            // occupied (sign bit set) keeps its marker: max with the sign-extended bit
+            const uint32_t nv = max(m, (uint32_t)((int32_t)hb >> 31));
+            changed |= nv < hb;
+            h[i][j] = __uint_as_float(nv);
           }
-        // forward raster sweep (up-left, up, up-right, left), then backward (mirror)
 #pragma unroll
-        for (int i = 1; i <= T; ++i)
+        for (int L = 0; L < 3 * T - 2; ++L)
 #pragma unroll
-          for (int j = 1; j <= T; ++j) {
-            float m = h[i][j];
-            m = fminf(m, h[i - 1][j - 1] + 1.414f);
-            m = fminf(m, h[i - 1][j] + 1.0f);
-            m = fminf(m, h[i - 1][j + 1] + 1.414f);
-            m = fminf(m, h[i][j - 1] + 1.0f);
-            const float nv = fmaxf(m, wall(freem, (i - 1) * T + (j - 1)));
-            changed |= nv < h[i][j];
-            h[i][j] = nv;
-          }
-#pragma unroll
-        for (int i = T; i >= 1; --i)
-#pragma unroll
-          for (int j = T; j >= 1; --j) {
-            float m = h[i][j];
-            m = fminf(m, h[i + 1][j + 1] + 1.414f);
-            m = fminf(m, h[i + 1][j] + 1.0f);
-            m = fminf(m, h[i + 1][j - 1] + 1.414f);
-            m = fminf(m, h[i][j + 1] + 1.0f);
-            const float nv = fmaxf(m, wall(freem, (i - 1) * T + (j - 1)));
-            changed |= nv < h[i][j];
-            h[i][j] = nv;
+          for (int i = T; i >= 1; --i) {
+            const int j = T - (L - 2 * (T - i));
+            if (j < 1 || j > T) continue;
+            const uint32_t hb = __float_as_uint(h[i][j]);
+            uint32_t m = min(hb, __float_as_uint(h[i + 1][j + 1] + 1.414f));
+            m = min(m, __float_as_uint(h[i + 1][j] + 1.0f));
+            m = min(m, __float_as_uint(h[i + 1][j - 1] + 1.414f));
+            m = min(m, __float_as_uint(h[i][j + 1] + 1.0f));
+            const uint32_t nv = max(m, (uint32_t)((int32_t)hb >> 31));
+            changed |= nv < hb;
+            h[i][j] = __uint_as_float(nv);
           }
         if (changed) {
 #pragma unroll
-          for (int i = 1; i <= T; ++i)
-#pragma unroll
-            for (int j = 1; j <= T; ++j)
-              if (i == 1 || i == T || j == 1 || j == T) cost[(r0 + i) * GP + c0 + j] = h[i][j];
+          for (int k = 0; k < T; ++k) {
+            edge[E_TOP][tp][k] = h[1][k + 1];
+            edge[E_BOT][tp][k] = h[T][k + 1];
+            edge[E_LEFT][tp][k] = h[k + 1][1];
+            edge[E_RIGHT][tp][k] = h[k + 1][T];
+          }
+          lastc[tp] = it;
         }
       }
       if (!__syncthreads_or(changed)) break;
     }
-    if (owner) {
-#pragma unroll
-      for (int i = 1; i <= T; ++i)
-#pragma unroll
-        for (int j = 1; j <= T; ++j) cost[(r0 + i) * GP + c0 + j] = h[i][j];
-    }
-    __syncthreads();
-    // ---- 3. raw cost out + per-env statistics (finite / infinite split) ----
-    float gmin = INFINITY, gmax = -INFINITY, jmin_f = INFINITY, jmax_f = -INFINITY, jall_f = 0.f;
-    float jrmin_i = INFINITY, jrmax_i = -INFINITY, jrall_i = 0.f;
-    int any_inf = 0, inside = 0;
+    USV_PHASE(field, 2);
+#ifdef USV_PHASE_PROBE
+    if (tid == 0 && blockIdx.x < 4096) g_probe_field[blockIdx.x][14] = clock64();
+#endif
+    // ---- 3. raw cost out (occupied marker -> +inf); statistics in k_field_stats ----
     float *Fe = b.field + (size_t)e * G2;
-    for (int q = tid; q < G2; q += kWaveThreads) {
-      const float g = cost[(q / G + 1) * GP + q % G + 1];
-      Fe[q] = g;
-      const float dte = sdf_s[q] - c.obstacle_radius;   // this thread's own phase-1 write
-      const bool ins = dte <= 0.f;
-      inside |= ins;
-      const float jr = j_raw(c, dte, inv_r);
-      if (isinf(g)) {
-        any_inf = 1;
-        jrall_i = fmaxf(jrall_i, jr);
-        if (!ins) { jrmin_i = fminf(jrmin_i, jr); jrmax_i = fmaxf(jrmax_i, jr); }
-      } else {
-        gmin = fminf(gmin, g);
-        gmax = fmaxf(gmax, g);
-        const float j = jr == 0.f && !(dte < c.influence_radius) ? 0.f : jr * goal_mask(c, g, cell);
-        jall_f = fmaxf(jall_f, j);
-        if (!ins) { jmin_f = fminf(jmin_f, j); jmax_f = fmaxf(jmax_f, j); }
-      }
+    if (tile_ok) {
+#pragma unroll
+      for (int i = 0; i < T; ++i)
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+          const float g = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
+          Fe[(r0 + i) * G + c0 + j] = g;
+        }
+      lastc[tp] = -1000;   // ready for the next slot
     }
-    float vals[10] = {wave_min(gmin), wave_max(gmax), 0.f, wave_min(jmin_f), wave_max(jmax_f), wave_max(jall_f),
-                      wave_min(jrmin_i), wave_max(jrmax_i), wave_max(jrall_i), 0.f};
-    if (lane == 0)
-      for (int k = 0; k < 10; ++k) red[k][wid] = vals[k];
-    const int has_inf = __syncthreads_or(any_inf);
-    const int has_inside = __syncthreads_or(inside);
     if (tid == 0) {
-      float a[10];
-      for (int k = 0; k < 10; ++k) a[k] = red[k][0];
-      for (int w = 1; w < kWaveThreads / 64; ++w) {
-        a[SS_GMIN_F] = fminf(a[SS_GMIN_F], red[SS_GMIN_F][w]);
-        a[SS_GMAX_F] = fmaxf(a[SS_GMAX_F], red[SS_GMAX_F][w]);
-        a[SS_JMIN_F_NI] = fminf(a[SS_JMIN_F_NI], red[SS_JMIN_F_NI][w]);
-        a[SS_JMAX_F_NI] = fmaxf(a[SS_JMAX_F_NI], red[SS_JMAX_F_NI][w]);
-        a[SS_JMAX_F_ALL] = fmaxf(a[SS_JMAX_F_ALL], red[SS_JMAX_F_ALL][w]);
-        a[SS_JRMIN_I_NI] = fminf(a[SS_JRMIN_I_NI], red[SS_JRMIN_I_NI][w]);
-        a[SS_JRMAX_I_NI] = fmaxf(a[SS_JRMAX_I_NI], red[SS_JRMAX_I_NI][w]);
-        a[SS_JRMAX_I_ALL] = fmaxf(a[SS_JRMAX_I_ALL], red[SS_JRMAX_I_ALL][w]);
-      }
-      float *st = b.slot_stats + (size_t)slot * 16;
-      for (int k = 0; k < 9; ++k) st[k] = a[k];
-      st[SS_ANY_INF] = has_inf ? 1.f : 0.f;
-      st[SS_INSIDE] = has_inside ? 1.f : 0.f;
-      st[SS_ITERS] = (float)it;   // iterations (diagnostic)
-      if (isfinite(a[SS_GMAX_F])) {
-        atomic_max_f32(&b.fscratch[0], a[SS_GMAX_F]);
-        atomicOr(&b.ctl[USV_CTL_ANY_FINITE], 1);
-      }
+      b.slot_stats[(size_t)slot * kSlotStride + SS_ITERS] = (float)it;   // iterations (diagnostic)
+#ifdef USV_PHASE_PROBE
+      if (blockIdx.x < 4096) g_probe_field[blockIdx.x][15] = (unsigned long long)it;
+#endif
     }
     __syncthreads();
+    USV_PHASE(field, 3);
   }
 }
 
@@ -281,7 +342,91 @@ __device__ __forceinline__ BatchK batch_k(const usv_cfg_t &c, const usv_bufs_t &
   return BatchK{inf_val, goal_mask(c, inf_val, cell)};
 }
 
-// ---------------------------------------------------------------- pass C ---
+// ------------------------------------------------------------- pass C1 ---
+// Per (slot, 2048-cell chunk): statistics split by finite / infinite cost so
+// the batch constant inf_val (known only when every env is done) enters
+// through one monotone scalar per batch.  Partials at slot_stats[slot][16 + 12 ch].
+__global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
+  __shared__ float red[10][4];
+  __shared__ int flags[2];
+  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const float cell = (float)((double)c.map_size / G);
+  const float inv_r = (float)(1.0 / (double)c.influence_radius);
+  const int items = count * kChunks;
+  for (int w = blockIdx.x; w < items; w += gridDim.x) {
+    const int slot = w / kChunks, ch = w % kChunks;
+    const int e = b.reset_ids[slot];
+    const float *Fe = b.field + (size_t)e * G2;
+    const float *sdf_s = b.sdf + (size_t)slot * G2;
+    if (tid < 2) flags[tid] = 0;
+    float gmin = INFINITY, gmax = -INFINITY, jmin_f = INFINITY, jmax_f = -INFINITY, jall_f = 0.f;
+    float jrmin_i = INFINITY, jrmax_i = -INFINITY, jrall_i = 0.f;
+    int any_inf = 0, inside = 0;
+    const int q1 = min(G2, (ch + 1) * kChunk);
+    constexpr int PER = kChunk / 256;
+    float gv[PER], sv[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int q = ch * kChunk + k * 256 + tid;
+      gv[k] = q < q1 ? Fe[q] : 0.f;
+      sv[k] = q < q1 ? sdf_s[q] : INFINITY;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int q = ch * kChunk + k * 256 + tid;
+      if (q >= q1) continue;
+      const float g = gv[k];
+      const float dte = sv[k] - c.obstacle_radius;
+      const bool ins = dte <= 0.f;
+      inside |= ins;
+      const float jr = j_raw(c, dte, inv_r);
+      if (isinf(g)) {
+        any_inf = 1;
+        jrall_i = fmaxf(jrall_i, jr);
+        if (!ins) { jrmin_i = fminf(jrmin_i, jr); jrmax_i = fmaxf(jrmax_i, jr); }
+      } else {
+        gmin = fminf(gmin, g);
+        gmax = fmaxf(gmax, g);
+        const float j = jr * goal_mask(c, g, cell);
+        jall_f = fmaxf(jall_f, j);
+        if (!ins) { jmin_f = fminf(jmin_f, j); jmax_f = fmaxf(jmax_f, j); }
+      }
+    }
+    float vals[9] = {wave_min(gmin), wave_max(gmax), wave_min(jmin_f), wave_max(jmax_f), wave_max(jall_f),
+                     wave_min(jrmin_i), wave_max(jrmax_i), wave_max(jrall_i), 0.f};
+    __syncthreads();   // flags reset visible
+    if (lane == 0)
+      for (int k = 0; k < 8; ++k) red[k][wid] = vals[k];
+    if (any_inf) flags[0] = 1;
+    if (inside) flags[1] = 1;
+    __syncthreads();
+    if (tid == 0) {
+      float a[8];
+      for (int k = 0; k < 8; ++k) a[k] = red[k][0];
+      for (int v = 1; v < 4; ++v) {
+        a[0] = fminf(a[0], red[0][v]); a[1] = fmaxf(a[1], red[1][v]);
+        a[2] = fminf(a[2], red[2][v]); a[3] = fmaxf(a[3], red[3][v]); a[4] = fmaxf(a[4], red[4][v]);
+        a[5] = fminf(a[5], red[5][v]); a[6] = fmaxf(a[6], red[6][v]); a[7] = fmaxf(a[7], red[7][v]);
+      }
+      float *pp = b.slot_stats + (size_t)slot * kSlotStride + 16 + 12 * ch;
+      pp[SS_GMIN_F] = a[0]; pp[SS_GMAX_F] = a[1]; pp[SS_ANY_INF] = flags[0] ? 1.f : 0.f;
+      pp[SS_JMIN_F_NI] = a[2]; pp[SS_JMAX_F_NI] = a[3]; pp[SS_JMAX_F_ALL] = a[4];
+      pp[SS_JRMIN_I_NI] = a[5]; pp[SS_JRMAX_I_NI] = a[6]; pp[SS_JRMAX_I_ALL] = a[7];
+      pp[SS_INSIDE] = flags[1] ? 1.f : 0.f;
+      if (isfinite(a[1])) {
+        atomic_max_f32(&b.fscratch[0], a[1]);      // batch max of finite costs (:205-210)
+        atomicOr(&b.ctl[USV_CTL_ANY_FINITE], 1);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// batch constants given every slot's statistics
+// ------------------------------------------------------------- pass C2 ---
+// fold each slot's chunk partials (fixed order), then the batch J max and the
+// any-inside flag (one workgroup)
 __global__ __launch_bounds__(1024) void k_field_batch(usv_cfg_t c, usv_bufs_t b) {
   __shared__ float red[16];
   __shared__ int ins;
@@ -293,11 +438,29 @@ __global__ __launch_bounds__(1024) void k_field_batch(usv_cfg_t c, usv_bufs_t b)
   __syncthreads();
   float jm = 0.f;
   int inside = 0;
-  for (int s = tid; s < count; s += 1024) {
-    const float *st = b.slot_stats + (size_t)s * 16;
-    jm = fmaxf(jm, st[SS_JMAX_F_ALL]);
-    if (st[SS_ANY_INF] != 0.f) jm = fmaxf(jm, st[SS_JRMAX_I_ALL] * k.mask_inf);   // monotone in the raw value
-    inside |= st[SS_INSIDE] != 0.f;
+  for (int sl = tid; sl < count; sl += 1024) {
+    float *st = b.slot_stats + (size_t)sl * kSlotStride;
+    float a[10];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) a[q] = st[16 + q];
+    for (int ch = 1; ch < kChunks; ++ch) {
+      const float *pp = st + 16 + 12 * ch;
+      a[SS_GMIN_F] = fminf(a[SS_GMIN_F], pp[SS_GMIN_F]);
+      a[SS_GMAX_F] = fmaxf(a[SS_GMAX_F], pp[SS_GMAX_F]);
+      a[SS_ANY_INF] = fmaxf(a[SS_ANY_INF], pp[SS_ANY_INF]);
+      a[SS_JMIN_F_NI] = fminf(a[SS_JMIN_F_NI], pp[SS_JMIN_F_NI]);
+      a[SS_JMAX_F_NI] = fmaxf(a[SS_JMAX_F_NI], pp[SS_JMAX_F_NI]);
+      a[SS_JMAX_F_ALL] = fmaxf(a[SS_JMAX_F_ALL], pp[SS_JMAX_F_ALL]);
+      a[SS_JRMIN_I_NI] = fminf(a[SS_JRMIN_I_NI], pp[SS_JRMIN_I_NI]);
+      a[SS_JRMAX_I_NI] = fmaxf(a[SS_JRMAX_I_NI], pp[SS_JRMAX_I_NI]);
+      a[SS_JRMAX_I_ALL] = fmaxf(a[SS_JRMAX_I_ALL], pp[SS_JRMAX_I_ALL]);
+      a[SS_INSIDE] = fmaxf(a[SS_INSIDE], pp[SS_INSIDE]);
+    }
+#pragma unroll
+    for (int q = 0; q < 10; ++q) st[q] = a[q];
+    jm = fmaxf(jm, a[SS_JMAX_F_ALL]);
+    if (a[SS_ANY_INF] != 0.f) jm = fmaxf(jm, a[SS_JRMAX_I_ALL] * k.mask_inf);   // monotone in the raw value
+    inside |= a[SS_INSIDE] != 0.f;
   }
   jm = wave_max(jm);
   if ((tid & 63) == 0) red[tid >> 6] = jm;
@@ -324,7 +487,7 @@ __global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) 
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
     const int slot = w / kChunks, ch = w % kChunks;
     const int e = b.reset_ids[slot];
-    const float *st = b.slot_stats + (size_t)slot * 16;
+    const float *st = b.slot_stats + (size_t)slot * kSlotStride;
     const bool has_inf = st[SS_ANY_INF] != 0.f;
     const bool has_inside = st[SS_INSIDE] != 0.f;
     const float gmin = has_inf ? fminf(st[SS_GMIN_F], k.inf_val) : st[SS_GMIN_F];
@@ -363,6 +526,8 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   const int grid_b = b->n < 512 ? b->n : 512;
   const int grid_d = b->n * kChunks < 4096 ? b->n * kChunks : 4096;
   hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
+  USV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_field_stats, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_batch, dim3(1), dim3(1024), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();

@@ -111,7 +111,7 @@ class USVVirtual:
         self.extras_buf = Z(NSTAT, **f32)
         self.extras_acc = Z(NSTAT, **f32)
         self.field_old_tgt = Z((2, n), **f32)
-        self.slot_stats = Z((n, 16), **f32)
+        self.slot_stats = Z((n, DEFINES["USV_FIELD_SLOT_STATS"]), **f32)
         self.sdf = torch.empty((n, GRID2), **f32)      # per-reset-slot SDF scratch of the field kernels
         self.lut = Z((2, 1000), **f32)
         tl, tr = thruster_tables(self._task_cfg)

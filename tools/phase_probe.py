@@ -1,0 +1,62 @@
+"""Per-phase timing of the instrumented kernels (k_mb_grad, k_field_wave) on the
+bench workload.  Needs the probe build (lib/libusv_hip_probe.so, built by
+`_capi.build(probe=True)`); run on the GPU box:  python tools/phase_probe.py"""
+import ctypes
+import os
+import sys
+
+os.environ["USV_HIP_PROBE"] = "1"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from omniisaacgymenvs_loop_amd import _capi  # noqa: E402
+
+
+def read(tu):
+    buf = np.zeros((4096, 16), np.uint64)
+    rc = getattr(_capi.lib(), f"usv_probe_read_{tu}")(ctypes.c_void_p(buf.ctypes.data))
+    assert rc == 0, rc
+    return buf.astype(np.int64)
+
+
+def report(name, buf, nblk, phases, extra_col=None):
+    b = buf[:nblk]
+    ok = b[:, 0] > 0
+    b = b[ok]
+    t0 = b[:, 0:1]
+    print(f"{name}: {len(b)} workgroups (wall_clock64 ticks = 10 ns)")
+    prev = 0
+    for k in range(1, phases):
+        d = (b[:, k] - t0[:, 0]) / 100.0
+        print(f"  phase {k}: t = {d.mean():8.2f} us (max {d.max():8.2f})  delta {d.mean() - prev:8.2f} us")
+        prev = d.mean()
+    if extra_col is not None:
+        it = b[:, extra_col]
+        print(f"  iterations: mean {it.mean():.1f} min {it.min()} max {it.max()}")
+        print(f"  obstacle/table setup: {np.mean(b[:, 12] - b[:, 0]) / 100:.2f} us")
+        dclk = (b[:, 14] - b[:, 13]).astype(np.float64)
+        dwall = (b[:, 2] - b[:, 1]).astype(np.float64) / 100e6
+        print(f"  shader clock during the sweeps: {np.mean(dclk / dwall) / 1e9:.2f} GHz "
+              f"({np.mean(dclk / np.maximum(it, 1)):.0f} cycles per iteration)")
+
+
+def main():
+    envs = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    _capi.build(probe=True)
+    env, task, agent = bench.build(envs, 0, 1, 42)
+    agent.obs = agent.env_reset()
+    for _ in range(4):
+        agent.train_epoch()
+    torch.cuda.synchronize()
+    report("k_mb_grad (last launch)", read("ppo"), agent.minibatch_size // 32, 9)
+    cnt = int(task.ctl[0].item())
+    print("reset count of the last step:", cnt)
+    report("k_field_wave (last launch)", read("field"), min(cnt, 512), 4, extra_col=15)
+
+
+if __name__ == "__main__":
+    main()
