@@ -169,12 +169,12 @@ def main():
     _capi.call = timed_call
 
     agent.obs = agent.env_reset()
-    for _ in range(args.warmup):
+    # warmup: the first epoch runs eagerly, the second captures the rollout and update HIP graphs
+    for _ in range(max(args.warmup, 2)):
         agent.train_epoch()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    timing[0] = True
     t0 = time.perf_counter()
     step_t = play_t = 0.0
     for _ in range(args.steps):
@@ -185,13 +185,23 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    timing[0] = False
     t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     frames = world * args.envs * agent.horizon_length * args.steps
     value = frames / elapsed
+
+    # per-launch kernel times: the same epochs launched eagerly (graph replays carry no per-kernel events),
+    # HIP events on the launch stream around each C-ABI call
+    use_graph = agent.use_graph
+    agent.use_graph = False
+    timing[0] = True
+    for _ in range(2):
+        agent.train_epoch()
+    torch.cuda.synchronize()
+    timing[0] = False
+    agent.use_graph = use_graph
 
     # env + inference only (play_steps) and env only (VecEnv.step with fixed actions), same sizes
     torch.cuda.synchronize()

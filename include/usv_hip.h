@@ -160,6 +160,10 @@ typedef struct usv_cfg {
   float obst_box, min_dist_safe, min_obs_sep;
   float init_vel;            /* 1.5 */
   int   stats_on;            /* accumulate episode_sums */
+  /* initial action bias (USV_Virtual.py:1070-1077): added to the command for the
+   * first act_bias_steps pre_physics_step calls; used in device-clock mode */
+  float act_bias;
+  int   act_bias_steps;
   int   pad_;
 } usv_cfg_t;
 
@@ -198,6 +202,11 @@ typedef struct usv_bufs {
   float   *slot_stats;             /* [n][USV_FIELD_SLOT_STATS] per-reset-slot field statistics (scratch) */
   float   *sdf;                    /* [n][150*150] per-reset-slot signed distance (scratch) */
   const float *grid_lin;           /* [150] cell centres of the field grid */
+  /* device step clock (nullable): [0] next step index, [1] next bias-call count,
+   * [2] current step, [3] current bias-call count.  When set, usv_reset advances
+   * it and the step / bias arguments of usv_reset / usv_env_step are ignored, so
+   * a captured HIP graph replays consecutive steps. */
+  uint64_t *clock;
 } usv_bufs_t;
 
 #define USV_FIELD_SLOT_STATS 160   /* 16 + 12 per 2048-cell chunk (11 chunks) */
@@ -210,6 +219,7 @@ typedef struct usv_bufs {
 #define USV_CTL_NAN_FLAG    4   /* device NaN probe (replaces USV_NAN_PROBE host syncs) */
 #define USV_CTL_ANY_INSIDE  5   /* potential field: any cell inside an obstacle in the batch */
 #define USV_CTL_ANY_FINITE  6   /* potential field: any finite cost in the batch */
+#define USV_CTL_OBST_DONE   7   /* completion counter of the obstacle kernel (extras finalisation) */
 #define USV_CTL_N           16
 
 /* ------------------------------------------------------------------------ */
@@ -306,13 +316,16 @@ typedef struct ppo_cfg {
  * ExperienceBuffer.update_data (experience.py:392-398).
  * params: [PPO_NPARAM]; obs_rms: double [2][33] (mean, var); val_rms double [2];
  * buffers of the experience store are env-major [n][H][...].
- * eps_inject: NULL => Philox normal draws, else device [n][2] N(0,1) draws. */
+ * eps_inject: NULL => Philox normal draws, else device [n][2] N(0,1) draws.
+ * step_dev (nullable): device counter read instead of `step` (graph replay);
+ * ppo_store_reward advances it. */
 int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
                     const double *val_rms, const float *obs, int t,
                     float *exp_obs, float *exp_act, float *exp_nlp, float *exp_val,
                     float *exp_mu, float *exp_sigma, uint8_t *exp_done,
                     const int64_t *dones_prev, float *actions_out,
-                    uint64_t seed, uint64_t step, const float *eps_inject, void *stream);
+                    uint64_t seed, uint64_t step, const uint64_t *step_dev,
+                    const float *eps_inject, void *stream);
 
 /* Value of the last observation (A2CBase.get_values, a2c_common.py:407-430). */
 int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
@@ -323,7 +336,7 @@ int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
  * meter: device [H][4] per-step (sum reward of done envs, sum shaped, sum length, count). */
 int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *dones, int t,
                      float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len,
-                     float *meter, void *stream);
+                     float *meter, uint64_t *step_dev, void *stream);
 
 /* GAE (A2CBase.discount_values a2c_common.py:525-540) + returns (:763) +
  * value RMS train/normalise (prepare_dataset a2c_common.py:1257-1290) +
@@ -348,7 +361,10 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
  * m, v: [PPO_NPARAM].  minibatch must be a multiple of 32 (workgroup row block).
  * grad must be 16-byte aligned.  losses (nullable) receives the minibatch means
  * (a_loss, c_loss, entropy, b_loss, kl) of this rank; kl_out (nullable) the KL
- * the LR schedule used (after the all-reduce), as kls[] of the reference log. */
+ * the LR schedule used (after the all-reduce), as kls[] of the reference log.
+ * grad has ppo_grad_floats() entries: [0, NPARAM) gradient, [NPARAM] kl, then
+ * the reduce kernel's per-workgroup squared norms; norm_from_partials = 1 (only
+ * when grad was NOT all-reduced) takes the clip norm from those. */
 int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rms,
                        const double *val_rms, int update_obs_rms, int mb_index,
                        const float *exp_obs, const float *exp_act, const float *exp_nlp,
@@ -356,10 +372,13 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        float *exp_mu, float *exp_sigma, float *grad, float *losses,
                        float *partials, double *work, void *stream);
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m,
-                        float *adam_v, float *opt, float grad_scale, float *kl_out, void *stream);
+                        float *adam_v, float *opt, float grad_scale, float *kl_out,
+                        int norm_from_partials, void *stream);
 
 /* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad */
 int ppo_partials_floats(int minibatch);
+/* size (floats) of the grad buffer of ppo_minibatch_grad / ppo_minibatch_apply */
+int ppo_grad_floats(void);
 /* library version */
 int usv_hip_version(void);
 

@@ -54,13 +54,14 @@ def _declare(lib):
         "usv_potential_field": [P, P, P],
         "usv_env_step": [P, P, P, P, F, U64, U64, P, P],
         "usv_forces": [P, P, P, P],
-        "ppo_policy_step": [P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, U64, U64, P, P],
+        "ppo_policy_step": [P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, U64, U64, P, P, P],
         "ppo_value": [P, P, P, P, P, P, P],
-        "ppo_store_reward": [P, P, P, I, P, P, P, P, P, P],
+        "ppo_store_reward": [P, P, P, I, P, P, P, P, P, P, P],
         "ppo_prepare": [P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_grad": [P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
-        "ppo_minibatch_apply": [P, P, P, P, P, P, F, P, P],
+        "ppo_minibatch_apply": [P, P, P, P, P, P, F, P, I, P],
         "ppo_partials_floats": [I],
+        "ppo_grad_floats": [],
         "usv_hip_version": [],
     }
     for name, args in sig.items():

@@ -65,35 +65,61 @@ struct MlpSmem {
   float tail[TAIL + 1];   // params from b2 on (T_* offsets)
 };
 
-// every load is issued before the first LDS store (the trip counts are compile-time)
-__device__ __forceinline__ void stage_weights(const float *__restrict__ P, MlpSmem &s) {
-  const int tid = threadIdx.x;
-  constexpr int NW2 = NH * NH / 2 / TB, NW1 = NH * XS / TB, NTL = (TAIL + TB - 1) / TB;
-  static_assert(NH * NH / 2 % TB == 0 && NH * XS % TB == 0, "staging trip counts");
-  const float2 *W2 = reinterpret_cast<const float2 *>(P + PPO_OFF_W2);   // PPO_OFF_W2 is even
+// Weight staging in two halves: every global load is issued up front into
+// registers (compile-time trip counts); W1 / biases / heads go to LDS before
+// layer 1, W2 is committed after layer 1's matrix-core loop so its loads
+// overlap the first layer.
+constexpr int NW2 = NH * NH / 2 / TB, NW1 = NH * XS / TB, NTL = (TAIL + TB - 1) / TB;
+static_assert(NH * NH / 2 % TB == 0 && NH * XS % TB == 0, "staging trip counts");
+struct StagedW {
   float2 w2r[NW2];
-  float w1r[NW1], tlr[NTL];
-#pragma unroll
-  for (int u = 0; u < NW2; ++u) w2r[u] = W2[tid + u * TB];
+  float w1r[NW1], tlr[NTL], b1r;
+};
+
+__device__ __forceinline__ void stage_load(const float *__restrict__ P, StagedW &r) {
+  const int tid = threadIdx.x;
+  const float2 *W2 = reinterpret_cast<const float2 *>(P + PPO_OFF_W2);   // PPO_OFF_W2 is even
 #pragma unroll
   for (int u = 0; u < NW1; ++u) {
     const int i = tid + u * TB, j = i / XS, k = i % XS;
-    w1r[u] = k < NIN ? P[PPO_OFF_W1 + j * NIN + k] : 0.f;
+    r.w1r[u] = k < NIN ? P[PPO_OFF_W1 + j * NIN + k] : 0.f;
   }
 #pragma unroll
-  for (int u = 0; u < NTL; ++u) tlr[u] = (tid + u * TB < TAIL) ? P[PPO_OFF_B2 + tid + u * TB] : 0.f;
-  const float b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
+  for (int u = 0; u < NTL; ++u) r.tlr[u] = (tid + u * TB < TAIL) ? P[PPO_OFF_B2 + tid + u * TB] : 0.f;
+  r.b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
+#pragma unroll
+  for (int u = 0; u < NW2; ++u) r.w2r[u] = W2[tid + u * TB];
+}
+
+__device__ __forceinline__ void stage_store_small(const StagedW &r, MlpSmem &s) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < NW1; ++u) s.w1[tid + u * TB] = r.w1r[u];
+#pragma unroll
+  for (int u = 0; u < NTL; ++u)
+    if (tid + u * TB < TAIL) s.tail[tid + u * TB] = r.tlr[u];
+  if (tid < NH) s.b1[tid] = r.b1r;
+}
+
+__device__ __forceinline__ void stage_store_w2(const StagedW &r, MlpSmem &s) {
+  const int tid = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < NW2; ++u) {
     const int i = tid + u * TB, j = i / (NH / 2), k2 = i % (NH / 2);
-    *reinterpret_cast<float2 *>(&s.w2[j * HS + 2 * k2]) = w2r[u];
+    *reinterpret_cast<float2 *>(&s.w2[j * HS + 2 * k2]) = r.w2r[u];
   }
-#pragma unroll
-  for (int u = 0; u < NW1; ++u) s.w1[tid + u * TB] = w1r[u];
-#pragma unroll
-  for (int u = 0; u < NTL; ++u)
-    if (tid + u * TB < TAIL) s.tail[tid + u * TB] = tlr[u];
-  if (tid < NH) s.b1[tid] = b1r;
+}
+
+// tanh from one exp2 and one reciprocal (v_exp_f32 / v_rcp_f32): |error| < 2e-7
+// absolute (vs the library's correctly rounded tanhf; parity tolerances are
+// 5e-5); a 3-term series below |x| = 2^-7 keeps small arguments relative-accurate
+__device__ __forceinline__ float fast_tanh(float x) {
+  const float ax = fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(ax * -2.8853900817779268f);   // exp(-2|x|)
+  const float big = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+  const float x2 = ax * ax;
+  const float small = ax * (1.0f - x2 * (0.33333334f - 0.13333334f * x2));
+  return copysignf(ax < 0.0078125f ? small : big, x);
 }
 
 __device__ __forceinline__ void stage_obs(const float *__restrict__ obs, int row0, int nrows, const double *obs_rms,
@@ -109,8 +135,9 @@ __device__ __forceinline__ void stage_obs(const float *__restrict__ obs, int row
   }
 }
 
-// Forward of the RB rows staged in s.x (weights staged); leaves h1, h2, out.
-__device__ void block_forward(const float *__restrict__ P, MlpSmem &s) {
+// Forward of the RB rows staged in s.x (W1, biases, heads staged; W2 still in
+// registers, committed after layer 1); leaves h1, h2, out.
+__device__ void block_forward(const StagedW &wr, MlpSmem &s) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
   // ---- layer 1: h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero) ----
@@ -123,8 +150,9 @@ __device__ void block_forward(const float *__restrict__ P, MlpSmem &s) {
     }
     const float bj = s.b1[n0 + i];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = tanhf(acc[r] + bj);
+    for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
   }
+  stage_store_w2(wr, s);
   __syncthreads();
   // ---- layer 2: h2 = tanh(h1 W2^T + b2) ----
   {
@@ -136,22 +164,26 @@ __device__ void block_forward(const float *__restrict__ P, MlpSmem &s) {
     }
     const float bj = s.tail[T_B2 + n0 + i];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = tanhf(acc[r] + bj);
+    for (int r = 0; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
   }
   __syncthreads();
-  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (4 threads per row) ----
-  if (tid < RB * 4) {
-    const int r = tid / 4, part = tid % 4;
+  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (8 threads per row, 16 k each) ----
+  {
+    const int r = tid / 8, part = tid % 8;
     float a0 = 0.f, a1 = 0.f, av = 0.f;
-    for (int k = part * 32; k < part * 32 + 32; ++k) {
+#pragma unroll
+    for (int k = part * 16; k < part * 16 + 16; ++k) {
       const float hv = s.h2[r * HS + k];
       a0 = fmaf(s.tail[T_WMU + k], hv, a0);
       a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
       av = fmaf(s.tail[T_WV + k], hv, av);
     }
-    a0 += __shfl_xor(a0, 1, 64); a0 += __shfl_xor(a0, 2, 64);
-    a1 += __shfl_xor(a1, 1, 64); a1 += __shfl_xor(a1, 2, 64);
-    av += __shfl_xor(av, 1, 64); av += __shfl_xor(av, 2, 64);
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      a0 += __shfl_xor(a0, m, 64);
+      a1 += __shfl_xor(a1, m, 64);
+      av += __shfl_xor(av, m, 64);
+    }
     if (part == 0) {
       s.out[r * 4 + 0] = a0 + s.tail[T_BMU];
       s.out[r * 4 + 1] = a1 + s.tail[T_BMU + 1];
@@ -168,9 +200,11 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
                                                     int t, float *exp_obs, float *exp_act, float *exp_nlp,
                                                     float *exp_val, float *exp_mu, float *exp_sigma, uint8_t *exp_done,
                                                     const int64_t *__restrict__ dones_prev, float *actions_out,
-                                                    uint64_t seed, uint64_t step, const float *eps_inject) {
+                                                    uint64_t seed, uint64_t step, const uint64_t *step_dev,
+                                                    const float *eps_inject) {
   __shared__ MlpSmem s;
   const int n = c.n_envs, H = c.horizon;
+  if (step_dev) step = *step_dev;
   const int row0 = blockIdx.x * RB;
   const int nrows = min(RB, n - row0);
   // raw obs into the experience buffer (row = env*H + t, swap_and_flatten01 layout)
@@ -178,10 +212,12 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
     const int r = i / NIN, k = i % NIN;
     exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = obs[(size_t)(row0 + r) * NIN + k];
   }
-  stage_weights(P, s);
+  StagedW wr;
+  stage_load(P, wr);
   stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  stage_store_small(wr, s);
   __syncthreads();
-  block_forward(P, s);
+  block_forward(wr, s);
   const int r = threadIdx.x;
   if (r < nrows) {
     const int e = row0 + r;
@@ -226,10 +262,12 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
   const int n = c.n_envs;
   const int row0 = blockIdx.x * RB;
   const int nrows = min(RB, n - row0);
-  stage_weights(P, s);
+  StagedW wr;
+  stage_load(P, wr);
   stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  stage_store_small(wr, s);
   __syncthreads();
-  block_forward(P, s);
+  block_forward(wr, s);
   const int r = threadIdx.x;
   if (r < nrows) {
     float vd = s.out[r * 4 + 2];
@@ -243,8 +281,10 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
 
 // rewards_shaper + episode meters (a2c_common.py:721-759, tr_helpers.py:33-43)
 __global__ void k_store_reward(ppo_cfg_t c, const float *__restrict__ rew, const int64_t *__restrict__ dones, int t,
-                               float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len, float *meter) {
+                               float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len, float *meter,
+                               uint64_t *step_dev) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (step_dev && e == 0) *step_dev += 1;   // the rollout's Philox step advances once per env step
   const int n = c.n_envs;
   float s_rew = 0.f, s_shaped = 0.f, s_len = 0.f, s_cnt = 0.f;
   if (e < n) {
@@ -445,11 +485,13 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
   const int rb0 = row0 + blockIdx.x * RB;             // global row of this block
   const float invB = 1.0f / (float)c.minibatch;
   USV_PHASE(ppo, 0);
-  stage_weights(P, s);
+  StagedW wr;
+  stage_load(P, wr);
   stage_obs(e_obs, rb0, RB, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  stage_store_small(wr, s);
   __syncthreads();
   USV_PHASE(ppo, 1);
-  block_forward(P, s);
+  block_forward(wr, s);
   USV_PHASE(ppo, 2);
   float *part = partials + (size_t)blockIdx.x * NPART;
   // ---- per-row losses and output gradients (wave 0, lanes < RB) ----
@@ -629,14 +671,20 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict
   }
   red[g][cidx] = acc;
   __syncthreads();
+  float sq = 0.f;
   if (g == 0 && p < PPO_NPARAM + 5) {
     const float sum = ((red[0][cidx] + red[1][cidx]) + red[2][cidx]) + red[3][cidx];
-    if (p < PPO_NPARAM) grad[p] = sum;
+    if (p < PPO_NPARAM) { grad[p] = sum; sq = sum * sum; }
     else {
       const int q = p - PPO_NPARAM;
       if (q == 4) grad[PPO_NPARAM] = sum * inv_b;      // kl mean rides with the gradient (all-reduce)
       if (losses) losses[q] = sum * inv_b;
     }
+  }
+  // this workgroup's share of the squared norm (single-process runs take the norm from these)
+  if (g == 0) {
+    sq = wave_sum(sq);
+    if (cidx == 0) grad[PPO_NPARAM + 8 + blockIdx.x] = sq;
   }
 }
 
@@ -644,11 +692,23 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict
 // total norm (same order), updates its 256 parameters; the last workgroup to
 // finish (completion counter in opt[7]) advances step / lr / kl / norm.
 constexpr int AP_TB = 256;
+constexpr int RED_BLOCKS = (PPO_NPARAM + 5 + 63) / 64;
 __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const float *__restrict__ grad_in,
-                                                 float *m, float *v, float *opt, float grad_scale, float *kl_out) {
+                                                 float *m, float *v, float *opt, float grad_scale, float *kl_out,
+                                                 int norm_from_partials) {
   __shared__ float red[AP_TB / 64];
   __shared__ bool last;
   const int tid = threadIdx.x;
+  float total_norm;
+  if (norm_from_partials) {
+    // the reduce kernel's per-workgroup squares (fixed order): no re-read of the gradient
+    float sq = 0.f;
+    for (int q = tid; q < RED_BLOCKS; q += AP_TB) sq += grad_in[PPO_NPARAM + 8 + q];
+    sq = wave_sum(sq);
+    if ((tid & 63) == 0) red[tid >> 6] = sq;
+    __syncthreads();
+    total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
+  } else {
   // total norm: every load issued up front (16-byte aligned gradient, checked on the host)
   constexpr int N4 = PPO_NPARAM / 4, U = (N4 + AP_TB - 1) / AP_TB;
   const float4 *g4 = reinterpret_cast<const float4 *>(grad_in);
@@ -669,7 +729,8 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   ss = wave_sum(ss);
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
-  const float total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
+  total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
+  }
   float coef = 1.0f;
   if (c.truncate_grads) {
     coef = c.grad_norm / (total_norm + 1e-6f);
@@ -726,12 +787,13 @@ extern "C" {
 int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, const double *val_rms,
                     const float *obs, int t, float *exp_obs, float *exp_act, float *exp_nlp, float *exp_val,
                     float *exp_mu, float *exp_sigma, uint8_t *exp_done, const int64_t *dones_prev,
-                    float *actions_out, uint64_t seed, uint64_t step, const float *eps_inject, void *stream) {
+                    float *actions_out, uint64_t seed, uint64_t step, const uint64_t *step_dev,
+                    const float *eps_inject, void *stream) {
   if (!cfg || !params || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
   const int grid = (cfg->n_envs + RB - 1) / RB;
   hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
                      obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
-                     actions_out, seed, step, eps_inject);
+                     actions_out, seed, step, step_dev, eps_inject);
   USV_CHECK_LAUNCH();
   return 0;
 }
@@ -747,10 +809,11 @@ int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, 
 }
 
 int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *dones, int t, float *exp_rew,
-                     float *cur_rew, float *cur_shaped, float *cur_len, float *meter, void *stream) {
+                     float *cur_rew, float *cur_shaped, float *cur_len, float *meter, uint64_t *step_dev,
+                     void *stream) {
   if (!cfg || !rew || !dones || cfg->n_envs <= 0) return 1;
   hipLaunchKernelGGL(k_store_reward, dim3((cfg->n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream, *cfg, rew,
-                     dones, t, exp_rew, cur_rew, cur_shaped, cur_len, meter);
+                     dones, t, exp_rew, cur_rew, cur_shaped, cur_len, meter, step_dev);
   USV_CHECK_LAUNCH();
   return 0;
 }
@@ -806,15 +869,16 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
 }
 
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m, float *adam_v, float *opt,
-                        float grad_scale, float *kl_out, void *stream) {
+                        float grad_scale, float *kl_out, int norm_from_partials, void *stream) {
   if (!cfg || !params || !grad || !adam_m || !adam_v || !opt) return 1;
   if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
   hipLaunchKernelGGL(k_apply, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB), dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params,
-                     grad, adam_m, adam_v, opt, grad_scale, kl_out);
+                     grad, adam_m, adam_v, opt, grad_scale, kl_out, norm_from_partials);
   USV_CHECK_LAUNCH();
   return 0;
 }
 
 int ppo_partials_floats(int minibatch) { return (minibatch / RB) * NPART; }
+int ppo_grad_floats(void) { return PPO_NPARAM + 8 + RED_BLOCKS; }
 
 }  // extern "C"

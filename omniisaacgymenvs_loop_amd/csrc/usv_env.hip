@@ -43,6 +43,13 @@ __global__ void k_build_lut(const float *__restrict__ tl, const float *__restric
   lut[USV_LUT_N + i] = fmaf(l0, tr[i0], l1 * tr[i0 + off]);
 }
 
+// step index / action bias of this step: the device clock when present
+__device__ __forceinline__ uint64_t step_of(const usv_bufs_t &b, uint64_t step) { return b.clock ? b.clock[2] : step; }
+__device__ __forceinline__ float bias_of(const usv_cfg_t &c, const usv_bufs_t &b, float bias) {
+  if (!b.clock) return bias;
+  return (c.act_bias_steps > 0 && b.clock[3] < (uint64_t)c.act_bias_steps) ? c.act_bias : 0.f;
+}
+
 // reset-slot uniform i of env e (injected row e, or Philox site 0x100)
 struct ResetRng {
   const float *inj;
@@ -67,6 +74,10 @@ struct ResetRng {
 // ------------------------------------------------------------------------
 __global__ void k_step_begin(usv_bufs_t b) {
   const int t = threadIdx.x;
+  if (t == 0 && b.clock) {   // device step clock: this step's index and bias-call count
+    b.clock[2] = b.clock[0]++;
+    b.clock[3] = b.clock[1]++;
+  }
   if (t == 0) b.ctl[USV_CTL_RESET_COUNT] = 0;
   if (t == 1) b.ctl[USV_CTL_ANY_INSIDE] = 0;
   if (t == 2) b.ctl[USV_CTL_ANY_FINITE] = 0;
@@ -112,6 +123,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   if (!active) return;
   const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
   b.reset_ids[slot] = e;
+  step = step_of(b, step);
   ResetRng U{inj, seed, step, (uint32_t)e};
   // ---- CaptureXYTask.reset (static_obs.py:767-778) ----
   b.goal_cnt[e] = 0;
@@ -219,6 +231,7 @@ __global__ __launch_bounds__(kBlock) void k_reset_obst(usv_cfg_t c, usv_bufs_t b
   const int count = b.ctl[USV_CTL_RESET_COUNT];
   const int lane = threadIdx.x & 63, o = lane & 15, gbase = lane & 48;
   const int groups = gridDim.x * (kBlock / 16);
+  step = step_of(b, step);
   for (int slot = (blockIdx.x * kBlock + threadIdx.x) / 16; slot < count; slot += groups) {
     const int e = b.reset_ids[slot];
     auto U = [&](int i) -> float {
@@ -260,6 +273,23 @@ __global__ __launch_bounds__(kBlock) void k_reset_obst(usv_cfg_t c, usv_bufs_t b
     b.obst[(size_t)(2 * o) * n + e] = ox;
     b.obst[(size_t)(2 * o + 1) * n + e] = oy;
   }
+  // the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612)
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(&b.ctl[USV_CTL_OBST_DONE], 1) == (int)gridDim.x - 1;
+    __threadfence();
+  }
+  __syncthreads();
+  if (!last) return;
+  const int q = threadIdx.x;
+  if (q < USV_NSTAT && count > 0) {
+    float m = b.extras_acc[q] / (float)count;
+    if (q != ST_SUCCESS && q != ST_COLLISION) m = m / (float)c.max_episode_length;
+    b.extras[q] = isnan(m) ? 0.f : m;
+  }
+  if (q == 0) b.ctl[USV_CTL_OBST_DONE] = 0;
 }
 
 // ------------------------------------------------------------------------
@@ -322,6 +352,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   const bool rew_valid = ctl[USV_CTL_REW_VALID] != 0;
   // obs row staged straight into LDS (odd row stride: conflict-free), clamped on write
   // (_process_data clamp, vec_env_rlgames.py:85-95)
+  step = step_of(b, step);
+  bias = bias_of(c, b, bias);
   float *obs = sobs + threadIdx.x * USV_NOBS;
   const float clip = c.clip_obs;
   auto put = [&](int q, float v) { obs[q] = clampt(v, -clip, clip); };
@@ -651,15 +683,6 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   }
 }
 
-__global__ void k_extras_finalize(usv_cfg_t c, usv_bufs_t b) {
-  const int q = threadIdx.x;
-  const int k = b.ctl[USV_CTL_RESET_COUNT];
-  if (q >= USV_NSTAT || k <= 0) return;
-  float m = b.extras_acc[q] / (float)k;
-  if (q != ST_SUCCESS && q != ST_COLLISION) m = m / (float)c.max_episode_length;
-  b.extras[q] = isnan(m) ? 0.f : m;
-}
-
 // planar forces only (parity with Hydrodynamics.ComputeHydrodynamicsEffects)
 __global__ void k_forces(usv_cfg_t c, usv_bufs_t b, float *__restrict__ out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -711,8 +734,6 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t
   const int grid_o = (int)(((size_t)b->n * 16 + kBlock - 1) / kBlock);
   hipLaunchKernelGGL(k_reset_obst, dim3(grid_o < 2048 ? grid_o : 2048), dim3(kBlock), 0, s, *cfg, *b, seed, step,
                      u_inject);
-  USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_extras_finalize, dim3(1), dim3(64), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   return 0;
 }

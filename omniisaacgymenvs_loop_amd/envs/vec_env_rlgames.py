@@ -44,7 +44,7 @@ class VecEnvRLGames:
         # clamp to clipActions happens inside the step kernel (vec_env_rlgames.py:136-140)
         obs, rew, dones = t.env_step(a)
         self.sim_frame_count += t.control_frequency_inv
-        obs_dict = {"obs": {"state": obs}, "states": t.get_states()}
+        obs_dict = {"obs": {"state": obs}, "states": t.states_buf}
         return obs_dict, rew, dones, t.extras
 
     def reset(self):
@@ -53,6 +53,11 @@ class VecEnvRLGames:
         actions = torch.zeros((self.num_envs, self._task.num_actions), device=self._task.rl_device)
         obs_dict, _, _, _ = self.step(actions)
         return obs_dict
+
+    def advance_host_clock(self, steps: int) -> None:
+        """A captured rollout graph was replayed: the device step clock advanced by `steps`."""
+        self._task.advance_host_clock(steps)
+        self.sim_frame_count += steps * self._task.control_frequency_inv
 
     def get_number_of_agents(self) -> int:
         return 1

@@ -207,6 +207,13 @@ class A2CAgent:
         self.nn_dir = os.path.join(self.experiment_dir, "nn")
         self.obs = None
         self._step_counter = 0
+        # HIP graphs: after one eager epoch, the rollout (+ GAE/prepare) and, on a single GPU, the whole
+        # minibatch update are captured once and replayed every epoch (the step / Philox counters live on
+        # the device, so a replay continues exactly where the eager loop would)
+        self.use_graph = bool(config.get("hip_graph", True))
+        self._graph_play = None
+        self._graph_update = None
+        self._eager_epochs = 0
         self.algo_observer.after_init(self)
 
     # ------------------------------------------------------------ buffers
@@ -225,7 +232,7 @@ class A2CAgent:
         self.obs_rms[NIN:2 * NIN] = 1.0
         self.obs_rms[2 * NIN] = 1.0
         self.val_rms = torch.tensor([0.0, 1.0, 1.0], **f64)
-        self.grad = torch.zeros(NPARAM + 8, **f32)
+        self.grad = torch.zeros(_capi.lib().ppo_grad_floats(), **f32)
         self.losses = torch.zeros(8, **f32)
         self.partials = torch.zeros(_capi.lib().ppo_partials_floats(self.minibatch_size), **f32)
         self.work = torch.zeros(8 + 8 * 4096 + N // 2 + 64, **f64)
@@ -246,6 +253,7 @@ class A2CAgent:
         self.cur_shaped = torch.zeros(N, **f32)
         self.cur_len = torch.zeros(N, **f32)
         self.meter = torch.zeros((H, 4), **f32)
+        self.step_dev = torch.zeros(1, device=dev, dtype=torch.int64)   # rollout Philox step (device clock)
         self.kls = torch.zeros(self.mini_epochs_num * self.num_minibatches, **f32)
         # per minibatch: a_loss, c_loss, entropy, b_loss, kl (this rank), written by the reduce kernel
         self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 8), **f32)
@@ -268,12 +276,13 @@ class A2CAgent:
                    c.ptr(obs), n, c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp),
                    c.ptr(self.exp_val), c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.exp_done),
                    c.ptr(self.dones), c.ptr(self.actions), self.seed + 7919 * self.rank, self._step_counter,
-                   None, s)
+                   c.ptr(self.step_dev), None, s)
             t0 = time.time()
             self.obs, rewards, self.dones, infos = self.vec_env.step(self.actions)
             step_time += time.time() - t0
             c.call("ppo_store_reward", cfg, c.ptr(rewards), c.ptr(self.dones), n, c.ptr(self.exp_rew),
-                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter), s)
+                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter),
+                   c.ptr(self.step_dev), s)
             self.algo_observer.process_infos(infos, None)
             self._step_counter += 1
         return {"played_frames": self.batch_size, "step_time": step_time}
@@ -307,24 +316,61 @@ class A2CAgent:
                        c.ptr(self.partials), c.ptr(self.work), s)
                 scale = self._allreduce_grad()
                 c.call("ppo_minibatch_apply", cfg, c.ptr(self.model_params), c.ptr(self.grad), c.ptr(self.adam_m),
-                       c.ptr(self.adam_v), c.ptr(self.opt), float(scale), c.ptr(self.kls[k:k + 1]), s)
+                       c.ptr(self.adam_v), c.ptr(self.opt), float(scale), c.ptr(self.kls[k:k + 1]),
+                       int(not (self.multi_gpu and self.rank_size > 1)), s)
                 k += 1
+
+    def _graph_capture(self, fn):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            fn()
+        return g
+
+    def _advance_host_clocks(self):
+        """A graph replay advanced the device clocks by one epoch: mirror it on the host counters."""
+        self._step_counter += self.horizon_length
+        adv = getattr(self.vec_env, "advance_host_clock", None)
+        if adv is not None:
+            adv(self.horizon_length)
+
+    def _play_and_prepare(self):
+        batch = self.play_steps()
+        self.prepare_dataset()
+        return batch
 
     def train_epoch(self):
         """ContinuousA2CBase.train_epoch (a2c_common.py:1152-1255)."""
         self.vec_env.set_train_info(self.frame, self)
         play_time_start = time.time()
-        batch = self.play_steps()
+        graphs = self.use_graph and self._eager_epochs >= 1
+        if graphs:
+            if self._graph_play is None:
+                self._graph_play = self._graph_capture(self._play_and_prepare)   # host clocks advance once here
+                self._graph_play.replay()
+            else:
+                self._graph_play.replay()
+                self._advance_host_clocks()
+            batch = {"played_frames": self.batch_size, "step_time": float("nan")}
+        else:
+            batch = self._play_and_prepare()
         play_time_end = time.time()
         self.curr_frames = batch["played_frames"]
-        self.prepare_dataset()
         self.algo_observer.after_steps()
-        self.update_epoch_minibatches()
+        if graphs and not self.multi_gpu:
+            if self._graph_update is None:
+                self._graph_update = self._graph_capture(self.update_epoch_minibatches)
+            self._graph_update.replay()
+        else:
+            self.update_epoch_minibatches()
         torch.cuda.current_stream().synchronize()
         update_time_end = time.time()
+        self._eager_epochs += 1
         self._replay_meters()
         self.last_lr = float(self.opt[0].item())
-        return (batch["step_time"], play_time_end - play_time_start, update_time_end - play_time_end,
+        step_time = batch["step_time"]
+        if step_time != step_time:   # graph replay: no per-step host timing
+            step_time = play_time_end - play_time_start
+        return (step_time, play_time_end - play_time_start, update_time_end - play_time_end,
                 update_time_end - play_time_start)
 
     def _replay_meters(self):

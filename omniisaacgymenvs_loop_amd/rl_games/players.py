@@ -63,7 +63,7 @@ class PpoPlayerContinuous:
         c.call("ppo_policy_step", c.byref(self.cfg), c.ptr(self.model_params), c.ptr(self.obs_rms),
                c.ptr(self.val_rms), c.ptr(obs.contiguous()), 0, c.ptr(sc["obs"]), c.ptr(sc["act"]), c.ptr(sc["nlp"]),
                c.ptr(sc["val"]), c.ptr(sc["mu"]), c.ptr(sc["sigma"]), c.ptr(self._done8), c.ptr(self._dones),
-               c.ptr(self._actions), int(self.params.get("seed", 42)), self._step, None, c.stream_ptr())
+               c.ptr(self._actions), int(self.params.get("seed", 42)), self._step, None, None, c.stream_ptr())
         self._step += 1
         if is_deterministic:
             return torch.clamp(sc["mu"], -1.0, 1.0)     # players.py:139-150: current_action = mu, clamped

@@ -286,6 +286,7 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     c.obst_box, c.min_dist_safe, c.min_obs_sep = 12.0, 3.0, 2.5
     c.init_vel = 1.5
     c.stats_on = 1
+    c.act_bias, c.act_bias_steps = action_bias_cfg(task_cfg)
     if bool((env.get("scene_replay", {}) or {}).get("enabled", False)):
         raise NotImplementedError("scene_replay (NPZ) is not supported yet; set env.scene_replay.enabled=False")
     if bool(env.get("water_current", {}).get("use_water_current", False)):

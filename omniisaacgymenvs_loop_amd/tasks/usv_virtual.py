@@ -112,6 +112,10 @@ class USVVirtual:
         self.extras_acc = Z(NSTAT, **f32)
         self.field_old_tgt = Z((2, n), **f32)
         self.slot_stats = Z((n, DEFINES["USV_FIELD_SLOT_STATS"]), **f32)
+        # device step clock (next step, next bias call, current step, current bias call): the kernels take
+        # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
+        self.clock = Z(4, device=dev, dtype=torch.int64)
+        self.states_buf = Z((n, 0), **f32)
         self.sdf = torch.empty((n, GRID2), **f32)      # per-reset-slot SDF scratch of the field kernels
         self.lut = Z((2, 1000), **f32)
         tl, tr = thruster_tables(self._task_cfg)
@@ -145,6 +149,7 @@ class USVVirtual:
         b.field_old_tgt = p(self.field_old_tgt)
         b.slot_stats = p(self.slot_stats)
         b.sdf = p(self.sdf)
+        b.clock = p(self.clock)
         b.grid_lin = p(self.grid_lin) if self.grid_lin is not None else None
         return b
 
@@ -195,7 +200,13 @@ class USVVirtual:
         return None
 
     def get_states(self) -> torch.Tensor:
-        return torch.zeros((self._num_envs, 0), device=self._device)
+        return self.states_buf
+
+    def advance_host_clock(self, steps: int) -> None:
+        """Mirror `steps` device-clock steps (graph replays) on the host counters."""
+        self._step_index += steps
+        self._action_bias_step_count += steps
+        self.step += steps / self._horizon
 
     def get_extras(self) -> Dict[str, Any]:
         return self.extras

@@ -71,7 +71,7 @@ def test_policy_kernel_vs_reference_rollout(ppo):
         c.call("ppo_policy_step", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
                c.ptr(obs), t, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp), c.ptr(ag.exp_val),
                c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.exp_done), c.ptr(dones_prev), c.ptr(ag.actions),
-               1, t, c.ptr(torch.tensor(eps, device=DEV)), c.stream_ptr())
+               1, t, None, c.ptr(torch.tensor(eps, device=DEV)), c.stream_ptr())
         torch.cuda.synchronize()
         np.testing.assert_allclose(ag.actions.cpu().numpy(), np.clip(ppo["exp_actions"][t], -1, 1), atol=2e-6)
     rows = lambda x: x.cpu().numpy()
