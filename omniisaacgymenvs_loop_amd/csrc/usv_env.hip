@@ -360,6 +360,39 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
 #pragma unroll
   for (int q = 0; q < USV_NOBS; ++q) obs[q] = 0.f;
   if (e < n) {
+    // ---- every per-env input that does not depend on this step's results is loaded
+    // here, up front, so the HBM latencies overlap each other and the physics (only
+    // the 4 field texels and the 2 LUT entries are data-dependent gathers) ----
+    const bool was_reset = b.just_reset[e] != 0;
+    const float2 a2 = reinterpret_cast<const float2 *>(actions)[e];
+    float px = b.px[e], py = b.py[e], yaw = b.yaw[e];
+    float vx = b.vx[e], vy = b.vy[e], wz = b.wz[e];
+    float fl = b.fl[e], fr = b.fr[e];
+    const float m = b.mass[e];
+    const float k_iz = b.k_iz[e], k_drag = b.k_drag[e], thr_l = b.thr_l[e], thr_r = b.thr_r[e];
+    const float comx = b.com_x[e], comy = b.com_y[e], comz = b.com_z[e];
+    float lin0 = c.lin_damp[0], lin1 = c.lin_damp[1], lin2 = c.lin_damp[2];
+    float qd0 = c.quad_damp[0], qd1 = c.quad_damp[1], qd2 = c.quad_damp[2];
+    if (b.lin_damp) {
+      lin0 = b.lin_damp[e]; lin1 = b.lin_damp[n + e]; lin2 = b.lin_damp[2 * n + e];
+      qd0 = b.quad_damp[e]; qd1 = b.quad_damp[n + e]; qd2 = b.quad_damp[2 * n + e];
+    }
+    const int progress0 = b.progress[e];
+    const float tgx = b.tgt_x[e], tgy = b.tgt_y[e];
+    float obx[USV_NOBST], oby[USV_NOBST];
+#pragma unroll
+    for (int o = 0; o < USV_NOBST; ++o) {
+      obx[o] = b.obst[(size_t)(2 * o) * n + e];
+      oby[o] = b.obst[(size_t)(2 * o + 1) * n + e];
+    }
+    const int goal_cnt0 = b.goal_cnt[e];
+    const float prev_d_mem = b.prev_dist[e], prev_head_mem = b.prev_head[e];
+    const float prev_pot_mem = b.prev_pot[e], prev_wz_mem = b.prev_wz[e];
+    float sums[USV_NSTAT];
+    if (kStats) {
+#pragma unroll
+      for (int q = 0; q < USV_NSTAT; ++q) sums[q] = b.stats[(size_t)q * n + e];
+    }
     // ---- uniforms of this step (SU_* layout) ----
     float u[USV_NU_STEP];
     if (inj) {
@@ -369,9 +402,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       philox_u4(seed, (uint32_t)e, step, 0u, u);
       philox_u4(seed, (uint32_t)e, step, 1u, u + 4);
     }
-    const bool was_reset = b.just_reset[e] != 0;
     // ---- VecEnvRLGames.step clamp (:136-140) + pre_physics_step (:1050-1099) ----
-    const float2 a2 = reinterpret_cast<const float2 *>(actions)[e];
     const float cmd0 = clampt(a2.x, -c.clip_actions, c.clip_actions);
     const float cmd1 = clampt(a2.y, -c.clip_actions, c.clip_actions);
     const float prev_cmd0 = was_reset ? 0.f : cmd0;
@@ -396,21 +427,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     i0 = min(max(i0, 0), USV_LUT_N - 1);
     i1 = min(max(i1, 0), USV_LUT_N - 1);
     float tgt0 = lut[i0], tgt1 = lut[USV_LUT_N + i1];
-    if (c.use_thr_mult) { tgt0 = tgt0 * b.thr_l[e]; tgt1 = tgt1 * b.thr_r[e]; }
+    if (c.use_thr_mult) { tgt0 = tgt0 * thr_l; tgt1 = tgt1 * thr_r; }
     // ---- 10 substeps: thruster lag, planar forces, semi-implicit Euler ----
-    float px = b.px[e], py = b.py[e], yaw = b.yaw[e];
-    float vx = b.vx[e], vy = b.vy[e], wz = b.wz[e];
-    float fl = b.fl[e], fr = b.fr[e];
-    const float m = b.mass[e];
-    const float izz = c.izz0 * b.k_iz[e];
-    const float kd = c.use_drag_scale ? b.k_drag[e] : 1.0f;
-    const float comy = b.com_y[e];
-    float lin0 = c.lin_damp[0], lin1 = c.lin_damp[1], lin2 = c.lin_damp[2];
-    float qd0 = c.quad_damp[0], qd1 = c.quad_damp[1], qd2 = c.quad_damp[2];
-    if (b.lin_damp) {
-      lin0 = b.lin_damp[e]; lin1 = b.lin_damp[n + e]; lin2 = b.lin_damp[2 * n + e];
-      qd0 = b.quad_damp[e]; qd1 = b.quad_damp[n + e]; qd2 = b.quad_damp[2 * n + e];
-    }
+    const float izz = c.izz0 * k_iz;
+    const float kd = c.use_drag_scale ? k_drag : 1.0f;
     const float al = c.thr_alpha, oma = 1.0f - c.thr_alpha;
     const float dt = c.dt;
     for (int s = 0; s < c.substeps; ++s) {
@@ -444,7 +464,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     b.vx[e] = vx; b.vy[e] = vy; b.wz[e] = wz;
     b.fl[e] = fl; b.fr[e] = fr;
     // ---- post_physics_step: progress, update_state noise (USV_Virtual.py:771-813) ----
-    const int progress = b.progress[e] + 1;
+    const int progress = progress0 + 1;
     b.progress[e] = progress;
     float pxn = px, pyn = py;
     if (c.pos_noise_on) {
@@ -466,7 +486,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     }
     const float hc = cosf(yawn), hs = sinf(yawn);
     // ---- get_state_observations (static_obs.py:193-299) ----
-    const float ex = b.tgt_x[e] - pxn, ey = b.tgt_y[e] - pyn;
+    const float ex = tgx - pxn, ey = tgy - pyn;
     const float theta = atan2f(hs, hc);
     const float beta = atan2f(ey, ex);
     const float alpha = fmodf((beta - theta) + USV_PI_F, USV_2PI_F) - USV_PI_F;
@@ -481,8 +501,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     float min_od = INFINITY, coll = 0.f;
 #pragma unroll
     for (int o = 0; o < USV_NOBST; ++o) {
-      const float rx = b.obst[(size_t)(2 * o) * n + e] - pxn;
-      const float ry = b.obst[(size_t)(2 * o + 1) * n + e] - pyn;
+      const float rx = obx[o] - pxn;
+      const float ry = oby[o] - pyn;
       const float d = tnorm2(rx, ry);
       min_od = fminf(min_od, d);
       coll += (float)(d < c.collision_threshold) * (-10.0f) * 10.0f;
@@ -533,7 +553,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       } else {
         const float den = (float)(fabs((double)c.base_mass) > 1e-6 ? fabs((double)c.base_mass) : 1e-6);
         mass_o = c.mass_relative ? (m - c.base_mass) / den : m;
-        const float cx = b.com_x[e], cz = b.com_z[e];
+        const float cx = comx, cz = comz;
         co0 = c.com_scaled ? cx / (c.com_scale[0] + 1e-6f) : cx;
         co1 = c.com_scaled ? comy / (c.com_scale[1] + 1e-6f) : comy;
         co2 = c.com_scaled ? cz / (c.com_scale[2] + 1e-6f) : cz;
@@ -549,7 +569,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
             kz = 0.5f * (c.kiz_min + c.kiz_max);
           } else { kdv = tl = tr = kz = 1.0f; }
         } else {
-          kdv = b.k_drag[e]; tl = b.thr_l[e]; tr = b.thr_r[e]; kz = b.k_iz[e];
+          kdv = k_drag; tl = thr_l; tr = thr_r; kz = k_iz;
         }
         if (c.priv_mode == 1) {
           kdv = enc_centered(kdv, c.kdrag_min, c.kdrag_max, c.priv_nominal);
@@ -569,9 +589,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     const float bover = maxf(dist - c.kill_dist, 0.f);
     const float bpen = -expm1f(minf(bover / 0.25f, 20.0f)) * c.boundary_cost;
     const int gir = dist < c.position_tolerance;
-    const int goal_cnt = b.goal_cnt[e] * gir + gir;
+    const int goal_cnt = goal_cnt0 * gir + gir;
     b.goal_cnt[e] = goal_cnt;
-    const float prev_d_mem = b.prev_dist[e];
     const float prev_err = rew_valid ? prev_d_mem : dist;
     float dist_r;
     if (c.reward_mode == 0) dist_r = c.position_scale * (prev_err - dist);
@@ -589,11 +608,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     dist_r = dist_r * maxf(0.6f, 1.0f - danger * 0.5f);
     const float g = clampt(cosf(herr), 0.f, 1.f);
     dist_r = minf(dist_r, 0.f) + g * maxf(dist_r, 0.f);
-    const float prev_h = (rew_valid && !was_reset) ? b.prev_head[e] : herr;
+    const float prev_h = (rew_valid && !was_reset) ? prev_head_mem : herr;
     const float hi = clampt(prev_h - herr, -0.4f, 0.4f);
     const float hi_r = hi * 0.05f;
     b.prev_head[e] = herr;
-    const float prev_pot = (pot_none || was_reset) ? pot : b.prev_pot[e];
+    const float prev_pot = (pot_none || was_reset) ? pot : prev_pot_mem;
     float praw = (prev_pot - pot) * 100.0f;
     if (fabsf(praw) < 0.01f) praw = 0.f;
     const float pa1 = 2.0f * tanhf(praw / (2.0f + 1e-6f));
@@ -627,7 +646,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     if (c.pen_lin_kind == PEN_NORM) p_lin = -tnorm2(vxn, vyn) * c.pen_lin_k + c.pen_lin_c;
     if (c.pen_ang_kind) p_ang = pen_scalar(c.pen_ang_kind, c.pen_ang_k, c.pen_ang_x0, c.pen_ang_c, wzn);
     if (c.pen_angv_kind) {
-      const float prev_w = pen_valid ? b.prev_wz[e] : wzn;
+      const float prev_w = pen_valid ? prev_wz_mem : wzn;
       p_angv = pen_scalar(c.pen_angv_kind, c.pen_angv_k, c.pen_angv_x0, c.pen_angv_c, wzn - prev_w);
     }
     if (c.pen_en_kind == PEN_SUM) p_en = -(pact0 + pact1) * c.pen_en_k + c.pen_en_c;
@@ -650,7 +669,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     b.just_reset[e] = 0;
     if (kStats) {
       float *S = b.stats;
-#define ADDS(k, v) S[(size_t)(k) * n + e] += (v)
+#define ADDS(k, v) sums[k] += (v)
       ADDS(ST_TOTAL_REWARD, total); ADDS(ST_DISTANCE_REWARD, dist_r); ADDS(ST_ALIGNMENT_REWARD, align_r);
       ADDS(ST_HEADING_IMPROVE_REWARD, hi_r); ADDS(ST_POTENTIAL_SHAPING_REWARD, shaping);
       ADDS(ST_SPEED_REWARD, speed_r); ADDS(ST_ANGULAR_REWARD, ang_r); ADDS(ST_TURN_HAZARD_PENALTY, turn_haz);
@@ -667,6 +686,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       ADDS(ST_U_LOW_RATE, ((float)(unit0 < 0.05f) + (float)(unit1 < 0.05f)) / 2.0f);
       ADDS(ST_U_SUM, unit0 + unit1);
 #undef ADDS
+#pragma unroll
+      for (int q = 0; q < USV_NSTAT; ++q) S[(size_t)q * n + e] = sums[q];
     }
   }
   // ---- coalesced obs store: rows of 33 floats staged through LDS ----
