@@ -144,6 +144,8 @@ def main():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (BASELINE configs[1]: 4096)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--overlap-reset", action="store_true", help="env reset path on a side stream")
+    ap.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph capture)")
     ap.add_argument("--env-only-envs", type=int, default=131072,
                     help="extra env-only throughput probe at the C5 per-GPU size (0 = skip)")
     args = ap.parse_args()
@@ -151,6 +153,8 @@ def main():
     import torch.distributed as dist
     rank, world, local = _dist_setup(args.gpus)
     env, task, agent = build(args.envs, local, world, args.seed + rank)
+    agent.overlap_reset = args.overlap_reset
+    agent.use_graph = not args.no_graph
     from omniisaacgymenvs_loop_amd import _capi
 
     # live per-launch timing of the fused env-step kernel and the PPO gradient kernel
@@ -191,6 +195,24 @@ def main():
     elapsed = float(t.item())
     frames = world * args.envs * agent.horizon_length * args.steps
     value = frames / elapsed
+
+    # phase split of one epoch with graph replays: rollout (+ GAE/prepare) vs minibatch update
+    phase = {}
+    if agent._graph_play is not None and agent._graph_update is not None:
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        tp = tu = 0.0
+        nrep = 5
+        for _ in range(nrep):
+            ev[0].record()
+            agent._graph_play.replay()
+            ev[1].record()
+            agent._graph_update.replay()
+            ev[2].record()
+            torch.cuda.synchronize()
+            agent._advance_host_clocks()
+            tp += ev[0].elapsed_time(ev[1])
+            tu += ev[1].elapsed_time(ev[2])
+        phase = {"rollout_ms": tp / nrep, "update_ms": tu / nrep}
 
     # per-launch kernel times: the same epochs launched eagerly (graph replays carry no per-kernel events),
     # HIP events on the launch stream around each C-ABI call
@@ -272,7 +294,7 @@ def main():
             "roofline_ppo": {"bound": "mfma", "kernel": "k_mb_grad (fp32 fwd+bwd, VALU)", "achieved": ppo_tfs,
                              "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},
-            "extra": extra,
+            "extra": dict(extra, **phase),
         }
         traffic_file = os.path.join(ROOT, "profiles", "env_step_traffic.json")
         if os.path.exists(traffic_file):

@@ -264,6 +264,15 @@ int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions
                  const float *lut_dev, float action_bias, uint64_t seed,
                  uint64_t step, const float *u_inject, void *stream);
 
+/* usv_env_step split in two so the non-reset envs can run while the reset envs'
+ * potential fields are built: part 1 = envs not reset this step (needs only
+ * usv_reset to have run), part 2 = the envs reset this step (after
+ * usv_potential_field); part 0 = all (== usv_env_step).  Parts 1 and 2 together
+ * produce exactly part 0's results. */
+int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions,
+                      const float *lut_dev, float action_bias, uint64_t seed, uint64_t step,
+                      const float *u_inject, int part, void *stream);
+
 /* Planar force/moment model only (no integration), for parity with
  * HydrodynamicsObject.ComputeHydrodynamicsEffects (Hydrodynamics.py:207-245)
  * and the thruster lever arms.  out: [n][3] body X, Y, N. */

@@ -53,6 +53,7 @@ def _declare(lib):
         "usv_reset": [P, P, U64, U64, P, P],
         "usv_potential_field": [P, P, P],
         "usv_env_step": [P, P, P, P, F, U64, U64, P, P],
+        "usv_env_step_part": [P, P, P, P, F, U64, U64, P, I, P],
         "usv_forces": [P, P, P, P],
         "ppo_policy_step": [P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, U64, U64, P, P, P],
         "ppo_value": [P, P, P, P, P, P, P],

@@ -342,10 +342,20 @@ __device__ __forceinline__ float enc_minmax(float x, float xmin, float xmax) {
 template <bool kStats>
 __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, const float *__restrict__ actions,
                                                      const float *__restrict__ lut, float bias, uint64_t seed,
-                                                     uint64_t step, const float *__restrict__ inj) {
+                                                     uint64_t step, const float *__restrict__ inj, int part) {
   __shared__ float sobs[kBlock * USV_NOBS];
+  __shared__ uint8_t keep[kBlock];
   const int n = b.n;
   const int e = blockIdx.x * kBlock + threadIdx.x;
+  // part 0: every env; 1: envs not reset this step (they do not read this step's new
+  // fields, so this part can run concurrently with the potential-field kernels);
+  // 2: the envs reset this step, after their fields are built
+  bool mine = e < n;
+  if (mine && part != 0) {
+    const bool jr = b.just_reset[e] != 0;
+    mine = (part == 1) ? !jr : jr;
+  }
+  keep[threadIdx.x] = mine ? 1 : 0;
   const int32_t *ctl = b.ctl;
   const bool pot_none = ctl[USV_CTL_POT_VALID] == 0 || ctl[USV_CTL_RESET_COUNT] > 0;
   const bool pen_valid = ctl[USV_CTL_PEN_VALID] != 0;
@@ -359,7 +369,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   auto put = [&](int q, float v) { obs[q] = clampt(v, -clip, clip); };
 #pragma unroll
   for (int q = 0; q < USV_NOBS; ++q) obs[q] = 0.f;
-  if (e < n) {
+  if (mine) {
     // ---- every per-env input that does not depend on this step's results is loaded
     // here, up front, so the HBM latencies overlap each other and the physics (only
     // the 4 field texels and the 2 LUT entries are data-dependent gathers) ----
@@ -695,9 +705,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   const int row0 = blockIdx.x * kBlock;
   const int rows = min(kBlock, n - row0);
   float *dst = b.obs + (size_t)row0 * USV_NOBS;
-  for (int i = threadIdx.x; i < rows * USV_NOBS; i += kBlock) dst[i] = sobs[i];
+  for (int i = threadIdx.x; i < rows * USV_NOBS; i += kBlock)
+    if (keep[i / USV_NOBS]) dst[i] = sobs[i];
   // ---- global flags: the step has consumed the Nones (:361, :448, USV_task_rewards.py:450) ----
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (part != 1 && blockIdx.x == 0 && threadIdx.x == 0) {
     b.ctl[USV_CTL_POT_VALID] = 1;
     b.ctl[USV_CTL_PEN_VALID] = 1;
     b.ctl[USV_CTL_REW_VALID] = 1;
@@ -759,20 +770,26 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t
   return 0;
 }
 
-int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions, const float *lut_dev,
-                 float action_bias, uint64_t seed, uint64_t step, const float *u_inject, void *stream) {
-  if (!cfg || !b || !actions || !lut_dev || b->n <= 0) return 1;
+int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions, const float *lut_dev,
+                      float action_bias, uint64_t seed, uint64_t step, const float *u_inject, int part,
+                      void *stream) {
+  if (!cfg || !b || !actions || !lut_dev || b->n <= 0 || part < 0 || part > 2) return 1;
   if (cfg->priv_dim != 4 && cfg->priv_dim != 8) return 3;
   const int grid = (b->n + kBlock - 1) / kBlock;
   hipStream_t s = (hipStream_t)stream;
   if (cfg->stats_on)
     hipLaunchKernelGGL(k_env_step<true>, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, actions, lut_dev, action_bias,
-                       seed, step, u_inject);
+                       seed, step, u_inject, part);
   else
     hipLaunchKernelGGL(k_env_step<false>, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, actions, lut_dev, action_bias,
-                       seed, step, u_inject);
+                       seed, step, u_inject, part);
   USV_CHECK_LAUNCH();
   return 0;
+}
+
+int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions, const float *lut_dev,
+                 float action_bias, uint64_t seed, uint64_t step, const float *u_inject, void *stream) {
+  return usv_env_step_part(cfg, b, actions, lut_dev, action_bias, seed, step, u_inject, 0, stream);
 }
 
 int usv_forces(const usv_cfg_t *cfg, const usv_bufs_t *b, float *out, void *stream) {

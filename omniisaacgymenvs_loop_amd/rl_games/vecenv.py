@@ -30,6 +30,12 @@ class RLGPUEnv:
     def __init__(self, config_name: str, num_actors: int, **kwargs):
         self.env = configurations[config_name]["env_creator"](**kwargs)
 
+    def __getattr__(self, name):
+        # optional env extensions (prepare_step, advance_host_clock, ...) pass through to the wrapped env
+        if name == "env":
+            raise AttributeError(name)
+        return getattr(self.env, name)
+
     def step(self, action):
         return self.env.step(action)
 
