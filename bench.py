@@ -159,18 +159,26 @@ def main():
 
     # live per-launch timing of the fused env-step kernel and the PPO gradient kernel
     env_timer, ppo_timer = KernelTimer(), KernelTimer()
-    orig_call = _capi.call
+    orig_call, orig_call_rc = _capi.call, _capi.call_rc
 
     def timed_call(name, *a):
-        if timing[0] and name == "usv_env_step":
+        if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
             env_timer(lambda: orig_call(name, *a))
         elif timing[0] and name == "ppo_minibatch_grad":
             ppo_timer(lambda: orig_call(name, *a))
         else:
             orig_call(name, *a)
 
+    def timed_call_rc(name, *a):
+        if timing[0] and name == "ppo_minibatch_fused":
+            rc = [0]
+            ppo_timer(lambda: rc.__setitem__(0, orig_call_rc(name, *a)))
+            return rc[0]
+        return orig_call_rc(name, *a)
+
     timing = [False]
     _capi.call = timed_call
+    _capi.call_rc = timed_call_rc
 
     agent.obs = agent.env_reset()
     # warmup: the first epoch runs eagerly, the second captures the rollout and update HIP graphs
@@ -291,7 +299,8 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_env_step": ENV_STEP_BYTES, "launch_ms": env_ms,
                          "envs_per_launch": args.envs},
-            "roofline_ppo": {"bound": "mfma", "kernel": "k_mb_grad (fp32 fwd+bwd, VALU)", "achieved": ppo_tfs,
+            "roofline_ppo": {"bound": "mfma", "kernel": "k_mb_fused (f32 MFMA fwd+bwd + reduction + Adam, one launch)",
+                             "achieved": ppo_tfs,
                              "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},
             "extra": dict(extra, **phase),

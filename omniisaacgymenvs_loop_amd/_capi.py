@@ -61,6 +61,7 @@ def _declare(lib):
         "ppo_prepare": [P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_grad": [P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_apply": [P, P, P, P, P, P, F, P, I, P],
+        "ppo_minibatch_fused": [P, P, P, P, I, I] + [P] * 16 + [I, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
         "usv_hip_version": [],
@@ -89,6 +90,11 @@ def call(name: str, *args) -> None:
         raise RuntimeError(f"{name} failed with status {rc}")
 
 
+def call_rc(name: str, *args) -> int:
+    """Like call() but hands the status back (for entry points with a documented fallback code)."""
+    return int(getattr(lib(), name)(*args))
+
+
 def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
@@ -101,4 +107,4 @@ def byref(s):
     return ctypes.byref(s)
 
 
-__all__ = ["build", "lib", "call", "ptr", "stream_ptr", "byref", "UsvCfg", "UsvBufs", "PpoCfg", "LIB_PATH"]
+__all__ = ["build", "lib", "call", "call_rc", "ptr", "stream_ptr", "byref", "UsvCfg", "UsvBufs", "PpoCfg", "LIB_PATH"]

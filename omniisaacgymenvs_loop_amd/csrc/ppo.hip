@@ -473,13 +473,12 @@ __global__ __launch_bounds__(TB) void k_obs_stats(ppo_cfg_t c, const float *__re
 }
 
 // ------------------------------------------------------ minibatch grad ----
-__global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
-                                                const double *__restrict__ obs_rms, int row0,
-                                                const float *__restrict__ e_obs, const float *__restrict__ e_act,
-                                                const float *__restrict__ e_nlp, const float *__restrict__ e_val,
-                                                const float *__restrict__ e_ret, const float *__restrict__ e_adv,
-                                                float *e_mu, float *e_sigma, float *partials) {
-  __shared__ MlpSmem s;
+__device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__restrict__ P,
+                                             const double *__restrict__ obs_rms, int row0,
+                                             const float *__restrict__ e_obs, const float *__restrict__ e_act,
+                                             const float *__restrict__ e_nlp, const float *__restrict__ e_val,
+                                             const float *__restrict__ e_ret, const float *__restrict__ e_adv,
+                                             float *e_mu, float *e_sigma, float *partials, MlpSmem &s) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int rb0 = row0 + blockIdx.x * RB;             // global row of this block
@@ -657,13 +656,25 @@ __global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__rest
   USV_PHASE(ppo, 8);
 }
 
+__global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
+                                                const double *__restrict__ obs_rms, int row0,
+                                                const float *__restrict__ e_obs, const float *__restrict__ e_act,
+                                                const float *__restrict__ e_nlp, const float *__restrict__ e_val,
+                                                const float *__restrict__ e_ret, const float *__restrict__ e_adv,
+                                                float *e_mu, float *e_sigma, float *partials) {
+  __shared__ MlpSmem s;
+  mb_grad_body(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
+}
+
 // sum the per-block partials (fixed order => deterministic) into grad[]:
 // 64 params x 4 block-strided groups per workgroup, combined in LDS.
-__global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
-                                                         float *losses, float inv_b) {
-  __shared__ float red[4][64];
+// chunk `chunk` = params [64 chunk, 64 chunk + 64), summed over the per-workgroup
+// partials in a fixed order (deterministic); writes grad, the kl / loss means and the
+// chunk's squared norm; returns the summed gradient in the g == 0 threads (0 elsewhere)
+__device__ __forceinline__ float reduce_chunk(const float *__restrict__ partials, int nblk, float *grad, float *losses,
+                                              float inv_b, int chunk, float (&red)[4][64]) {
   const int cidx = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int p = blockIdx.x * 64 + cidx;
+  const int p = chunk * 64 + cidx;
   float acc = 0.f;
   if (p < PPO_NPARAM + 5) {
 #pragma unroll 8
@@ -671,21 +682,33 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict
   }
   red[g][cidx] = acc;
   __syncthreads();
-  float sq = 0.f;
-  if (g == 0 && p < PPO_NPARAM + 5) {
-    const float sum = ((red[0][cidx] + red[1][cidx]) + red[2][cidx]) + red[3][cidx];
-    if (p < PPO_NPARAM) { grad[p] = sum; sq = sum * sum; }
-    else {
-      const int q = p - PPO_NPARAM;
-      if (q == 4) grad[PPO_NPARAM] = sum * inv_b;      // kl mean rides with the gradient (all-reduce)
-      if (losses) losses[q] = sum * inv_b;
-    }
-  }
-  // this workgroup's share of the squared norm (single-process runs take the norm from these)
+  float gsum = 0.f;
   if (g == 0) {
+    float sq = 0.f;
+    if (p < PPO_NPARAM + 5) {
+      const float sum = ((red[0][cidx] + red[1][cidx]) + red[2][cidx]) + red[3][cidx];
+      if (p < PPO_NPARAM) {
+        grad[p] = sum;
+        gsum = sum;
+        sq = sum * sum;
+      } else {
+        const int q = p - PPO_NPARAM;
+        if (q == 4) grad[PPO_NPARAM] = sum * inv_b;      // kl mean rides with the gradient (all-reduce)
+        if (losses) losses[q] = sum * inv_b;
+      }
+    }
+    // this chunk's share of the squared norm (single-process runs take the norm from these)
     sq = wave_sum(sq);
-    if (cidx == 0) grad[PPO_NPARAM + 8 + blockIdx.x] = sq;
+    if (cidx == 0) grad[PPO_NPARAM + 8 + chunk] = sq;
   }
+  __syncthreads();   // red[] is reused by the next chunk
+  return gsum;
+}
+
+__global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
+                                                         float *losses, float inv_b) {
+  __shared__ float red[4][64];
+  reduce_chunk(partials, nblk, grad, losses, inv_b, blockIdx.x, red);
 }
 
 // clip_grad_norm_ + Adam + AdaptiveScheduler.  Every workgroup forms the same
@@ -768,6 +791,116 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
     // AdaptiveScheduler.update on this minibatch's KL (schedulers.py:26-32)
     if (c.lr_adaptive) {
       const float kl = grad_in[PPO_NPARAM] * grad_scale;
+      float nl = lr;
+      if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
+      if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
+      opt[0] = nl;
+      opt[2] = kl;
+      if (kl_out) *kl_out = kl;
+    }
+    __threadfence();
+    atomicExch(reinterpret_cast<unsigned *>(opt + 7), 0u);
+  }
+}
+
+// ------------------------------------------------- fused minibatch kernel --
+// Sense-reversing grid barrier for co-resident workgroups (the host checks
+// that every workgroup of the launch fits the device at once): bar[0] arrival
+// count, bar[1] sense.  The spin is bounded: on timeout it raises *err instead
+// of hanging the device.
+__device__ __forceinline__ void grid_barrier(unsigned *bar, unsigned nblk, unsigned *err) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned s0 = atomicAdd(bar + 1, 0u);
+    __threadfence();
+    if (atomicAdd(bar, 1u) == nblk - 1) {
+      atomicExch(bar, 0u);
+      __threadfence();
+      atomicExch(bar + 1, s0 ^ 1u);
+    } else {
+      unsigned spins = 0;
+      while (atomicAdd(bar + 1, 0u) == s0) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) { atomicExch(err, 1u); break; }
+      }
+    }
+    __threadfence();
+  }
+  __syncthreads();
+}
+
+// One PPO minibatch in one launch: forward/backward partials (as k_mb_grad) ->
+// barrier -> fixed-order reduction, chunk by chunk -> [kApply: barrier -> clip
+// norm from the chunk squares -> Adam on the chunks this workgroup reduced ->
+// the last workgroup advances step / lr / kl].  Saves the two kernel
+// boundaries of the split path (their drain + dispatch dominate at 8192 rows).
+template <bool kApply>
+__global__ __launch_bounds__(TB) void k_mb_fused(ppo_cfg_t c, float *P, const double *__restrict__ obs_rms, int row0,
+                                                 const float *__restrict__ e_obs, const float *__restrict__ e_act,
+                                                 const float *__restrict__ e_nlp, const float *__restrict__ e_val,
+                                                 const float *__restrict__ e_ret, const float *__restrict__ e_adv,
+                                                 float *e_mu, float *e_sigma, float *partials, float *grad,
+                                                 float *losses, float *m, float *v, float *opt, float *kl_out) {
+  __shared__ MlpSmem s;
+  __shared__ float red[4][64];
+  __shared__ float nred[4];
+  __shared__ bool last;
+  unsigned *bar = reinterpret_cast<unsigned *>(opt + 5);
+  unsigned *err = reinterpret_cast<unsigned *>(opt + 4);
+  mb_grad_body(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
+  const unsigned nblk = gridDim.x;
+  grid_barrier(bar, nblk, err);
+  const float inv_b = 1.0f / (float)c.minibatch;
+  constexpr int MAXC = 2;   // chunks per workgroup (RED_BLOCKS <= 2 * 256)
+  float gk[MAXC];
+  int nck = 0;
+  for (int ch = blockIdx.x; ch < RED_BLOCKS; ch += nblk) gk[nck++] = reduce_chunk(partials, (int)nblk, grad, losses, inv_b, ch, red);
+  if (!kApply) return;
+  grid_barrier(bar, nblk, err);
+  // clip_grad_norm_ from the chunk squares (same order in every workgroup)
+  const int tid = threadIdx.x;
+  float sq = 0.f;
+  for (int q = tid; q < RED_BLOCKS; q += TB) sq += grad[PPO_NPARAM + 8 + q];
+  sq = wave_sum(sq);
+  if ((tid & 63) == 0) nred[tid >> 6] = sq;
+  __syncthreads();
+  const float total_norm = sqrtf(((nred[0] + nred[1]) + nred[2]) + nred[3]);
+  float coef = 1.0f;
+  if (c.truncate_grads) coef = fminf(c.grad_norm / (total_norm + 1e-6f), 1.0f);
+  const float lr = opt[0];
+  const float step = opt[1] + 1.0f;
+  const double bc1 = 1.0 - pow((double)c.adam_b1, (double)step);
+  const double bc2 = 1.0 - pow((double)c.adam_b2, (double)step);
+  const float step_size = (float)((double)lr / bc1);
+  const float bc2s = (float)sqrt(bc2);
+  if (tid < 64) {
+    int k = 0;
+    for (int ch = blockIdx.x; ch < RED_BLOCKS; ch += nblk, ++k) {
+      const int q = ch * 64 + tid;
+      if (q >= PPO_NPARAM) continue;
+      float g = gk[k] * coef;
+      if (c.weight_decay != 0.f) g = g + c.weight_decay * P[q];
+      float mi = m[q], vi = v[q];
+      mi = mi + (1.0f - c.adam_b1) * (g - mi);          // exp_avg.lerp_(grad, 1 - beta1)
+      vi = vi * c.adam_b2 + (1.0f - c.adam_b2) * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+      const float denom = sqrtf(vi) / bc2s + c.adam_eps;
+      P[q] = P[q] - step_size * (mi / denom);
+      m[q] = mi;
+      v[q] = vi;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    last = atomicAdd(reinterpret_cast<unsigned *>(opt + 7), 1u) == nblk - 1;
+    __threadfence();
+  }
+  __syncthreads();
+  if (last && tid == 0) {
+    opt[1] = step;
+    opt[3] = total_norm;
+    if (c.lr_adaptive) {   // AdaptiveScheduler.update on this minibatch's KL (schedulers.py:26-32)
+      const float kl = grad[PPO_NPARAM];
       float nl = lr;
       if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
       if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
@@ -874,6 +1007,51 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
   if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
   hipLaunchKernelGGL(k_apply, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB), dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params,
                      grad, adam_m, adam_v, opt, grad_scale, kl_out, norm_from_partials);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_minibatch_fused(const ppo_cfg_t *cfg, float *params, double *obs_rms, const double *val_rms,
+                        int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+                        const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
+                        float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
+                        float *adam_m, float *adam_v, float *opt, float *kl_out, int apply, void *stream) {
+  (void)val_rms;
+  if (!cfg || !params || !grad || !partials || !work || !opt) return 1;
+  if (apply && (!adam_m || !adam_v)) return 1;
+  if (cfg->minibatch % RB != 0) return 2;
+  const int nblk = cfg->minibatch / RB;
+  if (nblk * 2 < RED_BLOCKS) return 4;   // each workgroup reduces at most two chunks: use the split path
+  // every workgroup must be resident at once (grid barrier): 1 per CU at this LDS size
+  static int checked_dev = -1, capacity = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 5;
+  if (dev != checked_dev) {
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 5;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(k_mb_fused<true>), TB,
+                                                     0) != hipSuccess)
+      return 5;
+    capacity = cus * per_cu;
+    checked_dev = dev;
+  }
+  if (nblk > capacity) return 4;         // caller falls back to ppo_minibatch_grad + ppo_minibatch_apply
+  hipStream_t s = (hipStream_t)stream;
+  const int row0 = mb_index * cfg->minibatch;
+  if (update_obs_rms && cfg->normalize_input) {
+    const int nb = 64;
+    hipLaunchKernelGGL(k_obs_stats, dim3(nb), dim3(TB), 0, s, *cfg, exp_obs, row0, cfg->minibatch, work + 8, obs_rms,
+                       reinterpret_cast<unsigned *>(work + 7));
+    USV_CHECK_LAUNCH();
+  }
+  if (apply)
+    hipLaunchKernelGGL(k_mb_fused<true>, dim3(nblk), dim3(TB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act,
+                       exp_nlp, exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials, grad, losses, adam_m, adam_v,
+                       opt, kl_out);
+  else
+    hipLaunchKernelGGL(k_mb_fused<false>, dim3(nblk), dim3(TB), 0, s, *cfg, params, obs_rms, row0, exp_obs,
+                       exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials, grad, losses, adam_m,
+                       adam_v, opt, kl_out);
   USV_CHECK_LAUNCH();
   return 0;
 }
