@@ -40,14 +40,15 @@ PPO_FLOPS_PER_ROW = 2 * (33 * 128 + 128 * 128 + 3 * 128) + 2 * (2 * 128 * 128 + 
 def _dist_setup(gpus):
     import torch
     import torch.distributed as dist
+    from omniisaacgymenvs_loop_amd.rl_games import dist_util
     rank = int(os.getenv("RANK", "0"))
     world = int(os.getenv("WORLD_SIZE", "1"))
-    local = int(os.getenv("LOCAL_RANK", "0"))
     if world != gpus:
         raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}: launch with torch.distributed.run")
+    local = int(dist_util.local_device().split(":")[1])
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group(dist_util.backend(), rank=rank, world_size=world)
     return rank, world, local
 
 
@@ -299,7 +300,10 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_env_step": ENV_STEP_BYTES, "launch_ms": env_ms,
                          "envs_per_launch": args.envs},
-            "roofline_ppo": {"bound": "mfma", "kernel": "k_mb_fused (f32 MFMA fwd+bwd + reduction + Adam, one launch)",
+            "roofline_ppo": {"bound": "mfma",
+                             "kernel": ("k_mb_fused (f32 MFMA fwd+bwd + reduction + Adam, one launch)"
+                                        if agent.fused_update else
+                                        "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, fixed-order reduction)"),
                              "achieved": ppo_tfs,
                              "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},

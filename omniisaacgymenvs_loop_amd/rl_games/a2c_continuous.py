@@ -125,8 +125,9 @@ class A2CAgent:
             self.rank = int(os.getenv("LOCAL_RANK", "0"))
             self.rank_size = int(os.getenv("WORLD_SIZE", "1"))
             if not dist.is_initialized():
-                dist.init_process_group("nccl", rank=int(os.getenv("RANK", self.rank)), world_size=self.rank_size)
-            config["device"] = f"cuda:{self.rank}"
+                dist.init_process_group(dist_util.backend(), rank=int(os.getenv("RANK", self.rank)),
+                                        world_size=self.rank_size)
+            config["device"] = dist_util.local_device()
         self.ppo_device = config.get("device", "cuda:0")
         torch.cuda.set_device(torch.device(self.ppo_device))
         self.num_actors = int(config["num_actors"])

@@ -10,8 +10,22 @@ all-reduced KL, so no LR broadcast is needed.  The same functions run on gloo
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
+
+
+def local_device() -> str:
+    """The GPU of this rank: cuda:LOCAL_RANK (one process per GPU).  USV_RANKS_SHARE_DEVICE=<i>
+    puts every rank on cuda:<i> -- only for rehearsing the multi-process path on a one-GPU box."""
+    shared = os.getenv("USV_RANKS_SHARE_DEVICE")
+    return f"cuda:{int(shared)}" if shared is not None else f"cuda:{int(os.getenv('LOCAL_RANK', '0'))}"
+
+
+def backend() -> str:
+    """RCCL ("nccl") unless USV_DIST_BACKEND overrides it (gloo for the shared-device rehearsal)."""
+    return os.getenv("USV_DIST_BACKEND", "nccl")
 
 
 def world() -> int:

@@ -48,8 +48,8 @@ def build_config(ov: Dict[str, Any]) -> Dict[str, Any]:
     task = _load("task", ov.get("task", "USV/IROS2024/USV_Virtual_CaptureXY_SysID-TEST"))
     train = _load("train", ov.get("train", "USV/USV_PPOcontinuous_MLP"))
     multi_gpu = bool(ov.get("multi_gpu", False))
-    rank = int(os.getenv("LOCAL_RANK", "0"))
-    rl_device = f"cuda:{rank}" if multi_gpu else ov.get("rl_device", "cuda:0")
+    from ..rl_games.dist_util import local_device
+    rl_device = local_device() if multi_gpu else ov.get("rl_device", "cuda:0")
     num_envs = int(ov.get("num_envs", task["env"]["numEnvs"]))
     task["env"]["numEnvs"] = num_envs
     task["env"].setdefault("scene_replay", {})["enabled"] = False
