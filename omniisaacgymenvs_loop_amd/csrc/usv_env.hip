@@ -90,164 +90,46 @@ __global__ void k_step_begin(usv_bufs_t b) {
 // env; threads of envs with reset_buf==1 do the work.  The reset list is
 // compacted with a wave ballot + one atomic per wave (order is irrelevant:
 // draws are keyed by env id, the potential-field batch statistics are maxima).
-// Obstacle rejection sampling runs afterwards in k_reset_obst, 16 lanes per
-// reset env.
+// Obstacle rejection sampling follows in the same kernel, one whole wave per
+// reset env (place_obstacles).
 // ------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uint64_t seed, uint64_t step,
-                                                  const float *__restrict__ inj) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+// 64-lane (whole wave) obstacle placement for reset env ee (CaptureXYTask.get_spawns
+// obstacle part, static_obs.py:968-1048).  Lane (q, o) = (lane >> 4, lane & 15) holds
+// obstacle o (replicated over the four 16-lane groups) and draws the candidate of
+// iteration 4r + q of round r, so the Philox work of four rejection iterations runs in
+// parallel; the iterations themselves stay sequential and pick candidates by shuffle.
+// Box around the previous-episode target; an obstacle is redrawn while it is closer
+// than min_dist_safe to the spawn or the target, or closer than min_obs_sep to a
+// lower-index obstacle; after USV_SPAWN_ITERS redraws the leftovers go to limbo
+// (999, 999).  Same uniforms as the per-env restatement (reset slots RU_OBST + 2o,
+// RU_RESAMPLE + 32 it + 2o (+1)).
+__device__ void place_obstacles(const usv_cfg_t &c, const usv_bufs_t &b, int ee, float sx, float sy, float tx,
+                                float ty, uint64_t seed, uint64_t step, const float *__restrict__ inj) {
+  static_assert(USV_NOBST == 16, "16-lane groups");
   const int n = b.n;
-  const bool active = (e < n) && (b.reset_buf[e] != 0);
-  // ---- compaction: reset_buf.nonzero() (USV_Virtual.py:1045) ----
-  const uint64_t mask = __ballot(active);
-  if (mask == 0) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((long long)mask) - 1;
-  int base = 0;
-  if (lane == leader) base = atomicAdd(&b.ctl[USV_CTL_RESET_COUNT], __popcll(mask));
-  base = __shfl(base, leader, 64);
-  // ---- episode extras: sums of the envs being reset (:1591-1612), one atomic per wave ----
-  if (c.stats_on) {
-    for (int q = 0; q < USV_NSTAT; ++q) {
-      float v = 0.f;
-      if (active) {
-        v = b.stats[(size_t)q * n + e];
-        if (q == ST_SUCCESS) v = (float)b.done_succ[e];
-        if (q == ST_COLLISION) v = (float)b.done_coll[e];
-        b.stats[(size_t)q * n + e] = 0.f;
-      }
-      v = wave_sum(v);
-      if (lane == leader) atomicAdd(&b.extras_acc[q], v);
+  const int lane = threadIdx.x & 63, o = lane & 15, q = lane >> 4, gbase = lane & 48;
+  auto Ue = [&](int i) -> float {
+    if (inj) return inj[(size_t)ee * USV_NU_RESET + i];
+    float u4[4];
+    philox_u4(seed, (uint32_t)ee, step, 0x100u + (uint32_t)(i >> 2), u4);
+    return u4[i & 3];
+  };
+  const float mnx = tx - c.obst_box, mny = ty - c.obst_box;
+  const float dx_ = (tx + c.obst_box) - mnx, dy_ = (ty + c.obst_box) - mny;
+  float ox = Ue(RU_OBST + 2 * o) * dx_ + mnx;
+  float oy = Ue(RU_OBST + 2 * o + 1) * dy_ + mny;
+  const float sep2 = c.min_obs_sep * c.min_obs_sep;
+  bool done = false;
+  for (int r = 0; !done; ++r) {
+    const int itq = 4 * r + q;
+    float cx = 0.f, cy = 0.f;
+    if (itq < USV_SPAWN_ITERS) {
+      const int rb = RU_RESAMPLE + itq * USV_NOBST * 2;
+      cx = Ue(rb + 2 * o) * dx_ + mnx;
+      cy = Ue(rb + 2 * o + 1) * dy_ + mny;
     }
-  }
-  if (!active) return;
-  const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
-  b.reset_ids[slot] = e;
-  step = step_of(b, step);
-  ResetRng U{inj, seed, step, (uint32_t)e};
-  // ---- CaptureXYTask.reset (static_obs.py:767-778) ----
-  b.goal_cnt[e] = 0;
-  b.done_succ[e] = 0;
-  b.done_coll[e] = 0;
-  b.just_reset[e] = 1;
-  // ---- MassDistributionDisturbances.randomize_masses / _randomize_com (USV_disturbances.py:94-150) ----
-  float mass;
-  if (c.mass_dr_on) mass = U(RU_MASS) * (float)((double)c.mass_max - (double)c.mass_min) + c.mass_min;
-  else mass = U(RU_MASS) * 0.0f + c.base_mass;
-  float cx = c.base_com[0], cy = c.base_com[1], cz = c.base_com[2];
-  if (c.mass_dr_on && c.com_mode == 1) {
-    cx = c.base_com[0] + (U(RU_COM + 0) * 2.0f - 1.0f) * c.com_disp[0];
-    cy = c.base_com[1] + (U(RU_COM + 1) * 2.0f - 1.0f) * c.com_disp[1];
-    cz = c.base_com[2] + (U(RU_COM + 2) * 2.0f - 1.0f) * c.com_disp[2];
-  } else if (c.mass_dr_on && c.com_mode == 2 && c.com_legacy_r > 0.f) {
-    const float r = U(RU_COM) * c.com_legacy_r;
-    const float th = U(RU_COM + 1) * USV_PI_F * 2.0f;
-    cx = c.base_com[0] + cosf(th) * r;
-    cy = c.base_com[1] + sinf(th) * r;
-  }
-  b.mass[e] = mass;
-  b.com_x[e] = cx;
-  b.com_y[e] = cy;
-  b.com_z[e] = cz;
-  // ---- independent randomisations (yaw inertia :193-240, drag :136-174, thrusters :112-127) ----
-  if (c.indep_kiz_on && !c.couple_kiz) {
-    const float u = U(RU_KIZ);
-    b.k_iz[e] = c.kiz_log ? expf(logf(c.kiz_min) + u * (logf(c.kiz_max) - logf(c.kiz_min)))
-                          : c.kiz_min + u * (c.kiz_max - c.kiz_min);
-  }
-  if (c.drag_rand_on && b.lin_damp) {
-    for (int a = 0; a < 3; ++a) {
-      b.lin_damp[(size_t)a * n + e] = c.lin_damp[a] + (U(RU_DRAG + a) * 2.0f - 1.0f) * c.lin_rand[a];
-      b.quad_damp[(size_t)a * n + e] = c.quad_damp[a] + (U(RU_DRAG + 6 + a) * 2.0f - 1.0f) * c.quad_rand[a];
-    }
-  }
-  if (c.indep_kdrag_on) {
-    const float u = U(RU_KDRAG);
-    b.k_drag[e] = c.kdrag_log ? expf(logf(c.kdrag_min) + u * (logf(c.kdrag_max) - logf(c.kdrag_min)))
-                              : c.kdrag_min + u * (c.kdrag_max - c.kdrag_min);
-  }
-  if (c.indep_thr_on) {
-    if (c.thr_separate) {
-      b.thr_l[e] = U(RU_THR) * 2.0f * c.left_rand + (1.0f - c.left_rand);
-      b.thr_r[e] = U(RU_THR + 1) * 2.0f * c.right_rand + (1.0f - c.right_rand);
-    } else {
-      const float m = U(RU_THR) * 2.0f * c.thr_rand + (1.0f - c.thr_rand);
-      b.thr_l[e] = m;
-      b.thr_r[e] = m;
-    }
-  }
-  // ---- _apply_mass_driven_coupling (USV_Virtual.py:988-1040) ----
-  if (c.couple_drag || c.couple_thr || c.couple_kiz) {
-    const double den_d = (double)c.mass_max - (double)c.base_mass;
-    const float den = (float)(den_d > 1e-6 ? den_d : 1e-6);
-    const float r = clampt((mass - c.base_mass) / den, 0.f, 1.f);
-    b.mass_r[e] = r;
-    if (c.couple_drag) b.k_drag[e] = c.kdrag_min + r * (float)((double)c.kdrag_max - (double)c.kdrag_min);
-    if (c.couple_thr) {
-      const float s = clampt(1.0f - r * c.thr_rand, (float)(1.0 - (double)c.thr_rand), 1.0f);
-      b.thr_l[e] = s;
-      b.thr_r[e] = s;
-    }
-    if (c.couple_kiz) b.k_iz[e] = c.kiz_min + r * (float)((double)c.kiz_max - (double)c.kiz_min);
-  }
-  // ---- CaptureXYTask.get_spawns (static_obs.py:936-1060), previous-episode target ----
-  const float r = U(RU_SPAWN_R) * (c.spawn_rmax - c.spawn_rmin) + c.spawn_rmin;
-  const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
-  const float sx = r * cosf(th), sy = r * sinf(th);
-  const float yaw0 = U(RU_YAW) * USV_PI_F;
-  const float tx = b.tgt_x[e], ty = b.tgt_y[e];
-  b.field_old_tgt[e] = tx;
-  b.field_old_tgt[n + e] = ty;
-  // ---- pose / velocities / bookkeeping (USV_Virtual.py:1541-1579) ----
-  b.px[e] = sx;
-  b.py[e] = sy;
-  b.yaw[e] = yaw0;
-  b.vx[e] = U(RU_VX) * 3.0f - 1.5f;
-  b.vy[e] = U(RU_VY) * 3.0f - 1.5f;
-  b.wz[e] = 0.f;
-  b.reset_buf[e] = 0;
-  b.progress[e] = 0;
-  b.prev_cmd[e] = 0.f;
-  b.prev_cmd[n + e] = 0.f;
-  // ---- set_targets -> get_goals (static_obs.py:913-930) ----
-  const float g = c.goal_random_position;
-  b.tgt_x[e] = U(RU_GOAL) * g * 2.0f - g;
-  b.tgt_y[e] = U(RU_GOAL + 1) * g * 2.0f - g;
-}
-
-// ------------------------------------------------------------------------
-// Obstacle placement with rejection (CaptureXYTask.get_spawns obstacle part,
-// static_obs.py:968-1048): 16 lanes per reset env, lane o owns obstacle o.
-// Box around the previous-episode target; an obstacle is redrawn while it is
-// closer than min_dist_safe to the spawn or the target, or closer than
-// min_obs_sep to a lower-index obstacle; after USV_SPAWN_ITERS redraws the
-// leftovers go to limbo (999, 999).  Same uniforms as the per-env restatement
-// (reset slots RU_OBST + 2o, RU_RESAMPLE + 32 it + 2o (+1)).
-// ------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_reset_obst(usv_cfg_t c, usv_bufs_t b, uint64_t seed, uint64_t step,
-                                                       const float *__restrict__ inj) {
-  static_assert(USV_NOBST == 16, "one 16-lane group per env");
-  const int n = b.n;
-  const int count = b.ctl[USV_CTL_RESET_COUNT];
-  const int lane = threadIdx.x & 63, o = lane & 15, gbase = lane & 48;
-  const int groups = gridDim.x * (kBlock / 16);
-  step = step_of(b, step);
-  for (int slot = (blockIdx.x * kBlock + threadIdx.x) / 16; slot < count; slot += groups) {
-    const int e = b.reset_ids[slot];
-    auto U = [&](int i) -> float {
-      if (inj) return inj[(size_t)e * USV_NU_RESET + i];
-      float u4[4];
-      philox_u4(seed, (uint32_t)e, step, 0x100u + (uint32_t)(i >> 2), u4);
-      return u4[i & 3];
-    };
-    const float sx = b.px[e], sy = b.py[e];
-    const float tx = b.field_old_tgt[e], ty = b.field_old_tgt[n + e];
-    const float mnx = tx - c.obst_box, mny = ty - c.obst_box;
-    const float dx_ = (tx + c.obst_box) - mnx, dy_ = (ty + c.obst_box) - mny;
-    float ox = U(RU_OBST + 2 * o) * dx_ + mnx;
-    float oy = U(RU_OBST + 2 * o + 1) * dy_ + mny;
-    const float sep2 = c.min_obs_sep * c.min_obs_sep;
-    for (int it = 0; it <= USV_SPAWN_ITERS; ++it) {
+    for (int qq = 0; qq < 4; ++qq) {
+      const int it = 4 * r + qq;
       const float ds = tnorm2(ox - sx, oy - sy);
       const float dt = tnorm2(ox - tx, oy - ty);
       bool bad = (ds < c.min_dist_safe) || (dt < c.min_dist_safe);
@@ -258,22 +140,156 @@ __global__ __launch_bounds__(kBlock) void k_reset_obst(usv_cfg_t c, usv_bufs_t b
         const float ddx = xi - ox, ddy = yi - oy;
         if (i < o && vo && (xi < 900.f) && (ddx * ddx + ddy * ddy) < sep2) bad = true;
       }
-      const uint32_t inval = (uint32_t)((__ballot(bad) >> gbase) & 0xFFFFull);
-      if (inval == 0) break;
+      const uint32_t inval = (uint32_t)((__ballot(bad) >> gbase) & 0xFFFFull);   // same in every group
+      if (inval == 0) { done = true; break; }
       if (it == USV_SPAWN_ITERS) {  // leftovers to limbo (:1042-1048)
         if (bad) { ox = 999.0f; oy = 999.0f; }
+        done = true;
         break;
       }
-      if (bad) {
-        const int rb = RU_RESAMPLE + it * USV_NOBST * 2;
-        ox = U(rb + 2 * o) * dx_ + mnx;
-        oy = U(rb + 2 * o + 1) * dy_ + mny;
+      const float nx = __shfl(cx, 16 * qq + o, 64), ny = __shfl(cy, 16 * qq + o, 64);
+      if (bad) { ox = nx; oy = ny; }
+    }
+  }
+  if (q == 0) {
+    b.obst[(size_t)(2 * o) * n + ee] = ox;
+    b.obst[(size_t)(2 * o + 1) * n + ee] = oy;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uint64_t seed, uint64_t step,
+                                                  const float *__restrict__ inj) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = b.n;
+  const bool active = (e < n) && (b.reset_buf[e] != 0);
+  const int lane = threadIdx.x & 63;
+  step = step_of(b, step);
+  // ---- compaction: reset_buf.nonzero() (USV_Virtual.py:1045) ----
+  const uint64_t mask = __ballot(active);
+  if (mask != 0) {
+    const int leader = __ffsll((long long)mask) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&b.ctl[USV_CTL_RESET_COUNT], __popcll(mask));
+    base = __shfl(base, leader, 64);
+    // ---- episode extras: sums of the envs being reset (:1591-1612), one atomic per wave ----
+    if (c.stats_on) {
+      for (int q = 0; q < USV_NSTAT; ++q) {
+        float v = 0.f;
+        if (active) {
+          v = b.stats[(size_t)q * n + e];
+          if (q == ST_SUCCESS) v = (float)b.done_succ[e];
+          if (q == ST_COLLISION) v = (float)b.done_coll[e];
+          b.stats[(size_t)q * n + e] = 0.f;
+        }
+        v = wave_sum(v);
+        if (lane == leader) atomicAdd(&b.extras_acc[q], v);
       }
     }
-    b.obst[(size_t)(2 * o) * n + e] = ox;
-    b.obst[(size_t)(2 * o + 1) * n + e] = oy;
+    float sx = 0.f, sy = 0.f, tx = 0.f, ty = 0.f;
+    if (active) {
+      const int slot = base + __popcll(mask & ((1ull << lane) - 1ull));
+      b.reset_ids[slot] = e;
+      ResetRng U{inj, seed, step, (uint32_t)e};
+      // ---- CaptureXYTask.reset (static_obs.py:767-778) ----
+      b.goal_cnt[e] = 0;
+      b.done_succ[e] = 0;
+      b.done_coll[e] = 0;
+      b.just_reset[e] = 1;
+      // ---- MassDistributionDisturbances.randomize_masses / _randomize_com (USV_disturbances.py:94-150) ----
+      float mass;
+      if (c.mass_dr_on) mass = U(RU_MASS) * (float)((double)c.mass_max - (double)c.mass_min) + c.mass_min;
+      else mass = U(RU_MASS) * 0.0f + c.base_mass;
+      float cx = c.base_com[0], cy = c.base_com[1], cz = c.base_com[2];
+      if (c.mass_dr_on && c.com_mode == 1) {
+        cx = c.base_com[0] + (U(RU_COM + 0) * 2.0f - 1.0f) * c.com_disp[0];
+        cy = c.base_com[1] + (U(RU_COM + 1) * 2.0f - 1.0f) * c.com_disp[1];
+        cz = c.base_com[2] + (U(RU_COM + 2) * 2.0f - 1.0f) * c.com_disp[2];
+      } else if (c.mass_dr_on && c.com_mode == 2 && c.com_legacy_r > 0.f) {
+        const float r = U(RU_COM) * c.com_legacy_r;
+        const float th = U(RU_COM + 1) * USV_PI_F * 2.0f;
+        cx = c.base_com[0] + cosf(th) * r;
+        cy = c.base_com[1] + sinf(th) * r;
+      }
+      b.mass[e] = mass;
+      b.com_x[e] = cx;
+      b.com_y[e] = cy;
+      b.com_z[e] = cz;
+      // ---- independent randomisations (yaw inertia :193-240, drag :136-174, thrusters :112-127) ----
+      if (c.indep_kiz_on && !c.couple_kiz) {
+        const float u = U(RU_KIZ);
+        b.k_iz[e] = c.kiz_log ? expf(logf(c.kiz_min) + u * (logf(c.kiz_max) - logf(c.kiz_min)))
+                              : c.kiz_min + u * (c.kiz_max - c.kiz_min);
+      }
+      if (c.drag_rand_on && b.lin_damp) {
+        for (int a = 0; a < 3; ++a) {
+          b.lin_damp[(size_t)a * n + e] = c.lin_damp[a] + (U(RU_DRAG + a) * 2.0f - 1.0f) * c.lin_rand[a];
+          b.quad_damp[(size_t)a * n + e] = c.quad_damp[a] + (U(RU_DRAG + 6 + a) * 2.0f - 1.0f) * c.quad_rand[a];
+        }
+      }
+      if (c.indep_kdrag_on) {
+        const float u = U(RU_KDRAG);
+        b.k_drag[e] = c.kdrag_log ? expf(logf(c.kdrag_min) + u * (logf(c.kdrag_max) - logf(c.kdrag_min)))
+                                  : c.kdrag_min + u * (c.kdrag_max - c.kdrag_min);
+      }
+      if (c.indep_thr_on) {
+        if (c.thr_separate) {
+          b.thr_l[e] = U(RU_THR) * 2.0f * c.left_rand + (1.0f - c.left_rand);
+          b.thr_r[e] = U(RU_THR + 1) * 2.0f * c.right_rand + (1.0f - c.right_rand);
+        } else {
+          const float m = U(RU_THR) * 2.0f * c.thr_rand + (1.0f - c.thr_rand);
+          b.thr_l[e] = m;
+          b.thr_r[e] = m;
+        }
+      }
+      // ---- _apply_mass_driven_coupling (USV_Virtual.py:988-1040) ----
+      if (c.couple_drag || c.couple_thr || c.couple_kiz) {
+        const double den_d = (double)c.mass_max - (double)c.base_mass;
+        const float den = (float)(den_d > 1e-6 ? den_d : 1e-6);
+        const float r = clampt((mass - c.base_mass) / den, 0.f, 1.f);
+        b.mass_r[e] = r;
+        if (c.couple_drag) b.k_drag[e] = c.kdrag_min + r * (float)((double)c.kdrag_max - (double)c.kdrag_min);
+        if (c.couple_thr) {
+          const float s = clampt(1.0f - r * c.thr_rand, (float)(1.0 - (double)c.thr_rand), 1.0f);
+          b.thr_l[e] = s;
+          b.thr_r[e] = s;
+        }
+        if (c.couple_kiz) b.k_iz[e] = c.kiz_min + r * (float)((double)c.kiz_max - (double)c.kiz_min);
+      }
+      // ---- CaptureXYTask.get_spawns (static_obs.py:936-1060), previous-episode target ----
+      const float r = U(RU_SPAWN_R) * (c.spawn_rmax - c.spawn_rmin) + c.spawn_rmin;
+      const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
+      sx = r * cosf(th);
+      sy = r * sinf(th);
+      const float yaw0 = U(RU_YAW) * USV_PI_F;
+      tx = b.tgt_x[e];
+      ty = b.tgt_y[e];
+      b.field_old_tgt[e] = tx;
+      b.field_old_tgt[n + e] = ty;
+      // ---- pose / velocities / bookkeeping (USV_Virtual.py:1541-1579) ----
+      b.px[e] = sx;
+      b.py[e] = sy;
+      b.yaw[e] = yaw0;
+      b.vx[e] = U(RU_VX) * 3.0f - 1.5f;
+      b.vy[e] = U(RU_VY) * 3.0f - 1.5f;
+      b.wz[e] = 0.f;
+      b.reset_buf[e] = 0;
+      b.progress[e] = 0;
+      b.prev_cmd[e] = 0.f;
+      b.prev_cmd[n + e] = 0.f;
+      // ---- set_targets -> get_goals (static_obs.py:913-930) ----
+      const float g = c.goal_random_position;
+      b.tgt_x[e] = U(RU_GOAL) * g * 2.0f - g;
+      b.tgt_y[e] = U(RU_GOAL + 1) * g * 2.0f - g;
+    }
+    // ---- obstacles: the whole wave places each of its reset envs in turn ----
+    for (uint64_t mm = mask; mm; mm &= mm - 1) {
+      const int src = __ffsll((long long)mm) - 1;
+      const int ee = blockIdx.x * blockDim.x + (threadIdx.x & ~63) + src;
+      place_obstacles(c, b, ee, __shfl(sx, src, 64), __shfl(sy, src, 64), __shfl(tx, src, 64),
+                      __shfl(ty, src, 64), seed, step, inj);
+    }
   }
-  // the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612)
+  // ---- the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612) ----
   __shared__ bool last;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -283,13 +299,14 @@ __global__ __launch_bounds__(kBlock) void k_reset_obst(usv_cfg_t c, usv_bufs_t b
   }
   __syncthreads();
   if (!last) return;
-  const int q = threadIdx.x;
-  if (q < USV_NSTAT && count > 0) {
-    float m = b.extras_acc[q] / (float)count;
-    if (q != ST_SUCCESS && q != ST_COLLISION) m = m / (float)c.max_episode_length;
-    b.extras[q] = isnan(m) ? 0.f : m;
+  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int qs = threadIdx.x;
+  if (qs < USV_NSTAT && count > 0) {
+    float m = b.extras_acc[qs] / (float)count;
+    if (qs != ST_SUCCESS && qs != ST_COLLISION) m = m / (float)c.max_episode_length;
+    b.extras[qs] = isnan(m) ? 0.f : m;
   }
-  if (q == 0) b.ctl[USV_CTL_OBST_DONE] = 0;
+  if (qs == 0) b.ctl[USV_CTL_OBST_DONE] = 0;
 }
 
 // ------------------------------------------------------------------------
@@ -761,11 +778,6 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t
   USV_CHECK_LAUNCH();
   const int grid = (b->n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_reset, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, seed, step, u_inject);
-  USV_CHECK_LAUNCH();
-  // 16 lanes per reset env; the grid covers every env up to 2048 workgroups, then strides
-  const int grid_o = (int)(((size_t)b->n * 16 + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_reset_obst, dim3(grid_o < 2048 ? grid_o : 2048), dim3(kBlock), 0, s, *cfg, *b, seed, step,
-                     u_inject);
   USV_CHECK_LAUNCH();
   return 0;
 }
