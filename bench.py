@@ -283,7 +283,14 @@ def main():
         bms = big_timer.mean_ms()
         extra = {"env_only_envs": args.env_only_envs, "env_only_fps": args.env_only_envs * nb / tb,
                  "env_step_kernel_ms": bms,
-                 "env_step_kernel_gbs": ENV_STEP_BYTES * args.env_only_envs / (bms * 1e-3) / 1e9}
+                 "env_step_kernel_gbs": ENV_STEP_BYTES * args.env_only_envs / (bms * 1e-3) / 1e9,
+                 "env_step_kernel_frac": ENV_STEP_BYTES * args.env_only_envs / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        tf = os.path.join(ROOT, "profiles", f"env_step_traffic_{args.env_only_envs}.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                tr = json.load(f)
+            extra["env_step_kernel_traffic"] = tr.get("bytes_per_launch")
+            extra["env_step_kernel_traffic_gbs"] = tr.get("bytes_per_launch") / (bms * 1e-3) / 1e9
         del big
     if rank == 0:
         out = {
