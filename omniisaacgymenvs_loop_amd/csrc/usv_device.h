@@ -43,6 +43,15 @@ __device__ __forceinline__ float minf(float a, float b) { return a < b ? a : b; 
 __device__ __forceinline__ float clampt(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // torch.norm(v, dim=-1) of a 2-vector == sqrt(fma(y, y, x*x)) (PyTorch CPU reduction)
 __device__ __forceinline__ float tnorm2(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
+// x / b given y = RN(1/b): Markstein's correction (q = x*y, r = x - b*q exactly by fma,
+// q + r*y).  Equals the IEEE quotient whenever it lies in [2^-90, 2^120] (checked
+// exhaustively over every float x for each constant divisor used, and over random
+// divisors; below that range r underflows and the result may be 1 ulp off).
+__device__ __forceinline__ float div_rn(float x, float b, float y) {
+  const float q = x * y;
+  const float r = fmaf(-q, b, x);
+  return fmaf(r, y, q);
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -19,6 +19,9 @@
 // The rigid-body integrator replaces PhysX (no reference implementation).
 #include "usv_device.h"
 
+#include <algorithm>
+#include <cmath>
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -311,9 +314,14 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
 
 // ------------------------------------------------------------------------
 // grid_sample(field, 2*pos/map, bilinear, border, align_corners=False)
-// (static_obs.py:302-326) in the arithmetic of PyTorch's CPU kernel.
+// (static_obs.py:302-326) in the arithmetic of PyTorch's CPU kernel.  Split in
+// two: field_taps issues the 4 texel loads as soon as the position is known,
+// field_blend combines them where the reward needs the potential.
 // ------------------------------------------------------------------------
-__device__ __forceinline__ float sample_field(const float *__restrict__ F, float map_size, float x, float y) {
+struct FieldTaps {
+  float v_nw, v_ne, v_sw, v_se, nw, ne, sw, se;
+};
+__device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, float map_size, float x, float y) {
   constexpr int G = USV_GRID;
   const float gx = 2.0f * x / map_size, gy = 2.0f * y / map_size;
   const float half = (float)G / 2.0f;
@@ -324,13 +332,22 @@ __device__ __forceinline__ float sample_field(const float *__restrict__ F, float
   const float xw = floorf(ix), yn = floorf(iy);
   const float w = ix - xw, ee = 1.f - w;
   const float nn = iy - yn, ss = 1.f - nn;
-  const float nw = ss * ee, ne = ss * w, sw = nn * ee, se = nn * w;
+  FieldTaps t;
+  t.nw = ss * ee; t.ne = ss * w; t.sw = nn * ee; t.se = nn * w;
   const int i0 = (int)xw, j0 = (int)yn, i1 = i0 + 1, j1 = j0 + 1;
-  const float v_nw = F[j0 * G + i0];
-  const float v_ne = (i1 < G) ? F[j0 * G + i1] : 0.f;
-  const float v_sw = (j1 < G) ? F[j1 * G + i0] : 0.f;
-  const float v_se = (i1 < G && j1 < G) ? F[j1 * G + i1] : 0.f;
-  return fmaf(v_se, se, fmaf(v_sw, sw, fmaf(v_ne, ne, v_nw * nw)));
+  // border clamp: i1/j1 == G only when the weight of that tap is 0 (ix, iy <= G-1);
+  // the tap then reads the last column/row (any finite value) and is replaced by 0
+  const int i1c = min(i1, G - 1), j1c = min(j1, G - 1);
+  t.v_nw = F[j0 * G + i0];
+  t.v_ne = F[j0 * G + i1c];
+  t.v_sw = F[j1c * G + i0];
+  t.v_se = F[j1c * G + i1c];
+  if (i1 >= G) { t.v_ne = 0.f; t.v_se = 0.f; }
+  if (j1 >= G) { t.v_sw = 0.f; t.v_se = 0.f; }
+  return t;
+}
+__device__ __forceinline__ float field_blend(const FieldTaps &t) {
+  return fmaf(t.v_se, t.se, fmaf(t.v_sw, t.sw, fmaf(t.v_ne, t.ne, t.v_nw * t.nw)));
 }
 
 __device__ __forceinline__ float pen_scalar(int kind, float k, float x0, float cc, float x) {
@@ -339,95 +356,179 @@ __device__ __forceinline__ float pen_scalar(int kind, float k, float x0, float c
   return 0.f;
 }
 
-__device__ __forceinline__ float enc_centered(float x, float xmin, float xmax, float nominal) {
-  double s = fabs((double)xmin - nominal);
-  if (fabs((double)xmax - nominal) > s) s = fabs((double)xmax - nominal);
-  if (1e-6 > s) s = 1e-6;
-  return clampt((x - nominal) / (float)s, -1.f, 1.f);
+// ------------------------------------------------------------------------
+// Fused control step.  One thread per env.  Every per-env array lives in one
+// <2 GiB window of HBM (StepWin: byte offsets from the window base), so all
+// per-env loads/stores are buffer instructions with ONE shared 32-bit lane
+// offset and a scalar per-array offset: no per-access 64-bit address VALU work.
+// ------------------------------------------------------------------------
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+struct StepWin {
+  uint32_t px, py, yaw, vx, vy, wz, fl, fr, mass, k_iz, k_drag, thr_l, thr_r, com_x, com_y, com_z;
+  uint32_t lin_damp, quad_damp, progress, tgt_x, tgt_y, obst, goal_cnt, prev_dist, prev_head, prev_pot, prev_wz;
+  uint32_t stats, prev_cmd, rew, reset_buf, dones, done_coll, done_succ, just_reset, obs;
+  uint32_t n4;      // bytes of one [n] f32 row
+  uint32_t bytes;   // window size
+};
+// uniform constants derived on the host from usv_cfg_t (float/double arithmetic of the
+// reference done once; divisors with their correctly rounded reciprocals for div_rn)
+struct StepK {
+  float act_rng, pos_rng, vel_rng, head_rng;
+  float mass_den, inv_mass_den;
+  float com_div[3], inv_com_div[3];
+  float priv_base[8];             // the 8 privileged values when they do not depend on the env
+  float enc_lo[3], enc_r[3], inv_enc_r[3];   // kdrag, thr, kiz: minmax range / centered scale
+  int enc_ok[3];
+  float inv_exp_coeff;
+};
+
+__device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t R, uint32_t so, uint32_t vo) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(R, vo, so, 0));
 }
-__device__ __forceinline__ float enc_minmax(float x, float xmin, float xmax) {
-  if ((double)xmax - (double)xmin <= 1e-6) return 0.f;
-  const float z = (x - xmin) / (float)((double)xmax - (double)xmin);
-  return clampt(2.0f * z - 1.0f, -1.f, 1.f);
+__device__ __forceinline__ int32_t bldi(__amdgpu_buffer_rsrc_t R, uint32_t so, uint32_t vo) {
+  return (int32_t)__builtin_amdgcn_raw_buffer_load_b32(R, vo, so, 0);
+}
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t R, uint32_t so, uint32_t vo, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), R, vo, so, 0);
+}
+__device__ __forceinline__ void bsti(__amdgpu_buffer_rsrc_t R, uint32_t so, uint32_t vo, int32_t v) {
+  __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, R, vo, so, 0);
 }
 
-// ------------------------------------------------------------------------
-// Fused control step.  Reads per env: state (6) + lag (2) + DR params (6) +
-// task/history (~12) + obstacles (32) + 4 texels of the field; writes state,
-// lag, history, obs row (33), reward, done, stats.
-// ------------------------------------------------------------------------
-template <bool kStats>
-__global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, const float *__restrict__ actions,
+// 64-bit (distance bits, obstacle index) compare-exchange for the top-5 network:
+// keys are distinct, so the network reproduces torch.topk(largest=False)'s
+// order exactly (ties -> lower index first)
+__device__ __forceinline__ void cx64(uint64_t &a, uint64_t &b) {
+  const uint64_t lo = a < b ? a : b, hi = a < b ? b : a;
+  a = lo; b = hi;
+}
+__device__ __forceinline__ void mn64(uint64_t &a, uint64_t b) { a = a < b ? a : b; }
+__device__ __forceinline__ void mx64(uint64_t a, uint64_t &b) { b = a < b ? b : a; }
+
+// the 5 smallest of 16 keys in ascending order in k[0..4]: Batcher's odd-even
+// merge sort pruned to the comparators that reach outputs 0..4 (50 of 63;
+// checked exhaustively by the 0-1 principle)
+__device__ __forceinline__ void top5_of_16(uint64_t k[16]) {
+  cx64(k[0], k[1]); cx64(k[2], k[3]); cx64(k[0], k[2]); cx64(k[1], k[3]); cx64(k[1], k[2]);
+  cx64(k[4], k[5]); cx64(k[6], k[7]); cx64(k[4], k[6]); cx64(k[5], k[7]); cx64(k[5], k[6]);
+  cx64(k[0], k[4]); cx64(k[2], k[6]); cx64(k[2], k[4]); cx64(k[1], k[5]); mn64(k[3], k[7]);
+  cx64(k[3], k[5]); cx64(k[1], k[2]); cx64(k[3], k[4]); mn64(k[5], k[6]);
+  cx64(k[8], k[9]); cx64(k[10], k[11]); cx64(k[8], k[10]); cx64(k[9], k[11]); cx64(k[9], k[10]);
+  cx64(k[12], k[13]); cx64(k[14], k[15]); cx64(k[12], k[14]); cx64(k[13], k[15]); cx64(k[13], k[14]);
+  cx64(k[8], k[12]); cx64(k[10], k[14]); cx64(k[10], k[12]); cx64(k[9], k[13]); mn64(k[11], k[15]);
+  cx64(k[11], k[13]); cx64(k[9], k[10]); cx64(k[11], k[12]); mn64(k[13], k[14]);
+  cx64(k[0], k[8]); mn64(k[4], k[12]); mn64(k[4], k[8]); mn64(k[2], k[10]); cx64(k[2], k[4]);
+  cx64(k[1], k[9]); mn64(k[5], k[13]); mn64(k[5], k[9]); mn64(k[3], k[11]); mn64(k[3], k[5]);
+  cx64(k[1], k[2]); cx64(k[3], k[4]);
+}
+
+template <bool kStats, bool kInj>
+__global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, StepWin w, StepK K,
+                                                     const char *__restrict__ wbase, const float *__restrict__ actions,
                                                      const float *__restrict__ lut, float bias, uint64_t seed,
                                                      uint64_t step, const float *__restrict__ inj, int part) {
   __shared__ float sobs[kBlock * USV_NOBS];
+  __shared__ float2 sob[USV_NOBST][kBlock];
+  __shared__ float slut[2 * USV_LUT_N];
   __shared__ uint8_t keep[kBlock];
   const int n = b.n;
-  const int e = blockIdx.x * kBlock + threadIdx.x;
+  const int tid = threadIdx.x;
+  const int e = blockIdx.x * kBlock + tid;
+  const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc((void *)wbase, 0, (int)w.bytes, 0x00020000);
+  // thruster LUT -> registers first (the oldest loads in flight: waiting for them before
+  // the LDS write below does not wait for the per-env loads issued after them)
+  static_assert(2 * USV_LUT_N / 4 <= 2 * kBlock, "LUT staging: two float4 per thread");
+  const float4 *lut4 = reinterpret_cast<const float4 *>(lut);
+  const bool lut_hi = tid + kBlock < 2 * USV_LUT_N / 4;
+  const float4 lut_a = lut4[tid];
+  const float4 lut_b = lut4[min(tid + kBlock, 2 * USV_LUT_N / 4 - 1)];   // unconditional: no branch, no early wait
   // part 0: every env; 1: envs not reset this step (they do not read this step's new
   // fields, so this part can run concurrently with the potential-field kernels);
   // 2: the envs reset this step, after their fields are built
-  bool mine = e < n;
-  if (mine && part != 0) {
-    const bool jr = b.just_reset[e] != 0;
-    mine = (part == 1) ? !jr : jr;
-  }
-  keep[threadIdx.x] = mine ? 1 : 0;
+  // Every lane runs the whole step (lanes past n on env n-1); the stores of lanes that
+  // are not `mine` go to an offset past the window, which the buffer range check drops.
+  const int ec = min(e, n - 1);
+  const uint32_t v4 = (uint32_t)ec * 4u;
+  // loads in the order they are consumed (vmcnt waits retire loads in issue order):
+  // action + reset flag (LUT index), state and parameters (substeps), then the rest
+  const float2 a2 = reinterpret_cast<const float2 *>(actions)[ec];
+  const bool was_reset = __builtin_amdgcn_raw_buffer_load_b8(R, (uint32_t)ec, w.just_reset, 0) != 0;
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr uint32_t kDrop = 0x80000000u;   // > w.bytes
   const int32_t *ctl = b.ctl;
-  const bool pot_none = ctl[USV_CTL_POT_VALID] == 0 || ctl[USV_CTL_RESET_COUNT] > 0;
+  // control words: plain (non-short-circuit) scalar reads, so no branch waits on memory here
+  const int32_t ctl_pot = ctl[USV_CTL_POT_VALID], ctl_cnt = ctl[USV_CTL_RESET_COUNT];
+  const bool pot_none = (ctl_pot == 0) | (ctl_cnt > 0);
   const bool pen_valid = ctl[USV_CTL_PEN_VALID] != 0;
   const bool rew_valid = ctl[USV_CTL_REW_VALID] != 0;
-  // obs row staged straight into LDS (odd row stride: conflict-free), clamped on write
-  // (_process_data clamp, vec_env_rlgames.py:85-95)
   step = step_of(b, step);
   bias = bias_of(c, b, bias);
-  float *obs = sobs + threadIdx.x * USV_NOBS;
+  // obs row staged in LDS (odd row stride: conflict-free), clamped on write
+  // (_process_data clamp, vec_env_rlgames.py:85-95); slots no branch writes are zeroed
+  float *obs = sobs + tid * USV_NOBS;
   const float clip = c.clip_obs;
   auto put = [&](int q, float v) { obs[q] = clampt(v, -clip, clip); };
-#pragma unroll
-  for (int q = 0; q < USV_NOBS; ++q) obs[q] = 0.f;
-  if (mine) {
+  obs[6] = 0.f;
+  obs[7] = 0.f;
+  if (c.priv_dim == 4) { obs[23] = 0.f; obs[24] = 0.f; obs[25] = 0.f; obs[26] = 0.f; }
+  {
     // ---- every per-env input that does not depend on this step's results is loaded
-    // here, up front, so the HBM latencies overlap each other and the physics (only
-    // the 4 field texels and the 2 LUT entries are data-dependent gathers) ----
-    const bool was_reset = b.just_reset[e] != 0;
-    const float2 a2 = reinterpret_cast<const float2 *>(actions)[e];
-    float px = b.px[e], py = b.py[e], yaw = b.yaw[e];
-    float vx = b.vx[e], vy = b.vy[e], wz = b.wz[e];
-    float fl = b.fl[e], fr = b.fr[e];
-    const float m = b.mass[e];
-    const float k_iz = b.k_iz[e], k_drag = b.k_drag[e], thr_l = b.thr_l[e], thr_r = b.thr_r[e];
-    const float comx = b.com_x[e], comy = b.com_y[e], comz = b.com_z[e];
-    float lin0 = c.lin_damp[0], lin1 = c.lin_damp[1], lin2 = c.lin_damp[2];
-    float qd0 = c.quad_damp[0], qd1 = c.quad_damp[1], qd2 = c.quad_damp[2];
-    if (b.lin_damp) {
-      lin0 = b.lin_damp[e]; lin1 = b.lin_damp[n + e]; lin2 = b.lin_damp[2 * n + e];
-      qd0 = b.quad_damp[e]; qd1 = b.quad_damp[n + e]; qd2 = b.quad_damp[2 * n + e];
-    }
-    const int progress0 = b.progress[e];
-    const float tgx = b.tgt_x[e], tgy = b.tgt_y[e];
+    // up front, so the HBM latencies overlap each other and the physics ----
+    float px = bld(R, w.px, v4), py = bld(R, w.py, v4), yaw = bld(R, w.yaw, v4);
+    float vx = bld(R, w.vx, v4), vy = bld(R, w.vy, v4), wz = bld(R, w.wz, v4);
+    float fl = bld(R, w.fl, v4), fr = bld(R, w.fr, v4);
+    const float m = bld(R, w.mass, v4);
+    const float k_iz = bld(R, w.k_iz, v4), k_drag = bld(R, w.k_drag, v4);
+    const float thr_l = bld(R, w.thr_l, v4), thr_r = bld(R, w.thr_r, v4);
+    const float comx = bld(R, w.com_x, v4), comy = bld(R, w.com_y, v4), comz = bld(R, w.com_z, v4);
+    // per-env damping (drag DR) or the config's: loaded unconditionally (offset 0 is inside
+    // the window when absent) and selected, so no branch sits between the loads
+    const bool dr = b.lin_damp != nullptr;
+    const float l0 = bld(R, w.lin_damp, v4), l1 = bld(R, w.lin_damp + w.n4, v4), l2 = bld(R, w.lin_damp + 2 * w.n4, v4);
+    const float q0 = bld(R, w.quad_damp, v4), q1 = bld(R, w.quad_damp + w.n4, v4);
+    const float q2 = bld(R, w.quad_damp + 2 * w.n4, v4);
+    const float lin0 = dr ? l0 : c.lin_damp[0], lin1 = dr ? l1 : c.lin_damp[1], lin2 = dr ? l2 : c.lin_damp[2];
+    const float qd0 = dr ? q0 : c.quad_damp[0], qd1 = dr ? q1 : c.quad_damp[1], qd2 = dr ? q2 : c.quad_damp[2];
+    __builtin_amdgcn_sched_barrier(0);   // keep the substep inputs ahead of the loads below
+    const int progress0 = bldi(R, w.progress, v4);
+    const float tgx = bld(R, w.tgt_x, v4), tgy = bld(R, w.tgt_y, v4);
     float obx[USV_NOBST], oby[USV_NOBST];
 #pragma unroll
     for (int o = 0; o < USV_NOBST; ++o) {
-      obx[o] = b.obst[(size_t)(2 * o) * n + e];
-      oby[o] = b.obst[(size_t)(2 * o + 1) * n + e];
+      obx[o] = bld(R, w.obst + (uint32_t)(2 * o) * w.n4, v4);
+      oby[o] = bld(R, w.obst + (uint32_t)(2 * o + 1) * w.n4, v4);
     }
-    const int goal_cnt0 = b.goal_cnt[e];
-    const float prev_d_mem = b.prev_dist[e], prev_head_mem = b.prev_head[e];
-    const float prev_pot_mem = b.prev_pot[e], prev_wz_mem = b.prev_wz[e];
-    float sums[USV_NSTAT];
+    const int goal_cnt0 = bldi(R, w.goal_cnt, v4);
+
+    const float prev_d_mem = bld(R, w.prev_dist, v4), prev_head_mem = bld(R, w.prev_head, v4);
+    const float prev_pot_mem = bld(R, w.prev_pot, v4), prev_wz_mem = bld(R, w.prev_wz, v4);
+    // episode sums that this step adds to (the other keys are written by the reset path only)
+    constexpr int kSum[25] = {ST_TOTAL_REWARD, ST_DISTANCE_REWARD, ST_ALIGNMENT_REWARD, ST_HEADING_IMPROVE_REWARD,
+                              ST_POTENTIAL_SHAPING_REWARD, ST_SPEED_REWARD, ST_ANGULAR_REWARD,
+                              ST_TURN_HAZARD_PENALTY, ST_GOAL_REWARD, ST_TIME_REWARD, ST_COLLISION_REWARD,
+                              ST_DANGER_MEAN, ST_DANGER_HI_RATE, ST_G_GATE_MEAN, ST_POSITION_ERROR,
+                              ST_BOUNDARY_PENALTY, ST_ANGULAR_VEL_PENALTY, ST_ANGULAR_VEL_VARIATION_PENALTY,
+                              ST_ENERGY_PENALTY, ST_NORMED_LINEAR_VEL, ST_NORMED_ANGULAR_VEL, ST_CMD_NEG_RATE,
+                              ST_U_MEAN, ST_U_LOW_RATE, ST_U_SUM};
+    const bool sum_on[25] = {true, true, true, true, true, true, true, true, true, true, true, true, true,
+                             true, true, true, c.pen_ang_kind != 0, c.pen_angv_kind != 0, c.pen_en_kind != 0,
+                             true, true, true, true, true, true};
+    float sums[25];
     if (kStats) {
 #pragma unroll
-      for (int q = 0; q < USV_NSTAT; ++q) sums[q] = b.stats[(size_t)q * n + e];
+      for (int q = 0; q < 25; ++q) sums[q] = bld(R, w.stats + (uint32_t)kSum[q] * w.n4, v4);
     }
-    // ---- uniforms of this step (SU_* layout) ----
+    // ---- uniforms of this step (SU_* layout; the second Philox block only when drawn from) ----
     float u[USV_NU_STEP];
-    if (inj) {
+    if (kInj) {
 #pragma unroll
-      for (int i = 0; i < USV_NU_STEP; ++i) u[i] = inj[(size_t)e * USV_NU_STEP + i];
+      for (int i = 0; i < USV_NU_STEP; ++i) u[i] = inj[(size_t)ec * USV_NU_STEP + i];
     } else {
       philox_u4(seed, (uint32_t)e, step, 0u, u);
-      philox_u4(seed, (uint32_t)e, step, 1u, u + 4);
+      if (c.pos_noise_on || c.act_noise_on) philox_u4(seed, (uint32_t)e, step, 1u, u + 4);
+      else u[4] = u[5] = u[6] = u[7] = 0.f;
     }
     // ---- VecEnvRLGames.step clamp (:136-140) + pre_physics_step (:1050-1099) ----
     const float cmd0 = clampt(a2.x, -c.clip_actions, c.clip_actions);
@@ -437,9 +538,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     float t0 = cmd0, t1 = cmd1;
     if (bias != 0.f) { t0 = t0 + bias; t1 = t1 + bias; }
     if (c.act_noise_on) {
-      const float rng = (float)((double)c.act_noise_max - (double)c.act_noise_min);
-      t0 = t0 + (u[SU_ACT] * rng + c.act_noise_min);
-      t1 = t1 + (u[SU_ACT + 1] * rng + c.act_noise_min);
+      t0 = t0 + (u[SU_ACT] * K.act_rng + c.act_noise_min);
+      t1 = t1 + (u[SU_ACT + 1] * K.act_rng + c.act_noise_min);
     }
     t0 = clampt(t0, -1.f, 1.f);
     t1 = clampt(t1, -1.f, 1.f);
@@ -453,13 +553,25 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     int i1 = (int)rintf(((uu1 + 1.0f) / 2.0f) * (float)(USV_LUT_N - 1));
     i0 = min(max(i0, 0), USV_LUT_N - 1);
     i1 = min(max(i1, 0), USV_LUT_N - 1);
-    float tgt0 = lut[i0], tgt1 = lut[USV_LUT_N + i1];
+    bool mine = e < n;
+    if (part != 0) mine = mine && ((part == 1) ? !was_reset : was_reset);
+    keep[tid] = mine ? 1 : 0;
+    const uint32_t vs = mine ? v4 : kDrop;
+    reinterpret_cast<float4 *>(slut)[tid] = lut_a;
+    if (lut_hi) reinterpret_cast<float4 *>(slut)[tid + kBlock] = lut_b;
+    __syncthreads();   // LUT staged
+    float tgt0 = slut[i0], tgt1 = slut[USV_LUT_N + i1];
     if (c.use_thr_mult) { tgt0 = tgt0 * thr_l; tgt1 = tgt1 * thr_r; }
-    // ---- 10 substeps: thruster lag, planar forces, semi-implicit Euler ----
+    // ---- 10 substeps: thruster lag, planar forces, semi-implicit Euler.  The
+    // integrator is this build's own (it replaces PhysX): accelerations divide by
+    // m and Izz through their reciprocals with one correction step (div_rn == the
+    // IEEE quotient for quotients in [2^-90, 2^120]) ----
     const float izz = c.izz0 * k_iz;
+    const float inv_m = 1.0f / m, inv_izz = 1.0f / izz;
     const float kd = c.use_drag_scale ? k_drag : 1.0f;
     const float al = c.thr_alpha, oma = 1.0f - c.thr_alpha;
     const float dt = c.dt;
+    const float arm_l = -(c.thr_y - comy), arm_r = c.thr_y + comy;
     for (int s = 0; s < c.substeps; ++s) {
       fl = fl * al + oma * tgt0;                      // ThrusterDynamics.py:133-136
       fr = fr * al + oma * tgt1;
@@ -473,10 +585,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       if (c.use_drag_scale) { D0 = D0 * kd; D1 = D1 * kd; D2 = D2 * kd; }
       const float X = fl + fr + (-D0 * ub);           // Hydrodynamics.py:243
       const float Y = -D1 * vb;
-      const float N = -(c.thr_y - comy) * fl + (c.thr_y + comy) * fr + (-D2 * rb);
-      const float ax = (cy_ * X - sy_ * Y) / m;
-      const float ay = (sy_ * X + cy_ * Y) / m;
-      const float aw = N / izz;
+      const float N = arm_l * fl + arm_r * fr + (-D2 * rb);
+      const float ax = div_rn(cy_ * X - sy_ * Y, m, inv_m);
+      const float ay = div_rn(sy_ * X + cy_ * Y, m, inv_m);
+      const float aw = div_rn(N, izz, inv_izz);
       vx = vx + ax * dt;
       vy = vy + ay * dt;
       wz = wz + aw * dt;
@@ -487,31 +599,29 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       else if (yw <= -USV_PI_F) yw += USV_2PI_F;
       yaw = yw;
     }
-    b.px[e] = px; b.py[e] = py; b.yaw[e] = yaw;
-    b.vx[e] = vx; b.vy[e] = vy; b.wz[e] = wz;
-    b.fl[e] = fl; b.fr[e] = fr;
+    bst(R, w.px, vs, px); bst(R, w.py, vs, py); bst(R, w.yaw, vs, yaw);
+    bst(R, w.vx, vs, vx); bst(R, w.vy, vs, vy); bst(R, w.wz, vs, wz);
+    bst(R, w.fl, vs, fl); bst(R, w.fr, vs, fr);
     // ---- post_physics_step: progress, update_state noise (USV_Virtual.py:771-813) ----
     const int progress = progress0 + 1;
-    b.progress[e] = progress;
+    bsti(R, w.progress, vs, progress);
     float pxn = px, pyn = py;
     if (c.pos_noise_on) {
-      const float rng = (float)((double)c.pos_noise_max - (double)c.pos_noise_min);
-      pxn = pxn + (u[SU_PX] * rng + c.pos_noise_min);
-      pyn = pyn + (u[SU_PX + 1] * rng + c.pos_noise_min);
+      pxn = pxn + (u[SU_PX] * K.pos_rng + c.pos_noise_min);
+      pyn = pyn + (u[SU_PX + 1] * K.pos_rng + c.pos_noise_min);
     }
+    // the potential sample only needs the position: issue its 4 texel loads now
+    const FieldTaps taps = field_taps(b.field + (size_t)ec * USV_GRID2, c.map_size, pxn, pyn);
     float vxn = vx, vyn = vy, wzn = wz;
     if (c.vel_noise_on) {
-      const float rng = (float)((double)c.vel_noise_max - (double)c.vel_noise_min);
-      vxn = vxn + (u[SU_VX] * rng + c.vel_noise_min);
-      vyn = vyn + (u[SU_VY] * rng + c.vel_noise_min);
-      wzn = wzn + (u[SU_WZ] * rng + c.vel_noise_min);
+      vxn = vxn + (u[SU_VX] * K.vel_rng + c.vel_noise_min);
+      vyn = vyn + (u[SU_VY] * K.vel_rng + c.vel_noise_min);
+      wzn = wzn + (u[SU_WZ] * K.vel_rng + c.vel_noise_min);
     }
     float yawn = yaw;
-    if (c.head_noise_on) {
-      const float rng = (float)((double)c.head_noise_max - (double)c.head_noise_min);
-      yawn = yawn + (u[SU_HEAD] * rng + c.head_noise_min);
-    }
-    const float hc = cosf(yawn), hs = sinf(yawn);
+    if (c.head_noise_on) yawn = yawn + (u[SU_HEAD] * K.head_rng + c.head_noise_min);
+    float hs, hc;
+    sincosf(yawn, &hs, &hc);
     // ---- get_state_observations (static_obs.py:193-299) ----
     const float ex = tgx - pxn, ey = tgy - pyn;
     const float theta = atan2f(hs, hc);
@@ -520,30 +630,23 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     const float herr = fabsf(alpha);
     const float dist = sqrtf(ex * ex + ey * ey);
     const float dist_n = tnorm2(ex, ey);
-    const float ct = cosf(theta), st = sinf(theta);
-    // 16 obstacle distances, running top-5 (torch.topk largest=False, ascending)
-    float bd[USV_NCLOSE], bx[USV_NCLOSE], by[USV_NCLOSE];
-#pragma unroll
-    for (int q = 0; q < USV_NCLOSE; ++q) { bd[q] = INFINITY; bx[q] = 0.f; by[q] = 0.f; }
+    float st, ct, sa, ca;
+    sincosf(theta, &st, &ct);
+    sincosf(alpha, &sa, &ca);     // cos is even: ca == cosf(herr) as well
+    // 16 obstacle distances; the 5 nearest (torch.topk largest=False, ascending) by a
+    // selection network over (distance bits, index) keys -- distances are >= 0 so
+    // their bit patterns order like the floats
+    uint64_t key[USV_NOBST];
     float min_od = INFINITY, coll = 0.f;
 #pragma unroll
     for (int o = 0; o < USV_NOBST; ++o) {
-      const float rx = obx[o] - pxn;
-      const float ry = oby[o] - pyn;
-      const float d = tnorm2(rx, ry);
+      const float d = tnorm2(obx[o] - pxn, oby[o] - pyn);
       min_od = fminf(min_od, d);
       coll += (float)(d < c.collision_threshold) * (-10.0f) * 10.0f;
-      // insertion (strict <: ties keep the lower obstacle index first)
-      float cd = d, cx = rx, cy = ry;
-#pragma unroll
-      for (int q = 0; q < USV_NCLOSE; ++q) {
-        if (cd < bd[q]) {
-          const float td = bd[q], tx = bx[q], ty = by[q];
-          bd[q] = cd; bx[q] = cx; by[q] = cy;
-          cd = td; cx = tx; cy = ty;
-        }
-      }
+      key[o] = ((uint64_t)__float_as_uint(d) << 4) | (uint64_t)o;
+      sob[o][tid] = make_float2(obx[o], oby[o]);
     }
+    top5_of_16(key);
     if (c.obs_local) {
       put(0, hc * vxn + hs * vyn);
       put(1, -hs * vxn + hc * vyn);
@@ -552,102 +655,101 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       put(1, vyn);
     }
     put(2, wzn);
-    put(3, cosf(alpha));
-    put(4, sinf(alpha));
+    put(3, ca);
+    put(4, sa);
     put(5, dist_n);
 #pragma unroll
     for (int q = 0; q < USV_NCLOSE; ++q) {
-      const float vbx = bx[q] * ct + by[q] * st;
-      const float vby = -bx[q] * st + by[q] * ct;
+      const int o = (int)(key[q] & 15u);
+      const float2 ob = sob[o][tid];
+      const float bx = ob.x - pxn, by = ob.y - pyn;
+      const float bd = __uint_as_float((uint32_t)(key[q] >> 4));
+      const float vbx = bx * ct + by * st;
+      const float vby = -bx * st + by * ct;
       const float nf = sqrtf(vbx * vbx + vby * vby + 1e-6f);
-      put(8 + 3 * q, bd[q] - c.obstacle_radius);
-      put(9 + 3 * q, -vbx / nf);
-      put(10 + 3 * q, -vby / nf);
+      const float inv_nf = 1.0f / nf;
+      put(8 + 3 * q, bd - c.obstacle_radius);
+      put(9 + 3 * q, div_rn(-vbx, nf, inv_nf));
+      put(10 + 3 * q, div_rn(-vby, nf, inv_nf));
     }
     const int pa = USV_NOBS - c.priv_dim - 2;
     put(pa, prev_cmd0);
     put(pa + 1, prev_cmd1);
-    b.prev_cmd[e] = prev_cmd0;
-    b.prev_cmd[n + e] = prev_cmd1;
+    bst(R, w.prev_cmd, vs, prev_cmd0);
+    bst(R, w.prev_cmd + w.n4, vs, prev_cmd1);
     // ---- privileged tail (USV_Virtual.py:840-976) ----
     {
-      float mass_o, co0, co1, co2;
-      if (c.masscom_base) {
-        mass_o = c.mass_relative ? 0.f : c.base_mass;
-        co0 = c.com_scaled ? c.base_com[0] / (c.com_scale[0] + 1e-6f) : c.base_com[0];
-        co1 = c.com_scaled ? c.base_com[1] / (c.com_scale[1] + 1e-6f) : c.base_com[1];
-        co2 = c.com_scaled ? c.base_com[2] / (c.com_scale[2] + 1e-6f) : c.base_com[2];
-      } else {
-        const float den = (float)(fabs((double)c.base_mass) > 1e-6 ? fabs((double)c.base_mass) : 1e-6);
-        mass_o = c.mass_relative ? (m - c.base_mass) / den : m;
-        const float cx = comx, cz = comz;
-        co0 = c.com_scaled ? cx / (c.com_scale[0] + 1e-6f) : cx;
-        co1 = c.com_scaled ? comy / (c.com_scale[1] + 1e-6f) : comy;
-        co2 = c.com_scaled ? cz / (c.com_scale[2] + 1e-6f) : cz;
-      }
       const int pt = USV_NOBS - c.priv_dim;
-      put(pt, mass_o); put(pt + 1, co0); put(pt + 2, co1); put(pt + 3, co2);
-      if (c.priv_dim == 8) {
-        float kdv, tl, tr, kz;
-        if (c.masscom_base) {
-          if (c.priv_mode == 2) {
-            kdv = 0.5f * (c.kdrag_min + c.kdrag_max);
-            tl = tr = c.couple_thr ? (1.0f - 0.5f * c.thr_rand) : 1.0f;
-            kz = 0.5f * (c.kiz_min + c.kiz_max);
-          } else { kdv = tl = tr = kz = 1.0f; }
-        } else {
-          kdv = k_drag; tl = thr_l; tr = thr_r; kz = k_iz;
+      if (c.masscom_base) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (q < c.priv_dim) put(pt + q, K.priv_base[q]);
+      } else {
+        put(pt, c.mass_relative ? div_rn(m - c.base_mass, K.mass_den, K.inv_mass_den) : m);
+        put(pt + 1, c.com_scaled ? div_rn(comx, K.com_div[0], K.inv_com_div[0]) : comx);
+        put(pt + 2, c.com_scaled ? div_rn(comy, K.com_div[1], K.inv_com_div[1]) : comy);
+        put(pt + 3, c.com_scaled ? div_rn(comz, K.com_div[2], K.inv_com_div[2]) : comz);
+        if (c.priv_dim == 8) {
+          float v[4] = {k_drag, thr_l, thr_r, k_iz};
+          const bool on[4] = {c.priv_drag_on != 0, c.priv_thr_on != 0, c.priv_thr_on != 0, c.priv_kiz_on != 0};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int j = q == 0 ? 0 : (q == 3 ? 2 : 1);
+            if (c.priv_mode == 1) {          // enc_centered
+              v[q] = clampt(div_rn(v[q] - c.priv_nominal, K.enc_r[j], K.inv_enc_r[j]), -1.f, 1.f);
+            } else if (c.priv_mode == 2) {   // enc_minmax
+              if (!on[q] || !K.enc_ok[j]) {
+                v[q] = 0.f;
+              } else {
+                const float z = div_rn(v[q] - K.enc_lo[j], K.enc_r[j], K.inv_enc_r[j]);
+                v[q] = clampt(2.0f * z - 1.0f, -1.f, 1.f);
+              }
+            }
+            put(pt + 4 + q, v[q]);
+          }
         }
-        if (c.priv_mode == 1) {
-          kdv = enc_centered(kdv, c.kdrag_min, c.kdrag_max, c.priv_nominal);
-          tl = enc_centered(tl, c.thr_min, c.thr_max, c.priv_nominal);
-          tr = enc_centered(tr, c.thr_min, c.thr_max, c.priv_nominal);
-          kz = enc_centered(kz, c.kiz_min, c.kiz_max, c.priv_nominal);
-        } else if (c.priv_mode == 2) {
-          kdv = c.priv_drag_on ? enc_minmax(kdv, c.kdrag_min, c.kdrag_max) : 0.f;
-          tl = c.priv_thr_on ? enc_minmax(tl, c.thr_min, c.thr_max) : 0.f;
-          tr = c.priv_thr_on ? enc_minmax(tr, c.thr_min, c.thr_max) : 0.f;
-          kz = c.priv_kiz_on ? enc_minmax(kz, c.kiz_min, c.kiz_max) : 0.f;
-        }
-        put(pt + 4, kdv); put(pt + 5, tl); put(pt + 6, tr); put(pt + 7, kz);
       }
     }
     // ---- compute_reward (static_obs.py:335-657) ----
+    constexpr float kXs = 0.3f + 1e-6f, kPa = 2.0f + 1e-6f, kGv = (0.15f - 0.02f) + 1e-6f, kGd = 0.01f + 1e-6f;
+    constexpr float kSf = (0.60f - 0.15f) + 1e-6f, kSp = 0.8f + 1e-6f, kAn = 0.2f;
     const float bover = maxf(dist - c.kill_dist, 0.f);
     const float bpen = -expm1f(minf(bover / 0.25f, 20.0f)) * c.boundary_cost;
     const int gir = dist < c.position_tolerance;
     const int goal_cnt = goal_cnt0 * gir + gir;
-    b.goal_cnt[e] = goal_cnt;
+    bsti(R, w.goal_cnt, vs, goal_cnt);
     const float prev_err = rew_valid ? prev_d_mem : dist;
     float dist_r;
     if (c.reward_mode == 0) dist_r = c.position_scale * (prev_err - dist);
     else if (c.reward_mode == 1) dist_r = c.position_scale * (prev_err * prev_err - dist * dist);
-    else dist_r = c.position_scale * (expf(-dist / c.exp_coeff) - expf(-prev_err / c.exp_coeff));
+    else dist_r = c.position_scale * (expf(div_rn(-dist, c.exp_coeff, K.inv_exp_coeff)) -
+                                      expf(div_rn(-prev_err, c.exp_coeff, K.inv_exp_coeff)));
     const float h2 = herr * herr;
     float align_r = c.align_la1 * (expf(c.align_la2 * (h2 * h2)) + expf(c.align_la3 * h2));
     if (was_reset) dist_r = 0.f;
     const float prev_dist = was_reset ? dist : (rew_valid ? prev_d_mem : dist);
-    const float pot = sample_field(b.field + (size_t)e * USV_GRID2, c.map_size, pxn, pyn);
+    const float pot = field_blend(taps);
     const float pn = clampt(pot, 0.f, 1.f);
-    const float xs = clampt((pn - 0.6f) / (0.3f + 1e-6f), 0.f, 1.f);
+    const float xs = clampt(div_rn(pn - 0.6f, kXs, 1.0f / kXs), 0.f, 1.f);
     const float danger = xs * xs * (3.0f - 2.0f * xs);
     align_r = align_r * maxf(0.3f, 1.0f - danger);
     dist_r = dist_r * maxf(0.6f, 1.0f - danger * 0.5f);
-    const float g = clampt(cosf(herr), 0.f, 1.f);
+    const float g = clampt(ca, 0.f, 1.f);
     dist_r = minf(dist_r, 0.f) + g * maxf(dist_r, 0.f);
     const float prev_h = (rew_valid && !was_reset) ? prev_head_mem : herr;
     const float hi = clampt(prev_h - herr, -0.4f, 0.4f);
     const float hi_r = hi * 0.05f;
-    b.prev_head[e] = herr;
+    bst(R, w.prev_head, vs, herr);
     const float prev_pot = (pot_none || was_reset) ? pot : prev_pot_mem;
     float praw = (prev_pot - pot) * 100.0f;
     if (fabsf(praw) < 0.01f) praw = 0.f;
-    const float pa1 = 2.0f * tanhf(praw / (2.0f + 1e-6f));
-    const float gdx = ex / (dist + 1e-6f), gdy = ey / (dist + 1e-6f);
+    const float pa1 = 2.0f * tanhf(div_rn(praw, kPa, 1.0f / kPa));
+    const float dd = dist + 1e-6f, inv_dd = 1.0f / dd;
+    const float gdx = div_rn(ex, dd, inv_dd), gdy = div_rn(ey, dd, inv_dd);
     const float vtp = maxf(vxn * gdx + vyn * gdy, 0.f);
     const float ddp = maxf(prev_dist - dist, 0.f);
-    const float gv = clampt((vtp - 0.02f) / ((0.15f - 0.02f) + 1e-6f), 0.f, 1.f);
-    const float gd = clampt(ddp / (0.01f + 1e-6f), 0.f, 1.f);
+    const float gv = clampt(div_rn(vtp - 0.02f, kGv, 1.0f / kGv), 0.f, 1.f);
+    const float gd = clampt(div_rn(ddp, kGd, 1.0f / kGd), 0.f, 1.f);
     const float ggate = maxf(gv, gd) * g;
     const float ppos = maxf(pa1, 0.f), pneg = minf(pa1, 0.f);
     const float gate_pos = (ppos < 0.5f) ? 1.0f : ggate;
@@ -655,16 +757,16 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     const bool worsening = shaping < -0.05f;
     const bool turning = fabsf(wzn) > 0.2f;
     const float vfwd = vxn * hc + vyn * hs;
-    const float sf = clampt((fabsf(vfwd) - 0.15f) / ((0.60f - 0.15f) + 1e-6f), 0.f, 1.f);
+    const float sf = clampt(div_rn(fabsf(vfwd) - 0.15f, kSf, 1.0f / kSf), 0.f, 1.f);
     const float turn_haz = (float)(worsening && turning) * (-10.0f) * (g * g) * sf;
-    b.prev_pot[e] = pot;
-    const float speed_r = (1.0f - expf(-vtp / (0.8f + 1e-6f))) * 0.05f;
+    bst(R, w.prev_pot, vs, pot);
+    const float speed_r = (1.0f - expf(div_rn(-vtp, kSp, 1.0f / kSp))) * 0.05f;
     const float sgn = (alpha > 0.f) ? 1.f : ((alpha < 0.f) ? -1.f : 0.f);
     const float tang = (herr > 1.0f) ? sgn * 1.0f : sgn * 0.2f;
     const float dw = wzn - tang;
-    const float ang_r = expf(-(dw * dw) / 0.2f) * 0.03f;
+    const float ang_r = expf(div_rn(-(dw * dw), kAn, 1.0f / kAn)) * 0.03f;
     const float goal_r = ((float)goal_cnt * c.goal_reward) * 5.0f;
-    b.prev_dist[e] = dist;
+    bst(R, w.prev_dist, vs, dist);
     const float total = dist_r * 0.5f + align_r * 0.5f + shaping * 2.0f + turn_haz + goal_r + c.time_reward +
                         coll + speed_r + ang_r + hi_r;
     // ---- Penalties.compute_penalty (USV_task_rewards.py:440-523) ----
@@ -678,54 +780,53 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     }
     if (c.pen_en_kind == PEN_SUM) p_en = -(pact0 + pact1) * c.pen_en_k + c.pen_en_c;
     else if (c.pen_en_kind == PEN_SUMSQ) p_en = -(pact0 * pact0 + pact1 * pact1) * c.pen_en_k + c.pen_en_c;
-    b.prev_wz[e] = wzn;
-    b.rew[e] = total + (((p_lin + p_ang) + p_angv) + p_en);
+    bst(R, w.prev_wz, vs, wzn);
+    bst(R, w.rew, vs, total + (((p_lin + p_ang) + p_angv) + p_en));
     // ---- update_kills / is_done (static_obs.py:661-706, USV_Virtual.py:1223-1237) ----
     const bool dkill = dist > c.kill_dist;
     const bool ckill = min_od < c.collision_threshold;
     const bool skill = goal_cnt >= c.kill_after_n;
     const bool die = dkill || ckill || skill;
     if (die) {
-      b.done_coll[e] = ckill;
-      b.done_succ[e] = skill && !ckill;
+      bsti(R, w.done_coll, vs, ckill);
+      bsti(R, w.done_succ, vs, skill && !ckill);
     }
     const int tout = progress >= c.max_episode_length - 1;
     const int rb = c.fixed_horizon_eval ? tout : (tout ? 1 : (int)die);
-    b.reset_buf[e] = rb;
-    b.dones[e] = (int64_t)rb;
-    b.just_reset[e] = 0;
+    bsti(R, w.reset_buf, vs, rb);
+    const u32x2_t rb64 = {(uint32_t)rb, 0u};
+    __builtin_amdgcn_raw_buffer_store_b64(rb64, R, mine ? (uint32_t)ec * 8u : kDrop, w.dones, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, R, mine ? (uint32_t)ec : kDrop, w.just_reset, 0);
     if (kStats) {
-      float *S = b.stats;
-#define ADDS(k, v) sums[k] += (v)
-      ADDS(ST_TOTAL_REWARD, total); ADDS(ST_DISTANCE_REWARD, dist_r); ADDS(ST_ALIGNMENT_REWARD, align_r);
-      ADDS(ST_HEADING_IMPROVE_REWARD, hi_r); ADDS(ST_POTENTIAL_SHAPING_REWARD, shaping);
-      ADDS(ST_SPEED_REWARD, speed_r); ADDS(ST_ANGULAR_REWARD, ang_r); ADDS(ST_TURN_HAZARD_PENALTY, turn_haz);
-      ADDS(ST_GOAL_REWARD, goal_r); ADDS(ST_TIME_REWARD, c.time_reward); ADDS(ST_COLLISION_REWARD, coll);
-      ADDS(ST_DANGER_MEAN, danger); ADDS(ST_DANGER_HI_RATE, (float)(danger > 0.5f));
-      ADDS(ST_G_GATE_MEAN, gate_pos); ADDS(ST_POSITION_ERROR, dist); ADDS(ST_BOUNDARY_PENALTY, bpen);
-      if (c.pen_ang_kind) ADDS(ST_ANGULAR_VEL_PENALTY, p_ang);
-      if (c.pen_angv_kind) ADDS(ST_ANGULAR_VEL_VARIATION_PENALTY, p_angv);
-      if (c.pen_en_kind) ADDS(ST_ENERGY_PENALTY, p_en);
-      ADDS(ST_NORMED_LINEAR_VEL, tnorm2(vxn, vyn));
-      ADDS(ST_NORMED_ANGULAR_VEL, fabsf(wzn));
-      ADDS(ST_CMD_NEG_RATE, ((float)(t0 < 0.f) + (float)(t1 < 0.f)) / 2.0f);
-      ADDS(ST_U_MEAN, (unit0 + unit1) / 2.0f);
-      ADDS(ST_U_LOW_RATE, ((float)(unit0 < 0.05f) + (float)(unit1 < 0.05f)) / 2.0f);
-      ADDS(ST_U_SUM, unit0 + unit1);
-#undef ADDS
+      const float add[25] = {total, dist_r, align_r, hi_r, shaping, speed_r, ang_r, turn_haz, goal_r,
+                             c.time_reward, coll, danger, (float)(danger > 0.5f), gate_pos, dist, bpen,
+                             p_ang, p_angv, p_en, tnorm2(vxn, vyn), fabsf(wzn),
+                             ((float)(t0 < 0.f) + (float)(t1 < 0.f)) / 2.0f, (unit0 + unit1) / 2.0f,
+                             ((float)(unit0 < 0.05f) + (float)(unit1 < 0.05f)) / 2.0f, unit0 + unit1};
 #pragma unroll
-      for (int q = 0; q < USV_NSTAT; ++q) S[(size_t)q * n + e] = sums[q];
+      for (int q = 0; q < 25; ++q)
+        if (sum_on[q]) bst(R, w.stats + (uint32_t)kSum[q] * w.n4, vs, sums[q] + add[q]);
     }
   }
   // ---- coalesced obs store: rows of 33 floats staged through LDS ----
   __syncthreads();
   const int row0 = blockIdx.x * kBlock;
   const int rows = min(kBlock, n - row0);
-  float *dst = b.obs + (size_t)row0 * USV_NOBS;
-  for (int i = threadIdx.x; i < rows * USV_NOBS; i += kBlock)
-    if (keep[i / USV_NOBS]) dst[i] = sobs[i];
+  const uint32_t obase = (uint32_t)row0 * (uint32_t)(USV_NOBS * 4);
+  if (part == 0) {
+    const int nv = rows * USV_NOBS / 4;       // whole float4s (row0 * 33 * 4 B is 16-B aligned)
+    for (int i = tid; i < nv; i += kBlock) {
+      const float4 v = reinterpret_cast<const float4 *>(sobs)[i];
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v),
+                                             R, obase + (uint32_t)i * 16u, w.obs, 0);
+    }
+    for (int i = nv * 4 + tid; i < rows * USV_NOBS; i += kBlock) bst(R, w.obs, obase + (uint32_t)i * 4u, sobs[i]);
+  } else {
+    for (int i = tid; i < rows * USV_NOBS; i += kBlock)
+      if (keep[i / USV_NOBS]) bst(R, w.obs, obase + (uint32_t)i * 4u, sobs[i]);
+  }
   // ---- global flags: the step has consumed the Nones (:361, :448, USV_task_rewards.py:450) ----
-  if (part != 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (part != 1 && blockIdx.x == 0 && tid == 0) {
     b.ctl[USV_CTL_POT_VALID] = 1;
     b.ctl[USV_CTL_PEN_VALID] = 1;
     b.ctl[USV_CTL_REW_VALID] = 1;
@@ -755,6 +856,120 @@ __global__ void k_forces(usv_cfg_t c, usv_bufs_t b, float *__restrict__ out) {
   out[3 * e] = fl + fr + (-D0 * ub);
   out[3 * e + 1] = -D1 * vb;
   out[3 * e + 2] = -(c.thr_y - comy) * fl + (c.thr_y + comy) * fr + (-D2 * wz);
+}
+
+// ---- host side of the step launch ----
+// byte offsets of the step kernel's per-env arrays inside one window; status 2 when
+// they span 2 GiB or more (allocate them from one slab, as tasks/usv_virtual.py does)
+int step_window(const usv_cfg_t &c, const usv_bufs_t &b, const char **base, StepWin *w) {
+  const size_t n = (size_t)b.n, f = n * 4;
+  struct Arr {
+    const void *p;
+    size_t bytes;
+    uint32_t *off;
+    bool required;
+  };
+  const Arr arr[] = {
+      {b.px, f, &w->px, true}, {b.py, f, &w->py, true}, {b.yaw, f, &w->yaw, true}, {b.vx, f, &w->vx, true},
+      {b.vy, f, &w->vy, true}, {b.wz, f, &w->wz, true}, {b.fl, f, &w->fl, true}, {b.fr, f, &w->fr, true},
+      {b.mass, f, &w->mass, true}, {b.k_iz, f, &w->k_iz, true}, {b.k_drag, f, &w->k_drag, true},
+      {b.thr_l, f, &w->thr_l, true}, {b.thr_r, f, &w->thr_r, true}, {b.com_x, f, &w->com_x, true},
+      {b.com_y, f, &w->com_y, true}, {b.com_z, f, &w->com_z, true}, {b.lin_damp, 3 * f, &w->lin_damp, false},
+      {b.lin_damp ? b.quad_damp : nullptr, 3 * f, &w->quad_damp, b.lin_damp != nullptr},
+      {b.progress, f, &w->progress, true}, {b.tgt_x, f, &w->tgt_x, true}, {b.tgt_y, f, &w->tgt_y, true},
+      {b.obst, 2 * USV_NOBST * f, &w->obst, true}, {b.goal_cnt, f, &w->goal_cnt, true},
+      {b.prev_dist, f, &w->prev_dist, true}, {b.prev_head, f, &w->prev_head, true},
+      {b.prev_pot, f, &w->prev_pot, true}, {b.prev_wz, f, &w->prev_wz, true},
+      {c.stats_on ? b.stats : nullptr, USV_NSTAT * f, &w->stats, c.stats_on != 0},
+      {b.prev_cmd, 2 * f, &w->prev_cmd, true}, {b.rew, f, &w->rew, true}, {b.reset_buf, f, &w->reset_buf, true},
+      {b.dones, 2 * f, &w->dones, true}, {b.done_coll, f, &w->done_coll, true},
+      {b.done_succ, f, &w->done_succ, true}, {b.just_reset, n, &w->just_reset, true},
+      {b.obs, USV_NOBS * f, &w->obs, true}};
+  uintptr_t lo = UINTPTR_MAX, hi = 0;
+  for (const Arr &a : arr) {
+    if (!a.p) {
+      if (a.required) return 1;
+      continue;
+    }
+    lo = std::min(lo, (uintptr_t)a.p);
+    hi = std::max(hi, (uintptr_t)a.p + a.bytes);
+  }
+  if (hi - lo >= 0x7FFFFFFFull) return 2;
+  for (const Arr &a : arr) *a.off = a.p ? (uint32_t)((uintptr_t)a.p - lo) : 0u;
+  w->n4 = (uint32_t)f;
+  w->bytes = (uint32_t)(hi - lo);
+  *base = (const char *)lo;
+  return 0;
+}
+
+float enc_centered_scale(float xmin, float xmax, float nominal) {
+  double sc = std::fabs((double)xmin - nominal);
+  if (std::fabs((double)xmax - nominal) > sc) sc = std::fabs((double)xmax - nominal);
+  if (1e-6 > sc) sc = 1e-6;
+  return (float)sc;
+}
+// host restatements of the reference's privileged-observation encoders (USV_Virtual.py:97-151)
+float enc_centered_h(float x, float xmin, float xmax, float nominal) {
+  const float s = enc_centered_scale(xmin, xmax, nominal);
+  const float z = (x - nominal) / s;
+  return z < -1.f ? -1.f : (z > 1.f ? 1.f : z);
+}
+float enc_minmax_h(float x, float xmin, float xmax) {
+  if ((double)xmax - (double)xmin <= 1e-6) return 0.f;
+  const float z = (x - xmin) / (float)((double)xmax - (double)xmin);
+  const float y = 2.0f * z - 1.0f;
+  return y < -1.f ? -1.f : (y > 1.f ? 1.f : y);
+}
+
+StepK step_constants(const usv_cfg_t &c) {
+  StepK k{};
+  k.act_rng = (float)((double)c.act_noise_max - (double)c.act_noise_min);
+  k.pos_rng = (float)((double)c.pos_noise_max - (double)c.pos_noise_min);
+  k.vel_rng = (float)((double)c.vel_noise_max - (double)c.vel_noise_min);
+  k.head_rng = (float)((double)c.head_noise_max - (double)c.head_noise_min);
+  k.mass_den = (float)(std::fabs((double)c.base_mass) > 1e-6 ? std::fabs((double)c.base_mass) : 1e-6);
+  k.inv_mass_den = 1.0f / k.mass_den;
+  for (int i = 0; i < 3; ++i) {
+    k.com_div[i] = c.com_scale[i] + 1e-6f;
+    k.inv_com_div[i] = 1.0f / k.com_div[i];
+  }
+  const float lo3[3] = {c.kdrag_min, c.thr_min, c.kiz_min}, hi3[3] = {c.kdrag_max, c.thr_max, c.kiz_max};
+  for (int j = 0; j < 3; ++j) {
+    k.enc_lo[j] = lo3[j];
+    if (c.priv_mode == 1) {
+      k.enc_r[j] = enc_centered_scale(lo3[j], hi3[j], c.priv_nominal);
+      k.enc_ok[j] = 1;
+    } else {
+      k.enc_r[j] = (float)((double)hi3[j] - (double)lo3[j]);
+      k.enc_ok[j] = ((double)hi3[j] - (double)lo3[j]) > 1e-6;
+    }
+    k.inv_enc_r[j] = k.enc_r[j] != 0.f ? 1.0f / k.enc_r[j] : 0.f;
+  }
+  k.inv_exp_coeff = c.exp_coeff != 0.f ? 1.0f / c.exp_coeff : 0.f;
+  // privileged values of the "base" source: the same for every env
+  float v[8];
+  v[0] = c.mass_relative ? 0.f : c.base_mass;
+  for (int i = 0; i < 3; ++i) v[1 + i] = c.com_scaled ? c.base_com[i] / (c.com_scale[i] + 1e-6f) : c.base_com[i];
+  float kdv = 1.f, tl = 1.f, tr = 1.f, kz = 1.f;
+  if (c.priv_mode == 2) {
+    kdv = 0.5f * (c.kdrag_min + c.kdrag_max);
+    tl = tr = c.couple_thr ? (1.0f - 0.5f * c.thr_rand) : 1.0f;
+    kz = 0.5f * (c.kiz_min + c.kiz_max);
+  }
+  if (c.priv_mode == 1) {
+    kdv = enc_centered_h(kdv, c.kdrag_min, c.kdrag_max, c.priv_nominal);
+    tl = enc_centered_h(tl, c.thr_min, c.thr_max, c.priv_nominal);
+    tr = enc_centered_h(tr, c.thr_min, c.thr_max, c.priv_nominal);
+    kz = enc_centered_h(kz, c.kiz_min, c.kiz_max, c.priv_nominal);
+  } else if (c.priv_mode == 2) {
+    kdv = c.priv_drag_on ? enc_minmax_h(kdv, c.kdrag_min, c.kdrag_max) : 0.f;
+    tl = c.priv_thr_on ? enc_minmax_h(tl, c.thr_min, c.thr_max) : 0.f;
+    tr = c.priv_thr_on ? enc_minmax_h(tr, c.thr_min, c.thr_max) : 0.f;
+    kz = c.priv_kiz_on ? enc_minmax_h(kz, c.kiz_min, c.kiz_max) : 0.f;
+  }
+  v[4] = kdv; v[5] = tl; v[6] = tr; v[7] = kz;
+  for (int i = 0; i < 8; ++i) k.priv_base[i] = v[i];
+  return k;
 }
 
 }  // namespace
@@ -787,14 +1002,17 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
                       void *stream) {
   if (!cfg || !b || !actions || !lut_dev || b->n <= 0 || part < 0 || part > 2) return 1;
   if (cfg->priv_dim != 4 && cfg->priv_dim != 8) return 3;
+  StepWin w{};
+  const char *wbase = nullptr;
+  const int rc = step_window(*cfg, *b, &wbase, &w);
+  if (rc) return rc;
+  const StepK k = step_constants(*cfg);
   const int grid = (b->n + kBlock - 1) / kBlock;
   hipStream_t s = (hipStream_t)stream;
-  if (cfg->stats_on)
-    hipLaunchKernelGGL(k_env_step<true>, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, actions, lut_dev, action_bias,
-                       seed, step, u_inject, part);
-  else
-    hipLaunchKernelGGL(k_env_step<false>, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, actions, lut_dev, action_bias,
-                       seed, step, u_inject, part);
+  auto kern = cfg->stats_on ? (u_inject ? k_env_step<true, true> : k_env_step<true, false>)
+                            : (u_inject ? k_env_step<false, true> : k_env_step<false, false>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, w, k, wbase, actions, lut_dev, action_bias, seed,
+                     step, u_inject, part);
   USV_CHECK_LAUNCH();
   return 0;
 }

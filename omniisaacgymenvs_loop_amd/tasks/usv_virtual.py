@@ -84,33 +84,37 @@ class USVVirtual:
         f32 = dict(device=dev, dtype=torch.float32)
         i32 = dict(device=dev, dtype=torch.int32)
         Z = lambda *s, **k: torch.zeros(*s, **k)
-        self.state = Z((8, n), **f32)                  # px py yaw vx vy wz fl fr
-        self.params = Z((9, n), **f32)                 # mass com_x com_y com_z k_drag thr_l thr_r k_iz mass_r
+        # Every per-env array the step kernel touches comes from ONE slab, so they share a
+        # < 2 GiB window and the kernel addresses them with buffer instructions (one 32-bit
+        # lane offset + a scalar per-array offset; include/usv_hip.h, usv_env_step).
+        slab_spec = [("state", (8, n), torch.float32), ("params", (9, n), torch.float32),
+                     ("damp", (2, 3, n), torch.float32), ("tgt", (2, n), torch.float32),
+                     ("obst", (NOBST * 2, n), torch.float32), ("prev_cmd", (2, n), torch.float32),
+                     ("hist", (4, n), torch.float32), ("ibuf", (5, n), torch.int32),
+                     ("just_reset", (n,), torch.uint8), ("stats", (NSTAT, n), torch.float32),
+                     ("obs_buf_t", (n, NOBS), torch.float32), ("rew_buf", (n,), torch.float32),
+                     ("dones", (n,), torch.int64), ("field_old_tgt", (2, n), torch.float32),
+                     ("reset_ids", (n,), torch.int32)]
+        sizes = [int(np.prod(shape)) * torch.empty((), dtype=dt).element_size() for _, shape, dt in slab_spec]
+        offs = np.concatenate([[0], np.cumsum([(sz + 255) // 256 * 256 for sz in sizes])])
+        self._slab = torch.zeros(int(offs[-1]), device=dev, dtype=torch.uint8)
+        for (name, shape, dt), o, sz in zip(slab_spec, offs, sizes):
+            setattr(self, name, self._slab[int(o):int(o) + sz].view(dt).view(shape))
         self.params[0] = self.cfg.base_mass
         self.params[4:8] = 1.0
-        self.damp = Z((2, 3, n), **f32) if self.cfg.drag_rand_on else None
-        if self.damp is not None:
+        if self.cfg.drag_rand_on:
             for a in range(3):
                 self.damp[0, a] = self.cfg.lin_damp[a]
                 self.damp[1, a] = self.cfg.quad_damp[a]
-        self.tgt = Z((2, n), **f32)
-        self.obst = Z((NOBST * 2, n), **f32)
+        else:
+            self.damp = None
         self.field = Z((n, GRID2), **f32)
-        self.prev_cmd = Z((2, n), **f32)
-        self.hist = Z((4, n), **f32)                   # prev_dist prev_head prev_pot prev_wz
-        self.ibuf = Z((5, n), **i32)                   # goal_cnt progress reset_buf done_succ done_coll
         self.ibuf[2] = 1                               # RLTask.cleanup: reset_buf = ones
-        self.just_reset = torch.ones(n, device=dev, dtype=torch.uint8)
-        self.stats = Z((NSTAT, n), **f32)
-        self.obs_buf_t = Z((n, NOBS), **f32)
-        self.rew_buf = Z(n, **f32)
-        self.dones = Z(n, device=dev, dtype=torch.int64)
+        self.just_reset.fill_(1)
         self.ctl = Z(CTL_N, **i32)
-        self.reset_ids = Z(n, **i32)
         self.fscratch = Z(16, **f32)
         self.extras_buf = Z(NSTAT, **f32)
         self.extras_acc = Z(NSTAT, **f32)
-        self.field_old_tgt = Z((2, n), **f32)
         self.slot_stats = Z((n, DEFINES["USV_FIELD_SLOT_STATS"]), **f32)
         # device step clock (next step, next bias call, current step, current bias call): the kernels take
         # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
