@@ -677,8 +677,17 @@ __device__ __forceinline__ float reduce_chunk(const float *__restrict__ partials
   const int p = chunk * 64 + cidx;
   float acc = 0.f;
   if (p < PPO_NPARAM + 5) {
-#pragma unroll 8
-    for (int b = g; b < nblk; b += 4) acc += partials[(size_t)b * NPART + p];
+    // 32 loads in flight per thread, then added in block order (the order of the sum
+    // is b = g, g + 4, g + 8, ... whatever the batching)
+    constexpr int kB = 32;
+    for (int b0 = g; b0 < nblk; b0 += 4 * kB) {
+      float x[kB];
+#pragma unroll
+      for (int k = 0; k < kB; ++k) x[k] = partials[(size_t)min(b0 + 4 * k, nblk - 1) * NPART + p];
+#pragma unroll
+      for (int k = 0; k < kB; ++k)
+        if (b0 + 4 * k < nblk) acc += x[k];
+    }
   }
   red[g][cidx] = acc;
   __syncthreads();
@@ -716,65 +725,72 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict
 // finish (completion counter in opt[7]) advances step / lr / kl / norm.
 constexpr int AP_TB = 256;
 constexpr int RED_BLOCKS = (PPO_NPARAM + 5 + 63) / 64;
+template <bool kNormFromPartials>
 __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const float *__restrict__ grad_in,
-                                                 float *m, float *v, float *opt, float grad_scale, float *kl_out,
-                                                 int norm_from_partials) {
+                                                 float *m, float *v, float *opt, float grad_scale, float *kl_out) {
   __shared__ float red[AP_TB / 64];
   __shared__ bool last;
   const int tid = threadIdx.x;
-  float total_norm;
-  if (norm_from_partials) {
-    // the reduce kernel's per-workgroup squares (fixed order): no re-read of the gradient
-    float sq = 0.f;
-    for (int q = tid; q < RED_BLOCKS; q += AP_TB) sq += grad_in[PPO_NPARAM + 8 + q];
-    sq = wave_sum(sq);
-    if ((tid & 63) == 0) red[tid >> 6] = sq;
-    __syncthreads();
-    total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
-  } else {
-  // total norm: every load issued up front (16-byte aligned gradient, checked on the host)
-  constexpr int N4 = PPO_NPARAM / 4, U = (N4 + AP_TB - 1) / AP_TB;
-  const float4 *g4 = reinterpret_cast<const float4 *>(grad_in);
-  float4 gv[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) gv[u] = (tid + u * AP_TB < N4) ? g4[tid + u * AP_TB] : make_float4(0.f, 0.f, 0.f, 0.f);
-  float ss = 0.f;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const float x = gv[u].x * grad_scale, y = gv[u].y * grad_scale;
-    const float z = gv[u].z * grad_scale, w = gv[u].w * grad_scale;
-    ss = fmaf(x, x, ss); ss = fmaf(y, y, ss); ss = fmaf(z, z, ss); ss = fmaf(w, w, ss);
-  }
-  for (int q = 4 * N4 + tid; q < PPO_NPARAM; q += AP_TB) {
-    const float g = grad_in[q] * grad_scale;
-    ss = fmaf(g, g, ss);
-  }
-  ss = wave_sum(ss);
-  if ((tid & 63) == 0) red[tid >> 6] = ss;
-  __syncthreads();
-  total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
-  }
-  float coef = 1.0f;
-  if (c.truncate_grads) {
-    coef = c.grad_norm / (total_norm + 1e-6f);
-    coef = fminf(coef, 1.0f);
-  }
+  const int q = blockIdx.x * AP_TB + tid;
+  const int qc = min(q, PPO_NPARAM - 1);
+  // every load this thread needs is issued before anything waits: its parameter,
+  // moments and gradient, then the norm inputs; the double-precision bias
+  // corrections below are computed while they are in flight
+  const float g_raw = grad_in[qc], p_old = P[qc], m_old = m[qc], v_old = v[qc];
+  // the reduce kernel's per-chunk squares (fixed order; loaded unconditionally: no branch)
+  static_assert(RED_BLOCKS <= 2 * AP_TB, "two chunk squares per thread");
+  const float s0 = grad_in[PPO_NPARAM + 8 + min(tid, RED_BLOCKS - 1)];
+  const float s1 = grad_in[PPO_NPARAM + 8 + min(tid + AP_TB, RED_BLOCKS - 1)];
   const float lr = opt[0];
   const float step = opt[1] + 1.0f;
+  __builtin_amdgcn_sched_barrier(0);   // the loads above issue first
   // torch.optim.Adam forms the bias corrections in Python doubles
   const double bc1 = 1.0 - pow((double)c.adam_b1, (double)step);
   const double bc2 = 1.0 - pow((double)c.adam_b2, (double)step);
   const float step_size = (float)((double)lr / bc1);
   const float bc2s = (float)sqrt(bc2);
-  const int q = blockIdx.x * AP_TB + tid;
+  // pin the bias corrections here, in the shadow of the loads above (the scheduler
+  // would otherwise sink them past the norm's barrier onto the critical path)
+  __asm__ volatile("" : : "v"(step_size), "v"(bc2s));
+  float ss = 0.f;
+  if (kNormFromPartials) {
+    ss = (tid < RED_BLOCKS ? s0 : 0.f) + (tid + AP_TB < RED_BLOCKS ? s1 : 0.f);
+  } else {
+    // total norm of the (all-reduced) gradient: 16-byte aligned, checked on the host
+    constexpr int N4 = PPO_NPARAM / 4, U = (N4 + AP_TB - 1) / AP_TB;
+    const float4 *g4 = reinterpret_cast<const float4 *>(grad_in);
+    float4 gv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) gv[u] = g4[min(tid + u * AP_TB, N4 - 1)];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (tid + u * AP_TB >= N4) continue;
+      const float x = gv[u].x * grad_scale, y = gv[u].y * grad_scale;
+      const float z = gv[u].z * grad_scale, w = gv[u].w * grad_scale;
+      ss = fmaf(x, x, ss); ss = fmaf(y, y, ss); ss = fmaf(z, z, ss); ss = fmaf(w, w, ss);
+    }
+    for (int r = 4 * N4 + tid; r < PPO_NPARAM; r += AP_TB) {
+      const float g = grad_in[r] * grad_scale;
+      ss = fmaf(g, g, ss);
+    }
+  }
+  ss = wave_sum(ss);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
+  float coef = 1.0f;
+  if (c.truncate_grads) {
+    coef = c.grad_norm / (total_norm + 1e-6f);
+    coef = fminf(coef, 1.0f);
+  }
   if (q < PPO_NPARAM) {
-    float g = grad_in[q] * grad_scale * coef;
-    if (c.weight_decay != 0.f) g = g + c.weight_decay * P[q];
-    float mi = m[q], vi = v[q];
+    float g = g_raw * grad_scale * coef;
+    if (c.weight_decay != 0.f) g = g + c.weight_decay * p_old;
+    float mi = m_old, vi = v_old;
     mi = mi + (1.0f - c.adam_b1) * (g - mi);          // exp_avg.lerp_(grad, 1 - beta1)
     vi = vi * c.adam_b2 + (1.0f - c.adam_b2) * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
     const float denom = sqrtf(vi) / bc2s + c.adam_eps;
-    P[q] = P[q] - step_size * (mi / denom);
+    P[q] = p_old - step_size * (mi / denom);
     m[q] = mi;
     v[q] = vi;
   }
@@ -1005,8 +1021,8 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
                         float grad_scale, float *kl_out, int norm_from_partials, void *stream) {
   if (!cfg || !params || !grad || !adam_m || !adam_v || !opt) return 1;
   if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
-  hipLaunchKernelGGL(k_apply, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB), dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params,
-                     grad, adam_m, adam_v, opt, grad_scale, kl_out, norm_from_partials);
+  hipLaunchKernelGGL(norm_from_partials ? k_apply<true> : k_apply<false>, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB),
+                     dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params, grad, adam_m, adam_v, opt, grad_scale, kl_out);
   USV_CHECK_LAUNCH();
   return 0;
 }
