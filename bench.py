@@ -145,7 +145,6 @@ def main():
     ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (BASELINE configs[1]: 4096)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--overlap-reset", action="store_true", help="env reset path on a side stream")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph capture)")
     ap.add_argument("--env-only-envs", type=int, default=131072,
                     help="extra env-only throughput probe at the C5 per-GPU size (0 = skip)")
@@ -154,7 +153,6 @@ def main():
     import torch.distributed as dist
     rank, world, local = _dist_setup(args.gpus)
     env, task, agent = build(args.envs, local, world, args.seed + rank)
-    agent.overlap_reset = args.overlap_reset
     agent.use_graph = not args.no_graph
     from omniisaacgymenvs_loop_amd import _capi
 

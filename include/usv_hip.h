@@ -220,6 +220,14 @@ typedef struct usv_bufs {
 #define USV_CTL_ANY_INSIDE  5   /* potential field: any cell inside an obstacle in the batch */
 #define USV_CTL_ANY_FINITE  6   /* potential field: any finite cost in the batch */
 #define USV_CTL_OBST_DONE   7   /* completion counter of the obstacle kernel (extras finalisation) */
+#define USV_CTL_STEPPED     8   /* set by every env step; usv_reset promotes it to the 3 flags above */
+#define USV_CTL_PLACE       9   /* set by usv_reset: usv_potential_field places the reset envs' obstacles */
+#define USV_CTL_H_SEED_LO  10   /* usv_reset -> usv_potential_field: Philox key and step of the */
+#define USV_CTL_H_SEED_HI  11   /*   obstacle draws, and the injected-uniform buffer (or 0)      */
+#define USV_CTL_H_STEP_LO  12
+#define USV_CTL_H_STEP_HI  13
+#define USV_CTL_H_INJ_LO   14
+#define USV_CTL_H_INJ_HI   15
 #define USV_CTL_N           16
 
 /* ------------------------------------------------------------------------ */
@@ -326,8 +334,9 @@ typedef struct ppo_cfg {
  * params: [PPO_NPARAM]; obs_rms: double [2][33] (mean, var); val_rms double [2];
  * buffers of the experience store are env-major [n][H][...].
  * eps_inject: NULL => Philox normal draws, else device [n][2] N(0,1) draws.
- * step_dev (nullable): device counter read instead of `step` (graph replay);
- * ppo_store_reward advances it. */
+ * step_dev (nullable): device counter holding the rollout's first step; slot t draws
+ * with step *step_dev + t instead of `step` (graph replay).  ppo_store_reward of the
+ * last slot advances it by the horizon. */
 int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
                     const double *val_rms, const float *obs, int t,
                     float *exp_obs, float *exp_act, float *exp_nlp, float *exp_val,
@@ -342,7 +351,8 @@ int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
 
 /* Store rewards of slot t shaped by DefaultRewardsShaper (tr_helpers.py:33-43)
  * and accumulate the episode meters (a2c_common.py:738-759).
- * meter: device [H][4] per-step (sum reward of done envs, sum shaped, sum length, count). */
+ * meter: device [H][4] per-step (sum reward of done envs, sum shaped, sum length, count).
+ * step_dev (nullable): advanced by the horizon when t == horizon - 1. */
 int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *dones, int t,
                      float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len,
                      float *meter, uint64_t *step_dev, void *stream);

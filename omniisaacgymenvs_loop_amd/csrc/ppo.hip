@@ -204,7 +204,7 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
                                                     const float *eps_inject) {
   __shared__ MlpSmem s;
   const int n = c.n_envs, H = c.horizon;
-  if (step_dev) step = *step_dev;
+  if (step_dev) step = *step_dev + (uint64_t)t;   // the rollout's first step + slot
   const int row0 = blockIdx.x * RB;
   const int nrows = min(RB, n - row0);
   // raw obs into the experience buffer (row = env*H + t, swap_and_flatten01 layout)
@@ -284,7 +284,9 @@ __global__ void k_store_reward(ppo_cfg_t c, const float *__restrict__ rew, const
                                float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len, float *meter,
                                uint64_t *step_dev) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (step_dev && e == 0) *step_dev += 1;   // the rollout's Philox step advances once per env step
+  // the rollout's Philox step advances by the horizon after its last slot (the policy kernel of slot t
+  // reads step_dev + t, so no policy launch depends on this kernel within a rollout)
+  if (step_dev && e == 0 && t == c.horizon - 1) *step_dev += (uint64_t)c.horizon;
   const int n = c.n_envs;
   float s_rew = 0.f, s_shaped = 0.f, s_len = 0.f, s_cnt = 0.f;
   if (e < n) {

@@ -53,6 +53,69 @@ __device__ __forceinline__ float div_rn(float x, float b, float y) {
   return fmaf(r, y, q);
 }
 
+// ---------------------------------------------------------------------------
+// 64-lane (whole wave) obstacle placement for reset env ee (CaptureXYTask.get_spawns
+// obstacle part, static_obs.py:968-1048).  Lane (q, o) = (lane >> 4, lane & 15) holds
+// obstacle o (replicated over the four 16-lane groups) and draws the candidate of
+// iteration 4r + q of round r, so the Philox work of four rejection iterations runs in
+// parallel; the iterations themselves stay sequential and pick candidates by shuffle.
+// Box around the previous-episode target; an obstacle is redrawn while it is closer
+// than min_dist_safe to the spawn or the target, or closer than min_obs_sep to a
+// lower-index obstacle; after USV_SPAWN_ITERS redraws the leftovers go to limbo
+// (999, 999).  Same uniforms as the per-env restatement (reset slots RU_OBST + 2o,
+// RU_RESAMPLE + 32 it + 2o (+1)).
+__device__ __forceinline__ float2 place_obstacles(const usv_cfg_t &c, int ee, float sx, float sy, float tx, float ty,
+                                                  uint64_t seed, uint64_t step, const float *__restrict__ inj) {
+  static_assert(USV_NOBST == 16, "16-lane groups");
+  const int lane = threadIdx.x & 63, o = lane & 15, q = lane >> 4, gbase = lane & 48;
+  auto Ue = [&](int i) -> float {
+    if (inj) return inj[(size_t)ee * USV_NU_RESET + i];
+    float u4[4];
+    philox_u4(seed, (uint32_t)ee, step, 0x100u + (uint32_t)(i >> 2), u4);
+    return u4[i & 3];
+  };
+  const float mnx = tx - c.obst_box, mny = ty - c.obst_box;
+  const float dx_ = (tx + c.obst_box) - mnx, dy_ = (ty + c.obst_box) - mny;
+  float ox = Ue(RU_OBST + 2 * o) * dx_ + mnx;
+  float oy = Ue(RU_OBST + 2 * o + 1) * dy_ + mny;
+  const float sep2 = c.min_obs_sep * c.min_obs_sep;
+  bool done = false;
+  for (int r = 0; !done; ++r) {
+    const int itq = 4 * r + q;
+    float cx = 0.f, cy = 0.f;
+    if (itq < USV_SPAWN_ITERS) {
+      const int rb = RU_RESAMPLE + itq * USV_NOBST * 2;
+      cx = Ue(rb + 2 * o) * dx_ + mnx;
+      cy = Ue(rb + 2 * o + 1) * dy_ + mny;
+    }
+    for (int qq = 0; qq < 4; ++qq) {
+      const int it = 4 * r + qq;
+      const float ds = tnorm2(ox - sx, oy - sy);
+      const float dt = tnorm2(ox - tx, oy - ty);
+      bool bad = (ds < c.min_dist_safe) || (dt < c.min_dist_safe);
+      const bool vo = ox < 900.f;
+#pragma unroll
+      for (int i = 0; i < USV_NOBST - 1; ++i) {
+        const float xi = __shfl(ox, gbase + i, 64), yi = __shfl(oy, gbase + i, 64);
+        const float ddx = xi - ox, ddy = yi - oy;
+        if (i < o && vo && (xi < 900.f) && (ddx * ddx + ddy * ddy) < sep2) bad = true;
+      }
+      const uint32_t inval = (uint32_t)((__ballot(bad) >> gbase) & 0xFFFFull);   // same in every group
+      if (inval == 0) { done = true; break; }
+      if (it == USV_SPAWN_ITERS) {  // leftovers to limbo (:1042-1048)
+        if (bad) { ox = 999.0f; oy = 999.0f; }
+        done = true;
+        break;
+      }
+      const float nx = __shfl(cx, 16 * qq + o, 64), ny = __shfl(cy, 16 * qq + o, 64);
+      if (bad) { ox = nx; oy = ny; }
+    }
+  }
+  (void)q;
+  return make_float2(ox, oy);   // obstacle o's centre (every 16-lane group holds the same)
+}
+
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

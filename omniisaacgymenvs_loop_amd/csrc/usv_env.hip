@@ -82,6 +82,11 @@ __global__ void k_step_begin(usv_bufs_t b) {
     b.clock[3] = b.clock[1]++;
   }
   if (t == 0) b.ctl[USV_CTL_RESET_COUNT] = 0;
+  if (t == 3 && b.ctl[USV_CTL_STEPPED]) {   // a step has run: prev_* are no longer None
+    b.ctl[USV_CTL_POT_VALID] = 1;
+    b.ctl[USV_CTL_PEN_VALID] = 1;
+    b.ctl[USV_CTL_REW_VALID] = 1;
+  }
   if (t == 1) b.ctl[USV_CTL_ANY_INSIDE] = 0;
   if (t == 2) b.ctl[USV_CTL_ANY_FINITE] = 0;
   if (t < 4) b.fscratch[t] = 0.f;
@@ -96,70 +101,6 @@ __global__ void k_step_begin(usv_bufs_t b) {
 // Obstacle rejection sampling follows in the same kernel, one whole wave per
 // reset env (place_obstacles).
 // ------------------------------------------------------------------------
-// 64-lane (whole wave) obstacle placement for reset env ee (CaptureXYTask.get_spawns
-// obstacle part, static_obs.py:968-1048).  Lane (q, o) = (lane >> 4, lane & 15) holds
-// obstacle o (replicated over the four 16-lane groups) and draws the candidate of
-// iteration 4r + q of round r, so the Philox work of four rejection iterations runs in
-// parallel; the iterations themselves stay sequential and pick candidates by shuffle.
-// Box around the previous-episode target; an obstacle is redrawn while it is closer
-// than min_dist_safe to the spawn or the target, or closer than min_obs_sep to a
-// lower-index obstacle; after USV_SPAWN_ITERS redraws the leftovers go to limbo
-// (999, 999).  Same uniforms as the per-env restatement (reset slots RU_OBST + 2o,
-// RU_RESAMPLE + 32 it + 2o (+1)).
-__device__ void place_obstacles(const usv_cfg_t &c, const usv_bufs_t &b, int ee, float sx, float sy, float tx,
-                                float ty, uint64_t seed, uint64_t step, const float *__restrict__ inj) {
-  static_assert(USV_NOBST == 16, "16-lane groups");
-  const int n = b.n;
-  const int lane = threadIdx.x & 63, o = lane & 15, q = lane >> 4, gbase = lane & 48;
-  auto Ue = [&](int i) -> float {
-    if (inj) return inj[(size_t)ee * USV_NU_RESET + i];
-    float u4[4];
-    philox_u4(seed, (uint32_t)ee, step, 0x100u + (uint32_t)(i >> 2), u4);
-    return u4[i & 3];
-  };
-  const float mnx = tx - c.obst_box, mny = ty - c.obst_box;
-  const float dx_ = (tx + c.obst_box) - mnx, dy_ = (ty + c.obst_box) - mny;
-  float ox = Ue(RU_OBST + 2 * o) * dx_ + mnx;
-  float oy = Ue(RU_OBST + 2 * o + 1) * dy_ + mny;
-  const float sep2 = c.min_obs_sep * c.min_obs_sep;
-  bool done = false;
-  for (int r = 0; !done; ++r) {
-    const int itq = 4 * r + q;
-    float cx = 0.f, cy = 0.f;
-    if (itq < USV_SPAWN_ITERS) {
-      const int rb = RU_RESAMPLE + itq * USV_NOBST * 2;
-      cx = Ue(rb + 2 * o) * dx_ + mnx;
-      cy = Ue(rb + 2 * o + 1) * dy_ + mny;
-    }
-    for (int qq = 0; qq < 4; ++qq) {
-      const int it = 4 * r + qq;
-      const float ds = tnorm2(ox - sx, oy - sy);
-      const float dt = tnorm2(ox - tx, oy - ty);
-      bool bad = (ds < c.min_dist_safe) || (dt < c.min_dist_safe);
-      const bool vo = ox < 900.f;
-#pragma unroll
-      for (int i = 0; i < USV_NOBST - 1; ++i) {
-        const float xi = __shfl(ox, gbase + i, 64), yi = __shfl(oy, gbase + i, 64);
-        const float ddx = xi - ox, ddy = yi - oy;
-        if (i < o && vo && (xi < 900.f) && (ddx * ddx + ddy * ddy) < sep2) bad = true;
-      }
-      const uint32_t inval = (uint32_t)((__ballot(bad) >> gbase) & 0xFFFFull);   // same in every group
-      if (inval == 0) { done = true; break; }
-      if (it == USV_SPAWN_ITERS) {  // leftovers to limbo (:1042-1048)
-        if (bad) { ox = 999.0f; oy = 999.0f; }
-        done = true;
-        break;
-      }
-      const float nx = __shfl(cx, 16 * qq + o, 64), ny = __shfl(cy, 16 * qq + o, 64);
-      if (bad) { ox = nx; oy = ny; }
-    }
-  }
-  if (q == 0) {
-    b.obst[(size_t)(2 * o) * n + ee] = ox;
-    b.obst[(size_t)(2 * o + 1) * n + ee] = oy;
-  }
-}
-
 __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uint64_t seed, uint64_t step,
                                                   const float *__restrict__ inj) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -176,16 +117,22 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
     base = __shfl(base, leader, 64);
     // ---- episode extras: sums of the envs being reset (:1591-1612), one atomic per wave ----
     if (c.stats_on) {
-      for (int q = 0; q < USV_NSTAT; ++q) {
-        float v = 0.f;
-        if (active) {
-          v = b.stats[(size_t)q * n + e];
-          if (q == ST_SUCCESS) v = (float)b.done_succ[e];
-          if (q == ST_COLLISION) v = (float)b.done_coll[e];
-          b.stats[(size_t)q * n + e] = 0.f;
-        }
-        v = wave_sum(v);
-        if (lane == leader) atomicAdd(&b.extras_acc[q], v);
+      // all 28 loads first, then 28 independent wave sums (their shuffles interleave)
+      const int ec = min(e, n - 1);
+      float v[USV_NSTAT];
+#pragma unroll
+      for (int q = 0; q < USV_NSTAT; ++q) v[q] = b.stats[(size_t)q * n + ec];
+      v[ST_SUCCESS] = (float)b.done_succ[ec];
+      v[ST_COLLISION] = (float)b.done_coll[ec];
+      if (active) {
+#pragma unroll
+        for (int q = 0; q < USV_NSTAT; ++q) b.stats[(size_t)q * n + e] = 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < USV_NSTAT; ++q) v[q] = wave_sum(active ? v[q] : 0.f);
+      if (lane == leader) {
+#pragma unroll
+        for (int q = 0; q < USV_NSTAT; ++q) atomicAdd(&b.extras_acc[q], v[q]);
       }
     }
     float sx = 0.f, sy = 0.f, tx = 0.f, ty = 0.f;
@@ -284,13 +231,18 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
       b.tgt_x[e] = U(RU_GOAL) * g * 2.0f - g;
       b.tgt_y[e] = U(RU_GOAL + 1) * g * 2.0f - g;
     }
-    // ---- obstacles: the whole wave places each of its reset envs in turn ----
-    for (uint64_t mm = mask; mm; mm &= mm - 1) {
-      const int src = __ffsll((long long)mm) - 1;
-      const int ee = blockIdx.x * blockDim.x + (threadIdx.x & ~63) + src;
-      place_obstacles(c, b, ee, __shfl(sx, src, 64), __shfl(sy, src, 64), __shfl(tx, src, 64),
-                      __shfl(ty, src, 64), seed, step, inj);
-    }
+    (void)sx; (void)sy; (void)tx; (void)ty;
+  }
+  // ---- obstacles: placed by the potential-field kernel, one workgroup per reset env
+  // (place_obstacles, usv_device.h); this kernel hands over the draw keys ----
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    b.ctl[USV_CTL_H_SEED_LO] = (int32_t)(uint32_t)seed;
+    b.ctl[USV_CTL_H_SEED_HI] = (int32_t)(uint32_t)(seed >> 32);
+    b.ctl[USV_CTL_H_STEP_LO] = (int32_t)(uint32_t)step;
+    b.ctl[USV_CTL_H_STEP_HI] = (int32_t)(uint32_t)(step >> 32);
+    b.ctl[USV_CTL_H_INJ_LO] = (int32_t)(uint32_t)(uintptr_t)inj;
+    b.ctl[USV_CTL_H_INJ_HI] = (int32_t)(uint32_t)((uint64_t)(uintptr_t)inj >> 32);
+    b.ctl[USV_CTL_PLACE] = 1;
   }
   // ---- the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612) ----
   __shared__ bool last;
@@ -362,6 +314,41 @@ __device__ __forceinline__ float pen_scalar(int kind, float k, float x0, float c
 // per-env loads/stores are buffer instructions with ONE shared 32-bit lane
 // offset and a scalar per-array offset: no per-access 64-bit address VALU work.
 // ------------------------------------------------------------------------
+// reward terms of compute_reward (static_obs.py:335-657) that do not depend on the
+// potential, and the potential-dependent tail
+struct RewardPre {
+  float dist_r0, align0, g, ggate, turning, sf, goal_r, coll, speed_r, ang_r, hi_r, pen_sum;
+};
+struct RewardOut {
+  float pot, total, rew, dist_r, align_r, shaping, turn_haz, danger, gate_pos;
+};
+__device__ __forceinline__ RewardOut reward_tail(const usv_cfg_t &c, const RewardPre &p, float pot, bool pot_is_prev,
+                                                 float prev_pot_mem) {
+  constexpr float kXs = 0.3f + 1e-6f, kPa = 2.0f + 1e-6f;
+  RewardOut o;
+  o.pot = pot;
+  const float pn = clampt(pot, 0.f, 1.f);
+  const float xs = clampt(div_rn(pn - 0.6f, kXs, 1.0f / kXs), 0.f, 1.f);
+  o.danger = xs * xs * (3.0f - 2.0f * xs);
+  o.align_r = p.align0 * maxf(0.3f, 1.0f - o.danger);
+  float dist_r = p.dist_r0 * maxf(0.6f, 1.0f - o.danger * 0.5f);
+  dist_r = minf(dist_r, 0.f) + p.g * maxf(dist_r, 0.f);
+  o.dist_r = dist_r;
+  const float prev_pot = pot_is_prev ? pot : prev_pot_mem;
+  float praw = (prev_pot - pot) * 100.0f;
+  if (fabsf(praw) < 0.01f) praw = 0.f;
+  const float pa1 = 2.0f * tanhf(div_rn(praw, kPa, 1.0f / kPa));
+  const float ppos = maxf(pa1, 0.f), pneg = minf(pa1, 0.f);
+  o.gate_pos = (ppos < 0.5f) ? 1.0f : p.ggate;
+  o.shaping = o.gate_pos * ppos + pneg;
+  const bool worsening = o.shaping < -0.05f;
+  o.turn_haz = (float)(worsening && p.turning != 0.f) * (-10.0f) * (p.g * p.g) * p.sf;
+  o.total = dist_r * 0.5f + o.align_r * 0.5f + o.shaping * 2.0f + o.turn_haz + p.goal_r + c.time_reward + p.coll +
+            p.speed_r + p.ang_r + p.hi_r;
+  o.rew = o.total + p.pen_sum;
+  return o;
+}
+
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -554,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     i0 = min(max(i0, 0), USV_LUT_N - 1);
     i1 = min(max(i1, 0), USV_LUT_N - 1);
     bool mine = e < n;
-    if (part != 0) mine = mine && ((part == 1) ? !was_reset : was_reset);
+    if (part == 1 || part == 2) mine = mine && ((part == 1) ? !was_reset : was_reset);
     keep[tid] = mine ? 1 : 0;
     const uint32_t vs = mine ? v4 : kDrop;
     reinterpret_cast<float4 *>(slut)[tid] = lut_a;
@@ -710,8 +697,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
         }
       }
     }
-    // ---- compute_reward (static_obs.py:335-657) ----
-    constexpr float kXs = 0.3f + 1e-6f, kPa = 2.0f + 1e-6f, kGv = (0.15f - 0.02f) + 1e-6f, kGd = 0.01f + 1e-6f;
+    // ---- compute_reward (static_obs.py:335-657): the potential-independent terms first ----
+    constexpr float kGv = (0.15f - 0.02f) + 1e-6f, kGd = 0.01f + 1e-6f;
     constexpr float kSf = (0.60f - 0.15f) + 1e-6f, kSp = 0.8f + 1e-6f, kAn = 0.2f;
     const float bover = maxf(dist - c.kill_dist, 0.f);
     const float bpen = -expm1f(minf(bover / 0.25f, 20.0f)) * c.boundary_cost;
@@ -719,56 +706,38 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     const int goal_cnt = goal_cnt0 * gir + gir;
     bsti(R, w.goal_cnt, vs, goal_cnt);
     const float prev_err = rew_valid ? prev_d_mem : dist;
-    float dist_r;
-    if (c.reward_mode == 0) dist_r = c.position_scale * (prev_err - dist);
-    else if (c.reward_mode == 1) dist_r = c.position_scale * (prev_err * prev_err - dist * dist);
-    else dist_r = c.position_scale * (expf(div_rn(-dist, c.exp_coeff, K.inv_exp_coeff)) -
-                                      expf(div_rn(-prev_err, c.exp_coeff, K.inv_exp_coeff)));
+    RewardPre rp;
+    if (c.reward_mode == 0) rp.dist_r0 = c.position_scale * (prev_err - dist);
+    else if (c.reward_mode == 1) rp.dist_r0 = c.position_scale * (prev_err * prev_err - dist * dist);
+    else rp.dist_r0 = c.position_scale * (expf(div_rn(-dist, c.exp_coeff, K.inv_exp_coeff)) -
+                                          expf(div_rn(-prev_err, c.exp_coeff, K.inv_exp_coeff)));
     const float h2 = herr * herr;
-    float align_r = c.align_la1 * (expf(c.align_la2 * (h2 * h2)) + expf(c.align_la3 * h2));
-    if (was_reset) dist_r = 0.f;
+    rp.align0 = c.align_la1 * (expf(c.align_la2 * (h2 * h2)) + expf(c.align_la3 * h2));
+    if (was_reset) rp.dist_r0 = 0.f;
     const float prev_dist = was_reset ? dist : (rew_valid ? prev_d_mem : dist);
-    const float pot = field_blend(taps);
-    const float pn = clampt(pot, 0.f, 1.f);
-    const float xs = clampt(div_rn(pn - 0.6f, kXs, 1.0f / kXs), 0.f, 1.f);
-    const float danger = xs * xs * (3.0f - 2.0f * xs);
-    align_r = align_r * maxf(0.3f, 1.0f - danger);
-    dist_r = dist_r * maxf(0.6f, 1.0f - danger * 0.5f);
-    const float g = clampt(ca, 0.f, 1.f);
-    dist_r = minf(dist_r, 0.f) + g * maxf(dist_r, 0.f);
+    rp.g = clampt(ca, 0.f, 1.f);
     const float prev_h = (rew_valid && !was_reset) ? prev_head_mem : herr;
     const float hi = clampt(prev_h - herr, -0.4f, 0.4f);
-    const float hi_r = hi * 0.05f;
+    rp.hi_r = hi * 0.05f;
     bst(R, w.prev_head, vs, herr);
-    const float prev_pot = (pot_none || was_reset) ? pot : prev_pot_mem;
-    float praw = (prev_pot - pot) * 100.0f;
-    if (fabsf(praw) < 0.01f) praw = 0.f;
-    const float pa1 = 2.0f * tanhf(div_rn(praw, kPa, 1.0f / kPa));
     const float dd = dist + 1e-6f, inv_dd = 1.0f / dd;
     const float gdx = div_rn(ex, dd, inv_dd), gdy = div_rn(ey, dd, inv_dd);
     const float vtp = maxf(vxn * gdx + vyn * gdy, 0.f);
     const float ddp = maxf(prev_dist - dist, 0.f);
     const float gv = clampt(div_rn(vtp - 0.02f, kGv, 1.0f / kGv), 0.f, 1.f);
     const float gd = clampt(div_rn(ddp, kGd, 1.0f / kGd), 0.f, 1.f);
-    const float ggate = maxf(gv, gd) * g;
-    const float ppos = maxf(pa1, 0.f), pneg = minf(pa1, 0.f);
-    const float gate_pos = (ppos < 0.5f) ? 1.0f : ggate;
-    const float shaping = gate_pos * ppos + pneg;
-    const bool worsening = shaping < -0.05f;
-    const bool turning = fabsf(wzn) > 0.2f;
+    rp.ggate = maxf(gv, gd) * rp.g;
+    rp.turning = fabsf(wzn) > 0.2f ? 1.f : 0.f;
     const float vfwd = vxn * hc + vyn * hs;
-    const float sf = clampt(div_rn(fabsf(vfwd) - 0.15f, kSf, 1.0f / kSf), 0.f, 1.f);
-    const float turn_haz = (float)(worsening && turning) * (-10.0f) * (g * g) * sf;
-    bst(R, w.prev_pot, vs, pot);
-    const float speed_r = (1.0f - expf(div_rn(-vtp, kSp, 1.0f / kSp))) * 0.05f;
+    rp.sf = clampt(div_rn(fabsf(vfwd) - 0.15f, kSf, 1.0f / kSf), 0.f, 1.f);
+    rp.speed_r = (1.0f - expf(div_rn(-vtp, kSp, 1.0f / kSp))) * 0.05f;
     const float sgn = (alpha > 0.f) ? 1.f : ((alpha < 0.f) ? -1.f : 0.f);
     const float tang = (herr > 1.0f) ? sgn * 1.0f : sgn * 0.2f;
     const float dw = wzn - tang;
-    const float ang_r = expf(div_rn(-(dw * dw), kAn, 1.0f / kAn)) * 0.03f;
-    const float goal_r = ((float)goal_cnt * c.goal_reward) * 5.0f;
+    rp.ang_r = expf(div_rn(-(dw * dw), kAn, 1.0f / kAn)) * 0.03f;
+    rp.goal_r = ((float)goal_cnt * c.goal_reward) * 5.0f;
+    rp.coll = coll;
     bst(R, w.prev_dist, vs, dist);
-    const float total = dist_r * 0.5f + align_r * 0.5f + shaping * 2.0f + turn_haz + goal_r + c.time_reward +
-                        coll + speed_r + ang_r + hi_r;
     // ---- Penalties.compute_penalty (USV_task_rewards.py:440-523) ----
     const float pact0 = c.pen_use_u ? unit0 : cmd0, pact1 = c.pen_use_u ? unit1 : cmd1;
     float p_lin = 0.f, p_ang = 0.f, p_angv = 0.f, p_en = 0.f;
@@ -781,7 +750,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     if (c.pen_en_kind == PEN_SUM) p_en = -(pact0 + pact1) * c.pen_en_k + c.pen_en_c;
     else if (c.pen_en_kind == PEN_SUMSQ) p_en = -(pact0 * pact0 + pact1 * pact1) * c.pen_en_k + c.pen_en_c;
     bst(R, w.prev_wz, vs, wzn);
-    bst(R, w.rew, vs, total + (((p_lin + p_ang) + p_angv) + p_en));
+    rp.pen_sum = ((p_lin + p_ang) + p_angv) + p_en;
+    // ---- the potential-dependent tail ----
+    const RewardOut ro = reward_tail(c, rp, field_blend(taps), pot_none || was_reset, prev_pot_mem);
+    bst(R, w.prev_pot, vs, ro.pot);
+    bst(R, w.rew, vs, ro.rew);
     // ---- update_kills / is_done (static_obs.py:661-706, USV_Virtual.py:1223-1237) ----
     const bool dkill = dist > c.kill_dist;
     const bool ckill = min_od < c.collision_threshold;
@@ -798,9 +771,9 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     __builtin_amdgcn_raw_buffer_store_b64(rb64, R, mine ? (uint32_t)ec * 8u : kDrop, w.dones, 0);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, R, mine ? (uint32_t)ec : kDrop, w.just_reset, 0);
     if (kStats) {
-      const float add[25] = {total, dist_r, align_r, hi_r, shaping, speed_r, ang_r, turn_haz, goal_r,
-                             c.time_reward, coll, danger, (float)(danger > 0.5f), gate_pos, dist, bpen,
-                             p_ang, p_angv, p_en, tnorm2(vxn, vyn), fabsf(wzn),
+      const float add[25] = {ro.total, ro.dist_r, ro.align_r, rp.hi_r, ro.shaping, rp.speed_r, rp.ang_r, ro.turn_haz,
+                             rp.goal_r, c.time_reward, coll, ro.danger, (float)(ro.danger > 0.5f), ro.gate_pos, dist,
+                             bpen, p_ang, p_angv, p_en, tnorm2(vxn, vyn), fabsf(wzn),
                              ((float)(t0 < 0.f) + (float)(t1 < 0.f)) / 2.0f, (unit0 + unit1) / 2.0f,
                              ((float)(unit0 < 0.05f) + (float)(unit1 < 0.05f)) / 2.0f, unit0 + unit1};
 #pragma unroll
@@ -825,12 +798,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     for (int i = tid; i < rows * USV_NOBS; i += kBlock)
       if (keep[i / USV_NOBS]) bst(R, w.obs, obase + (uint32_t)i * 4u, sobs[i]);
   }
-  // ---- global flags: the step has consumed the Nones (:361, :448, USV_task_rewards.py:450) ----
-  if (part != 1 && blockIdx.x == 0 && tid == 0) {
-    b.ctl[USV_CTL_POT_VALID] = 1;
-    b.ctl[USV_CTL_PEN_VALID] = 1;
-    b.ctl[USV_CTL_REW_VALID] = 1;
-  }
+  // ---- the step has consumed the Nones (:361, :448, USV_task_rewards.py:450): marked here,
+  // promoted to the POT/PEN/REW_VALID flags by the next usv_reset, so the flags never change
+  // while a step kernel that reads them runs ----
+  if (blockIdx.x == 0 && tid == 0) b.ctl[USV_CTL_STEPPED] = 1;
 }
 
 // planar forces only (parity with Hydrodynamics.ComputeHydrodynamicsEffects)

@@ -113,6 +113,12 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
   const int count = b.ctl[USV_CTL_RESET_COUNT];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
+  // obstacle placement handed over by usv_reset (keys of its draws)
+  const bool place = b.ctl[USV_CTL_PLACE] != 0;
+  const uint64_t h_seed = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_HI] << 32);
+  const uint64_t h_step = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_HI] << 32);
+  const float *h_inj = reinterpret_cast<const float *>(
+      (uintptr_t)((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_HI] << 32)));
   // tile of this thread; waves own compact quadrants of the tile grid (8x8,
   // 8x7, 7x8, 7x7 tiles) so a wave idles as a whole while its region is ahead
   // of / behind the front
@@ -137,7 +143,23 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
   for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
     USV_PHASE(field, 0);
     const int e = b.reset_ids[slot];
-    if (tid < 2 * USV_NOBST) so[tid] = b.obst[(size_t)tid * n + e];
+    if (place) {
+      // CaptureXYTask.get_spawns obstacle part (static_obs.py:968-1048) for this reset env: wave 0
+      // runs the rejection sampling around the previous-episode target (usv_reset left the spawn
+      // in px/py and that target in field_old_tgt) and publishes the centres
+      if (wid == 0) {
+        const float2 oc = place_obstacles(c, e, b.px[e], b.py[e], b.field_old_tgt[e], b.field_old_tgt[n + e],
+                                          h_seed, h_step, h_inj);
+        if (lane < USV_NOBST) {
+          so[2 * lane] = oc.x;
+          so[2 * lane + 1] = oc.y;
+          b.obst[(size_t)(2 * lane) * n + e] = oc.x;
+          b.obst[(size_t)(2 * lane + 1) * n + e] = oc.y;
+        }
+      }
+    } else if (tid < 2 * USV_NOBST) {
+      so[tid] = b.obst[(size_t)tid * n + e];
+    }
     if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
     __syncthreads();
 #ifdef USV_PHASE_PROBE

@@ -54,12 +54,6 @@ class VecEnvRLGames:
         obs_dict, _, _, _ = self.step(actions)
         return obs_dict
 
-    def prepare_step(self) -> None:
-        """Start the next step's reset path (reset + potential fields) early, on a side stream, so it
-        overlaps the caller's policy forward (see USVVirtual.pre_step).  Optional: step() alone is
-        the reference contract."""
-        self._task.pre_step()
-
     def advance_host_clock(self, steps: int) -> None:
         """A captured rollout graph was replayed: the device step clock advanced by `steps`."""
         self._task.advance_host_clock(steps)

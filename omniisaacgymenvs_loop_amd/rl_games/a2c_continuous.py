@@ -212,10 +212,6 @@ class A2CAgent:
         # minibatch update are captured once and replayed every epoch (the step / Philox counters live on
         # the device, so a replay continues exactly where the eager loop would)
         self.use_graph = bool(config.get("hip_graph", True))
-        # start each step's env reset path on a side stream so it overlaps the policy forward
-        # (VecEnv.prepare_step); off by default: on MI355X the cross-stream joins cost more than the
-        # overlap saves at 4096 envs (profiles/r01 notes)
-        self.overlap_reset = bool(config.get("overlap_reset", False))
         # one kernel per minibatch with grid barriers (ppo_minibatch_fused): bit-identical to the split
         # kernels but slower on MI355X (256 cross-XCD arrivals per barrier cost more than the two kernel
         # boundaries it removes), so off by default
@@ -279,11 +275,8 @@ class A2CAgent:
         s = c.stream_ptr()
         self.meter.zero_()
         step_time = 0.0
-        prepare = getattr(self.vec_env, "prepare_step", None) if self.overlap_reset else None
         for n in range(self.horizon_length):
             obs = self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"]
-            if prepare is not None:
-                prepare()      # the env's reset path for this step overlaps the policy forward
             c.call("ppo_policy_step", cfg, c.ptr(self.model_params), c.ptr(self.obs_rms), c.ptr(self.val_rms),
                    c.ptr(obs), n, c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp),
                    c.ptr(self.exp_val), c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.exp_done),

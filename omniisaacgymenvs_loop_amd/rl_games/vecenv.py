@@ -31,7 +31,7 @@ class RLGPUEnv:
         self.env = configurations[config_name]["env_creator"](**kwargs)
 
     def __getattr__(self, name):
-        # optional env extensions (prepare_step, advance_host_clock, ...) pass through to the wrapped env
+        # optional env extensions (advance_host_clock, ...) pass through to the wrapped env
         if name == "env":
             raise AttributeError(name)
         return getattr(self.env, name)

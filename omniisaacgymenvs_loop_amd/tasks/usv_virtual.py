@@ -120,10 +120,6 @@ class USVVirtual:
         # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
         self.clock = Z(4, device=dev, dtype=torch.int64)
         self.states_buf = Z((n, 0), **f32)
-        self._side_stream = None
-        self._side_done = None
-        self._reset_done = None
-        self._pre_stepped = False
         self.sdf = torch.empty((n, GRID2), **f32)      # per-reset-slot SDF scratch of the field kernels
         self.lut = Z((2, 1000), **f32)
         tl, tr = thruster_tables(self._task_cfg)
@@ -225,62 +221,38 @@ class USVVirtual:
             return float(self._initial_action_bias)
         return 0.0
 
-    def pre_step(self) -> None:
-        """Launch this step's reset path (usv_reset + usv_potential_field) on a side stream.
-
-        The reset of step t only needs step t-1's dones, so it can run while the policy computes
-        step t's actions; env_step() then runs the non-reset envs right away and the reset envs once
-        their potential fields are built (usv_env_step_part 1 / 2).  Same results as env_step alone."""
-        if self._side_stream is None:
-            self._side_stream = torch.cuda.Stream(device=self._device)
-            self._reset_done = torch.cuda.Event()
-            self._side_done = torch.cuda.Event()
-        main = torch.cuda.current_stream(self._device)
-        side = self._side_stream
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            s = _capi.stream_ptr()
-            cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
-            _capi.call("usv_reset", cfg, b, self.seed, self._step_index, None, s)
-            self._reset_done.record(side)
-            _capi.call("usv_potential_field", cfg, b, s)
-            self._side_done.record(side)
-        self._pre_stepped = True
-
     def env_step(self, actions: torch.Tensor, u_step: Optional[torch.Tensor] = None,
                  u_reset: Optional[torch.Tensor] = None):
         """pre_physics_step + 10 substeps + post_physics_step (USV_Virtual.py:1042-1652).
 
-        Returns the device tensors (obs [n,33], rew [n], dones int64 [n])."""
-        if actions.dtype != torch.float32 or not actions.is_contiguous():
-            actions = actions.to(torch.float32).contiguous()
+        Returns the device tensors (obs [n,33], rew [n], dones int64 [n]).  u_step / u_reset replay
+        recorded uniforms (parity tests) instead of the in-kernel Philox draws."""
+        actions = self._f32(actions)
         s = _capi.stream_ptr()
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
+        bias, k = self._advance()
+        _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
+        _capi.call("usv_potential_field", cfg, b, s)
+        _capi.call("usv_env_step", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
+                   self.seed, k, _capi.ptr(u_step), s)
+        return self.obs_buf_t, self.rew_buf, self.dones
+
+    def _f32(self, actions: torch.Tensor) -> torch.Tensor:
+        if actions.dtype != torch.float32 or not actions.is_contiguous():
+            actions = actions.to(torch.float32).contiguous()
+        return actions
+
+    def _advance(self):
+        """Host mirror of the step clock: (action bias, step index) of this step."""
         bias = self.current_action_bias()
         self._action_bias_step_count += 1
         k = self._step_index
-        if self._pre_stepped and u_step is None and u_reset is None:
-            self._pre_stepped = False
-            main = torch.cuda.current_stream(self._device)
-            main.wait_event(self._reset_done)      # part 1 needs this step's reset flags and states
-            _capi.call("usv_env_step_part", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
-                       self.seed, k, None, 1, s)
-            main.wait_event(self._side_done)       # part 2 needs the reset envs' new fields
-            _capi.call("usv_env_step_part", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
-                       self.seed, k, None, 2, s)
-        else:
-            if self._pre_stepped:
-                raise RuntimeError("pre_step() was called: env_step() cannot inject uniforms for that step")
-            _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
-            _capi.call("usv_potential_field", cfg, b, s)
-            _capi.call("usv_env_step", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
-                       self.seed, k, _capi.ptr(u_step), s)
         self._step_index += 1
         self.step += 1.0 / self._horizon
         if k == 0 or "episode" not in self.extras:
             # extras["episode"]: 0-d views of the device buffer written at every reset (USV_Virtual.py:1591-1612)
             self.extras = {"episode": {name: self.extras_buf[i] for i, name in enumerate(STAT_NAMES)}}
-        return self.obs_buf_t, self.rew_buf, self.dones
+        return bias, k
 
     def forces(self) -> torch.Tensor:
         out = torch.empty((self._num_envs, 3), device=self._device, dtype=torch.float32)
