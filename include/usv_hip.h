@@ -54,7 +54,11 @@ extern "C" {
 #define RU_VX       695     /* USVVirtual.reset_idx:1561 */
 #define RU_VY       696     /* :1564 */
 #define RU_GOAL     697     /* CaptureXYTask.get_goals:924 (2) */
-#define USV_NU_RESET 699
+#define RU_FSIN     699     /* ForceDisturbance.generate_force:342-362 (x_freq, y_freq, x_shift, y_shift, amp) */
+#define RU_FCONST   704     /* :369-374 (r, theta) */
+#define RU_TSIN     706     /* TorqueDisturbance.generate_torque:484-494 (freq, shift, amp) */
+#define RU_TCONST   709     /* :500-506 (r, sign draw) */
+#define USV_NU_RESET 711
 /* Layout of the uniform draws of one env step (device [n][USV_NU_STEP] when
  * injected; otherwise Philox(ctr={env, step_lo, step_hi, i/4})[i%4]).
  * Only the draws of the LAST update_state of the step reach obs/reward
@@ -164,8 +168,23 @@ typedef struct usv_cfg {
    * first act_bias_steps pre_physics_step calls; used in device-clock mode */
   float act_bias;
   int   act_bias_steps;
-  int   pad_;
+  /* ---- force / torque disturbances (USV_disturbances.py:268-530, TEST yaml
+   * disturbances.forces/torques) and water current (Hydrodynamics.py:224-237) ---- */
+  int   fdist_on, fconst_on, fsin_on;
+  float fconst_min, fconst_max, fsin_min, fsin_max, ffreq_min, ffreq_max, fshift_min, fshift_max;
+  int   tdist_on, tconst_on, tsin_on;
+  float tconst_min, tconst_max, tsin_min, tsin_max, tfreq_min, tfreq_max, tshift_min, tshift_max;
+  int   current_on;
+  float flow_vel[2];        /* world-frame water velocity x, y */
 } usv_cfg_t;
+
+/* per-env disturbance parameters (rows of usv_bufs_t.dist, drawn at reset) */
+enum usv_dist_row {
+  DI_FCX = 0, DI_FCY,                          /* disturbance_forces_const x, y */
+  DI_FXF, DI_FYF, DI_FXS, DI_FYS, DI_FAMP,     /* _force_{x,y}_freq, _force_{x,y}_shift, _force_amp */
+  DI_TC, DI_TF, DI_TS, DI_TAMP,                /* disturbance_torques_const z, _torque_freq/shift/amp */
+  USV_NDIST
+};
 
 /* Device buffers of the env (SoA).  All arrays have n entries unless noted. */
 typedef struct usv_bufs {
@@ -202,6 +221,8 @@ typedef struct usv_bufs {
   float   *slot_stats;             /* [n][USV_FIELD_SLOT_STATS] per-reset-slot field statistics (scratch) */
   float   *sdf;                    /* [n][150*150] per-reset-slot signed distance (scratch) */
   const float *grid_lin;           /* [150] cell centres of the field grid */
+  float   *dist;                   /* [USV_NDIST][n] disturbance parameters; NULL when no disturbance is on */
+  const float *env_org;            /* [2][n] world x, y of each env's origin (RLTask._env_pos); NULL = 0 */
   /* device step clock (nullable): [0] next step index, [1] next bias-call count,
    * [2] current step, [3] current bias-call count.  When set, usv_reset advances
    * it and the step / bias arguments of usv_reset / usv_env_step are ignored, so

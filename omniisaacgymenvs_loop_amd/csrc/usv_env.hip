@@ -191,6 +191,37 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
           b.thr_r[e] = m;
         }
       }
+      // ---- ForceDisturbance.generate_force / TorqueDisturbance.generate_torque
+      // (USV_disturbances.py:327-508, called from reset_idx:1517-1518) ----
+      if (b.dist) {
+        float *D = b.dist;
+        const size_t nn = (size_t)n;
+        if (c.fdist_on && c.fsin_on) {
+          const float fr_ = (float)((double)c.ffreq_max - (double)c.ffreq_min);
+          const float sr_ = (float)((double)c.fshift_max - (double)c.fshift_min);
+          D[DI_FXF * nn + e] = U(RU_FSIN) * fr_ + c.ffreq_min;
+          D[DI_FYF * nn + e] = U(RU_FSIN + 1) * fr_ + c.ffreq_min;
+          D[DI_FXS * nn + e] = U(RU_FSIN + 2) * sr_ + c.fshift_min;
+          D[DI_FYS * nn + e] = U(RU_FSIN + 3) * sr_ + c.fshift_min;
+          D[DI_FAMP * nn + e] = U(RU_FSIN + 4) * (float)((double)c.fsin_max - (double)c.fsin_min) + c.fsin_min;
+        }
+        if (c.fdist_on && c.fconst_on) {
+          const float r = U(RU_FCONST) * (float)((double)c.fconst_max - (double)c.fconst_min) + c.fconst_min;
+          const float th = U(RU_FCONST + 1) * USV_PI_F * 2.0f;
+          D[DI_FCX * nn + e] = cosf(th) * r;
+          D[DI_FCY * nn + e] = sinf(th) * r;
+        }
+        if (c.tdist_on && c.tsin_on) {
+          D[DI_TF * nn + e] = U(RU_TSIN) * (float)((double)c.tfreq_max - (double)c.tfreq_min) + c.tfreq_min;
+          D[DI_TS * nn + e] = U(RU_TSIN + 1) * (float)((double)c.tshift_max - (double)c.tshift_min) + c.tshift_min;
+          D[DI_TAMP * nn + e] = U(RU_TSIN + 2) * (float)((double)c.tsin_max - (double)c.tsin_min) + c.tsin_min;
+        }
+        if (c.tdist_on && c.tconst_on) {
+          float r = U(RU_TCONST) * (float)((double)c.tconst_max - (double)c.tconst_min) + c.tconst_min;
+          if (U(RU_TCONST + 1) > 0.5f) r = r * -1.0f;   // half of the envs at random (:505-507)
+          D[DI_TC * nn + e] = r;
+        }
+      }
       // ---- _apply_mass_driven_coupling (USV_Virtual.py:988-1040) ----
       if (c.couple_drag || c.couple_thr || c.couple_kiz) {
         const double den_d = (double)c.mass_max - (double)c.base_mass;
@@ -356,6 +387,7 @@ struct StepWin {
   uint32_t px, py, yaw, vx, vy, wz, fl, fr, mass, k_iz, k_drag, thr_l, thr_r, com_x, com_y, com_z;
   uint32_t lin_damp, quad_damp, progress, tgt_x, tgt_y, obst, goal_cnt, prev_dist, prev_head, prev_pot, prev_wz;
   uint32_t stats, prev_cmd, rew, reset_buf, dones, done_coll, done_succ, just_reset, obs;
+  uint32_t dist, env_org;
   uint32_t n4;      // bytes of one [n] f32 row
   uint32_t bytes;   // window size
 };
@@ -411,7 +443,7 @@ __device__ __forceinline__ void top5_of_16(uint64_t k[16]) {
   cx64(k[1], k[2]); cx64(k[3], k[4]);
 }
 
-template <bool kStats, bool kInj>
+template <bool kStats, bool kInj, bool kDist>
 __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, StepWin w, StepK K,
                                                      const char *__restrict__ wbase, const float *__restrict__ actions,
                                                      const float *__restrict__ lut, float bias, uint64_t seed,
@@ -478,6 +510,15 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     const float q2 = bld(R, w.quad_damp + 2 * w.n4, v4);
     const float lin0 = dr ? l0 : c.lin_damp[0], lin1 = dr ? l1 : c.lin_damp[1], lin2 = dr ? l2 : c.lin_damp[2];
     const float qd0 = dr ? q0 : c.quad_damp[0], qd1 = dr ? q1 : c.quad_damp[1], qd2 = dr ? q2 : c.quad_damp[2];
+    // disturbance parameters (drawn at reset) and the env origin (root_pos is world-frame)
+    float dp[USV_NDIST], orgx = 0.f, orgy = 0.f;
+    if (kDist) {
+#pragma unroll
+      for (int q = 0; q < USV_NDIST; ++q) dp[q] = bld(R, w.dist + (uint32_t)q * w.n4, v4);
+      const float ox_ = bld(R, w.env_org, v4), oy_ = bld(R, w.env_org + w.n4, v4);
+      orgx = b.env_org ? ox_ : 0.f;
+      orgy = b.env_org ? oy_ : 0.f;
+    }
     __builtin_amdgcn_sched_barrier(0);   // keep the substep inputs ahead of the loads below
     const int progress0 = bldi(R, w.progress, v4);
     const float tgx = bld(R, w.tgt_x, v4), tgy = bld(R, w.tgt_y, v4);
@@ -564,15 +605,33 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       fr = fr * al + oma * tgt1;
       float sy_, cy_;
       sincosf(yaw, &sy_, &cy_);
-      const float ub = cy_ * vx + sy_ * vy;           // R^T v (Utils.py:8-12)
-      const float vb = -sy_ * vx + cy_ * vy;
+      float ub = cy_ * vx + sy_ * vy;                 // R^T v (Utils.py:8-12)
+      float vb = -sy_ * vx + cy_ * vy;
       const float rb = wz;
+      float dfx = 0.f, dfy = 0.f, dtz = 0.f;
+      if (kDist) {
+        if (c.current_on) {                           // relative to the water (Hydrodynamics.py:224-237)
+          ub = ub - (cy_ * c.flow_vel[0] + sy_ * c.flow_vel[1]);
+          vb = vb - (-sy_ * c.flow_vel[0] + cy_ * c.flow_vel[1]);
+        }
+        // get_disturbance_forces / get_torque_disturbance at root_pos (USV_disturbances.py:386-410,510-530)
+        const float wx = px + orgx, wy = py + orgy;
+        dfx = dp[DI_FCX];
+        dfy = dp[DI_FCY];
+        dtz = dp[DI_TC];
+        if (c.fsin_on) {
+          dfx = dfx + sinf(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
+          dfy = dfy + sinf(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
+        }
+        if (c.tsin_on) dtz = dtz + sinf((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
+      }
       float D0 = lin0 + qd0 * fabsf(ub), D1 = lin1 + qd1 * fabsf(vb), D2 = lin2 + qd2 * fabsf(rb);
       D0 = D0 * c.scaling_damping; D1 = D1 * c.scaling_damping; D2 = D2 * c.scaling_damping;
       if (c.use_drag_scale) { D0 = D0 * kd; D1 = D1 * kd; D2 = D2 * kd; }
-      const float X = fl + fr + (-D0 * ub);           // Hydrodynamics.py:243
-      const float Y = -D1 * vb;
-      const float N = arm_l * fl + arm_r * fr + (-D2 * rb);
+      // base force = disturbance + drag (+ hydrostatics, 0 in the plane), thrusters (USV_Virtual.py:1118-1132)
+      const float X = kDist ? fl + fr + (dfx + (-D0 * ub)) : fl + fr + (-D0 * ub);   // Hydrodynamics.py:243
+      const float Y = kDist ? dfy + (-D1 * vb) : -D1 * vb;
+      const float N = kDist ? arm_l * fl + arm_r * fr + (dtz + (-D2 * rb)) : arm_l * fl + arm_r * fr + (-D2 * rb);
       const float ax = div_rn(cy_ * X - sy_ * Y, m, inv_m);
       const float ay = div_rn(sy_ * X + cy_ * Y, m, inv_m);
       const float aw = div_rn(N, izz, inv_izz);
@@ -812,7 +871,11 @@ __global__ void k_forces(usv_cfg_t c, usv_bufs_t b, float *__restrict__ out) {
   float sy_, cy_;
   sincosf(b.yaw[e], &sy_, &cy_);
   const float vx = b.vx[e], vy = b.vy[e], wz = b.wz[e];
-  const float ub = cy_ * vx + sy_ * vy, vb = -sy_ * vx + cy_ * vy;
+  float ub = cy_ * vx + sy_ * vy, vb = -sy_ * vx + cy_ * vy;
+  if (c.current_on) {   // relative to the water (Hydrodynamics.py:224-237)
+    ub = ub - (cy_ * c.flow_vel[0] + sy_ * c.flow_vel[1]);
+    vb = vb - (-sy_ * c.flow_vel[0] + cy_ * c.flow_vel[1]);
+  }
   float lin0 = c.lin_damp[0], lin1 = c.lin_damp[1], lin2 = c.lin_damp[2];
   float qd0 = c.quad_damp[0], qd1 = c.quad_damp[1], qd2 = c.quad_damp[2];
   if (b.lin_damp) {
@@ -855,7 +918,8 @@ int step_window(const usv_cfg_t &c, const usv_bufs_t &b, const char **base, Step
       {b.prev_cmd, 2 * f, &w->prev_cmd, true}, {b.rew, f, &w->rew, true}, {b.reset_buf, f, &w->reset_buf, true},
       {b.dones, 2 * f, &w->dones, true}, {b.done_coll, f, &w->done_coll, true},
       {b.done_succ, f, &w->done_succ, true}, {b.just_reset, n, &w->just_reset, true},
-      {b.obs, USV_NOBS * f, &w->obs, true}};
+      {b.obs, USV_NOBS * f, &w->obs, true}, {b.dist, USV_NDIST * f, &w->dist, false},
+      {b.dist ? b.env_org : nullptr, 2 * f, &w->env_org, false}};
   uintptr_t lo = UINTPTR_MAX, hi = 0;
   for (const Arr &a : arr) {
     if (!a.p) {
@@ -872,6 +936,9 @@ int step_window(const usv_cfg_t &c, const usv_bufs_t &b, const char **base, Step
   *base = (const char *)lo;
   return 0;
 }
+
+// any per-substep disturbance term on (then usv_bufs_t.dist must be set)
+bool step_has_dist(const usv_cfg_t &c) { return c.fdist_on || c.tdist_on || c.current_on; }
 
 float enc_centered_scale(float xmin, float xmax, float nominal) {
   double sc = std::fabs((double)xmin - nominal);
@@ -980,8 +1047,12 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
   const StepK k = step_constants(*cfg);
   const int grid = (b->n + kBlock - 1) / kBlock;
   hipStream_t s = (hipStream_t)stream;
-  auto kern = cfg->stats_on ? (u_inject ? k_env_step<true, true> : k_env_step<true, false>)
-                            : (u_inject ? k_env_step<false, true> : k_env_step<false, false>);
+  const bool dist = b->dist != nullptr;
+  if (step_has_dist(*cfg) && !dist) return 4;   // a disturbance / water current is on: dist is required
+  auto kern = dist ? (cfg->stats_on ? (u_inject ? k_env_step<true, true, true> : k_env_step<true, false, true>)
+                                    : (u_inject ? k_env_step<false, true, true> : k_env_step<false, false, true>))
+                   : (cfg->stats_on ? (u_inject ? k_env_step<true, true, false> : k_env_step<true, false, false>)
+                                    : (u_inject ? k_env_step<false, true, false> : k_env_step<false, false, false>));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, w, k, wbase, actions, lut_dev, action_bias, seed,
                      step, u_inject, part);
   USV_CHECK_LAUNCH();

@@ -289,9 +289,46 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     c.act_bias, c.act_bias_steps = action_bias_cfg(task_cfg)
     if bool((env.get("scene_replay", {}) or {}).get("enabled", False)):
         raise NotImplementedError("scene_replay (NPZ) is not supported yet; set env.scene_replay.enabled=False")
-    if bool(env.get("water_current", {}).get("use_water_current", False)):
-        raise NotImplementedError("water current is not on the CaptureXY hot path")
+    # ---- disturbances (ForceDisturbance / TorqueDisturbance.__init__, USV_disturbances.py:268-298,
+    # 412-440) and water current (USVVirtual.__init__ -> ComputeHydrodynamicsEffects) ----
+    fd = dist.get("forces", {}) or {}
+    c.fdist_on = int(bool(fd.get("use_force_disturbance", False)))
+    c.fconst_on = int(bool(fd.get("use_constant_force", False)))
+    c.fsin_on = int(bool(fd.get("use_sinusoidal_force", False)))
+    for k, key in (("fconst_min", "force_const_min"), ("fconst_max", "force_const_max"),
+                   ("fsin_min", "force_sin_min"), ("fsin_max", "force_sin_max"),
+                   ("ffreq_min", "force_min_freq"), ("ffreq_max", "force_max_freq"),
+                   ("fshift_min", "force_min_shift"), ("fshift_max", "force_max_shift")):
+        v = float(fd.get(key, 0.0))
+        if k in ("fconst_min", "fconst_max", "fsin_min", "fsin_max"):
+            v = math.sqrt(v ** 2 / 2)   # per-axis magnitude (USV_disturbances.py:281-288)
+        setattr(c, k, v)
+    td = dist.get("torques", {}) or {}
+    c.tdist_on = int(bool(td.get("use_torque_disturbance", False)))
+    c.tconst_on = int(bool(td.get("use_constant_torque", False)))
+    c.tsin_on = int(bool(td.get("use_sinusoidal_torque", False)))
+    for k, key in (("tconst_min", "torque_const_min"), ("tconst_max", "torque_const_max"),
+                   ("tsin_min", "torque_sin_min"), ("tsin_max", "torque_sin_max"),
+                   ("tfreq_min", "torque_min_freq"), ("tfreq_max", "torque_max_freq"),
+                   ("tshift_min", "torque_min_shift"), ("tshift_max", "torque_max_shift")):
+        setattr(c, k, float(td.get(key, 0.0)))
+    wc = env.get("water_current", {}) or {}
+    c.current_on = int(bool(wc.get("use_water_current", False)))
+    flow = list(wc.get("flow_velocity", [0.0, 0.0, 0.0]) or [0.0, 0.0, 0.0])
+    c.flow_vel[0], c.flow_vel[1] = float(flow[0]), float(flow[1])
     return c
+
+
+def has_disturbance(c: UsvCfg) -> bool:
+    """Any per-substep disturbance term on (the kernels then need usv_bufs_t.dist)."""
+    return bool(c.fdist_on or c.tdist_on or c.current_on)
+
+
+def env_origins(num_envs: int, spacing: float = 50.0, per_row: int = 8) -> np.ndarray:
+    """RLTask._env_pos when the stage has no env translate (USV_Virtual.py:1670-1696):
+    x = (i % per_row) * spacing, y = (i // per_row) * spacing ([2][n] float32)."""
+    i = np.arange(num_envs)
+    return np.stack([(i % per_row) * spacing, (i // per_row) * spacing]).astype(np.float32)
 
 
 def action_bias_cfg(task_cfg: Dict[str, Any]):

@@ -18,9 +18,9 @@ import numpy as np
 import torch
 
 from .. import _capi
-from .._abi import DEFINES, STAT_NAMES, UsvBufs
+from .._abi import DEFINES, STAT_NAMES, UsvBufs, enum_values
 from ..utils.spaces import Box, DictSpace
-from .usv_config import action_bias_cfg, build_usv_cfg, thruster_tables
+from .usv_config import action_bias_cfg, build_usv_cfg, env_origins, has_disturbance, thruster_tables
 
 NOBS = DEFINES["USV_NOBS"]
 NOBST = DEFINES["USV_NOBST"]
@@ -28,6 +28,7 @@ GRID2 = DEFINES["USV_GRID"] ** 2
 NSTAT = DEFINES["USV_NSTAT"]
 NU_RESET = DEFINES["USV_NU_RESET"]
 NU_STEP = DEFINES["USV_NU_STEP"]
+NDIST = enum_values("usv_dist_row")["USV_NDIST"]
 CTL_N = DEFINES["USV_CTL_N"]
 
 
@@ -94,7 +95,8 @@ class USVVirtual:
                      ("just_reset", (n,), torch.uint8), ("stats", (NSTAT, n), torch.float32),
                      ("obs_buf_t", (n, NOBS), torch.float32), ("rew_buf", (n,), torch.float32),
                      ("dones", (n,), torch.int64), ("field_old_tgt", (2, n), torch.float32),
-                     ("reset_ids", (n,), torch.int32)]
+                     ("reset_ids", (n,), torch.int32), ("dist", (NDIST, n), torch.float32),
+                     ("env_org", (2, n), torch.float32)]
         sizes = [int(np.prod(shape)) * torch.empty((), dtype=dt).element_size() for _, shape, dt in slab_spec]
         offs = np.concatenate([[0], np.cumsum([(sz + 255) // 256 * 256 for sz in sizes])])
         self._slab = torch.zeros(int(offs[-1]), device=dev, dtype=torch.uint8)
@@ -108,6 +110,10 @@ class USVVirtual:
                 self.damp[1, a] = self.cfg.quad_damp[a]
         else:
             self.damp = None
+        if not has_disturbance(self.cfg):
+            self.dist = None
+        # RLTask._env_pos (x, y): only the disturbance sinusoids read world positions
+        self.env_org.copy_(torch.from_numpy(env_origins(n)))
         self.field = Z((n, GRID2), **f32)
         self.ibuf[2] = 1                               # RLTask.cleanup: reset_buf = ones
         self.just_reset.fill_(1)
@@ -155,7 +161,13 @@ class USVVirtual:
         b.sdf = p(self.sdf)
         b.clock = p(self.clock)
         b.grid_lin = p(self.grid_lin) if self.grid_lin is not None else None
+        b.dist = p(self.dist) if self.dist is not None else None
+        b.env_org = p(self.env_org)
         return b
+
+    def set_env_origins(self, org: torch.Tensor) -> None:
+        """World x, y of each env's origin ([2][n]; RLTask._env_pos from the stage)."""
+        self.env_org.copy_(org.to(self._device, torch.float32).reshape(2, self._num_envs))
 
     def set_grid_lin(self, lin: torch.Tensor) -> None:
         """Override the field grid's cell centres (parity tests vs CPU fixtures)."""

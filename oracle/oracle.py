@@ -17,7 +17,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libusv_oracle.so")
 
 NOBS, NOBST, GRID, NSTAT = 33, 16, 150, 28
-NU_RESET, NU_STEP = 699, 8
+NU_RESET, NU_STEP = 711, 8
+NDIST = 11
 CTL_POT_VALID, CTL_PEN_VALID, CTL_REW_VALID = 1, 2, 3
 
 _lib = None
@@ -69,7 +70,8 @@ _PTR_FIELDS =  ("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr",
 class _OracleEnvC(ctypes.Structure):
     _fields_ = ([("n", ctypes.c_int)] + [(k, ctypes.c_void_p) for k in _PTR_FIELDS] +
                 [("ctl", ctypes.c_int32 * 16), ("extras", ctypes.c_float * NSTAT), ("dbg", ctypes.c_void_p),
-                 ("tmp", ctypes.c_void_p), ("grid_lin", ctypes.c_void_p)])
+                 ("tmp", ctypes.c_void_p), ("grid_lin", ctypes.c_void_p), ("dist", ctypes.c_void_p),
+                 ("env_org", ctypes.c_void_p)])
 
 
 class OracleEnv:
@@ -116,6 +118,14 @@ class OracleEnv:
         self.c.tmp = _p(self.tmp)
         self.c.lin_damp = _p(self.lin_damp) if self.lin_damp is not None else None
         self.c.quad_damp = _p(self.quad_damp) if self.quad_damp is not None else None
+        # disturbance parameters (zeros until drawn at reset) and env origins
+        self.dist = np.zeros((NDIST, n), np.float32) if has_dist(cfg) else None
+        self.c.dist = _p(self.dist) if self.dist is not None else None
+        self.env_org = None
+
+    def set_env_origins(self, org):
+        self.env_org = np.ascontiguousarray(org, np.float32).reshape(2, self.n)
+        self.c.env_org = _p(self.env_org)
 
     @property
     def extras(self):
@@ -173,6 +183,10 @@ class OracleEnv:
         out = np.zeros((self.n, 3), np.float32)
         lib().oracle_forces(ctypes.byref(self.cfg), ctypes.byref(self.c), _p(out))
         return out
+
+
+def has_dist(cfg) -> bool:
+    return bool(cfg.fdist_on or cfg.tdist_on or cfg.current_on)
 
 
 def make_lut(table_l, table_r, n_out=1000):

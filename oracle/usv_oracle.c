@@ -117,6 +117,8 @@ typedef struct oracle_env {
   float *dbg;                       /* [n][16]: u_l, u_r, target_l, target_r, pot, danger, ... */
   float *tmp;                       /* [n][8]: cmd[2], thrust[2], unit[2], target force[2] */
   const float *grid_lin;            /* [150] potential-field cell centres, NULL => linspace formula */
+  float *dist;                      /* [USV_NDIST][n] disturbance parameters or NULL */
+  const float *env_org;             /* [2][n] env origins (RLTask._env_pos) or NULL */
 } oracle_env_t;
 
 /* ------------------------------------------------------------------------ */
@@ -125,12 +127,17 @@ typedef struct oracle_env {
  * at the heron.usd lever arms.                           */
 /* ------------------------------------------------------------------------ */
 static void planar_forces(const usv_cfg_t *c, const oracle_env_t *E, int e, float cy, float sy,
-                          float fl, float fr, float *X, float *Y, float *N) {
+                          float fl, float fr, const float *dist3 /* disturbance fx, fy, tz or NULL */,
+                          float *X, float *Y, float *N) {
   const float vx = E->vx[e], vy = E->vy[e], wz = E->wz[e];
   /* getLocalLinearVelocities: R^T v  (Utils.py:8-12) */
-  const float u = cy * vx + sy * vy;
-  const float v = -sy * vx + cy * vy;
+  float u = cy * vx + sy * vy;
+  float v = -sy * vx + cy * vy;
   const float r = wz;
+  if (c->current_on) {   /* relative to the water current (Hydrodynamics.py:224-237): R^T v - R^T flow */
+    u = u - (cy * c->flow_vel[0] + sy * c->flow_vel[1]);
+    v = v - (-sy * c->flow_vel[0] + cy * c->flow_vel[1]);
+  }
   float lin[3], quad[3];
   for (int k = 0; k < 3; ++k) {
     lin[k] = E->lin_damp ? E->lin_damp[k * E->n + e] : c->lin_damp[k];
@@ -145,16 +152,41 @@ static void planar_forces(const usv_cfg_t *c, const oracle_env_t *E, int e, floa
     drag[k] = -D * vel[k];                                 /* (:243) */
   }
   const float comy = E->com_y[e];
+  if (dist3) {   /* base force = disturbance + drag (USV_Virtual.py:1118-1125) */
+    *X = fl + fr + (dist3[0] + drag[0]);
+    *Y = dist3[1] + drag[1];
+    *N = -(c->thr_y - comy) * fl + (c->thr_y + comy) * fr + (dist3[2] + drag[2]);
+    return;
+  }
   *X = fl + fr + drag[0];
   *Y = drag[1];
   *N = -(c->thr_y - comy) * fl + (c->thr_y + comy) * fr + drag[2];
+}
+
+/* ForceDisturbance.get_disturbance_forces / TorqueDisturbance.get_torque_disturbance
+ * (USV_disturbances.py:386-410, 510-530) at the world root position (root_pos =
+ * local + RLTask._env_pos); body-frame base force / yaw torque (is_global=False,
+ * USV_Virtual.py:1118-1125). */
+static void disturbance(const usv_cfg_t *c, const oracle_env_t *E, int e, float *fx, float *fy, float *tz) {
+  const int n = E->n;
+  const float *D = E->dist;
+  const float wx = E->px[e] + (E->env_org ? E->env_org[e] : 0.f);
+  const float wy = E->py[e] + (E->env_org ? E->env_org[n + e] : 0.f);
+  *fx = D[DI_FCX * n + e];
+  *fy = D[DI_FCY * n + e];
+  *tz = D[DI_TC * n + e];
+  if (c->fsin_on) {
+    *fx = *fx + sinf(wx * D[DI_FXF * n + e] + D[DI_FXS * n + e]) * D[DI_FAMP * n + e];
+    *fy = *fy + sinf(wy * D[DI_FYF * n + e] + D[DI_FYS * n + e]) * D[DI_FAMP * n + e];
+  }
+  if (c->tsin_on) *tz = *tz + sinf((wx + wy) * D[DI_TF * n + e] + D[DI_TS * n + e]) * D[DI_TAMP * n + e];
 }
 
 void oracle_forces(const usv_cfg_t *c, oracle_env_t *E, float *out /*[n][3]*/) {
   for (int e = 0; e < E->n; ++e) {
     const float cy = cosf(E->yaw[e]), sy = sinf(E->yaw[e]);
     float X, Y, N;
-    planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], &X, &Y, &N);
+    planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], NULL, &X, &Y, &N);
     out[e * 3 + 0] = X; out[e * 3 + 1] = Y; out[e * 3 + 2] = N;
   }
 }
@@ -437,6 +469,36 @@ void oracle_reset(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids
         E->thr_l[e] = m; E->thr_r[e] = m;
       }
     }
+    /* ForceDisturbance.generate_force / TorqueDisturbance.generate_torque
+     * (USV_disturbances.py:327-508, reset_idx:1517-1518) */
+    if (E->dist) {
+      float *D = E->dist;
+      if (c->fdist_on && c->fsin_on) {
+        const float fr_ = (float)((double)c->ffreq_max - (double)c->ffreq_min);
+        const float sr_ = (float)((double)c->fshift_max - (double)c->fshift_min);
+        D[DI_FXF * n + e] = u[RU_FSIN] * fr_ + c->ffreq_min;
+        D[DI_FYF * n + e] = u[RU_FSIN + 1] * fr_ + c->ffreq_min;
+        D[DI_FXS * n + e] = u[RU_FSIN + 2] * sr_ + c->fshift_min;
+        D[DI_FYS * n + e] = u[RU_FSIN + 3] * sr_ + c->fshift_min;
+        D[DI_FAMP * n + e] = u[RU_FSIN + 4] * (float)((double)c->fsin_max - (double)c->fsin_min) + c->fsin_min;
+      }
+      if (c->fdist_on && c->fconst_on) {
+        const float rr = u[RU_FCONST] * (float)((double)c->fconst_max - (double)c->fconst_min) + c->fconst_min;
+        const float tt = u[RU_FCONST + 1] * (float)OPI * 2.0f;
+        D[DI_FCX * n + e] = cosf(tt) * rr;
+        D[DI_FCY * n + e] = sinf(tt) * rr;
+      }
+      if (c->tdist_on && c->tsin_on) {
+        D[DI_TF * n + e] = u[RU_TSIN] * (float)((double)c->tfreq_max - (double)c->tfreq_min) + c->tfreq_min;
+        D[DI_TS * n + e] = u[RU_TSIN + 1] * (float)((double)c->tshift_max - (double)c->tshift_min) + c->tshift_min;
+        D[DI_TAMP * n + e] = u[RU_TSIN + 2] * (float)((double)c->tsin_max - (double)c->tsin_min) + c->tsin_min;
+      }
+      if (c->tdist_on && c->tconst_on) {
+        float rr = u[RU_TCONST] * (float)((double)c->tconst_max - (double)c->tconst_min) + c->tconst_min;
+        if (u[RU_TCONST + 1] > 0.5f) rr = rr * -1.0f;
+        D[DI_TC * n + e] = rr;
+      }
+    }
     /* _apply_mass_driven_coupling (USV_Virtual.py:988-1040) */
     if (c->couple_drag || c->couple_thr || c->couple_kiz) {
       const double denom = ((double)c->mass_max - (double)c->base_mass) > 1e-6 ? ((double)c->mass_max - (double)c->base_mass) : 1e-6;
@@ -599,8 +661,9 @@ void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E) {
       E->fl[e] = E->fl[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[0];
       E->fr[e] = E->fr[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[1];
       const float cy = cosf(E->yaw[e]), sy = sinf(E->yaw[e]);
-      float X, Y, N;
-      planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], &X, &Y, &N);
+      float X, Y, N, d3[3];
+      if (E->dist) disturbance(c, E, e, &d3[0], &d3[1], &d3[2]);
+      planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], E->dist ? d3 : NULL, &X, &Y, &N);
       /* build's 3-DoF semi-implicit Euler (no reference: PhysX) */
       const float ax = (cy * X - sy * Y) / m;
       const float ay = (sy * X + cy * Y) / m;

@@ -39,7 +39,16 @@ def golden():
 
     def load(name):
         if name not in cache:
-            cache[name] = dict(np.load(os.path.join(GOLDEN, name), allow_pickle=False))
+            d = dict(np.load(os.path.join(GOLDEN, name), allow_pickle=False))
+            ru = d.get("reset_U")
+            if ru is not None:
+                # fixtures recorded before later reset draw sites existed (RU_* of
+                # include/usv_hip.h) never reached those sites: pad their columns
+                from omniisaacgymenvs_loop_amd._abi import DEFINES
+                nu = DEFINES["USV_NU_RESET"]
+                if ru.shape[1] < nu:
+                    d["reset_U"] = np.concatenate([ru, np.zeros((ru.shape[0], nu - ru.shape[1]), ru.dtype)], 1)
+            cache[name] = d
         return cache[name]
 
     return load

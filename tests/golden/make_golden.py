@@ -321,6 +321,17 @@ def load_task_cfg(variant: str):
         env["reward_parameters"]["reward_mode"] = "exponential"
         env["task_parameters"]["goal_random_position"] = 0.0
         env["maxEpisodeLength"] = 40
+    if variant == "C":
+        # disturbance variant: constant + sinusoidal force and torque disturbances
+        # (USV_disturbances.py:268-530) and a water current (Hydrodynamics.py:224-237)
+        env = cfg["env"]
+        for key in ("use_force_disturbance", "use_constant_force", "use_sinusoidal_force"):
+            env["disturbances"]["forces"][key] = True
+        for key in ("use_torque_disturbance", "use_constant_torque", "use_sinusoidal_torque"):
+            env["disturbances"]["torques"][key] = True
+        env["water_current"]["use_water_current"] = True
+        env["water_current"]["flow_velocity"] = [0.3, -0.2, 0.0]
+        env["maxEpisodeLength"] = 30
     return cfg
 
 
@@ -380,8 +391,15 @@ def make_vecenv(torch, usv, world):
 # draw-site mapping into the kernel layouts (include/usv_hip.h RU_* / SU_*)
 # --------------------------------------------------------------------------
 RU = dict(MASS=0, COM=1, KIZ=4, KDRAG=5, THR=6, DRAG=8, SPAWN_R=20, SPAWN_TH=21, YAW=22, OBST=23,
-          RESAMPLE=55, VX=695, VY=696, GOAL=697)
-NU_RESET, NU_STEP = 699, 8
+          RESAMPLE=55, VX=695, VY=696, GOAL=697, FSIN=699, FCONST=704, TSIN=706, TCONST=709)
+NU_RESET, NU_STEP = 711, 8
+# draw sites of the disturbance generators (USV_disturbances.py line -> slot)
+DIST_SITES = {("generate_force", 342): RU["FSIN"], ("generate_force", 347): RU["FSIN"] + 1,
+              ("generate_force", 352): RU["FSIN"] + 2, ("generate_force", 357): RU["FSIN"] + 3,
+              ("generate_force", 362): RU["FSIN"] + 4, ("generate_force", 369): RU["FCONST"],
+              ("generate_force", 374): RU["FCONST"] + 1, ("generate_torque", 484): RU["TSIN"],
+              ("generate_torque", 489): RU["TSIN"] + 1, ("generate_torque", 494): RU["TSIN"] + 2,
+              ("generate_torque", 500): RU["TCONST"], ("generate_torque", 506): RU["TCONST"] + 1}
 
 
 def map_reset_draws(draws, k):
@@ -419,6 +437,8 @@ def map_reset_draws(draws, k):
             vel += 1
         elif fn == "get_goals":
             U[:, RU["GOAL"]:RU["GOAL"] + 2] = a.reshape(k, 2)
+        elif (fn, line) in DIST_SITES:
+            U[:, DIST_SITES[(fn, line)]] = a.reshape(k)
         else:
             raise RuntimeError(f"unmapped reset draw site {fn}:{line} ({fname})")
     return U
@@ -636,6 +656,13 @@ def gen_episode(torch, variant, n, steps, seed):
                                            tk._total_reward, pen.angular_vel_penalty,
                                            pen.angular_vel_variation_penalty, pen.energy_penalty,
                                            tk._danger_factor, tk.prev_potential], 1).numpy().astype(np.float32))
+            if variant == "C":
+                uf, td_ = usv.UF, usv.TD
+                data.setdefault("dist", []).append(torch.stack([
+                    uf.disturbance_forces_const[:, 0], uf.disturbance_forces_const[:, 1], uf._force_x_freq,
+                    uf._force_y_freq, uf._force_x_shift, uf._force_y_shift, uf._force_amp,
+                    td_.disturbance_torques_const[:, 2], td_._torque_freq, td_._torque_shift, td_._torque_amp],
+                    0).numpy().copy())
             ex = extras.get("episode", {})
             data["extras"].append(np.array([float(ex[k]) if k in ex else np.nan for k in STAT_NAMES], np.float32))
     out = {k: np.stack(v) for k, v in data.items()}
@@ -792,6 +819,7 @@ def main():
         "field": lambda: gen_field(torch),
         "episodeA": lambda: gen_episode(torch, "A", 16, 64, 1234),
         "episodeB": lambda: gen_episode(torch, "B", 12, 56, 99),
+        "episodeC": lambda: gen_episode(torch, "C", 12, 64, 77),
         "ppo": lambda: gen_ppo(torch),
     }
     for name, fn in jobs.items():

@@ -25,13 +25,14 @@ def _task(cfg_d, n):
     return USVVirtual(cfg_d, num_envs=n, device=DEV, seed=7)
 
 
-@pytest.mark.parametrize("variant", ["A", "B"])
+@pytest.mark.parametrize("variant", ["A", "B", "C"])
 def test_fixture_replay_on_gpu(golden, variant):
     d = golden(f"episode_{variant}.npz")
     cfg_d = json.loads(bytes(d["config_json"]).decode())
     T, n = d["obs"].shape[:2]
     task = _task(cfg_d, n)
     task.set_grid_lin(torch.tensor(d["grid_lin"]))
+    task.set_env_origins(torch.zeros(2, n))   # the fixtures' _env_pos (make_golden.build_usv)
     task.tgt[0] = torch.tensor(d["init_tgt"][:, 0], device=DEV)
     task.tgt[1] = torch.tensor(d["init_tgt"][:, 1], device=DEV)
     ru = 0
@@ -52,6 +53,8 @@ def test_fixture_replay_on_gpu(golden, variant):
         np.testing.assert_array_equal(dones.cpu().numpy(), d["reset"][t])
         if len(ids):
             np.testing.assert_allclose(task.extras_buf.cpu().numpy(), d["extras"][t], rtol=1e-5, atol=1e-6)
+        if "dist" in d:   # disturbance parameters drawn by the reset kernel (USV_disturbances.py:327-508)
+            np.testing.assert_allclose(task.dist.cpu().numpy(), d["dist"][t], rtol=1e-6, atol=1e-6)
 
 
 def _oracle_for(cfg, n, task_cfg):
@@ -78,6 +81,35 @@ def test_philox_mode_matches_oracle():
     # per-episode parameters drawn by the reset kernel
     np.testing.assert_allclose(task.params[0].cpu().numpy(), E.mass, rtol=1e-6)
     np.testing.assert_allclose(task.obst.cpu().numpy().reshape(16, 2, n), E.obst, rtol=1e-6, atol=1e-5)
+
+
+def test_philox_mode_disturbances_matches_oracle():
+    """Force / torque disturbances + water current, env origins on the reference's
+    fallback grid (USV_Virtual.py:1670-1696): kernels vs the oracle on Philox draws."""
+    task_cfg = load_yaml(TEST_YAML)
+    dist = task_cfg["env"]["disturbances"]
+    for key in ("use_force_disturbance", "use_constant_force", "use_sinusoidal_force"):
+        dist["forces"][key] = True
+    for key in ("use_torque_disturbance", "use_constant_torque", "use_sinusoidal_torque"):
+        dist["torques"][key] = True
+    task_cfg["env"]["water_current"] = {"use_water_current": True, "flow_velocity": [-0.2, 0.35, 0.0]}
+    task_cfg["env"]["maxEpisodeLength"] = 20
+    n, T = 1024, 30
+    task = _task(task_cfg, n)
+    E = _oracle_for(task.cfg, n, task_cfg)
+    E.set_env_origins(task.env_org.cpu().numpy())
+    assert float(task.env_org.max()) > 0
+    rng = np.random.default_rng(5)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        bias = task.current_action_bias()
+        obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
+        E.full_step(a, bias, t, seed=task.seed)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(task.dist.cpu().numpy(), E.dist, rtol=1e-6, atol=1e-6, err_msg=f"dist t={t}")
+        np.testing.assert_array_equal(dones.cpu().numpy(), E.reset_buf, err_msg=f"dones t={t}")
+        np.testing.assert_allclose(obs.cpu().numpy(), E.obs, rtol=1e-4, atol=1e-4, err_msg=f"obs t={t}")
+        np.testing.assert_allclose(rew.cpu().numpy(), E.rew, rtol=1e-3, atol=1e-3, err_msg=f"rew t={t}")
 
 
 def _run_field(task, ids, obst, tgt, lin=None):

@@ -115,12 +115,25 @@ def _replay(d, post_only):
             for k in ("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr"):
                 getattr(E, k)[:] = d[k][t]
         E.step_post(d["u_step"][t])
+        if "dist" in d:
+            # ForceDisturbance / TorqueDisturbance parameters drawn at reset (USV_disturbances.py:327-508)
+            np.testing.assert_allclose(E.dist, d["dist"][t], rtol=1e-6, atol=1e-6, err_msg=f"dist step {t}")
         out.append((E.obs.copy(), E.rew.copy(), E.reset_buf.copy(), E.mass.copy(), E.k_drag.copy(), E.thr_l.copy(),
                     E.thr_r.copy(), E.k_iz.copy(), E.obst.copy(), E.progress.copy(), E.goal_cnt.copy()))
     return out
 
 
-@pytest.mark.parametrize("variant", ["A", "B"])
+def test_episode_c_exercises_disturbances(golden):
+    """The disturbance fixture has every generator on and draws non-trivial parameters."""
+    d = golden("episode_C.npz")
+    cfg = build_usv_cfg(_cfg_from(d))
+    assert cfg.fdist_on and cfg.fconst_on and cfg.fsin_on and cfg.tdist_on and cfg.tconst_on and cfg.tsin_on
+    assert cfg.current_on and abs(cfg.flow_vel[0] - 0.3) < 1e-7
+    assert np.all(np.abs(d["dist"][-1]).sum(0) > 0)
+    assert (d["dist"][-1][7] < 0).any() and (d["dist"][-1][7] > 0).any()   # torque sign flip
+
+
+@pytest.mark.parametrize("variant", ["A", "B", "C"])
 def test_episode_post_physics(golden, variant):
     """obs / reward / done / DR / spawns given the reference's post-integration state."""
     d = golden(f"episode_{variant}.npz")
@@ -138,7 +151,7 @@ def test_episode_post_physics(golden, variant):
         np.testing.assert_array_equal(obst.transpose(2, 0, 1), d["obst"][t])
 
 
-@pytest.mark.parametrize("variant", ["A", "B"])
+@pytest.mark.parametrize("variant", ["A", "B", "C"])
 def test_episode_end_to_end(golden, variant):
     """Full replay incl. this build's integrator; the reference's potential-shaping
     term amplifies ~1e-7 state differences by 100, hence the reward tolerance."""
