@@ -58,7 +58,8 @@ extern "C" {
 #define RU_FCONST   704     /* :369-374 (r, theta) */
 #define RU_TSIN     706     /* TorqueDisturbance.generate_torque:484-494 (freq, shift, amp) */
 #define RU_TCONST   709     /* :500-506 (r, sign draw) */
-#define USV_NU_RESET 711
+#define RU_GOAL_H   711     /* GoToPoseTask.get_goals:248 heading / TrackXYOVelocityTask.get_goals:193 angular velocity */
+#define USV_NU_RESET 712
 /* Layout of the uniform draws of one env step (device [n][USV_NU_STEP] when
  * injected; otherwise Philox(ctr={env, step_lo, step_hi, i/4})[i%4]).
  * Only the draws of the LAST update_state of the step reach obs/reward
@@ -176,7 +177,28 @@ typedef struct usv_cfg {
   float tconst_min, tconst_max, tsin_min, tsin_max, tfreq_min, tfreq_max, tshift_min, tshift_max;
   int   current_on;
   float flow_vel[2];        /* world-frame water velocity x, y */
+  /* ---- task selection (USV_task_factory.py:58-64) and the GoToPose /
+   * TrackXYOVelocity parameters (USV_task_parameters.py:74-148,
+   * USV_task_rewards.py:160-393).  Index 0 = position / linear velocity term,
+   * 1 = heading / angular velocity term. ---- */
+  int   task_kind;          /* USV_TASK_* */
+  int   tk_mode[2];         /* 0 linear, 1 square, 2 exponential */
+  float tk_coeff[2];        /* *_exponential_reward_coeff */
+  float tk_scale[2];        /* position_scale/heading_scale, linear_scale/angular_scale */
+  float tk_tol[2];          /* TrackXYO lin_vel_tolerance, ang_vel_tolerance */
+  float tk_goal_rand[2];    /* TrackXYO goal_random_linear_velocity, goal_random_angular_velocity */
+  float sig_gain;           /* GoToPoseReward.sig_gain */
 } usv_cfg_t;
+
+#define USV_TASK_CAPTURE_XY   0
+#define USV_TASK_GO_TO_POSE   1
+#define USV_TASK_TRACK_XYO    2
+/* per-env scratch rows of the two-phase TrackXYOVelocity step (usv_bufs_t.task_scratch) */
+#define USV_TS_LIN_REW 0
+#define USV_TS_PEN     1
+#define USV_TS_LIN_OK  2
+#define USV_TS_POS_KILL 3
+#define USV_TS_ROWS    4
 
 /* per-env disturbance parameters (rows of usv_bufs_t.dist, drawn at reset) */
 enum usv_dist_row {
@@ -223,6 +245,9 @@ typedef struct usv_bufs {
   const float *grid_lin;           /* [150] cell centres of the field grid */
   float   *dist;                   /* [USV_NDIST][n] disturbance parameters; NULL when no disturbance is on */
   const float *env_org;            /* [2][n] world x, y of each env's origin (RLTask._env_pos); NULL = 0 */
+  float   *tgt_h;                  /* [n] GoToPose target heading / TrackXYO target angular velocity (tgt_x/y:
+                                      target position / target linear velocity); NULL for CaptureXY */
+  float   *task_scratch;           /* TrackXYO: [USV_TS_ROWS][n] + [ceil(n/256)] partial sums; else NULL */
   /* device step clock (nullable): [0] next step index, [1] next bias-call count,
    * [2] current step, [3] current bias-call count.  When set, usv_reset advances
    * it and the step / bias arguments of usv_reset / usv_env_step are ignored, so

@@ -236,16 +236,27 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         }
         if (c.couple_kiz) b.k_iz[e] = c.kiz_min + r * (float)((double)c.kiz_max - (double)c.kiz_min);
       }
-      // ---- CaptureXYTask.get_spawns (static_obs.py:936-1060), previous-episode target ----
-      const float r = U(RU_SPAWN_R) * (c.spawn_rmax - c.spawn_rmin) + c.spawn_rmin;
-      const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
-      sx = r * cosf(th);
-      sy = r * sinf(th);
-      const float yaw0 = U(RU_YAW) * USV_PI_F;
+      // ---- task.get_spawns, previous-episode target (get_goals runs later, USV_Virtual.py:1618) ----
       tx = b.tgt_x[e];
       ty = b.tgt_y[e];
-      b.field_old_tgt[e] = tx;
-      b.field_old_tgt[n + e] = ty;
+      const float yaw0 = U(RU_YAW) * USV_PI_F;
+      if (c.task_kind == USV_TASK_CAPTURE_XY) {   // CaptureXYTask.get_spawns (static_obs.py:936-1060)
+        const float r = U(RU_SPAWN_R) * (c.spawn_rmax - c.spawn_rmin) + c.spawn_rmin;
+        const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
+        sx = r * cosf(th);
+        sy = r * sinf(th);
+        b.field_old_tgt[e] = tx;
+        b.field_old_tgt[n + e] = ty;
+      } else if (c.task_kind == USV_TASK_GO_TO_POSE) {   // GoToPoseTask.get_spawns (USV_go_to_pose.py:256-319)
+        const float r = U(RU_SPAWN_R) * (float)((double)c.spawn_rmax - (double)c.spawn_rmin) + c.spawn_rmin;
+        const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
+        sx = r * cosf(th) + tx;
+        sy = r * sinf(th) + ty;
+        b.prev_dist[e] = 0.f;                            // GoToPoseTask.reset: prev_position_dist = 0 (:227)
+      } else {                                           // TrackXYOVelocityTask.get_spawns (:203-219): env origin
+        sx = 0.f;
+        sy = 0.f;
+      }
       // ---- pose / velocities / bookkeeping (USV_Virtual.py:1541-1579) ----
       b.px[e] = sx;
       b.py[e] = sy;
@@ -257,10 +268,18 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
       b.progress[e] = 0;
       b.prev_cmd[e] = 0.f;
       b.prev_cmd[n + e] = 0.f;
-      // ---- set_targets -> get_goals (static_obs.py:913-930) ----
-      const float g = c.goal_random_position;
-      b.tgt_x[e] = U(RU_GOAL) * g * 2.0f - g;
-      b.tgt_y[e] = U(RU_GOAL + 1) * g * 2.0f - g;
+      // ---- set_targets -> task.get_goals ----
+      if (c.task_kind != USV_TASK_TRACK_XYO) {   // static_obs.py:913-930, USV_go_to_pose.py:229-254
+        const float g = c.goal_random_position;
+        b.tgt_x[e] = U(RU_GOAL) * g * 2.0f - g;
+        b.tgt_y[e] = U(RU_GOAL + 1) * g * 2.0f - g;
+        if (c.task_kind == USV_TASK_GO_TO_POSE) b.tgt_h[e] = U(RU_GOAL_H) * USV_PI_F * 2.0f;
+      } else {                                   // USV_track_xyo_velocity.py:178-199: target velocities
+        const float gl = c.tk_goal_rand[0], ga = c.tk_goal_rand[1];
+        b.tgt_x[e] = U(RU_GOAL) * gl * 2.0f - gl;
+        b.tgt_y[e] = U(RU_GOAL + 1) * gl * 2.0f - gl;
+        b.tgt_h[e] = U(RU_GOAL_H) * ga * 2.0f - ga;
+      }
     }
     (void)sx; (void)sy; (void)tx; (void)ty;
   }
@@ -402,6 +421,43 @@ struct StepK {
   int enc_ok[3];
   float inv_exp_coeff;
 };
+
+// privileged observation tail (USV_Virtual.py:840-976): raw / centered / minmax encoders
+template <class Put>
+__device__ __forceinline__ void write_priv_tail(const usv_cfg_t &c, const StepK &K, float m, float comx, float comy,
+                                                float comz, float k_drag, float thr_l, float thr_r, float k_iz,
+                                                Put put) {
+  const int pt = USV_NOBS - c.priv_dim;
+  if (c.masscom_base) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (q < c.priv_dim) put(pt + q, K.priv_base[q]);
+    return;
+  }
+  put(pt, c.mass_relative ? div_rn(m - c.base_mass, K.mass_den, K.inv_mass_den) : m);
+  put(pt + 1, c.com_scaled ? div_rn(comx, K.com_div[0], K.inv_com_div[0]) : comx);
+  put(pt + 2, c.com_scaled ? div_rn(comy, K.com_div[1], K.inv_com_div[1]) : comy);
+  put(pt + 3, c.com_scaled ? div_rn(comz, K.com_div[2], K.inv_com_div[2]) : comz);
+  if (c.priv_dim == 8) {
+    float v[4] = {k_drag, thr_l, thr_r, k_iz};
+    const bool on[4] = {c.priv_drag_on != 0, c.priv_thr_on != 0, c.priv_thr_on != 0, c.priv_kiz_on != 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = q == 0 ? 0 : (q == 3 ? 2 : 1);
+      if (c.priv_mode == 1) {          // enc_centered
+        v[q] = clampt(div_rn(v[q] - c.priv_nominal, K.enc_r[j], K.inv_enc_r[j]), -1.f, 1.f);
+      } else if (c.priv_mode == 2) {   // enc_minmax
+        if (!on[q] || !K.enc_ok[j]) {
+          v[q] = 0.f;
+        } else {
+          const float z = div_rn(v[q] - K.enc_lo[j], K.enc_r[j], K.inv_enc_r[j]);
+          v[q] = clampt(2.0f * z - 1.0f, -1.f, 1.f);
+        }
+      }
+      put(pt + 4 + q, v[q]);
+    }
+  }
+}
 
 __device__ __forceinline__ float bld(__amdgpu_buffer_rsrc_t R, uint32_t so, uint32_t vo) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(R, vo, so, 0));
@@ -724,38 +780,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     bst(R, w.prev_cmd, vs, prev_cmd0);
     bst(R, w.prev_cmd + w.n4, vs, prev_cmd1);
     // ---- privileged tail (USV_Virtual.py:840-976) ----
-    {
-      const int pt = USV_NOBS - c.priv_dim;
-      if (c.masscom_base) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (q < c.priv_dim) put(pt + q, K.priv_base[q]);
-      } else {
-        put(pt, c.mass_relative ? div_rn(m - c.base_mass, K.mass_den, K.inv_mass_den) : m);
-        put(pt + 1, c.com_scaled ? div_rn(comx, K.com_div[0], K.inv_com_div[0]) : comx);
-        put(pt + 2, c.com_scaled ? div_rn(comy, K.com_div[1], K.inv_com_div[1]) : comy);
-        put(pt + 3, c.com_scaled ? div_rn(comz, K.com_div[2], K.inv_com_div[2]) : comz);
-        if (c.priv_dim == 8) {
-          float v[4] = {k_drag, thr_l, thr_r, k_iz};
-          const bool on[4] = {c.priv_drag_on != 0, c.priv_thr_on != 0, c.priv_thr_on != 0, c.priv_kiz_on != 0};
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int j = q == 0 ? 0 : (q == 3 ? 2 : 1);
-            if (c.priv_mode == 1) {          // enc_centered
-              v[q] = clampt(div_rn(v[q] - c.priv_nominal, K.enc_r[j], K.inv_enc_r[j]), -1.f, 1.f);
-            } else if (c.priv_mode == 2) {   // enc_minmax
-              if (!on[q] || !K.enc_ok[j]) {
-                v[q] = 0.f;
-              } else {
-                const float z = div_rn(v[q] - K.enc_lo[j], K.enc_r[j], K.inv_enc_r[j]);
-                v[q] = clampt(2.0f * z - 1.0f, -1.f, 1.f);
-              }
-            }
-            put(pt + 4 + q, v[q]);
-          }
-        }
-      }
-    }
+    write_priv_tail(c, K, m, comx, comy, comz, k_drag, thr_l, thr_r, k_iz, put);
     // ---- compute_reward (static_obs.py:335-657): the potential-independent terms first ----
     constexpr float kGv = (0.15f - 0.02f) + 1e-6f, kGd = 0.01f + 1e-6f;
     constexpr float kSf = (0.60f - 0.15f) + 1e-6f, kSp = 0.8f + 1e-6f, kAn = 0.2f;
@@ -861,6 +886,354 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   // promoted to the POT/PEN/REW_VALID flags by the next usv_reset, so the flags never change
   // while a step kernel that reads them runs ----
   if (blockIdx.x == 0 && tid == 0) b.ctl[USV_CTL_STEPPED] = 1;
+}
+
+// ------------------------------------------------------------------------
+// GoToPose / TrackXYOVelocity control step.  Same physics, action
+// mapping, noise, penalties and privileged tail as the CaptureXY step; the task
+// part follows GoToPoseTask (tasks/USV/USV_go_to_pose.py:89-209) and
+// TrackXYOVelocityTask (USV_track_xyo_velocity.py:75-166) with their rewards
+// (USV_task_rewards.py:160-249, 328-393).  Glue where the reference cannot run
+// these tasks: the task_data block is the Core layout's 20 columns
+// (unwritten columns 0), update_kills(step) is the task's own, the reward is
+// task.compute_reward(current_state, actions) + penalties as calculate_metrics
+// (USV_Virtual.py:1628-1652) does for every task.
+// TrackXYOVelocity's angular error is reduced over ALL envs
+// (torch.square(err).sum(-1) of a 1-D tensor, :121-123), so its step is two
+// launches: this kernel writes per-block partial sums, k_track_finish completes.
+// ------------------------------------------------------------------------
+__device__ __forceinline__ float task_term(int mode, float x, float coeff) {
+  if (mode == 0) return 1.0f / (1.0f + x);
+  if (mode == 1) return 1.0f / (1.0f + x * x);
+  return expf(-x / coeff);
+}
+
+template <int kKind, bool kStats, bool kInj>
+__global__ __launch_bounds__(kBlock) void k_env_step_task(usv_cfg_t c, usv_bufs_t b, StepK K,
+                                                          const float *__restrict__ actions,
+                                                          const float *__restrict__ lut, float bias, uint64_t seed,
+                                                          uint64_t step, const float *__restrict__ inj) {
+  __shared__ float sobs[kBlock * USV_NOBS];
+  __shared__ float sred[kBlock / 64];
+  const int n = b.n;
+  const int tid = threadIdx.x;
+  const int e = blockIdx.x * kBlock + tid;
+  const int ec = min(e, n - 1);
+  const bool mine = e < n;
+  const size_t nn = (size_t)n;
+  step = step_of(b, step);
+  bias = bias_of(c, b, bias);
+  const bool pen_valid = b.ctl[USV_CTL_PEN_VALID] != 0;
+  float *obs = sobs + tid * USV_NOBS;
+  const float clip = c.clip_obs;
+  auto put = [&](int q, float v) { obs[q] = clampt(v, -clip, clip); };
+  // ---- loads ----
+  const float2 a2 = reinterpret_cast<const float2 *>(actions)[ec];
+  const bool was_reset = b.just_reset[ec] != 0;
+  float px = b.px[ec], py = b.py[ec], yaw = b.yaw[ec], vx = b.vx[ec], vy = b.vy[ec], wz = b.wz[ec];
+  float fl = b.fl[ec], fr = b.fr[ec];
+  const float m = b.mass[ec], k_iz = b.k_iz[ec], k_drag = b.k_drag[ec];
+  const float thr_l = b.thr_l[ec], thr_r = b.thr_r[ec];
+  const float comx = b.com_x[ec], comy = b.com_y[ec], comz = b.com_z[ec];
+  float lin0 = c.lin_damp[0], lin1 = c.lin_damp[1], lin2 = c.lin_damp[2];
+  float qd0 = c.quad_damp[0], qd1 = c.quad_damp[1], qd2 = c.quad_damp[2];
+  if (b.lin_damp) {
+    lin0 = b.lin_damp[ec]; lin1 = b.lin_damp[nn + ec]; lin2 = b.lin_damp[2 * nn + ec];
+    qd0 = b.quad_damp[ec]; qd1 = b.quad_damp[nn + ec]; qd2 = b.quad_damp[2 * nn + ec];
+  }
+  float dp[USV_NDIST], orgx = 0.f, orgy = 0.f;
+  const bool has_dist = b.dist != nullptr;
+  if (has_dist) {
+#pragma unroll
+    for (int q = 0; q < USV_NDIST; ++q) dp[q] = b.dist[q * nn + ec];
+    if (b.env_org) { orgx = b.env_org[ec]; orgy = b.env_org[nn + ec]; }
+  }
+  const int progress0 = b.progress[ec], goal_cnt0 = b.goal_cnt[ec];
+  const float tgx = b.tgt_x[ec], tgy = b.tgt_y[ec], tgh = b.tgt_h[ec];
+  const float prev_pd = b.prev_dist[ec], prev_wz_mem = b.prev_wz[ec];
+  float sums[USV_NSTAT];
+  if (kStats) {
+#pragma unroll
+    for (int q = 0; q < USV_NSTAT; ++q) sums[q] = b.stats[q * nn + ec];
+  }
+  float u[USV_NU_STEP];
+  if (kInj) {
+#pragma unroll
+    for (int i = 0; i < USV_NU_STEP; ++i) u[i] = inj[(size_t)ec * USV_NU_STEP + i];
+  } else {
+    philox_u4(seed, (uint32_t)e, step, 0u, u);
+    if (c.pos_noise_on || c.act_noise_on) philox_u4(seed, (uint32_t)e, step, 1u, u + 4);
+    else u[4] = u[5] = u[6] = u[7] = 0.f;
+  }
+  // ---- VecEnvRLGames.step clamp + pre_physics_step (USV_Virtual.py:1050-1099) ----
+  const float cmd0 = clampt(a2.x, -c.clip_actions, c.clip_actions);
+  const float cmd1 = clampt(a2.y, -c.clip_actions, c.clip_actions);
+  const float prev_cmd0 = was_reset ? 0.f : cmd0, prev_cmd1 = was_reset ? 0.f : cmd1;
+  float t0 = cmd0, t1 = cmd1;
+  if (bias != 0.f) { t0 = t0 + bias; t1 = t1 + bias; }
+  if (c.act_noise_on) {
+    t0 = t0 + (u[SU_ACT] * K.act_rng + c.act_noise_min);
+    t1 = t1 + (u[SU_ACT + 1] * K.act_rng + c.act_noise_min);
+  }
+  t0 = clampt(t0, -1.f, 1.f);
+  t1 = clampt(t1, -1.f, 1.f);
+  float unit0 = c.affine_thrust ? 0.5f * (t0 + 1.0f) : clampt(t0, 0.f, 1.f);
+  float unit1 = c.affine_thrust ? 0.5f * (t1 + 1.0f) : clampt(t1, 0.f, 1.f);
+  unit0 = clampt(unit0, 0.f, 1.f);
+  unit1 = clampt(unit1, 0.f, 1.f);
+  const float uu0 = was_reset ? 0.f : unit0, uu1 = was_reset ? 0.f : unit1;
+  int i0 = (int)rintf(((uu0 + 1.0f) / 2.0f) * (float)(USV_LUT_N - 1));
+  int i1 = (int)rintf(((uu1 + 1.0f) / 2.0f) * (float)(USV_LUT_N - 1));
+  i0 = min(max(i0, 0), USV_LUT_N - 1);
+  i1 = min(max(i1, 0), USV_LUT_N - 1);
+  float tgt0 = lut[i0], tgt1 = lut[USV_LUT_N + i1];
+  if (c.use_thr_mult) { tgt0 = tgt0 * thr_l; tgt1 = tgt1 * thr_r; }
+  // ---- substeps: the CaptureXY step's integrator (thruster lag, planar forces, semi-implicit Euler) ----
+  const float izz = c.izz0 * k_iz;
+  const float inv_m = 1.0f / m, inv_izz = 1.0f / izz;
+  const float kd = c.use_drag_scale ? k_drag : 1.0f;
+  const float al = c.thr_alpha, oma = 1.0f - c.thr_alpha;
+  const float dt = c.dt;
+  const float arm_l = -(c.thr_y - comy), arm_r = c.thr_y + comy;
+  for (int s = 0; s < c.substeps; ++s) {
+    fl = fl * al + oma * tgt0;
+    fr = fr * al + oma * tgt1;
+    float sy_, cy_;
+    sincosf(yaw, &sy_, &cy_);
+    float ub = cy_ * vx + sy_ * vy;
+    float vb = -sy_ * vx + cy_ * vy;
+    const float rb = wz;
+    float dfx = 0.f, dfy = 0.f, dtz = 0.f;
+    if (has_dist) {
+      if (c.current_on) {
+        ub = ub - (cy_ * c.flow_vel[0] + sy_ * c.flow_vel[1]);
+        vb = vb - (-sy_ * c.flow_vel[0] + cy_ * c.flow_vel[1]);
+      }
+      const float wx = px + orgx, wy = py + orgy;
+      dfx = dp[DI_FCX];
+      dfy = dp[DI_FCY];
+      dtz = dp[DI_TC];
+      if (c.fsin_on) {
+        dfx = dfx + sinf(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
+        dfy = dfy + sinf(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
+      }
+      if (c.tsin_on) dtz = dtz + sinf((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
+    }
+    float D0 = lin0 + qd0 * fabsf(ub), D1 = lin1 + qd1 * fabsf(vb), D2 = lin2 + qd2 * fabsf(rb);
+    D0 = D0 * c.scaling_damping; D1 = D1 * c.scaling_damping; D2 = D2 * c.scaling_damping;
+    if (c.use_drag_scale) { D0 = D0 * kd; D1 = D1 * kd; D2 = D2 * kd; }
+    const float X = has_dist ? fl + fr + (dfx + (-D0 * ub)) : fl + fr + (-D0 * ub);
+    const float Y = has_dist ? dfy + (-D1 * vb) : -D1 * vb;
+    const float N = has_dist ? arm_l * fl + arm_r * fr + (dtz + (-D2 * rb)) : arm_l * fl + arm_r * fr + (-D2 * rb);
+    const float ax = div_rn(cy_ * X - sy_ * Y, m, inv_m);
+    const float ay = div_rn(sy_ * X + cy_ * Y, m, inv_m);
+    const float aw = div_rn(N, izz, inv_izz);
+    vx = vx + ax * dt;
+    vy = vy + ay * dt;
+    wz = wz + aw * dt;
+    px = px + vx * dt;
+    py = py + vy * dt;
+    float yw = yaw + wz * dt;
+    if (yw > USV_PI_F) yw -= USV_2PI_F;
+    else if (yw <= -USV_PI_F) yw += USV_2PI_F;
+    yaw = yw;
+  }
+  if (mine) {
+    b.px[e] = px; b.py[e] = py; b.yaw[e] = yaw; b.vx[e] = vx; b.vy[e] = vy; b.wz[e] = wz;
+    b.fl[e] = fl; b.fr[e] = fr;
+  }
+  // ---- post_physics_step: progress, update_state noise (USV_Virtual.py:771-813) ----
+  const int progress = progress0 + 1;
+  float pxn = px, pyn = py;
+  if (c.pos_noise_on) {
+    pxn = pxn + (u[SU_PX] * K.pos_rng + c.pos_noise_min);
+    pyn = pyn + (u[SU_PX + 1] * K.pos_rng + c.pos_noise_min);
+  }
+  float vxn = vx, vyn = vy, wzn = wz;
+  if (c.vel_noise_on) {
+    vxn = vxn + (u[SU_VX] * K.vel_rng + c.vel_noise_min);
+    vyn = vyn + (u[SU_VY] * K.vel_rng + c.vel_noise_min);
+    wzn = wzn + (u[SU_WZ] * K.vel_rng + c.vel_noise_min);
+  }
+  float yawn = yaw;
+  if (c.head_noise_on) yawn = yawn + (u[SU_HEAD] * K.head_rng + c.head_noise_min);
+  float hs, hc;
+  sincosf(yawn, &hs, &hc);
+  // ---- Core.update_observation_tensor (USV_core.py:55-121) ----
+  if (c.obs_local) {
+    put(0, hc * vxn + hs * vyn);
+    put(1, -hs * vxn + hc * vyn);
+  } else {
+    put(0, vxn);
+    put(1, vyn);
+  }
+  put(2, wzn);
+#pragma unroll
+  for (int q = 3; q < USV_NOBS - 10; ++q) obs[q] = 0.f;   // task_data columns no task writes
+  const int pa = USV_NOBS - c.priv_dim - 2;
+  for (int q = pa + 2; q < USV_NOBS - c.priv_dim; ++q) obs[q] = 0.f;
+  if (c.priv_dim == 4) { obs[23] = 0.f; obs[24] = 0.f; obs[25] = 0.f; obs[26] = 0.f; }
+  put(pa, prev_cmd0);
+  put(pa + 1, prev_cmd1);
+  write_priv_tail(c, K, m, comx, comy, comz, k_drag, thr_l, thr_r, k_iz, put);
+  // ---- Penalties.compute_penalty (USV_task_rewards.py:440-523) ----
+  const float pact0 = c.pen_use_u ? unit0 : cmd0, pact1 = c.pen_use_u ? unit1 : cmd1;
+  float p_lin = 0.f, p_ang = 0.f, p_angv = 0.f, p_en = 0.f;
+  if (c.pen_lin_kind == PEN_NORM) p_lin = -tnorm2(vxn, vyn) * c.pen_lin_k + c.pen_lin_c;
+  if (c.pen_ang_kind) p_ang = pen_scalar(c.pen_ang_kind, c.pen_ang_k, c.pen_ang_x0, c.pen_ang_c, wzn);
+  if (c.pen_angv_kind) {
+    const float prev_w = pen_valid ? prev_wz_mem : wzn;
+    p_angv = pen_scalar(c.pen_angv_kind, c.pen_angv_k, c.pen_angv_x0, c.pen_angv_c, wzn - prev_w);
+  }
+  if (c.pen_en_kind == PEN_SUM) p_en = -(pact0 + pact1) * c.pen_en_k + c.pen_en_c;
+  else if (c.pen_en_kind == PEN_SUMSQ) p_en = -(pact0 * pact0 + pact1 * pact1) * c.pen_en_k + c.pen_en_c;
+  const float pen_sum = ((p_lin + p_ang) + p_angv) + p_en;
+  const int tout = progress >= c.max_episode_length - 1;
+  float t_add[4];
+  float overall = 0.f;
+  int goal_cnt = goal_cnt0, die = 0;
+  if (kKind == USV_TASK_GO_TO_POSE) {
+    // GoToPoseTask.get_state_observations (:89-130)
+    const float ex = tgx - pxn, ey = tgy - pyn;
+    const float theta = atan2f(hs, hc);
+    const float beta = atan2f(ey, ex);
+    const float alpha = fmodf((beta - theta) + USV_PI_F, USV_2PI_F) - USV_PI_F;
+    const float hraw = fmodf((tgh - theta) + USV_PI_F, USV_2PI_F) - USV_PI_F;
+    const float herr = atan2f(sinf(hraw), cosf(hraw));
+    float sa, ca, sh, ch;
+    sincosf(alpha, &sa, &ca);
+    sincosf(herr, &sh, &ch);
+    put(3, ca);
+    put(4, sa);
+    put(5, tnorm2(ex, ey));
+    put(6, ch);
+    put(7, sh);
+    // compute_reward (:134-181)
+    const float pdist = sqrtf(ex * ex + ey * ey);
+    const float hdist = fabsf(herr);
+    const float prog_r = 2.0f * clampt(prev_pd - pdist, -2.0f, 2.0f);
+    if (mine) b.prev_dist[e] = pdist;
+    const float speed = tnorm2(vxn, vyn);
+    const int gir = (pdist < c.position_tolerance) & (speed < 0.1f);
+    goal_cnt = goal_cnt0 * gir + gir;
+    // GoToPoseReward.compute_reward (USV_task_rewards.py:190-233)
+    const float hw = 1.0f - 1.0f / (1.0f + expf(-c.sig_gain * (pdist - 2.0f)));
+    const float pos_r = c.tk_scale[0] * task_term(c.tk_mode[0], pdist, c.tk_coeff[0]);
+    const float head_r = hw * c.tk_scale[1] * task_term(c.tk_mode[1], hdist, c.tk_coeff[1]);
+    const float act_pen = -0.05f * (fabsf(cmd0) + fabsf(cmd1));
+    overall = (((pos_r + head_r) + prog_r) + 2.0f * (float)gir) + act_pen;
+    // update_kills (:183-209): kill_dist / goal counter
+    die = (pdist > c.kill_dist) || (goal_cnt >= c.kill_after_n);
+    t_add[0] = pos_r; t_add[1] = head_r; t_add[2] = pdist; t_add[3] = speed;   // update_statistics (:211-219)
+  } else {
+    // TrackXYOVelocityTask.get_state_observations (:75-101)
+    const float lex = tgx - vxn, ley = tgy - vyn, aerr = tgh - wzn;
+    put(3, lex);
+    put(4, ley);
+    put(5, aerr);
+    // compute_reward (:103-141): the angular part waits for the all-env sum
+    const float pos_d = sqrtf(pxn * pxn + pyn * pyn);
+    const float lin_d = sqrtf(lex * lex + ley * ley);
+    const float lin_r = task_term(c.tk_mode[0], lin_d, c.tk_coeff[0]) * c.tk_scale[0];
+    float part = mine ? aerr * aerr : 0.f;
+    part = wave_sum(part);
+    if ((tid & 63) == 0) sred[tid >> 6] = part;
+    float *ts = b.task_scratch;
+    if (mine) {
+      ts[USV_TS_LIN_REW * nn + e] = lin_r;
+      ts[USV_TS_PEN * nn + e] = pen_sum;
+      ts[USV_TS_LIN_OK * nn + e] = (float)(lin_d < c.tk_tol[0]);
+      ts[USV_TS_POS_KILL * nn + e] = (float)(pos_d > c.kill_dist);
+    }
+    t_add[0] = lin_r; t_add[1] = lin_d; t_add[2] = 0.f; t_add[3] = 0.f;
+  }
+  if (mine) {
+    b.progress[e] = progress;
+    b.prev_cmd[e] = prev_cmd0;
+    b.prev_cmd[nn + e] = prev_cmd1;
+    b.prev_wz[e] = wzn;
+    b.just_reset[e] = 0;
+    if (kKind == USV_TASK_GO_TO_POSE) {
+      const float rew = overall + pen_sum;
+      const int rb = c.fixed_horizon_eval ? tout : (tout ? 1 : die);
+      b.goal_cnt[e] = goal_cnt;
+      b.rew[e] = rew;
+      b.reset_buf[e] = rb;
+      b.dones[e] = rb;
+    }
+    if (kStats) {
+      const float vn = tnorm2(vxn, vyn);
+      float add[USV_NSTAT];
+#pragma unroll
+      for (int q = 0; q < USV_NSTAT; ++q) add[q] = 0.f;
+      add[0] = t_add[0]; add[1] = t_add[1]; add[2] = t_add[2]; add[3] = t_add[3];
+      add[ST_ANGULAR_VEL_PENALTY] = p_ang;
+      add[ST_ANGULAR_VEL_VARIATION_PENALTY] = p_angv;
+      add[ST_ENERGY_PENALTY] = p_en;
+      add[ST_NORMED_LINEAR_VEL] = vn;
+      add[ST_NORMED_ANGULAR_VEL] = fabsf(wzn);
+      add[ST_CMD_NEG_RATE] = ((float)(t0 < 0.f) + (float)(t1 < 0.f)) / 2.0f;
+      add[ST_U_MEAN] = (unit0 + unit1) / 2.0f;
+      add[ST_U_LOW_RATE] = ((float)(unit0 < 0.05f) + (float)(unit1 < 0.05f)) / 2.0f;
+      add[ST_U_SUM] = unit0 + unit1;
+#pragma unroll
+      for (int q = 0; q < USV_NSTAT; ++q)
+        if (q != ST_SUCCESS && q != ST_COLLISION && (kKind == USV_TASK_GO_TO_POSE || (q != 2 && q != 3)))
+          b.stats[q * nn + e] = sums[q] + add[q];
+    }
+  }
+  __syncthreads();
+  if (kKind == USV_TASK_TRACK_XYO && tid == 0) {
+    float sblk = 0.f;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) sblk += sred[w];
+    b.task_scratch[USV_TS_ROWS * nn + blockIdx.x] = sblk;
+  }
+  // ---- coalesced obs store ----
+  const int row0 = blockIdx.x * kBlock;
+  const int rows = min(kBlock, n - row0);
+  float *ob = b.obs + (size_t)row0 * USV_NOBS;
+  for (int i = tid; i < rows * USV_NOBS; i += kBlock) ob[i] = sobs[i];
+  if (blockIdx.x == 0 && tid == 0) b.ctl[USV_CTL_STEPPED] = 1;
+}
+
+// TrackXYOVelocity, phase 2: angular velocity distance over all envs, then the
+// angular reward, goal counter, kills and dones of every env (:103-166)
+template <bool kStats>
+__global__ __launch_bounds__(kBlock) void k_track_finish(usv_cfg_t c, usv_bufs_t b, int nblk) {
+  __shared__ float sred[kBlock];
+  const int n = b.n;
+  const size_t nn = (size_t)n;
+  const int tid = threadIdx.x;
+  const float *part = b.task_scratch + USV_TS_ROWS * nn;
+  float acc = 0.f;
+  for (int i = tid; i < nblk; i += kBlock) acc += part[i];   // fixed order: every block gets the same sum
+  sred[tid] = acc;
+  __syncthreads();
+  for (int w = kBlock / 2; w > 0; w >>= 1) {
+    if (tid < w) sred[tid] += sred[tid + w];
+    __syncthreads();
+  }
+  const float ang_d = sqrtf(sred[0]);
+  const int e = blockIdx.x * kBlock + tid;
+  if (e >= n) return;
+  const float *ts = b.task_scratch;
+  const int ang_ok = ang_d < c.tk_tol[1];
+  const int gir = (int)ts[USV_TS_LIN_OK * nn + e] * ang_ok;
+  const int goal_cnt = b.goal_cnt[e] * gir + gir;
+  const float ang_r = task_term(c.tk_mode[1], ang_d, c.tk_coeff[1]) * c.tk_scale[1];
+  const float rew = (ts[USV_TS_LIN_REW * nn + e] + ang_r) + ts[USV_TS_PEN * nn + e];
+  const int die = (ts[USV_TS_POS_KILL * nn + e] != 0.f) || (goal_cnt > c.kill_after_n);
+  const int tout = b.progress[e] >= c.max_episode_length - 1;
+  const int rb = c.fixed_horizon_eval ? tout : (tout ? 1 : die);
+  b.goal_cnt[e] = goal_cnt;
+  b.rew[e] = rew;
+  b.reset_buf[e] = rb;
+  b.dones[e] = rb;
+  if (kStats) {
+    b.stats[2 * nn + e] += ang_r;
+    b.stats[3 * nn + e] += ang_d;
+  }
 }
 
 // planar forces only (parity with Hydrodynamics.ComputeHydrodynamicsEffects)
@@ -1040,6 +1413,34 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
                       void *stream) {
   if (!cfg || !b || !actions || !lut_dev || b->n <= 0 || part < 0 || part > 2) return 1;
   if (cfg->priv_dim != 4 && cfg->priv_dim != 8) return 3;
+  if (cfg->task_kind != USV_TASK_CAPTURE_XY) {
+    // GoToPose / TrackXYOVelocity: no potential field, so no split step
+    if (part != 0 || !b->tgt_h) return 1;
+    if (step_has_dist(*cfg) && !b->dist) return 4;
+    if (cfg->task_kind == USV_TASK_TRACK_XYO && !b->task_scratch) return 1;
+    const StepK k = step_constants(*cfg);
+    const int grid = (b->n + kBlock - 1) / kBlock;
+    hipStream_t s = (hipStream_t)stream;
+    const bool st = cfg->stats_on != 0, ij = u_inject != nullptr;
+    if (cfg->task_kind == USV_TASK_GO_TO_POSE) {
+      auto kern = st ? (ij ? k_env_step_task<USV_TASK_GO_TO_POSE, true, true> : k_env_step_task<USV_TASK_GO_TO_POSE, true, false>)
+                     : (ij ? k_env_step_task<USV_TASK_GO_TO_POSE, false, true> : k_env_step_task<USV_TASK_GO_TO_POSE, false, false>);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, k, actions, lut_dev, action_bias, seed, step,
+                         u_inject);
+    } else if (cfg->task_kind == USV_TASK_TRACK_XYO) {
+      auto kern = st ? (ij ? k_env_step_task<USV_TASK_TRACK_XYO, true, true> : k_env_step_task<USV_TASK_TRACK_XYO, true, false>)
+                     : (ij ? k_env_step_task<USV_TASK_TRACK_XYO, false, true> : k_env_step_task<USV_TASK_TRACK_XYO, false, false>);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, k, actions, lut_dev, action_bias, seed, step,
+                         u_inject);
+      USV_CHECK_LAUNCH();
+      hipLaunchKernelGGL(st ? k_track_finish<true> : k_track_finish<false>, dim3(grid), dim3(kBlock), 0, s, *cfg, *b,
+                         grid);
+    } else {
+      return 1;
+    }
+    USV_CHECK_LAUNCH();
+    return 0;
+  }
   StepWin w{};
   const char *wbase = nullptr;
   const int rc = step_window(*cfg, *b, &wbase, &w);

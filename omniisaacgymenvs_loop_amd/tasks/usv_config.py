@@ -233,10 +233,12 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     c.priv_kiz_on = int(bool(inertia.get("use_yaw_inertia_randomization", False)) or bool(c.couple_kiz))
 
     # ---- task / reward ----
+    name = env["task_parameters"].get("name", "CaptureXY")
+    if name not in TASK_KINDS:
+        raise ValueError(f"task {name!r}: this kernel set implements {sorted(TASK_KINDS)}")
+    c.task_kind = TASK_KINDS[name]
     tp = dict(_TASK_DEFAULTS)
-    tp.update(env["task_parameters"])
-    if tp.get("name", "CaptureXY") != "CaptureXY":
-        raise ValueError("this kernel set implements the CaptureXY task")
+    tp.update(env["task_parameters"] if name == "CaptureXY" else _pose_task_cfg(c, name, env))
     c.position_tolerance = tp["position_tolerance"]
     c.kill_after_n = int(tp["kill_after_n_steps_in_tolerance"])
     c.kill_dist, c.boundary_cost = tp["kill_dist"], tp["boundary_cost"]
@@ -244,7 +246,8 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     c.goal_random_position = tp["goal_random_position"]
     c.spawn_rmin, c.spawn_rmax = tp["min_spawn_dist"], tp["max_spawn_dist"]
     rp = dict(_REWARD_DEFAULTS)
-    rp.update(env["reward_parameters"])
+    if name == "CaptureXY":
+        rp.update(env["reward_parameters"])
     rm = rp["reward_mode"].lower()
     if rm not in ("linear", "square", "exponential"):
         raise ValueError("Linear, Square and Exponential are the only currently supported mode.")
@@ -317,6 +320,85 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     flow = list(wc.get("flow_velocity", [0.0, 0.0, 0.0]) or [0.0, 0.0, 0.0])
     c.flow_vel[0], c.flow_vel[1] = float(flow[0]), float(flow[1])
     return c
+
+
+TASK_KINDS = {"CaptureXY": 0, "GoToPose": 1, "TrackXYOVelocity": 2}   # USV_TASK_* (include/usv_hip.h)
+_MODES = {"linear": 0, "square": 1, "exponential": 2}
+# GoToPoseParameters / TrackXYOVelocityParameters and their reward dataclasses
+# (USV_task_parameters.py:74-148, USV_task_rewards.py:160-393)
+_POSE_DEFAULTS = dict(position_tolerance=0.01, heading_tolerance=0.025, kill_after_n_steps_in_tolerance=500,
+                      goal_random_position=0.0, max_spawn_dist=3.0, min_spawn_dist=0.5, kill_dist=10.0,
+                      spawn_curriculum=False)
+_POSE_REWARD = dict(position_reward_mode="exponential", heading_reward_mode="exponential",
+                    position_exponential_reward_coeff=0.25, heading_exponential_reward_coeff=0.25,
+                    position_scale=1.0, heading_scale=5.0, sig_gain=3.0)
+_TRACK_DEFAULTS = dict(lin_vel_tolerance=0.01, ang_vel_tolerance=0.025, kill_after_n_steps_in_tolerance=50,
+                       goal_random_linear_velocity=0.75, goal_random_angular_velocity=1.0, kill_dist=500.0)
+_TRACK_REWARD = dict(linear_reward_mode="exponential", angular_reward_mode="exponential",
+                     linear_exponential_reward_coeff=0.25, angular_exponential_reward_coeff=0.25,
+                     linear_scale=1.0, angular_scale=1.0)
+
+
+def _mode(v: str) -> int:
+    m = str(v).lower()
+    if m not in _MODES:
+        raise ValueError("Linear, Square and Exponential are the only currently supported mode.")
+    return _MODES[m]
+
+
+def _pose_task_cfg(c: UsvCfg, name: str, env: Dict[str, Any]) -> Dict[str, Any]:
+    """GoToPose / TrackXYOVelocity constants; the task's own parameter defaults
+    replace CaptureXY's (env.task_parameters / env.reward_parameters override)."""
+    if name == "GoToPose":
+        tp = dict(_POSE_DEFAULTS)
+        tp.update(env["task_parameters"])
+        rp = dict(_POSE_REWARD)
+        rp.update(env.get("reward_parameters", {}) or {})
+        if bool(tp.get("spawn_curriculum", False)):
+            raise NotImplementedError("GoToPose spawn_curriculum is not supported (off in every packaged config)")
+        c.tk_mode[0], c.tk_mode[1] = _mode(rp["position_reward_mode"]), _mode(rp["heading_reward_mode"])
+        c.tk_coeff[0] = rp["position_exponential_reward_coeff"]
+        c.tk_coeff[1] = rp["heading_exponential_reward_coeff"]
+        c.tk_scale[0], c.tk_scale[1] = rp["position_scale"], rp["heading_scale"]
+        c.sig_gain = rp["sig_gain"]
+    else:
+        tp = dict(_TRACK_DEFAULTS)
+        tp.update(env["task_parameters"])
+        rp = dict(_TRACK_REWARD)
+        rp.update(env.get("reward_parameters", {}) or {})
+        c.tk_mode[0], c.tk_mode[1] = _mode(rp["linear_reward_mode"]), _mode(rp["angular_reward_mode"])
+        c.tk_coeff[0] = rp["linear_exponential_reward_coeff"]
+        c.tk_coeff[1] = rp["angular_exponential_reward_coeff"]
+        c.tk_scale[0], c.tk_scale[1] = rp["linear_scale"], rp["angular_scale"]
+        c.tk_tol[0], c.tk_tol[1] = tp["lin_vel_tolerance"], tp["ang_vel_tolerance"]
+        c.tk_goal_rand[0] = tp["goal_random_linear_velocity"]
+        c.tk_goal_rand[1] = tp["goal_random_angular_velocity"]
+        tp.setdefault("position_tolerance", 0.0)   # read by the common parser, unused by this task
+    return tp
+
+
+def stat_names(c: UsvCfg):
+    """(extras["episode"] key, episode-sum slot) pairs in the reference's dict order:
+    task.create_stats, Penalties.get_stats_name, success/collision, state statistics
+    (USV_Virtual.py:584-601).  CaptureXY keeps the fixed 28-key layout of _abi.STAT_NAMES."""
+    from .._abi import STAT_KEYS_ENUM as S, STAT_NAMES
+    if c.task_kind == 0:
+        return list(zip(STAT_NAMES, range(len(STAT_NAMES))))
+    task = (["position_reward", "position_error", "heading_reward", "heading_error"] if c.task_kind == 1 else
+            ["linear_velocity_reward", "linear_velocity_error", "angular_velocity_reward", "angular_velocity_error"])
+    slot = ({"position_reward": 0, "heading_reward": 1, "position_error": 2, "heading_error": 3} if c.task_kind == 1
+            else {k: i for i, k in enumerate(task)})
+    out = [(k, slot[k]) for k in task]
+    if c.pen_ang_kind:
+        out.append(("angular_vel_penalty", S["ST_ANGULAR_VEL_PENALTY"]))
+    if c.pen_angv_kind:
+        out.append(("angular_vel_variation_penalty", S["ST_ANGULAR_VEL_VARIATION_PENALTY"]))
+    if c.pen_en_kind:
+        out.append(("energy_penalty", S["ST_ENERGY_PENALTY"]))
+    for k in ("success", "collision", "normed_linear_vel", "normed_angular_vel", "cmd_neg_rate", "u_mean",
+              "u_low_rate", "u_sum"):
+        out.append((k, S["ST_" + k.upper()]))
+    return out
 
 
 def has_disturbance(c: UsvCfg) -> bool:

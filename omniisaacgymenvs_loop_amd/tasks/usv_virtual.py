@@ -18,9 +18,9 @@ import numpy as np
 import torch
 
 from .. import _capi
-from .._abi import DEFINES, STAT_NAMES, UsvBufs, enum_values
+from .._abi import DEFINES, UsvBufs, enum_values
 from ..utils.spaces import Box, DictSpace
-from .usv_config import action_bias_cfg, build_usv_cfg, env_origins, has_disturbance, thruster_tables
+from .usv_config import action_bias_cfg, build_usv_cfg, env_origins, has_disturbance, stat_names, thruster_tables
 
 NOBS = DEFINES["USV_NOBS"]
 NOBST = DEFINES["USV_NOBST"]
@@ -29,6 +29,8 @@ NSTAT = DEFINES["USV_NSTAT"]
 NU_RESET = DEFINES["USV_NU_RESET"]
 NU_STEP = DEFINES["USV_NU_STEP"]
 NDIST = enum_values("usv_dist_row")["USV_NDIST"]
+TASK_CAPTURE_XY, TASK_TRACK_XYO = DEFINES["USV_TASK_CAPTURE_XY"], DEFINES["USV_TASK_TRACK_XYO"]
+TS_ROWS = DEFINES["USV_TS_ROWS"]
 CTL_N = DEFINES["USV_CTL_N"]
 
 
@@ -96,7 +98,7 @@ class USVVirtual:
                      ("obs_buf_t", (n, NOBS), torch.float32), ("rew_buf", (n,), torch.float32),
                      ("dones", (n,), torch.int64), ("field_old_tgt", (2, n), torch.float32),
                      ("reset_ids", (n,), torch.int32), ("dist", (NDIST, n), torch.float32),
-                     ("env_org", (2, n), torch.float32)]
+                     ("env_org", (2, n), torch.float32), ("tgt_h", (n,), torch.float32)]
         sizes = [int(np.prod(shape)) * torch.empty((), dtype=dt).element_size() for _, shape, dt in slab_spec]
         offs = np.concatenate([[0], np.cumsum([(sz + 255) // 256 * 256 for sz in sizes])])
         self._slab = torch.zeros(int(offs[-1]), device=dev, dtype=torch.uint8)
@@ -114,7 +116,11 @@ class USVVirtual:
             self.dist = None
         # RLTask._env_pos (x, y): only the disturbance sinusoids read world positions
         self.env_org.copy_(torch.from_numpy(env_origins(n)))
-        self.field = Z((n, GRID2), **f32)
+        # TrackXYOVelocity's two-phase step: per-env rows + per-256-env-block partial sums
+        self.task_scratch = (Z(TS_ROWS * n + (n + 255) // 256, **f32) if self.cfg.task_kind == TASK_TRACK_XYO
+                             else None)
+        self._has_field = self.cfg.task_kind == TASK_CAPTURE_XY
+        self.field = Z((n if self._has_field else 1, GRID2), **f32)
         self.ibuf[2] = 1                               # RLTask.cleanup: reset_buf = ones
         self.just_reset.fill_(1)
         self.ctl = Z(CTL_N, **i32)
@@ -126,7 +132,7 @@ class USVVirtual:
         # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
         self.clock = Z(4, device=dev, dtype=torch.int64)
         self.states_buf = Z((n, 0), **f32)
-        self.sdf = torch.empty((n, GRID2), **f32)      # per-reset-slot SDF scratch of the field kernels
+        self.sdf = torch.empty((n if self._has_field else 1, GRID2), **f32)   # per-reset-slot SDF scratch
         self.lut = Z((2, 1000), **f32)
         tl, tr = thruster_tables(self._task_cfg)
         self._tables = torch.tensor(np.stack([tl, tr]), **f32)
@@ -163,6 +169,8 @@ class USVVirtual:
         b.grid_lin = p(self.grid_lin) if self.grid_lin is not None else None
         b.dist = p(self.dist) if self.dist is not None else None
         b.env_org = p(self.env_org)
+        b.tgt_h = p(self.tgt_h)
+        b.task_scratch = p(self.task_scratch) if self.task_scratch is not None else None
         return b
 
     def set_env_origins(self, org: torch.Tensor) -> None:
@@ -244,7 +252,8 @@ class USVVirtual:
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
         bias, k = self._advance()
         _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
-        _capi.call("usv_potential_field", cfg, b, s)
+        if self._has_field:   # CaptureXY only (GoToPose / TrackXYOVelocity have no obstacles)
+            _capi.call("usv_potential_field", cfg, b, s)
         _capi.call("usv_env_step", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
                    self.seed, k, _capi.ptr(u_step), s)
         return self.obs_buf_t, self.rew_buf, self.dones
@@ -263,7 +272,7 @@ class USVVirtual:
         self.step += 1.0 / self._horizon
         if k == 0 or "episode" not in self.extras:
             # extras["episode"]: 0-d views of the device buffer written at every reset (USV_Virtual.py:1591-1612)
-            self.extras = {"episode": {name: self.extras_buf[i] for i, name in enumerate(STAT_NAMES)}}
+            self.extras = {"episode": {name: self.extras_buf[i] for name, i in stat_names(self.cfg)}}
         return bias, k
 
     def forces(self) -> torch.Tensor:

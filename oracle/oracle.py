@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libusv_oracle.so")
 
 NOBS, NOBST, GRID, NSTAT = 33, 16, 150, 28
-NU_RESET, NU_STEP = 711, 8
+NU_RESET, NU_STEP = 712, 8
 NDIST = 11
 CTL_POT_VALID, CTL_PEN_VALID, CTL_REW_VALID = 1, 2, 3
 
@@ -71,14 +71,14 @@ class _OracleEnvC(ctypes.Structure):
     _fields_ = ([("n", ctypes.c_int)] + [(k, ctypes.c_void_p) for k in _PTR_FIELDS] +
                 [("ctl", ctypes.c_int32 * 16), ("extras", ctypes.c_float * NSTAT), ("dbg", ctypes.c_void_p),
                  ("tmp", ctypes.c_void_p), ("grid_lin", ctypes.c_void_p), ("dist", ctypes.c_void_p),
-                 ("env_org", ctypes.c_void_p)])
+                 ("env_org", ctypes.c_void_p), ("tgt_h", ctypes.c_void_p)])
 
 
 class OracleEnv:
     """Host SoA env state driven by the C oracle (mirrors usv_bufs_t)."""
 
     F32 = ("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr", "mass", "com_x", "com_y", "com_z", "k_drag",
-           "thr_l", "thr_r", "k_iz", "mass_r", "tgt_x", "tgt_y", "prev_dist", "prev_head", "prev_pot",
+           "thr_l", "thr_r", "k_iz", "mass_r", "tgt_x", "tgt_y", "tgt_h", "prev_dist", "prev_head", "prev_pot",
            "prev_wz", "rew")
     I32 = ("goal_cnt", "progress", "reset_buf", "done_succ", "done_coll")
 
@@ -97,7 +97,7 @@ class OracleEnv:
         self.reset_buf[:] = 1
         self.just_reset = np.ones(n, np.uint8)
         self.obst = np.zeros((NOBST, 2, n), np.float32)
-        self.field = np.zeros((n, GRID * GRID), np.float32)
+        self.field = np.zeros((n if cfg.task_kind == 0 else 1, GRID * GRID), np.float32)
         self.prev_cmd = np.zeros((2, n), np.float32)
         self.stats = np.zeros((NSTAT, n), np.float32)
         self.obs = np.zeros((n, NOBS), np.float32)

@@ -119,6 +119,7 @@ typedef struct oracle_env {
   const float *grid_lin;            /* [150] potential-field cell centres, NULL => linspace formula */
   float *dist;                      /* [USV_NDIST][n] disturbance parameters or NULL */
   const float *env_org;             /* [2][n] env origins (RLTask._env_pos) or NULL */
+  float *tgt_h;                     /* [n] GoToPose target heading / TrackXYO target yaw rate */
 } oracle_env_t;
 
 /* ------------------------------------------------------------------------ */
@@ -517,10 +518,43 @@ void oracle_reset(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids
      * obstacle box use the target of the PREVIOUS episode: get_goals runs later
      * in set_targets (USV_Virtual.py:1618). */
     const float rmin = c->spawn_rmin, rmax = c->spawn_rmax;
-    const float r = u[RU_SPAWN_R] * (rmax - rmin) + rmin;
-    const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
-    const float sx = r * cosf(th), sy = r * sinf(th);
     const float yaw0 = u[RU_YAW] * (float)OPI;
+    float sx, sy;
+    if (c->task_kind == USV_TASK_GO_TO_POSE) {
+      /* GoToPoseTask.get_spawns (USV_go_to_pose.py:256-319): disk around the previous target */
+      const float r = u[RU_SPAWN_R] * (float)((double)rmax - (double)rmin) + rmin;
+      const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
+      sx = r * cosf(th) + E->tgt_x[e];
+      sy = r * sinf(th) + E->tgt_y[e];
+      E->prev_dist[e] = 0.f;   /* GoToPoseTask.reset: prev_position_dist = 0 (:227) */
+    } else if (c->task_kind == USV_TASK_TRACK_XYO) {
+      sx = 0.f; sy = 0.f;      /* TrackXYOVelocityTask.get_spawns (:203-219): heading only */
+    } else {
+      const float r = u[RU_SPAWN_R] * (rmax - rmin) + rmin;
+      const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
+      sx = r * cosf(th); sy = r * sinf(th);
+    }
+    if (c->task_kind != USV_TASK_CAPTURE_XY) {
+      E->px[e] = sx; E->py[e] = sy; E->yaw[e] = yaw0;
+      E->vx[e] = u[RU_VX] * 3.0f - 1.5f;
+      E->vy[e] = u[RU_VY] * 3.0f - 1.5f;
+      E->wz[e] = 0.f;
+      E->reset_buf[e] = 0; E->progress[e] = 0;
+      E->prev_cmd[0 * n + e] = 0.f; E->prev_cmd[1 * n + e] = 0.f;
+      for (int q = 0; q < USV_NSTAT; ++q) E->stats[q * n + e] = 0.f;
+      if (c->task_kind == USV_TASK_GO_TO_POSE) {   /* get_goals (USV_go_to_pose.py:229-254) */
+        const float g = c->goal_random_position;
+        E->tgt_x[e] = u[RU_GOAL + 0] * g * 2.0f - g;
+        E->tgt_y[e] = u[RU_GOAL + 1] * g * 2.0f - g;
+        E->tgt_h[e] = u[RU_GOAL_H] * (float)OPI * 2.0f;
+      } else {                                     /* get_goals (USV_track_xyo_velocity.py:178-199) */
+        const float gl = c->tk_goal_rand[0], ga = c->tk_goal_rand[1];
+        E->tgt_x[e] = u[RU_GOAL + 0] * gl * 2.0f - gl;
+        E->tgt_y[e] = u[RU_GOAL + 1] * gl * 2.0f - gl;
+        E->tgt_h[e] = u[RU_GOAL_H] * ga * 2.0f - ga;
+      }
+      continue;
+    }
     /* quaternion (cos(yaw/2),0,0,sin(yaw/2)) -> yaw: identical in the planar state */
     const float tx = E->tgt_x[e], ty = E->tgt_y[e];
     float oc[USV_NOBST][2];
@@ -588,9 +622,11 @@ void oracle_reset(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids
     E->tgt_y[e] = u[RU_GOAL + 1] * g * 2.0f - g;
   }
   /* potential field of the reset batch (static_obs.py:1054-1057) */
-  oracle_potential_field(c, k, obst_k, tgt_k, fld_k, NULL, E->grid_lin);
-  for (int s = 0; s < k; ++s)
-    memcpy(E->field + (size_t)ids[s] * USV_GRID2, fld_k + (size_t)s * USV_GRID2, sizeof(float) * USV_GRID2);
+  if (c->task_kind == USV_TASK_CAPTURE_XY) {
+    oracle_potential_field(c, k, obst_k, tgt_k, fld_k, NULL, E->grid_lin);
+    for (int s = 0; s < k; ++s)
+      memcpy(E->field + (size_t)ids[s] * USV_GRID2, fld_k + (size_t)s * USV_GRID2, sizeof(float) * USV_GRID2);
+  }
   free(obst_k); free(tgt_k); free(fld_k);
 }
 
@@ -681,7 +717,52 @@ void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E) {
   }
 }
 
+/* privileged tail (USV_Virtual.py:840-976; MDD.get_masses USV_disturbances.py:153-194) */
+static void priv_tail(const usv_cfg_t *c, const oracle_env_t *E, int e, float *obs) {
+  float mass_o, com_o[3];
+  const float comv[3] = {E->com_x[e], E->com_y[e], E->com_z[e]};
+  if (c->masscom_base) {
+    mass_o = c->mass_relative ? 0.f : c->base_mass;
+    for (int a = 0; a < 3; ++a) com_o[a] = c->com_scaled ? c->base_com[a] / (c->com_scale[a] + 1e-6f) : c->base_com[a];
+  } else {
+    const float denom = (float)(fabs((double)c->base_mass) > 1e-6 ? fabs((double)c->base_mass) : 1e-6);
+    mass_o = c->mass_relative ? (E->mass[e] - c->base_mass) / denom : E->mass[e];
+    for (int a = 0; a < 3; ++a) com_o[a] = c->com_scaled ? comv[a] / (c->com_scale[a] + 1e-6f) : comv[a];
+  }
+  float *pt = obs + USV_NOBS - c->priv_dim;
+  pt[0] = mass_o; pt[1] = com_o[0]; pt[2] = com_o[1]; pt[3] = com_o[2];
+  if (c->priv_dim == 8) {
+    float kd, tl, tr, kz;
+    if (c->masscom_base) {
+      if (c->priv_mode == 2) {
+        kd = 0.5f * (c->kdrag_min + c->kdrag_max);
+        tl = tr = c->couple_thr ? (1.0f - 0.5f * c->thr_rand) : 1.0f;
+        kz = 0.5f * (c->kiz_min + c->kiz_max);
+      } else { kd = tl = tr = kz = 1.0f; }
+    } else {
+      kd = E->k_drag[e];
+      tl = E->thr_l[e]; tr = E->thr_r[e];
+      kz = E->k_iz[e];
+    }
+    if (c->priv_mode == 1) {
+      kd = enc_centered(kd, c->kdrag_min, c->kdrag_max, c->priv_nominal);
+      tl = enc_centered(tl, c->thr_min, c->thr_max, c->priv_nominal);
+      tr = enc_centered(tr, c->thr_min, c->thr_max, c->priv_nominal);
+      kz = enc_centered(kz, c->kiz_min, c->kiz_max, c->priv_nominal);
+    } else if (c->priv_mode == 2) {
+      kd = c->priv_drag_on ? enc_minmax(kd, c->kdrag_min, c->kdrag_max) : 0.f;
+      tl = c->priv_thr_on ? enc_minmax(tl, c->thr_min, c->thr_max) : 0.f;
+      tr = c->priv_thr_on ? enc_minmax(tr, c->thr_min, c->thr_max) : 0.f;
+      kz = c->priv_kiz_on ? enc_minmax(kz, c->kiz_min, c->kiz_max) : 0.f;
+    }
+    pt[4] = kd; pt[5] = tl; pt[6] = tr; pt[7] = kz;
+  }
+}
+
+static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const float *U);
+
 void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
+  if (c->task_kind != USV_TASK_CAPTURE_XY) { oracle_step_post_task(c, E, U); return; }
   const int n = E->n;
   const int any_reset_none = (E->ctl[USV_CTL_POT_VALID] == 0);
   const int pen_valid = E->ctl[USV_CTL_PEN_VALID];
@@ -766,47 +847,7 @@ void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
     const int pa = USV_NOBS - c->priv_dim - 2;
     obs[pa + 0] = E->prev_cmd[0 * n + e];
     obs[pa + 1] = E->prev_cmd[1 * n + e];
-    /* privileged tail (USV_Virtual.py:840-976; MDD.get_masses USV_disturbances.py:153-194) */
-    {
-      float mass_o, com_o[3];
-      const float comv[3] = {E->com_x[e], E->com_y[e], E->com_z[e]};
-      if (c->masscom_base) {
-        mass_o = c->mass_relative ? 0.f : c->base_mass;
-        for (int a = 0; a < 3; ++a) com_o[a] = c->com_scaled ? c->base_com[a] / (c->com_scale[a] + 1e-6f) : c->base_com[a];
-      } else {
-        const float denom = (float)(fabs((double)c->base_mass) > 1e-6 ? fabs((double)c->base_mass) : 1e-6);
-        mass_o = c->mass_relative ? (E->mass[e] - c->base_mass) / denom : E->mass[e];
-        for (int a = 0; a < 3; ++a) com_o[a] = c->com_scaled ? comv[a] / (c->com_scale[a] + 1e-6f) : comv[a];
-      }
-      float *pt = obs + USV_NOBS - c->priv_dim;
-      pt[0] = mass_o; pt[1] = com_o[0]; pt[2] = com_o[1]; pt[3] = com_o[2];
-      if (c->priv_dim == 8) {
-        float kd, tl, tr, kz;
-        if (c->masscom_base) {
-          if (c->priv_mode == 2) {
-            kd = 0.5f * (c->kdrag_min + c->kdrag_max);
-            tl = tr = c->couple_thr ? (1.0f - 0.5f * c->thr_rand) : 1.0f;
-            kz = 0.5f * (c->kiz_min + c->kiz_max);
-          } else { kd = tl = tr = kz = 1.0f; }
-        } else {
-          kd = E->k_drag[e];
-          tl = E->thr_l[e]; tr = E->thr_r[e];
-          kz = E->k_iz[e];
-        }
-        if (c->priv_mode == 1) {
-          kd = enc_centered(kd, c->kdrag_min, c->kdrag_max, c->priv_nominal);
-          tl = enc_centered(tl, c->thr_min, c->thr_max, c->priv_nominal);
-          tr = enc_centered(tr, c->thr_min, c->thr_max, c->priv_nominal);
-          kz = enc_centered(kz, c->kiz_min, c->kiz_max, c->priv_nominal);
-        } else if (c->priv_mode == 2) {
-          kd = c->priv_drag_on ? enc_minmax(kd, c->kdrag_min, c->kdrag_max) : 0.f;
-          tl = c->priv_thr_on ? enc_minmax(tl, c->thr_min, c->thr_max) : 0.f;
-          tr = c->priv_thr_on ? enc_minmax(tr, c->thr_min, c->thr_max) : 0.f;
-          kz = c->priv_kiz_on ? enc_minmax(kz, c->kiz_min, c->kiz_max) : 0.f;
-        }
-        pt[4] = kd; pt[5] = tl; pt[6] = tr; pt[7] = kz;
-      }
-    }
+    priv_tail(c, E, e, obs);
     /* ---- calculate_metrics -> CaptureXYTask.compute_reward (static_obs.py:335-657) ---- */
     const float bover = maxf_(dist - c->kill_dist, 0.f);
     const float bx_ = minf_(bover / 0.25f, 20.0f);
@@ -917,6 +958,166 @@ void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
     for (int q = 0; q < USV_NOBS; ++q) E->obs[(size_t)e * USV_NOBS + q] = clampf_(obs[q], -c->clip_obs, c->clip_obs);
     E->just_reset[e] = 0;
   }
+  E->ctl[USV_CTL_POT_VALID] = 1;
+  E->ctl[USV_CTL_PEN_VALID] = 1;
+  E->ctl[USV_CTL_REW_VALID] = 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* GoToPose / TrackXYOVelocity post-physics step:               */
+/* GoToPoseTask.get_state_observations/compute_reward/update_kills           */
+/* (tasks/USV/USV_go_to_pose.py:89-209), GoToPoseReward (USV_task_rewards.py: */
+/* 160-233); TrackXYOVelocityTask (USV_track_xyo_velocity.py:75-166),         */
+/* TrackXYOVelocityReward (USV_task_rewards.py:328-393).  Glue as calculate_   */
+/* metrics / is_done do for every task (USV_Virtual.py:1223-1237,1628-1652);  */
+/* the task_data block is Core's 20 columns (unwritten ones 0).              */
+/* ------------------------------------------------------------------------ */
+static float task_term(int mode, float x, float coeff) {
+  if (mode == 0) return 1.0f / (1.0f + x);
+  if (mode == 1) return 1.0f / (1.0f + x * x);
+  return expf(-x / coeff);
+}
+
+static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
+  const int n = E->n;
+  const int pen_valid = E->ctl[USV_CTL_PEN_VALID];
+  const float PI_F = (float)OPI, TWO_PI_F = (float)(2.0 * OPI);
+  const int track = c->task_kind == USV_TASK_TRACK_XYO;
+  /* TrackXYOVelocity: torch.square(ang_err).sum(-1) of a 1-D tensor sums over ALL envs (:121-123) */
+  double ang_sq = 0.0;
+  float *lin_r = (float *)malloc(sizeof(float) * (size_t)n), *pen_v = (float *)malloc(sizeof(float) * (size_t)n);
+  int *lin_ok = (int *)malloc(sizeof(int) * (size_t)n), *pkill = (int *)malloc(sizeof(int) * (size_t)n);
+  for (int e = 0; e < n; ++e) {
+    const float *u = U + (size_t)e * USV_NU_STEP;
+    const float *tmp = E->tmp + (size_t)e * 8;
+    const float cmd[2] = {tmp[0], tmp[1]}, thrust[2] = {tmp[2], tmp[3]}, unit[2] = {tmp[4], tmp[5]};
+    E->progress[e] += 1;
+    float px = E->px[e], py = E->py[e];
+    if (c->pos_noise_on) {
+      const float rng = (float)((double)c->pos_noise_max - (double)c->pos_noise_min);
+      px = px + (u[SU_PX] * rng + c->pos_noise_min);
+      py = py + (u[SU_PX + 1] * rng + c->pos_noise_min);
+    }
+    float vxn = E->vx[e], vyn = E->vy[e], wzn = E->wz[e];
+    if (c->vel_noise_on) {
+      const float rng = (float)((double)c->vel_noise_max - (double)c->vel_noise_min);
+      vxn = vxn + (u[SU_VX] * rng + c->vel_noise_min);
+      vyn = vyn + (u[SU_VY] * rng + c->vel_noise_min);
+      wzn = wzn + (u[SU_WZ] * rng + c->vel_noise_min);
+    }
+    float yawn = E->yaw[e];
+    if (c->head_noise_on) {
+      const float rng = (float)((double)c->head_noise_max - (double)c->head_noise_min);
+      yawn = yawn + (u[SU_HEAD] * rng + c->head_noise_min);
+    }
+    const float hc = cosf(yawn), hs = sinf(yawn);
+    float obs[USV_NOBS];
+    memset(obs, 0, sizeof(obs));
+    if (c->obs_local) {
+      obs[0] = hc * vxn + hs * vyn;
+      obs[1] = -hs * vxn + hc * vyn;
+    } else {
+      obs[0] = vxn; obs[1] = vyn;
+    }
+    obs[2] = wzn;
+    const int pa = USV_NOBS - c->priv_dim - 2;
+    obs[pa + 0] = E->prev_cmd[0 * n + e];
+    obs[pa + 1] = E->prev_cmd[1 * n + e];
+    priv_tail(c, E, e, obs);
+    /* Penalties.compute_penalty (USV_task_rewards.py:440-523) */
+    const float pact0 = c->pen_use_u ? unit[0] : cmd[0];
+    const float pact1 = c->pen_use_u ? unit[1] : cmd[1];
+    float p_lin = 0.f, p_ang = 0.f, p_angv = 0.f, p_en = 0.f;
+    if (c->pen_lin_kind == PEN_NORM) p_lin = -tnorm2(vxn, vyn) * c->pen_lin_k + c->pen_lin_c;
+    if (c->pen_ang_kind) p_ang = pen_scalar(c->pen_ang_kind, c->pen_ang_k, c->pen_ang_x0, c->pen_ang_c, wzn);
+    if (c->pen_angv_kind) {
+      const float prev_w = pen_valid ? E->prev_wz[e] : wzn;
+      p_angv = pen_scalar(c->pen_angv_kind, c->pen_angv_k, c->pen_angv_x0, c->pen_angv_c, wzn - prev_w);
+    }
+    if (c->pen_en_kind == PEN_SUM) p_en = -(pact0 + pact1) * c->pen_en_k + c->pen_en_c;
+    else if (c->pen_en_kind == PEN_SUMSQ) p_en = -(pact0 * pact0 + pact1 * pact1) * c->pen_en_k + c->pen_en_c;
+    E->prev_wz[e] = wzn;
+    const float pens = p_lin + p_ang + p_angv + p_en;
+    float t_add[4] = {0.f, 0.f, 0.f, 0.f};
+    if (!track) {
+      /* GoToPoseTask.get_state_observations (:89-130) */
+      const float ex = E->tgt_x[e] - px, ey = E->tgt_y[e] - py;
+      const float theta = atan2f(hs, hc);
+      const float beta = atan2f(ey, ex);
+      const float alpha = fmodf((beta - theta) + PI_F, TWO_PI_F) - PI_F;
+      const float hraw = fmodf((E->tgt_h[e] - theta) + PI_F, TWO_PI_F) - PI_F;
+      const float herr = atan2f(sinf(hraw), cosf(hraw));
+      obs[3] = cosf(alpha); obs[4] = sinf(alpha); obs[5] = tnorm2(ex, ey);
+      obs[6] = cosf(herr); obs[7] = sinf(herr);
+      /* compute_reward (:134-181) */
+      const float pdist = sqrtf(ex * ex + ey * ey);
+      const float hdist = fabsf(herr);
+      const float prog = 2.0f * clampf_(E->prev_dist[e] - pdist, -2.0f, 2.0f);
+      E->prev_dist[e] = pdist;
+      const float speed = tnorm2(vxn, vyn);
+      const int gir = (pdist < c->position_tolerance) && (speed < 0.1f);
+      E->goal_cnt[e] = E->goal_cnt[e] * gir + gir;
+      const float hw = 1.0f - 1.0f / (1.0f + expf(-c->sig_gain * (pdist - 2.0f)));
+      const float pos_r = c->tk_scale[0] * task_term(c->tk_mode[0], pdist, c->tk_coeff[0]);
+      const float head_r = hw * c->tk_scale[1] * task_term(c->tk_mode[1], hdist, c->tk_coeff[1]);
+      const float act_pen = -0.05f * (fabsf(cmd[0]) + fabsf(cmd[1]));
+      const float overall = pos_r + head_r + prog + 2.0f * (float)gir + act_pen;
+      E->rew[e] = overall + pens;
+      /* update_kills (:183-209) */
+      const int die = (pdist > c->kill_dist) || (E->goal_cnt[e] >= c->kill_after_n);
+      const int tout = E->progress[e] >= c->max_episode_length - 1;
+      E->reset_buf[e] = c->fixed_horizon_eval ? tout : (tout ? 1 : die);
+      t_add[0] = pos_r; t_add[1] = head_r; t_add[2] = pdist; t_add[3] = speed;   /* update_statistics (:211-219) */
+    } else {
+      /* TrackXYOVelocityTask.get_state_observations (:75-101) */
+      const float lex = E->tgt_x[e] - vxn, ley = E->tgt_y[e] - vyn, aerr = E->tgt_h[e] - wzn;
+      obs[3] = lex; obs[4] = ley; obs[5] = aerr;
+      const float pos_d = sqrtf(px * px + py * py);
+      const float lin_d = sqrtf(lex * lex + ley * ley);
+      ang_sq += (double)(aerr * aerr);
+      lin_r[e] = task_term(c->tk_mode[0], lin_d, c->tk_coeff[0]) * c->tk_scale[0];
+      lin_ok[e] = lin_d < c->tk_tol[0];
+      pkill[e] = pos_d > c->kill_dist;
+      pen_v[e] = pens;
+      t_add[0] = lin_r[e]; t_add[1] = lin_d;
+    }
+    if (c->stats_on) {
+      float *S = E->stats;
+#define ADDS(k, v) S[(k) * n + e] += (v)
+      ADDS(0, t_add[0]); ADDS(1, t_add[1]);
+      if (!track) { ADDS(2, t_add[2]); ADDS(3, t_add[3]); }
+      if (c->pen_ang_kind) ADDS(ST_ANGULAR_VEL_PENALTY, p_ang);
+      if (c->pen_angv_kind) ADDS(ST_ANGULAR_VEL_VARIATION_PENALTY, p_angv);
+      if (c->pen_en_kind) ADDS(ST_ENERGY_PENALTY, p_en);
+      ADDS(ST_NORMED_LINEAR_VEL, tnorm2(vxn, vyn));
+      ADDS(ST_NORMED_ANGULAR_VEL, fabsf(wzn));
+      ADDS(ST_CMD_NEG_RATE, ((float)(thrust[0] < 0.f) + (float)(thrust[1] < 0.f)) / 2.0f);
+      ADDS(ST_U_MEAN, (unit[0] + unit[1]) / 2.0f);
+      ADDS(ST_U_LOW_RATE, ((float)(unit[0] < 0.05f) + (float)(unit[1] < 0.05f)) / 2.0f);
+      ADDS(ST_U_SUM, unit[0] + unit[1]);
+#undef ADDS
+    }
+    for (int q = 0; q < USV_NOBS; ++q) E->obs[(size_t)e * USV_NOBS + q] = clampf_(obs[q], -c->clip_obs, c->clip_obs);
+    E->just_reset[e] = 0;
+  }
+  if (track) {   /* TrackXYOVelocityTask.compute_reward / update_kills (:103-166) with the all-env angular distance */
+    const float ang_d = sqrtf((float)ang_sq);
+    const int ang_ok = ang_d < c->tk_tol[1];
+    const float ang_r = task_term(c->tk_mode[1], ang_d, c->tk_coeff[1]) * c->tk_scale[1];
+    for (int e = 0; e < n; ++e) {
+      const int gir = lin_ok[e] * ang_ok;
+      E->goal_cnt[e] = E->goal_cnt[e] * gir + gir;
+      E->rew[e] = (lin_r[e] + ang_r) + pen_v[e];
+      const int die = pkill[e] || (E->goal_cnt[e] > c->kill_after_n);
+      const int tout = E->progress[e] >= c->max_episode_length - 1;
+      E->reset_buf[e] = c->fixed_horizon_eval ? tout : (tout ? 1 : die);
+      if (c->stats_on) {
+        E->stats[2 * n + e] += ang_r;
+        E->stats[3 * n + e] += ang_d;
+      }
+    }
+  }
+  free(lin_r); free(pen_v); free(lin_ok); free(pkill);
   E->ctl[USV_CTL_POT_VALID] = 1;
   E->ctl[USV_CTL_PEN_VALID] = 1;
   E->ctl[USV_CTL_REW_VALID] = 1;

@@ -332,6 +332,20 @@ def load_task_cfg(variant: str):
         env["water_current"]["use_water_current"] = True
         env["water_current"]["flow_velocity"] = [0.3, -0.2, 0.0]
         env["maxEpisodeLength"] = 30
+    if variant in ("P", "T"):
+        # SURVEY A20 tasks on the TEST glue: the task's own yaml task/reward parameters
+        # (cfg/task/USV/USV_Virtual_GoToPose.yaml, USV_Virtual_TrackXYOVelocity.yaml)
+        import yaml
+        name = "USV_Virtual_GoToPose.yaml" if variant == "P" else "USV_Virtual_TrackXYOVelocity.yaml"
+        with open(os.path.join(REF, "omniisaacgymenvs/cfg/task/USV", name)) as f:
+            tcfg = yaml.safe_load(f)
+        env = cfg["env"]
+        env["task_parameters"] = dict(tcfg["env"]["task_parameters"])
+        env["reward_parameters"] = dict(tcfg["env"]["reward_parameters"])
+        if variant == "P":
+            env["task_parameters"]["goal_random_position"] = 2.0
+            env["task_parameters"]["position_tolerance"] = 0.3   # reachable within the short episode
+        env["maxEpisodeLength"] = 40
     return cfg
 
 
@@ -370,6 +384,15 @@ def build_usv(torch, n, variant):
     usv._heron = heron
     usv._env_pos = torch.zeros((n, 3))
     usv.task._env = usv
+    if variant in ("P", "T"):
+        # the live glue cannot run these tasks; minimal harness fixes:
+        # Core's 20-column task_data block, the marker buffer set_targets reads, and
+        # update_kills(step) called with the extra current_state argument
+        t = usv.task
+        t._task_data = torch.zeros((n, t._num_observations - 3 - t.action_dim - t.priv_dim))
+        t._blue_pin_positions = torch.zeros((n, 16, 3))
+        orig_kills = t.update_kills
+        t.update_kills = lambda step, *a: orig_kills(step)
     usv.get_USV_dynamics()
     usv._marker = None
     usv._blue_markers = [None] * 16
@@ -392,7 +415,13 @@ def make_vecenv(torch, usv, world):
 # --------------------------------------------------------------------------
 RU = dict(MASS=0, COM=1, KIZ=4, KDRAG=5, THR=6, DRAG=8, SPAWN_R=20, SPAWN_TH=21, YAW=22, OBST=23,
           RESAMPLE=55, VX=695, VY=696, GOAL=697, FSIN=699, FCONST=704, TSIN=706, TCONST=709)
-NU_RESET, NU_STEP = 711, 8
+NU_RESET, NU_STEP = 712, 8
+RU["GOAL_H"] = 711
+# draw sites of the GoToPose / TrackXYOVelocity spawn + goal generators
+POSE_SITES = {("USV_go_to_pose.py", 240): RU["GOAL"], ("USV_go_to_pose.py", 248): RU["GOAL_H"],
+              ("USV_go_to_pose.py", 305): RU["SPAWN_R"], ("USV_go_to_pose.py", 306): RU["SPAWN_TH"],
+              ("USV_go_to_pose.py", 316): RU["YAW"], ("USV_track_xyo_velocity.py", 187): RU["GOAL"],
+              ("USV_track_xyo_velocity.py", 193): RU["GOAL_H"], ("USV_track_xyo_velocity.py", 216): RU["YAW"]}
 # draw sites of the disturbance generators (USV_disturbances.py line -> slot)
 DIST_SITES = {("generate_force", 342): RU["FSIN"], ("generate_force", 347): RU["FSIN"] + 1,
               ("generate_force", 352): RU["FSIN"] + 2, ("generate_force", 357): RU["FSIN"] + 3,
@@ -409,7 +438,11 @@ def map_reset_draws(draws, k):
     spawn = 0
     for fn, line, fname, t in draws:
         a = t.numpy().astype(np.float32)
-        if fn == "randomize_masses":
+        if (fname, line) in POSE_SITES:
+            slot = POSE_SITES[(fname, line)]
+            w = 2 if slot == RU["GOAL"] else 1
+            U[:, slot:slot + w] = a.reshape(k, w)
+        elif fn == "randomize_masses":
             U[:, RU["MASS"]] = a.reshape(k)
         elif fn == "_randomize_com":
             U[:, RU["COM"]:RU["COM"] + a.reshape(k, -1).shape[1]] = a.reshape(k, -1)
@@ -574,6 +607,14 @@ def policy_actions(rng, n, t):
     return a
 
 
+def _task_targets(task):
+    """(target xy [n,2], target heading / yaw rate [n]) of the task object."""
+    if hasattr(task, "_target_linear_velocities"):   # TrackXYOVelocityTask
+        return (task._target_linear_velocities.numpy().copy(), task._target_angular_velocities.numpy().copy())
+    h = task._target_headings.numpy().copy() if hasattr(task, "_target_headings") else None
+    return task._target_positions.numpy().copy(), h
+
+
 def gen_episode(torch, variant, n, steps, seed):
     torch.manual_seed(seed)
     usv, heron, world, task_cfg = build_usv(torch, n, variant)
@@ -592,7 +633,7 @@ def gen_episode(torch, variant, n, steps, seed):
     with rec:
         usv.post_reset()
         init_draws = rec.take()
-        init_tgt = usv.task._target_positions.numpy().copy()
+        init_tgt = _task_targets(usv.task)[0]
         usv.task.reset(torch.arange(n))   # flags only (reset via VecEnv.reset below)
         rec.take()
     data = {k: [] for k in ("actions", "obs", "rew", "reset", "progress", "px", "py", "yaw", "vx", "vy", "wz",
@@ -645,12 +686,19 @@ def gen_episode(torch, variant, n, steps, seed):
                 data["thr_l"].append(td.thruster_multiplier[:, 0].numpy().copy())
                 data["thr_r"].append(td.thruster_multiplier[:, 0].numpy().copy())
             data["k_iz"].append(usv.k_Iz[:, 0].numpy().copy())
-            data["obst"].append(usv.task.xunlian_pos[:, :, :2].numpy().copy())
-            data["tgt"].append(usv.task._target_positions.numpy().copy())
+            if variant in ("P", "T"):
+                data["obst"].append(np.zeros((n, 16, 2), np.float32))
+                data.setdefault("tgt_h", []).append(_task_targets(usv.task)[1])
+            else:
+                data["obst"].append(usv.task.xunlian_pos[:, :, :2].numpy().copy())
+            data["tgt"].append(_task_targets(usv.task)[0])
             data["goal_cnt"].append(usv.task._goal_reached.numpy().copy())
             tk = usv.task
             pen = usv._penalties
-            data["terms"].append(torch.stack([tk.distance_reward, tk.alignment_reward, tk.potential_shaping_reward,
+            if variant in ("P", "T"):
+                data["terms"].append(np.zeros((n, 15), np.float32))
+            else:
+              data["terms"].append(torch.stack([tk.distance_reward, tk.alignment_reward, tk.potential_shaping_reward,
                                            tk._turn_hazard_penalty, tk._speed_reward, tk._angular_reward,
                                            tk._heading_improve_reward, tk.collision_reward, tk._goal_reward,
                                            tk._total_reward, pen.angular_vel_penalty,
@@ -664,13 +712,17 @@ def gen_episode(torch, variant, n, steps, seed):
                     td_.disturbance_torques_const[:, 2], td_._torque_freq, td_._torque_shift, td_._torque_amp],
                     0).numpy().copy())
             ex = extras.get("episode", {})
-            data["extras"].append(np.array([float(ex[k]) if k in ex else np.nan for k in STAT_NAMES], np.float32))
+            names = STAT_NAMES if variant not in ("P", "T") else list(usv.episode_sums.keys())
+            data["extras"].append(np.array([float(ex[k]) if k in ex else np.nan for k in names], np.float32))
     out = {k: np.stack(v) for k, v in data.items()}
     out["reset_U"] = np.concatenate(reset_U, 0) if reset_U else np.zeros((0, NU_RESET), np.float32)
     out["init_tgt"] = init_tgt
-    out["grid_lin"] = usv.task.gpu_map.grid_coords[0, 0, :, 0].numpy().copy()
+    out["grid_lin"] = (usv.task.gpu_map.grid_coords[0, 0, :, 0].numpy().copy() if hasattr(usv.task, "gpu_map")
+                       else np.zeros(150, np.float32))
     out["config_json"] = np.frombuffer(json.dumps(task_cfg).encode(), dtype=np.uint8)
     out["bias_steps"] = np.int64(usv._initial_action_bias_steps)
+    if variant in ("P", "T"):
+        out["extras_names"] = np.array(list(usv.episode_sums.keys()))
     np.savez_compressed(os.path.join(OUT, f"episode_{variant}.npz"), **out)
     print(f"episode_{variant}: resets per step", out["reset_mask"].sum(1).tolist())
 
@@ -820,6 +872,8 @@ def main():
         "episodeA": lambda: gen_episode(torch, "A", 16, 64, 1234),
         "episodeB": lambda: gen_episode(torch, "B", 12, 56, 99),
         "episodeC": lambda: gen_episode(torch, "C", 12, 64, 77),
+        "episodeP": lambda: gen_episode(torch, "P", 12, 64, 31),
+        "episodeT": lambda: gen_episode(torch, "T", 12, 64, 32),
         "ppo": lambda: gen_ppo(torch),
     }
     for name, fn in jobs.items():

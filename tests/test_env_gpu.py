@@ -13,7 +13,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 from oracle import oracle as O
-from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg, load_yaml, thruster_tables
+from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg, load_yaml, stat_names, thruster_tables
 from tests.test_oracle_golden import TEST_YAML
 
 pytestmark = pytest.mark.gpu
@@ -25,7 +25,7 @@ def _task(cfg_d, n):
     return USVVirtual(cfg_d, num_envs=n, device=DEV, seed=7)
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T"])
 def test_fixture_replay_on_gpu(golden, variant):
     d = golden(f"episode_{variant}.npz")
     cfg_d = json.loads(bytes(d["config_json"]).decode())
@@ -52,7 +52,13 @@ def test_fixture_replay_on_gpu(golden, variant):
         np.testing.assert_allclose(rew.cpu().numpy(), d["rew"][t], rtol=2e-4, atol=2e-4, err_msg=f"rew t={t}")
         np.testing.assert_array_equal(dones.cpu().numpy(), d["reset"][t])
         if len(ids):
-            np.testing.assert_allclose(task.extras_buf.cpu().numpy(), d["extras"][t], rtol=1e-5, atol=1e-6)
+            ex = task.extras_buf.cpu().numpy()
+            if "extras_names" in d:   # GoToPose / TrackXYOVelocity episode_sums keys
+                ex = ex[[slot for _, slot in stat_names(task.cfg)]]
+            np.testing.assert_allclose(ex, d["extras"][t], rtol=1e-5, atol=1e-6)
+        if "tgt_h" in d:
+            np.testing.assert_allclose(task.tgt.cpu().numpy().T, d["tgt"][t], rtol=1e-6, atol=1e-6)
+            np.testing.assert_allclose(task.tgt_h.cpu().numpy(), d["tgt_h"][t], rtol=1e-6, atol=1e-6)
         if "dist" in d:   # disturbance parameters drawn by the reset kernel (USV_disturbances.py:327-508)
             np.testing.assert_allclose(task.dist.cpu().numpy(), d["dist"][t], rtol=1e-6, atol=1e-6)
 
@@ -110,6 +116,30 @@ def test_philox_mode_disturbances_matches_oracle():
         np.testing.assert_array_equal(dones.cpu().numpy(), E.reset_buf, err_msg=f"dones t={t}")
         np.testing.assert_allclose(obs.cpu().numpy(), E.obs, rtol=1e-4, atol=1e-4, err_msg=f"obs t={t}")
         np.testing.assert_allclose(rew.cpu().numpy(), E.rew, rtol=1e-3, atol=1e-3, err_msg=f"rew t={t}")
+
+
+@pytest.mark.parametrize("name", ["GoToPose", "TrackXYOVelocity"])
+def test_philox_mode_pose_tasks_match_oracle(golden, name):
+    """SURVEY A20 tasks at 4096 envs with in-kernel draws vs the oracle (TrackXYOVelocity's
+    all-env angular sum included)."""
+    d = golden("episode_P.npz" if name == "GoToPose" else "episode_T.npz")
+    task_cfg = json.loads(bytes(d["config_json"]).decode())
+    task_cfg["env"]["maxEpisodeLength"] = 25
+    n, T = 4096, 40
+    task = _task(task_cfg, n)
+    E = _oracle_for(task.cfg, n, task_cfg)
+    rng = np.random.default_rng(9)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        bias = task.current_action_bias()
+        obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
+        E.full_step(a, bias, t, seed=task.seed)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dones.cpu().numpy(), E.reset_buf, err_msg=f"dones t={t}")
+        np.testing.assert_allclose(obs.cpu().numpy(), E.obs, rtol=1e-4, atol=1e-4, err_msg=f"obs t={t}")
+        np.testing.assert_allclose(rew.cpu().numpy(), E.rew, rtol=1e-4, atol=1e-4, err_msg=f"rew t={t}")
+        np.testing.assert_array_equal(task.ibuf[0].cpu().numpy(), E.goal_cnt)
+    np.testing.assert_allclose(task.stats.cpu().numpy(), E.stats, rtol=1e-4, atol=1e-3)
 
 
 def _run_field(task, ids, obst, tgt, lin=None):

@@ -10,7 +10,8 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg, load_yaml, parse_penalty_fn, thruster_tables
+from omniisaacgymenvs_loop_amd.tasks.usv_config import (build_usv_cfg, load_yaml, parse_penalty_fn, stat_names,
+                                                         thruster_tables)
 from omniisaacgymenvs_loop_amd._abi import PEN
 import os
 
@@ -108,7 +109,13 @@ def _replay(d, post_only):
             E.reset(ids, d["reset_U"][ru:ru + len(ids)])
             ru += len(ids)
             ex = d["extras"][t]
-            np.testing.assert_allclose(E.extras, ex, rtol=1e-5, atol=1e-6)
+            if "extras_names" in d:   # task-specific episode_sums keys (USV_Virtual.py:584-601)
+                layout = stat_names(cfg)
+                assert [k for k, _ in layout] == [str(k) for k in d["extras_names"]]
+                ex = np.array([ex[i] for i in range(len(layout))], np.float32)
+                np.testing.assert_allclose(E.extras[[sl for _, sl in layout]], ex, rtol=1e-5, atol=1e-6)
+            else:
+                np.testing.assert_allclose(E.extras, ex, rtol=1e-5, atol=1e-6)
         E.step_pre(d["actions"][t], float(d["bias"][t]), d["u_step"][t])
         E.step_physics()
         if post_only:
@@ -133,7 +140,7 @@ def test_episode_c_exercises_disturbances(golden):
     assert (d["dist"][-1][7] < 0).any() and (d["dist"][-1][7] > 0).any()   # torque sign flip
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T"])
 def test_episode_post_physics(golden, variant):
     """obs / reward / done / DR / spawns given the reference's post-integration state."""
     d = golden(f"episode_{variant}.npz")
@@ -151,7 +158,7 @@ def test_episode_post_physics(golden, variant):
         np.testing.assert_array_equal(obst.transpose(2, 0, 1), d["obst"][t])
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T"])
 def test_episode_end_to_end(golden, variant):
     """Full replay incl. this build's integrator; the reference's potential-shaping
     term amplifies ~1e-7 state differences by 100, hence the reward tolerance."""
