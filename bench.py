@@ -32,6 +32,14 @@ FP32_PEAK_TFS = 157.3          # MI355X fp32 vector / f32-MFMA peak (same table)
 # read-modify-write the reference performs every step (25 x 8 B) - counted
 # exactly from k_env_step's loads/stores: 357 B read + 313 B written.
 ENV_STEP_BYTES = 670
+# --task: packaged task yamls and the algorithmic bytes per env-step of their step kernels
+# (k_env_step_task): GoToPose 221 B read + 309 B written; TrackXYOVelocity
+# 221 + 293 in the first launch and 32 + 28 in k_track_finish
+TASKS = {"CaptureXY": ("USV/IROS2024/USV_Virtual_CaptureXY_SysID-TEST", ENV_STEP_BYTES,
+                       "k_env_step (fused 10-substep integrator + obs/reward/done)"),
+         "GoToPose": ("USV/USV_Virtual_GoToPose", 530, "k_env_step_task<GoToPose> (integrator + obs/reward/done)"),
+         "TrackXYOVelocity": ("USV/USV_Virtual_TrackXYOVelocity", 574,
+                              "k_env_step_task<TrackXYO> + k_track_finish (integrator + obs/reward/done)")}
 # PPO minibatch gradient kernel: forward (2*(33*128+128*128+128*3)) + backward
 # (2x the two hidden GEMMs + heads) = 6 x 21,120 + 2 x 384 flops per row.
 PPO_FLOPS_PER_ROW = 2 * (33 * 128 + 128 * 128 + 3 * 128) + 2 * (2 * 128 * 128 + 2 * 33 * 128 + 128 * 128 + 3 * 128)
@@ -52,13 +60,14 @@ def _dist_setup(gpus):
     return rank, world, local
 
 
-def build(envs, local, world, seed):
+def build(envs, local, world, seed, task_name="CaptureXY"):
     from omniisaacgymenvs_loop_amd.envs.vec_env_rlgames import VecEnvRLGames
     from omniisaacgymenvs_loop_amd.rl_games import vecenv
     from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
     from omniisaacgymenvs_loop_amd.scripts.rlgames_train import build_config
     from omniisaacgymenvs_loop_amd.utils.task_util import initialize_task
-    cfg = build_config({"num_envs": envs, "seed": seed, "multi_gpu": world > 1, "rl_device": f"cuda:{local}"})
+    cfg = build_config({"num_envs": envs, "seed": seed, "multi_gpu": world > 1, "rl_device": f"cuda:{local}",
+                        "task": TASKS[task_name][0]})
     cfg["train"]["params"]["config"]["train_dir"] = "/tmp/bench_runs"
     env = VecEnvRLGames(headless=True)
     task = initialize_task(cfg, env)
@@ -146,13 +155,17 @@ def main():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph capture)")
+    ap.add_argument("--task", default="CaptureXY", choices=sorted(TASKS) + ["multitask"],
+                    help="multitask: even ranks GoToPose, odd ranks TrackXYOVelocity, one shared policy (C4)")
     ap.add_argument("--env-only-envs", type=int, default=131072,
                     help="extra env-only throughput probe at the C5 per-GPU size (0 = skip)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
     rank, world, local = _dist_setup(args.gpus)
-    env, task, agent = build(args.envs, local, world, args.seed + rank)
+    task_name = args.task if args.task != "multitask" else ("GoToPose", "TrackXYOVelocity")[rank % 2]
+    step_bytes, step_kernel = TASKS[task_name][1], TASKS[task_name][2]
+    env, task, agent = build(args.envs, local, world, args.seed + rank, task_name)
     agent.use_graph = not args.no_graph
     from omniisaacgymenvs_loop_amd import _capi
 
@@ -250,7 +263,7 @@ def main():
 
     env_ms = env_timer.mean_ms()
     ppo_ms = ppo_timer.mean_ms()
-    achieved = ENV_STEP_BYTES * args.envs / (env_ms * 1e-3) / 1e9
+    achieved = step_bytes * args.envs / (env_ms * 1e-3) / 1e9
     ppo_tfs = PPO_FLOPS_PER_ROW * agent.minibatch_size / (ppo_ms * 1e-3) / 1e12
     extra = {}
     if args.env_only_envs and rank == 0 and world == 1:
@@ -281,10 +294,10 @@ def main():
         bms = big_timer.mean_ms()
         extra = {"env_only_envs": args.env_only_envs, "env_only_fps": args.env_only_envs * nb / tb,
                  "env_step_kernel_ms": bms,
-                 "env_step_kernel_gbs": ENV_STEP_BYTES * args.env_only_envs / (bms * 1e-3) / 1e9,
-                 "env_step_kernel_frac": ENV_STEP_BYTES * args.env_only_envs / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                 "env_step_kernel_gbs": step_bytes * args.env_only_envs / (bms * 1e-3) / 1e9,
+                 "env_step_kernel_frac": step_bytes * args.env_only_envs / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS}
         tf = os.path.join(ROOT, "profiles", f"env_step_traffic_{args.env_only_envs}.json")
-        if os.path.exists(tf):
+        if os.path.exists(tf) and task_name == "CaptureXY":
             with open(tf) as f:
                 tr = json.load(f)
             extra["env_step_kernel_traffic"] = tr.get("bytes_per_launch")
@@ -296,14 +309,16 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init policy, "
             "randomised spawns/obstacles/DR from the reset path)",
-            "config": {"workload": "USV_Virtual_CaptureXY num_envs=4096/GPU PPO-MLP fp32 (BASELINE configs[1])",
+            "config": {"workload": (f"USV_Virtual_CaptureXY num_envs={args.envs}/GPU PPO-MLP fp32 (BASELINE configs[1])"
+                                    if args.task == "CaptureXY" else
+                                    f"USV_Virtual_{args.task} num_envs={args.envs}/GPU PPO-MLP fp32"),
                        "num_envs_per_gpu": args.envs, "horizon_length": agent.horizon_length,
                        "minibatch_size": agent.minibatch_size, "mini_epochs": agent.mini_epochs_num,
                        "parallelism": f"dp{world}"},
             "fps_step_inference": play_fps, "fps_step_env_only": env_fps,
-            "roofline": {"bound": "hbm", "kernel": "k_env_step (fused 10-substep integrator + obs/reward/done)",
+            "roofline": {"bound": "hbm", "kernel": step_kernel,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "bytes_per_env_step": ENV_STEP_BYTES, "launch_ms": env_ms,
+                         "traffic": None, "bytes_per_env_step": step_bytes, "launch_ms": env_ms,
                          "envs_per_launch": args.envs},
             "roofline_ppo": {"bound": "mfma",
                              "kernel": ("k_mb_fused (f32 MFMA fwd+bwd + reduction + Adam, one launch)"
@@ -318,10 +333,10 @@ def main():
         if os.path.exists(traffic_file):
             with open(traffic_file) as f:
                 tr = json.load(f)
-            if tr.get("envs") == args.envs:
+            if tr.get("envs") == args.envs and task_name == "CaptureXY":
                 out["roofline"]["traffic"] = tr.get("bytes_per_launch")
                 out["roofline"]["traffic_source"] = tr.get("source")
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.task == "CaptureXY":
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))
     if world > 1:
