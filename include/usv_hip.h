@@ -248,12 +248,27 @@ typedef struct usv_bufs {
   float   *tgt_h;                  /* [n] GoToPose target heading / TrackXYO target angular velocity (tgt_x/y:
                                       target position / target linear velocity); NULL for CaptureXY */
   float   *task_scratch;           /* TrackXYO: [USV_TS_ROWS][n] + [ceil(n/256)] partial sums; else NULL */
+  /* scene replay (USVVirtual._scene_replay_*, USV_Virtual.py:1329-1457): NULL scene = random spawns */
+  const float *scene;              /* [n_scenes][USV_SCENE_STRIDE] (USV_SC_* layout) */
+  int32_t *scene_next;             /* [n] next scene index of each env (starts at scene_replay.start_index) */
+  int32_t *scene_last;             /* [n] scene index applied at the env's last reset */
+  int32_t n_scenes, scene_cycle;
   /* device step clock (nullable): [0] next step index, [1] next bias-call count,
    * [2] current step, [3] current bias-call count.  When set, usv_reset advances
    * it and the step / bias arguments of usv_reset / usv_env_step are ignored, so
    * a captured HIP graph replays consecutive steps. */
   uint64_t *clock;
 } usv_bufs_t;
+
+/* one replay scene (scripts/build_usv_scenes.py:566-577 keys; obstacles padded to
+ * 16 with limbo (999, 999) past obstacles_count as CaptureXYTask.apply_scene does,
+ * static_obs.py:829-842) */
+#define USV_SC_OBST      0    /* 16 x (x, y) */
+#define USV_SC_START    32    /* start_pos x, y */
+#define USV_SC_YAW      34    /* start_yaw */
+#define USV_SC_VEL      35    /* start_vel x, y */
+#define USV_SC_GOAL     37    /* goal_pos x, y */
+#define USV_SCENE_STRIDE 40
 
 #define USV_FIELD_SLOT_STATS 160   /* 16 + 12 per 2048-cell chunk (11 chunks) */
 
@@ -274,7 +289,8 @@ typedef struct usv_bufs {
 #define USV_CTL_H_STEP_HI  13
 #define USV_CTL_H_INJ_LO   14
 #define USV_CTL_H_INJ_HI   15
-#define USV_CTL_N           16
+#define USV_CTL_SCENE_ERR  16   /* scene replay: an index fell outside [0, n_scenes) with cycle off */
+#define USV_CTL_N           20
 
 /* ------------------------------------------------------------------------ */
 /* Env entry points                                                          */

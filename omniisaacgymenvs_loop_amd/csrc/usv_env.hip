@@ -258,18 +258,48 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         sy = 0.f;
       }
       // ---- pose / velocities / bookkeeping (USV_Virtual.py:1541-1579) ----
-      b.px[e] = sx;
-      b.py[e] = sy;
-      b.yaw[e] = yaw0;
-      b.vx[e] = U(RU_VX) * 3.0f - 1.5f;
-      b.vy[e] = U(RU_VY) * 3.0f - 1.5f;
+      if (b.scene) {
+        // scene replay (_scene_replay_take_scene_indices / _scene_replay_apply, USV_Virtual.py:1372-1457,
+        // CaptureXYTask.apply_scene static_obs.py:785-863): pose, velocity, goal and obstacles from the
+        // env's next scene; the field is built for the NEW goal; no spawn / velocity / goal draws
+        int idx = b.scene_next[e];
+        b.scene_next[e] = idx + 1;
+        const int ns = b.n_scenes;
+        if (b.scene_cycle) {
+          idx %= ns;
+          if (idx < 0) idx += ns;   // torch's floor modulo
+        } else if (idx < 0 || idx >= ns) {
+          atomicOr(&b.ctl[USV_CTL_SCENE_ERR], 1);   // the reference raises IndexError (:1387-1391)
+          idx = min(max(idx, 0), ns - 1);
+        }
+        b.scene_last[e] = idx;
+        const float *sc = b.scene + (size_t)idx * USV_SCENE_STRIDE;
+#pragma unroll
+        for (int q = 0; q < 2 * USV_NOBST; ++q) b.obst[(size_t)q * n + e] = sc[USV_SC_OBST + q];
+        b.px[e] = sc[USV_SC_START];
+        b.py[e] = sc[USV_SC_START + 1];
+        b.yaw[e] = sc[USV_SC_YAW];
+        b.vx[e] = sc[USV_SC_VEL];
+        b.vy[e] = sc[USV_SC_VEL + 1];
+        b.tgt_x[e] = sc[USV_SC_GOAL];
+        b.tgt_y[e] = sc[USV_SC_GOAL + 1];
+        b.field_old_tgt[e] = sc[USV_SC_GOAL];
+        b.field_old_tgt[n + e] = sc[USV_SC_GOAL + 1];
+      } else {
+        b.px[e] = sx;
+        b.py[e] = sy;
+        b.yaw[e] = yaw0;
+        b.vx[e] = U(RU_VX) * 3.0f - 1.5f;
+        b.vy[e] = U(RU_VY) * 3.0f - 1.5f;
+      }
       b.wz[e] = 0.f;
       b.reset_buf[e] = 0;
       b.progress[e] = 0;
       b.prev_cmd[e] = 0.f;
       b.prev_cmd[n + e] = 0.f;
-      // ---- set_targets -> task.get_goals ----
-      if (c.task_kind != USV_TASK_TRACK_XYO) {   // static_obs.py:913-930, USV_go_to_pose.py:229-254
+      // ---- set_targets -> task.get_goals (not called under scene replay, :1613-1616) ----
+      if (b.scene) {
+      } else if (c.task_kind != USV_TASK_TRACK_XYO) {   // static_obs.py:913-930, USV_go_to_pose.py:229-254
         const float g = c.goal_random_position;
         b.tgt_x[e] = U(RU_GOAL) * g * 2.0f - g;
         b.tgt_y[e] = U(RU_GOAL + 1) * g * 2.0f - g;
@@ -292,7 +322,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
     b.ctl[USV_CTL_H_STEP_HI] = (int32_t)(uint32_t)(step >> 32);
     b.ctl[USV_CTL_H_INJ_LO] = (int32_t)(uint32_t)(uintptr_t)inj;
     b.ctl[USV_CTL_H_INJ_HI] = (int32_t)(uint32_t)((uint64_t)(uintptr_t)inj >> 32);
-    b.ctl[USV_CTL_PLACE] = 1;
+    b.ctl[USV_CTL_PLACE] = b.scene ? 0 : 1;   // scene replay: obstacles come from the scene
   }
   // ---- the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612) ----
   __shared__ bool last;
@@ -1398,6 +1428,8 @@ int usv_build_lut(const float *table_l21, const float *table_r21, int n_table, f
 int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t step, const float *u_inject,
               void *stream) {
   if (!cfg || !b || b->n <= 0) return 1;
+  if (b->scene && (b->n_scenes <= 0 || !b->scene_next || !b->scene_last || cfg->task_kind != USV_TASK_CAPTURE_XY))
+    return 1;
   hipStream_t s = (hipStream_t)stream;
   // per-step scratch: reset count, field maxima, extras sums
   hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, s, *b);

@@ -52,7 +52,6 @@ def build_config(ov: Dict[str, Any]) -> Dict[str, Any]:
     rl_device = local_device() if multi_gpu else ov.get("rl_device", "cuda:0")
     num_envs = int(ov.get("num_envs", task["env"]["numEnvs"]))
     task["env"]["numEnvs"] = num_envs
-    task["env"].setdefault("scene_replay", {})["enabled"] = False
     cfg = {"task": task, "train": train, "seed": int(ov.get("seed", 42)), "num_envs": num_envs,
            "rl_device": rl_device, "multi_gpu": multi_gpu, "test": bool(ov.get("test", False)),
            "checkpoint": ov.get("checkpoint", "")}

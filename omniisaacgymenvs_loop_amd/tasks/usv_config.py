@@ -290,8 +290,9 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     c.init_vel = 1.5
     c.stats_on = 1
     c.act_bias, c.act_bias_steps = action_bias_cfg(task_cfg)
-    if bool((env.get("scene_replay", {}) or {}).get("enabled", False)):
-        raise NotImplementedError("scene_replay (NPZ) is not supported yet; set env.scene_replay.enabled=False")
+    if bool((env.get("scene_replay", {}) or {}).get("enabled", False)) and c.task_kind != 0:
+        # only CaptureXYTask implements apply_scene (USV_Virtual.py:1427-1428 raises AttributeError)
+        raise AttributeError("Inner task does not implement apply_scene(); cannot use scene_replay")
     # ---- disturbances (ForceDisturbance / TorqueDisturbance.__init__, USV_disturbances.py:268-298,
     # 412-440) and water current (USVVirtual.__init__ -> ComputeHydrodynamicsEffects) ----
     fd = dist.get("forces", {}) or {}

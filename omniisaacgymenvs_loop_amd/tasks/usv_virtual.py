@@ -12,6 +12,7 @@ kernel launches (reset, potential field, step) with no host synchronisation.
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Any, Dict, Optional
 
 import numpy as np
@@ -138,8 +139,39 @@ class USVVirtual:
         self._tables = torch.tensor(np.stack([tl, tr]), **f32)
         _capi.call("usv_build_lut", _capi.ptr(self._tables[0]), _capi.ptr(self._tables[1]), int(len(tl)),
                    _capi.ptr(self.lut), _capi.stream_ptr())
+        self._init_scene_replay()
         self._bufs = self._make_bufs()
         self.extras: Dict[str, Any] = {}
+
+    def _init_scene_replay(self) -> None:
+        """env.scene_replay (USV_Virtual.py:324-341): scenes on the device, per-env counters."""
+        sr = self._task_cfg["env"].get("scene_replay", {}) or {}
+        self.scene_replay_enabled = bool(sr.get("enabled", False))
+        self.scene = self.scene_next = self.scene_last = None
+        self.scene_replay_num_scenes = 0
+        if not self.scene_replay_enabled:
+            return
+        from .scene_replay import load_scene_arrays, pack_scenes
+        self.scene_replay_npz_path = os.path.abspath(str(sr.get("npz_path", "") or ""))
+        self.scene_replay_cycle = bool(sr.get("cycle", True))
+        rows = pack_scenes(load_scene_arrays(str(sr.get("npz_path", "") or ""), bool(sr.get("strict_hash", True))))
+        self.scene = torch.tensor(rows, device=self._device)
+        self.scene_replay_num_scenes = int(rows.shape[0])
+        n = self._num_envs
+        self.scene_next = torch.full((n,), int(sr.get("start_index", 0) or 0), device=self._device, dtype=torch.int32)
+        self.scene_last = torch.full((n,), -1, device=self._device, dtype=torch.int32)
+
+    @property
+    def scene_replay_last_scene_idx(self) -> torch.Tensor:
+        """Scene index applied at each env's last reset (-1 before the first), on the CPU."""
+        if self.scene_last is None:
+            return torch.full((self._num_envs,), -1, dtype=torch.long)
+        return self.scene_last.long().cpu()
+
+    def check_scene_replay(self) -> None:
+        """Raise the reference's IndexError if a reset ran past the scenes with cycle off (host sync)."""
+        if self.scene is not None and int(self.ctl[DEFINES["USV_CTL_SCENE_ERR"]].item()):
+            raise IndexError(f"scene_replay index out of range: num_scenes={self.scene_replay_num_scenes}")
 
     def _make_bufs(self) -> UsvBufs:
         b = UsvBufs()
@@ -171,6 +203,9 @@ class USVVirtual:
         b.env_org = p(self.env_org)
         b.tgt_h = p(self.tgt_h)
         b.task_scratch = p(self.task_scratch) if self.task_scratch is not None else None
+        if self.scene is not None:
+            b.scene, b.scene_next, b.scene_last = p(self.scene), p(self.scene_next), p(self.scene_last)
+            b.n_scenes, b.scene_cycle = self.scene_replay_num_scenes, int(self.scene_replay_cycle)
         return b
 
     def set_env_origins(self, org: torch.Tensor) -> None:

@@ -38,6 +38,7 @@ def lib():
         P = ctypes.c_void_p
         _lib.oracle_step.argtypes = [P, P, P, P, ctypes.c_float, P]
         _lib.oracle_reset.argtypes = [P, P, ctypes.c_int, P, P]
+        _lib.oracle_reset_scene.argtypes = [P, P, ctypes.c_int, P, P, P]
         _lib.oracle_potential_field.argtypes = [P, ctypes.c_int, P, P, P, P, P]
         _lib.oracle_step_pre.argtypes = [P, P, P, P, ctypes.c_float, P]
         _lib.oracle_step_physics.argtypes = [P, P]
@@ -69,7 +70,7 @@ _PTR_FIELDS =  ("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr",
 
 class _OracleEnvC(ctypes.Structure):
     _fields_ = ([("n", ctypes.c_int)] + [(k, ctypes.c_void_p) for k in _PTR_FIELDS] +
-                [("ctl", ctypes.c_int32 * 16), ("extras", ctypes.c_float * NSTAT), ("dbg", ctypes.c_void_p),
+                [("ctl", ctypes.c_int32 * 20), ("extras", ctypes.c_float * NSTAT), ("dbg", ctypes.c_void_p),
                  ("tmp", ctypes.c_void_p), ("grid_lin", ctypes.c_void_p), ("dist", ctypes.c_void_p),
                  ("env_org", ctypes.c_void_p), ("tgt_h", ctypes.c_void_p)])
 
@@ -122,6 +123,7 @@ class OracleEnv:
         self.dist = np.zeros((NDIST, n), np.float32) if has_dist(cfg) else None
         self.c.dist = _p(self.dist) if self.dist is not None else None
         self.env_org = None
+        self.scenes = None
 
     def set_env_origins(self, org):
         self.env_org = np.ascontiguousarray(org, np.float32).reshape(2, self.n)
@@ -142,7 +144,26 @@ class OracleEnv:
     def reset(self, ids: np.ndarray, U: np.ndarray):
         ids = np.ascontiguousarray(ids, np.int32)
         U = np.ascontiguousarray(U, np.float32).reshape(len(ids), NU_RESET)
-        lib().oracle_reset(ctypes.byref(self.cfg), ctypes.byref(self.c), len(ids), _p(ids), _p(U))
+        rows = None
+        if self.scenes is not None:
+            # USVVirtual._scene_replay_take_scene_indices (USV_Virtual.py:1372-1393)
+            idx = self.scene_next[ids].copy()
+            self.scene_next[ids] += 1
+            if self.scene_cycle:
+                idx = idx % len(self.scenes)
+            elif (idx < 0).any() or (idx >= len(self.scenes)).any():
+                raise IndexError(f"scene_replay index out of range: idx={idx.tolist()}")
+            self.scene_last[ids] = idx
+            rows = np.ascontiguousarray(self.scenes[idx], np.float32)
+        lib().oracle_reset_scene(ctypes.byref(self.cfg), ctypes.byref(self.c), len(ids), _p(ids), _p(U),
+                                 _p(rows) if rows is not None else None)
+
+    def set_scenes(self, rows, start_index=0, cycle=True):
+        """Scene replay: packed scene rows [S][USV_SCENE_STRIDE] and the per-env counters."""
+        self.scenes = np.ascontiguousarray(rows, np.float32)
+        self.scene_next = np.full(self.n, start_index, np.int64)
+        self.scene_last = np.full(self.n, -1, np.int64)
+        self.scene_cycle = cycle
 
     def step(self, actions: np.ndarray, bias: float, U: np.ndarray):
         actions = np.ascontiguousarray(actions, np.float32)

@@ -391,7 +391,15 @@ static float enc_minmax(float x, float xmin, float xmax) {
 /* Reset path: USVVirtual.reset_idx (USV_Virtual.py:1502-1618)               */
 /* ids: compacted reset list (reset_buf.nonzero(), :1045); u: [k][NU_RESET]. */
 /* ------------------------------------------------------------------------ */
+void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids, const float *U,
+                        const float *rows);
 void oracle_reset(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids, const float *U) {
+  oracle_reset_scene(c, E, k, ids, U, NULL);
+}
+
+/* rows: NULL, or [k][USV_SCENE_STRIDE] replay scenes of the reset slots (scene replay) */
+void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids, const float *U,
+                        const float *rows) {
   const int n = E->n;
   if (k <= 0) return;
   float *obst_k = (float *)malloc(sizeof(float) * (size_t)k * USV_NOBST * 2);
@@ -553,6 +561,27 @@ void oracle_reset(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids
         E->tgt_y[e] = u[RU_GOAL + 1] * gl * 2.0f - gl;
         E->tgt_h[e] = u[RU_GOAL_H] * ga * 2.0f - ga;
       }
+      continue;
+    }
+    if (rows) {
+      /* scene replay (USVVirtual._scene_replay_apply, USV_Virtual.py:1395-1457; CaptureXYTask.apply_scene
+       * static_obs.py:785-863): pose / velocity / goal / obstacles from the scene row; the field uses
+       * the NEW goal; no spawn, velocity or goal draws; set_targets is not called */
+      const float *sc = rows + (size_t)s * USV_SCENE_STRIDE;
+      for (int o = 0; o < USV_NOBST; ++o)
+        for (int a = 0; a < 2; ++a) {
+          const float v = sc[USV_SC_OBST + 2 * o + a];
+          E->obst[(o * 2 + a) * n + e] = v;
+          obst_k[(s * USV_NOBST + o) * 2 + a] = v;
+        }
+      E->tgt_x[e] = sc[USV_SC_GOAL]; E->tgt_y[e] = sc[USV_SC_GOAL + 1];
+      tgt_k[s * 2 + 0] = sc[USV_SC_GOAL]; tgt_k[s * 2 + 1] = sc[USV_SC_GOAL + 1];
+      E->px[e] = sc[USV_SC_START]; E->py[e] = sc[USV_SC_START + 1]; E->yaw[e] = sc[USV_SC_YAW];
+      E->vx[e] = sc[USV_SC_VEL]; E->vy[e] = sc[USV_SC_VEL + 1];
+      E->wz[e] = 0.f;
+      E->reset_buf[e] = 0; E->progress[e] = 0;
+      E->prev_cmd[0 * n + e] = 0.f; E->prev_cmd[1 * n + e] = 0.f;
+      for (int q = 0; q < USV_NSTAT; ++q) E->stats[q * n + e] = 0.f;
       continue;
     }
     /* quaternion (cos(yaw/2),0,0,sin(yaw/2)) -> yaw: identical in the planar state */

@@ -332,6 +332,12 @@ def load_task_cfg(variant: str):
         env["water_current"]["use_water_current"] = True
         env["water_current"]["flow_velocity"] = [0.3, -0.2, 0.0]
         env["maxEpisodeLength"] = 30
+    if variant == "S":
+        # scene replay (8f-2): deterministic scenes from tests/golden/scenes_S.npz
+        sr = cfg["env"]["scene_replay"]
+        sr.update(enabled=True, npz_path=os.path.join(OUT, "scenes_S.npz"), start_index=2, cycle=True,
+                  strict_hash=True)
+        cfg["env"]["maxEpisodeLength"] = 24
     if variant in ("P", "T"):
         # SURVEY A20 tasks on the TEST glue: the task's own yaml task/reward parameters
         # (cfg/task/USV/USV_Virtual_GoToPose.yaml, USV_Virtual_TrackXYOVelocity.yaml)
@@ -615,6 +621,26 @@ def _task_targets(task):
     return task._target_positions.numpy().copy(), h
 
 
+def make_scene_file():
+    """tests/golden/scenes_S.npz: 7 scenes in build_usv_scenes.py's format (own writer)."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from omniisaacgymenvs_loop_amd.tasks.scene_replay import write_scenes_npz
+    rng = np.random.default_rng(2024)
+    S, M = 7, 16
+    counts = np.array([16, 0, 5, 16, 9, 3, 12], np.int32)
+    obs = np.full((S, M, 2), np.nan, np.float32)
+    goal = rng.uniform(-2, 2, (S, 2)).astype(np.float32)
+    for i in range(S):
+        obs[i, :counts[i]] = goal[i] + rng.uniform(-12, 12, (counts[i], 2)).astype(np.float32)
+    r = rng.uniform(9, 12, S)
+    th = rng.uniform(0, 2 * np.pi, S)
+    start = np.stack([r * np.cos(th), r * np.sin(th)], 1).astype(np.float32)
+    yaw = rng.uniform(0, np.pi, S).astype(np.float32)
+    vel = rng.uniform(-1.5, 1.5, (S, 2)).astype(np.float32)
+    write_scenes_npz(os.path.join(OUT, "scenes_S.npz"), obs, counts, start, yaw, vel, goal, seed=2024,
+                     generator_cfg={"task_name": "golden", "num_episodes": S})
+
+
 def gen_episode(torch, variant, n, steps, seed):
     torch.manual_seed(seed)
     usv, heron, world, task_cfg = build_usv(torch, n, variant)
@@ -704,6 +730,8 @@ def gen_episode(torch, variant, n, steps, seed):
                                            tk._total_reward, pen.angular_vel_penalty,
                                            pen.angular_vel_variation_penalty, pen.energy_penalty,
                                            tk._danger_factor, tk.prev_potential], 1).numpy().astype(np.float32))
+            if variant == "S":
+                data.setdefault("scene_last", []).append(usv.scene_replay_last_scene_idx.numpy().copy())
             if variant == "C":
                 uf, td_ = usv.UF, usv.TD
                 data.setdefault("dist", []).append(torch.stack([
@@ -873,6 +901,7 @@ def main():
         "episodeB": lambda: gen_episode(torch, "B", 12, 56, 99),
         "episodeC": lambda: gen_episode(torch, "C", 12, 64, 77),
         "episodeP": lambda: gen_episode(torch, "P", 12, 64, 31),
+        "episodeS": lambda: (make_scene_file(), gen_episode(torch, "S", 6, 64, 41)),
         "episodeT": lambda: gen_episode(torch, "T", 12, 64, 32),
         "ppo": lambda: gen_ppo(torch),
     }

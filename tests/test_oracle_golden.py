@@ -15,6 +15,7 @@ from omniisaacgymenvs_loop_amd.tasks.usv_config import (build_usv_cfg, load_yaml
 from omniisaacgymenvs_loop_amd._abi import PEN
 import os
 
+GOLDEN_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 TEST_YAML = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "omniisaacgymenvs_loop_amd",
                          "cfg", "task", "USV", "IROS2024", "USV_Virtual_CaptureXY_SysID-TEST.yaml")
 
@@ -98,6 +99,9 @@ def _replay(d, post_only):
     T, n = d["obs"].shape[:2]
     E = O.OracleEnv(cfg, n, lut)
     E.set_grid_lin(d["grid_lin"])
+    if "scene_last" in d:   # scene replay: the fixture's scene file, start_index / cycle of its config
+        sr = cfg_d["env"]["scene_replay"]
+        E.set_scenes(scene_rows(), int(sr["start_index"]), bool(sr["cycle"]))
     E.tgt_x[:] = d["init_tgt"][:, 0]
     E.tgt_y[:] = d["init_tgt"][:, 1]
     ru = 0
@@ -109,25 +113,57 @@ def _replay(d, post_only):
             E.reset(ids, d["reset_U"][ru:ru + len(ids)])
             ru += len(ids)
             ex = d["extras"][t]
+            # episode means of per-step sums; end to end they carry the integrator's ~1e-7 drift
+            rtol, atol = (1e-5, 1e-6) if post_only else (1e-4, 1e-5)
             if "extras_names" in d:   # task-specific episode_sums keys (USV_Virtual.py:584-601)
                 layout = stat_names(cfg)
                 assert [k for k, _ in layout] == [str(k) for k in d["extras_names"]]
                 ex = np.array([ex[i] for i in range(len(layout))], np.float32)
-                np.testing.assert_allclose(E.extras[[sl for _, sl in layout]], ex, rtol=1e-5, atol=1e-6)
+                np.testing.assert_allclose(E.extras[[sl for _, sl in layout]], ex, rtol=rtol, atol=atol)
             else:
-                np.testing.assert_allclose(E.extras, ex, rtol=1e-5, atol=1e-6)
+                np.testing.assert_allclose(E.extras, ex, rtol=rtol, atol=atol)
         E.step_pre(d["actions"][t], float(d["bias"][t]), d["u_step"][t])
         E.step_physics()
         if post_only:
             for k in ("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr"):
                 getattr(E, k)[:] = d[k][t]
         E.step_post(d["u_step"][t])
+        if "scene_last" in d:
+            np.testing.assert_array_equal(E.scene_last, d["scene_last"][t])
         if "dist" in d:
             # ForceDisturbance / TorqueDisturbance parameters drawn at reset (USV_disturbances.py:327-508)
             np.testing.assert_allclose(E.dist, d["dist"][t], rtol=1e-6, atol=1e-6, err_msg=f"dist step {t}")
         out.append((E.obs.copy(), E.rew.copy(), E.reset_buf.copy(), E.mass.copy(), E.k_drag.copy(), E.thr_l.copy(),
                     E.thr_r.copy(), E.k_iz.copy(), E.obst.copy(), E.progress.copy(), E.goal_cnt.copy()))
     return out
+
+
+def scene_rows():
+    from omniisaacgymenvs_loop_amd.tasks.scene_replay import load_scene_arrays, pack_scenes
+    return pack_scenes(load_scene_arrays(os.path.join(GOLDEN_DIR, "scenes_S.npz")))
+
+
+def test_scene_file_format_and_hash(tmp_path):
+    """build_usv_scenes.py format: required keys, NaN padding -> limbo past obstacles_count, sha1 sidecar."""
+    from omniisaacgymenvs_loop_amd.tasks import scene_replay as SR
+    rows = scene_rows()
+    d = np.load(os.path.join(GOLDEN_DIR, "scenes_S.npz"), allow_pickle=False)
+    assert rows.shape == (7, 40)
+    for i, cnt in enumerate(d["obstacles_count"]):
+        ob = rows[i, :32].reshape(16, 2)
+        np.testing.assert_array_equal(ob[:cnt], d["obstacles_xy"][i, :cnt])
+        assert (ob[cnt:] == 999.0).all()
+    np.testing.assert_array_equal(rows[:, 37:39], d["goal_pos"])
+    bad = tmp_path / "s.npz"
+    SR.write_scenes_npz(str(bad), d["obstacles_xy"], d["obstacles_count"], d["start_pos"], d["start_yaw"],
+                        d["start_vel"], d["goal_pos"])
+    SR.load_scene_arrays(str(bad))
+    (tmp_path / "s.npz.sha1").write_text("0" * 40)
+    with pytest.raises(ValueError):
+        SR.load_scene_arrays(str(bad))
+    SR.load_scene_arrays(str(bad), strict_hash=False)
+    with pytest.raises(FileNotFoundError):
+        SR.load_scene_arrays(str(tmp_path / "missing.npz"))
 
 
 def test_episode_c_exercises_disturbances(golden):
@@ -140,7 +176,7 @@ def test_episode_c_exercises_disturbances(golden):
     assert (d["dist"][-1][7] < 0).any() and (d["dist"][-1][7] > 0).any()   # torque sign flip
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T", "S"])
 def test_episode_post_physics(golden, variant):
     """obs / reward / done / DR / spawns given the reference's post-integration state."""
     d = golden(f"episode_{variant}.npz")
@@ -158,7 +194,7 @@ def test_episode_post_physics(golden, variant):
         np.testing.assert_array_equal(obst.transpose(2, 0, 1), d["obst"][t])
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T", "S"])
 def test_episode_end_to_end(golden, variant):
     """Full replay incl. this build's integrator; the reference's potential-shaping
     term amplifies ~1e-7 state differences by 100, hence the reward tolerance."""
