@@ -77,6 +77,10 @@ def lib():
     global _lib
     if _lib is None:
         path = PROBE_LIB_PATH if os.getenv("USV_HIP_PROBE") == "1" else LIB_PATH
+        # A/B builds of the same ABI (tools/gpu_ab.sh): lib/<name>.so inside the tree only
+        alt = os.getenv("USV_HIP_LIB")
+        if alt:
+            path = os.path.join(LIB_DIR, os.path.basename(alt))
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
                                f"g.build()'` (hipcc --offload-arch=gfx950)")
