@@ -543,8 +543,10 @@ __device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__
       const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
       const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
       // d nlp / d logstd = 1 - z^2 (through sigma = exp(logstd) and the sum of logstd)
-      gs0 = dnlp * (1.f - z0 * z0);
-      gs1 = dnlp * (1.f - z1 * z1);
+      // - entropy_coef * mean(entropy): d entropy / d logstd = 1 per row (Normal.entropy, fixed sigma)
+      const float dent = -c.entropy_coef * invB;
+      gs0 = dnlp * (1.f - z0 * z0) + dent;
+      gs1 = dnlp * (1.f - z1 * z1) + dent;
       const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
       // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
       const float om0 = e_mu[row * 2], om1 = e_mu[row * 2 + 1];

@@ -194,8 +194,6 @@ class A2CAgent:
         c.reward_scale = float(rs.get("scale_value", 1.0))
         c.reward_shift = float(rs.get("shift_value", 0.0))
         c.rms_eps = 1e-5
-        if c.entropy_coef != 0.0:
-            raise NotImplementedError("entropy_coef != 0 (gradient of the entropy bonus) is not implemented")
         self._alloc()
         self.frame = 0
         self.epoch_num = 0

@@ -178,7 +178,8 @@ def minibatch_grad(P: dict, xn, act, old_nlp, old_val, ret, adv, old_mu, old_sig
     bh, bl = np.maximum(mu - F(1.1), 0), np.minimum(mu + F(1.1), 0)
     b_loss = (bl ** 2 + bh ** 2).sum(-1)
     dmu = dnlp[:, None] * (-z / sigma) + F(cfg.bounds_loss_coef / B) * F(2) * (bh + bl)
-    dsig = (dnlp[:, None] * (F(1) - z * z)).sum(0)
+    # loss - entropy_coef * mean(entropy) (a2c_continuous.py:159): d entropy / d logstd = 1 per row
+    dsig = (dnlp[:, None] * (F(1) - z * z) + F(-cfg.entropy_coef / B)).sum(0)
     ent = (F(0.5) + F(0.5 * math.log(2 * math.pi)) + logstd).sum(-1)
     kl = (np.log(old_sigma / sigma + F(1e-5)) + (sigma ** 2 + (old_mu - mu) ** 2) /
           (F(2) * (old_sigma ** 2 + F(1e-5))) - F(0.5)).sum(-1).mean()

@@ -138,10 +138,13 @@ def test_minibatch_epoch_vs_reference(ppo):
         np.testing.assert_allclose(Pf[k], v, rtol=0, atol=5e-5, err_msg=k)
 
 
-def test_minibatch_gradient_vs_oracle_full_size():
-    """One 8192-row minibatch (BASELINE minibatch_size) vs the numpy oracle's gradient."""
+@pytest.mark.parametrize("entropy_coef", [0.0, 0.01])
+def test_minibatch_gradient_vs_oracle_full_size(entropy_coef):
+    """One 8192-row minibatch (BASELINE minibatch_size) vs the numpy oracle's gradient (with and without
+    the entropy bonus of a2c_continuous.py:159)."""
     N, H = 512, 16
     ag = _agent(N, 8192, mini_epochs=1)
+    ag.cfg.entropy_coef = entropy_coef
     rng = np.random.default_rng(0)
     B = N * H
     obs = rng.normal(0, 2, (B, 33)).astype(np.float32)
@@ -169,7 +172,7 @@ def test_minibatch_gradient_vs_oracle_full_size():
     orms.update(obs)
     np.testing.assert_allclose(ag.obs_rms.cpu().numpy()[:33], orms.mean, rtol=1e-6, atol=1e-9)
     g_ref, losses, kl, _, _ = PO.minibatch_grad(P, orms.norm(obs), act, nlp0, val, ret, adv, mu0 + 0.01, sig0,
-                                                PO.PPOConfig(minibatch=8192))
+                                                PO.PPOConfig(minibatch=8192, entropy_coef=entropy_coef))
     g = ag.grad.cpu().numpy()[:PO.NPARAM]
     scale = np.abs(g_ref).max()
     np.testing.assert_allclose(g, g_ref, rtol=0, atol=2e-4 * scale)
