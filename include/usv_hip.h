@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define USV_NOBS        33   /* obs dim: 3 + (5 + 5*3) + 2 + 8   (tasks/USV/USV_core.py:46) */
+#define USV_NOBS        33   /* obs row: 3 + (5 + 5*3) + 2 + priv_dim (tasks/USV/USV_core.py:46), priv_dim <= 8 */
+#define USV_NOBS_BASE   25   /* columns before the privileged tail; a priv_dim = 4 row is the reference's
+                                29 columns followed by 4 zero columns (the policy's padded input) */
 #define USV_NOBST       16   /* obstacles per env                 (USV_capture_xy_static_obs.py:70) */
 #define USV_NCLOSE       5   /* closest obstacles in obs          (USV_core.py:33) */
 #define USV_GRID       150   /* potential-field grid              (USV_capture_xy_static_obs.py:30) */

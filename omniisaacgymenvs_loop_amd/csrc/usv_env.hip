@@ -457,7 +457,7 @@ template <class Put>
 __device__ __forceinline__ void write_priv_tail(const usv_cfg_t &c, const StepK &K, float m, float comx, float comy,
                                                 float comz, float k_drag, float thr_l, float thr_r, float k_iz,
                                                 Put put) {
-  const int pt = USV_NOBS - c.priv_dim;
+  const int pt = USV_NOBS_BASE;
   if (c.masscom_base) {
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   auto put = [&](int q, float v) { obs[q] = clampt(v, -clip, clip); };
   obs[6] = 0.f;
   obs[7] = 0.f;
-  if (c.priv_dim == 4) { obs[23] = 0.f; obs[24] = 0.f; obs[25] = 0.f; obs[26] = 0.f; }
+  if (c.priv_dim == 4) { obs[29] = 0.f; obs[30] = 0.f; obs[31] = 0.f; obs[32] = 0.f; }   // input padding
   {
     // ---- every per-env input that does not depend on this step's results is loaded
     // up front, so the HBM latencies overlap each other and the physics ----
@@ -804,7 +804,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       put(9 + 3 * q, div_rn(-vbx, nf, inv_nf));
       put(10 + 3 * q, div_rn(-vby, nf, inv_nf));
     }
-    const int pa = USV_NOBS - c.priv_dim - 2;
+    const int pa = USV_NOBS_BASE - 2;
     put(pa, prev_cmd0);
     put(pa + 1, prev_cmd1);
     bst(R, w.prev_cmd, vs, prev_cmd0);
@@ -1100,9 +1100,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(usv_cfg_t c, usv_bufs_
   put(2, wzn);
 #pragma unroll
   for (int q = 3; q < USV_NOBS - 10; ++q) obs[q] = 0.f;   // task_data columns no task writes
-  const int pa = USV_NOBS - c.priv_dim - 2;
-  for (int q = pa + 2; q < USV_NOBS - c.priv_dim; ++q) obs[q] = 0.f;
-  if (c.priv_dim == 4) { obs[23] = 0.f; obs[24] = 0.f; obs[25] = 0.f; obs[26] = 0.f; }
+  const int pa = USV_NOBS_BASE - 2;
+  if (c.priv_dim == 4) { obs[29] = 0.f; obs[30] = 0.f; obs[31] = 0.f; obs[32] = 0.f; }   // input padding
   put(pa, prev_cmd0);
   put(pa + 1, prev_cmd1);
   write_priv_tail(c, K, m, comx, comy, comz, k_drag, thr_l, thr_r, k_iz, put);

@@ -86,10 +86,11 @@ class DefaultAlgoObserver:
         pass
 
 
-def default_linear_init(seed: int) -> torch.Tensor:
+def default_linear_init(seed: int, obs_dim: int = NIN) -> torch.Tensor:
     """PyTorch nn.Linear default init in the reference's construction order
-    (actor_mlp 33->128, 128->128, value 128->1, mu 128->2), biases zeroed,
-    sigma = const 0 (network_builder.py:1520-1575)."""
+    (actor_mlp obs_dim->128, 128->128, value 128->1, mu 128->2), biases zeroed,
+    sigma = const 0 (network_builder.py:1520-1575).  obs_dim < NIN: W1's extra
+    columns are zero (the padded input of a priv_dim = 4 task)."""
     g = torch.Generator().manual_seed(int(seed))
     parts = {"sigma": torch.zeros(NA)}
 
@@ -99,7 +100,8 @@ def default_linear_init(seed: int) -> torch.Tensor:
         torch.rand((o,), generator=g)   # bias draw (then zeroed by the builder)
         return w, torch.zeros(o)
 
-    W1, b1 = lin(NIN, NH)
+    W1, b1 = lin(obs_dim, NH)
+    W1 = torch.cat([W1, torch.zeros(NH, NIN - obs_dim)], 1)
     W2, b2 = lin(NH, NH)
     Wv, bv = lin(NH, 1)
     Wmu, bmu = lin(NH, NA)
@@ -144,8 +146,11 @@ class A2CAgent:
                 inner._task.update_state()
         obs_space = self.env_info["observation_space"]
         obs_shape = obs_space.spaces["state"].shape if hasattr(obs_space, "spaces") else obs_space.shape
-        if tuple(obs_shape) != (NIN,):
-            raise ValueError(f"observation 'state' must be ({NIN},), got {obs_shape}")
+        if len(obs_shape) != 1 or not (0 < obs_shape[0] <= NIN):
+            raise ValueError(f"observation 'state' must be (k,) with k <= {NIN}, got {obs_shape}")
+        # k < NIN (priv_dim = 4 tasks: 29): the kernels keep NIN inputs, the extra W1 columns see zero
+        # inputs, get zero gradients and stay zero -- exactly the reference's k-input network
+        self.obs_dim = int(obs_shape[0])
         self.actions_num = self.env_info["action_space"].shape[0]
         if self.actions_num != NA:
             raise ValueError(f"action space must have {NA} dims")
@@ -219,12 +224,21 @@ class A2CAgent:
         self._eager_epochs = 0
         self.algo_observer.after_init(self)
 
+    def _obs_in(self, obs: torch.Tensor) -> torch.Tensor:
+        """The policy kernels' [N, NIN] input: the env rows as they are, or (obs_dim < NIN) copied into
+        the zero-padded buffer."""
+        if self._obs_pad is None:
+            return obs if obs.is_contiguous() else obs.contiguous()
+        self._obs_pad[:, :self.obs_dim].copy_(obs)
+        return self._obs_pad
+
     # ------------------------------------------------------------ buffers
     def _alloc(self):
         dev = self.ppo_device
         f32, f64 = dict(device=dev, dtype=torch.float32), dict(device=dev, dtype=torch.float64)
         N, H = self.num_actors, self.horizon_length
-        self.model_params = default_linear_init(self.seed).to(dev)
+        self.model_params = default_linear_init(self.seed, self.obs_dim).to(dev)
+        self._obs_pad = torch.zeros((N, NIN), **f32) if self.obs_dim < NIN else None
         if self.multi_gpu:
             dist_util.broadcast_params(self.model_params, 0)   # a2c_common.py:1354 (initial weights from rank 0)
         self.adam_m = torch.zeros(NPARAM, **f32)
@@ -274,7 +288,7 @@ class A2CAgent:
         self.meter.zero_()
         step_time = 0.0
         for n in range(self.horizon_length):
-            obs = self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"]
+            obs = self._obs_in(self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"])
             c.call("ppo_policy_step", cfg, c.ptr(self.model_params), c.ptr(self.obs_rms), c.ptr(self.val_rms),
                    c.ptr(obs), n, c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp),
                    c.ptr(self.exp_val), c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.exp_done),
@@ -293,7 +307,7 @@ class A2CAgent:
     def prepare_dataset(self) -> None:
         """GAE + returns + value RMS + advantage normalisation (a2c_common.py:525-540, 1257-1332)."""
         c = _capi
-        obs = self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"]
+        obs = self._obs_in(self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"])
         c.call("ppo_prepare", c.byref(self.cfg), c.ptr(self.model_params), c.ptr(self.obs_rms),
                c.ptr(self.val_rms), c.ptr(obs), c.ptr(self.dones), c.ptr(self.exp_done), c.ptr(self.exp_val),
                c.ptr(self.exp_rew), c.ptr(self.exp_ret), c.ptr(self.exp_adv), c.ptr(self.work), c.stream_ptr())
@@ -466,18 +480,18 @@ class A2CAgent:
     # ----------------------------------------------------------- checkpoints
     def get_full_state_weights(self) -> Dict[str, Any]:
         step = float(self.opt[1].item())
-        return {"model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms),
+        return {"model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms, self.obs_dim),
                 "epoch": self.epoch_num,
                 "optimizer": ckpt.optimizer_state_dict(self.adam_m, self.adam_v, step, float(self.opt[0].item()),
-                                                       self.cfg.weight_decay),
+                                                       self.cfg.weight_decay, self.obs_dim),
                 "frame": self.frame,
                 "last_mean_rewards": self.last_mean_rewards,
                 "env_state": self.vec_env.get_env_state() if self.vec_env is not None else None}
 
     def set_full_state_weights(self, weights: Dict[str, Any]) -> None:
-        ckpt.load_model_state_dict(weights["model"], self.model_params, self.obs_rms, self.val_rms)
+        ckpt.load_model_state_dict(weights["model"], self.model_params, self.obs_rms, self.val_rms, self.obs_dim)
         self.epoch_num = int(weights["epoch"])
-        step, lr = ckpt.load_optimizer_state_dict(weights["optimizer"], self.adam_m, self.adam_v)
+        step, lr = ckpt.load_optimizer_state_dict(weights["optimizer"], self.adam_m, self.adam_v, self.obs_dim)
         self.opt[1] = step
         self.opt[0] = lr
         self.last_lr = lr
@@ -493,7 +507,7 @@ class A2CAgent:
         self.set_full_state_weights(ckpt.load_checkpoint(fn))
 
     def get_weights(self):
-        return {"model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms)}
+        return {"model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms, self.obs_dim)}
 
     def set_weights(self, weights):
-        ckpt.load_model_state_dict(weights["model"], self.model_params, self.obs_rms, self.val_rms)
+        ckpt.load_model_state_dict(weights["model"], self.model_params, self.obs_rms, self.val_rms, self.obs_dim)

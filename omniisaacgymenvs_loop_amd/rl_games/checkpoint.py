@@ -33,16 +33,31 @@ NPARAM = sum(int(np.prod(s)) for _, s in PARAM_LAYOUT)
 assert NPARAM == DEFINES["PPO_NPARAM"]
 
 
-def split_flat(flat: torch.Tensor) -> Dict[str, torch.Tensor]:
+W1_KEY = "a2c_network.actor_mlp.0.weight"
+
+
+def split_flat(flat: torch.Tensor, obs_dim: int = NIN) -> Dict[str, torch.Tensor]:
+    """Flat parameter vector -> state_dict tensors; obs_dim < NIN drops W1's zero padding columns
+    (the reference's network of a priv_dim = 4 task has obs_dim = 29 inputs)."""
     out, o = OrderedDict(), 0
     for k, s in PARAM_LAYOUT:
         m = int(np.prod(s))
         out[k] = flat[o:o + m].view(*s)
+        if k == W1_KEY:
+            out[k] = out[k][:, :obs_dim]
         o += m
     return out
 
 
-def model_state_dict(params: torch.Tensor, obs_rms: torch.Tensor, val_rms: torch.Tensor) -> "OrderedDict":
+def _pad_w1(t: torch.Tensor) -> torch.Tensor:
+    """[NH, k] -> [NH, NIN] with zero columns (k <= NIN)."""
+    if t.shape[1] == NIN:
+        return t
+    return torch.cat([t, torch.zeros(t.shape[0], NIN - t.shape[1], dtype=t.dtype)], 1)
+
+
+def model_state_dict(params: torch.Tensor, obs_rms: torch.Tensor, val_rms: torch.Tensor,
+                     obs_dim: int = NIN) -> "OrderedDict":
     """ModelA2CContinuousLogStd.state_dict() key order: value_mean_std, running_mean_std, a2c_network."""
     sd = OrderedDict()
     v = val_rms.detach().cpu()
@@ -50,35 +65,38 @@ def model_state_dict(params: torch.Tensor, obs_rms: torch.Tensor, val_rms: torch
     sd["value_mean_std.running_mean"] = v[0:1].clone()
     sd["value_mean_std.running_var"] = v[1:2].clone()
     sd["value_mean_std.count"] = v[2].clone()
-    sd["running_mean_std.running_mean_std.state.running_mean"] = o[0:NIN].clone()
-    sd["running_mean_std.running_mean_std.state.running_var"] = o[NIN:2 * NIN].clone()
+    sd["running_mean_std.running_mean_std.state.running_mean"] = o[0:obs_dim].clone()
+    sd["running_mean_std.running_mean_std.state.running_var"] = o[NIN:NIN + obs_dim].clone()
     sd["running_mean_std.running_mean_std.state.count"] = o[2 * NIN].clone()
-    for k, t in split_flat(params.detach().cpu()).items():
+    for k, t in split_flat(params.detach().cpu(), obs_dim).items():
         sd[k] = t.clone()
     return sd
 
 
 def load_model_state_dict(sd: Dict[str, torch.Tensor], params: torch.Tensor, obs_rms: torch.Tensor,
-                          val_rms: torch.Tensor) -> None:
+                          val_rms: torch.Tensor, obs_dim: int = NIN) -> None:
     for k, s in PARAM_LAYOUT:
-        if tuple(sd[k].shape) != tuple(s):
-            raise ValueError(f"checkpoint tensor {k} has shape {tuple(sd[k].shape)}, expected {s}")
-    flat = torch.cat([sd[k].reshape(-1).to(torch.float32) for k, _ in PARAM_LAYOUT])
+        want = (NH, obs_dim) if k == W1_KEY else tuple(s)
+        if tuple(sd[k].shape) != want:
+            raise ValueError(f"checkpoint tensor {k} has shape {tuple(sd[k].shape)}, expected {want}")
+    flat = torch.cat([(_pad_w1(sd[k].float()) if k == W1_KEY else sd[k]).reshape(-1).to(torch.float32)
+                      for k, _ in PARAM_LAYOUT])
     params.copy_(flat.to(params.device))
-    o = torch.cat([sd["running_mean_std.running_mean_std.state.running_mean"].double(),
-                   sd["running_mean_std.running_mean_std.state.running_var"].double(),
-                   sd["running_mean_std.running_mean_std.state.count"].double().reshape(1)])
-    obs_rms[:o.numel()].copy_(o.to(obs_rms.device))
+    o = obs_rms.detach().cpu().clone()
+    o[0:obs_dim] = sd["running_mean_std.running_mean_std.state.running_mean"].double()
+    o[NIN:NIN + obs_dim] = sd["running_mean_std.running_mean_std.state.running_var"].double()
+    o[2 * NIN] = sd["running_mean_std.running_mean_std.state.count"].double().reshape(())
+    obs_rms.copy_(o.to(obs_rms.device))
     v = torch.cat([sd["value_mean_std.running_mean"].double(), sd["value_mean_std.running_var"].double(),
                    sd["value_mean_std.count"].double().reshape(1)])
     val_rms[:3].copy_(v.to(val_rms.device))
 
 
 def optimizer_state_dict(adam_m: torch.Tensor, adam_v: torch.Tensor, step: float, lr: float,
-                         weight_decay: float = 0.0) -> Dict[str, Any]:
+                         weight_decay: float = 0.0, obs_dim: int = NIN) -> Dict[str, Any]:
     """torch.optim.Adam.state_dict() layout (one param group, params 0..8)."""
-    m = split_flat(adam_m.detach().cpu())
-    v = split_flat(adam_v.detach().cpu())
+    m = split_flat(adam_m.detach().cpu(), obs_dim)
+    v = split_flat(adam_v.detach().cpu(), obs_dim)
     state = {}
     for i, (k, _) in enumerate(PARAM_LAYOUT):
         state[i] = {"step": torch.tensor(float(step)), "exp_avg": m[k].clone(), "exp_avg_sq": v[k].clone()}
@@ -88,7 +106,7 @@ def optimizer_state_dict(adam_m: torch.Tensor, adam_v: torch.Tensor, step: float
     return {"state": state, "param_groups": [group]}
 
 
-def load_optimizer_state_dict(osd: Dict[str, Any], adam_m: torch.Tensor, adam_v: torch.Tensor):
+def load_optimizer_state_dict(osd: Dict[str, Any], adam_m: torch.Tensor, adam_v: torch.Tensor, obs_dim: int = NIN):
     ms, vs, step = [], [], 0.0
     for i, (k, s) in enumerate(PARAM_LAYOUT):
         st = osd["state"].get(i)
@@ -96,8 +114,9 @@ def load_optimizer_state_dict(osd: Dict[str, Any], adam_m: torch.Tensor, adam_v:
             ms.append(torch.zeros(int(np.prod(s))))
             vs.append(torch.zeros(int(np.prod(s))))
             continue
-        ms.append(st["exp_avg"].reshape(-1).float())
-        vs.append(st["exp_avg_sq"].reshape(-1).float())
+        fix = (lambda t: _pad_w1(t.reshape(NH, obs_dim))) if k == W1_KEY else (lambda t: t)
+        ms.append(fix(st["exp_avg"].float()).reshape(-1))
+        vs.append(fix(st["exp_avg_sq"].float()).reshape(-1))
         step = float(st["step"])
     adam_m.copy_(torch.cat(ms).to(adam_m.device))
     adam_v.copy_(torch.cat(vs).to(adam_v.device))

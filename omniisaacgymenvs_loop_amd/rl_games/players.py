@@ -31,7 +31,10 @@ class PpoPlayerContinuous:
         self.games_num = int(pcfg.get("games_num", 2000))
         self.max_steps = int(pcfg.get("max_steps", 27000))
         dev = self.device
-        self.model_params = default_linear_init(int(params.get("seed", 42))).to(dev)
+        info = self.env.get_env_info()
+        osp = info["observation_space"]
+        self.obs_dim = int((osp.spaces["state"].shape if hasattr(osp, "spaces") else osp.shape)[0])
+        self.model_params = default_linear_init(int(params.get("seed", 42)), self.obs_dim).to(dev)
         self.obs_rms = torch.zeros(2 * NIN + 1, device=dev, dtype=torch.float64)
         self.obs_rms[NIN:2 * NIN] = 1.0
         self.obs_rms[2 * NIN] = 1.0
@@ -52,14 +55,18 @@ class PpoPlayerContinuous:
         self._dones = torch.zeros(N, device=dev, dtype=torch.int64)
         self._actions = torch.zeros((N, NA), **f32)
         self._step = 0
+        self._obs_pad = torch.zeros((N, NIN), **f32) if self.obs_dim < NIN else None
 
     def restore(self, fn: str) -> None:
         w = ckpt.load_checkpoint(fn)
-        ckpt.load_model_state_dict(w["model"], self.model_params, self.obs_rms, self.val_rms)
+        ckpt.load_model_state_dict(w["model"], self.model_params, self.obs_rms, self.val_rms, self.obs_dim)
 
     def get_action(self, obs: torch.Tensor, is_deterministic: bool = True) -> torch.Tensor:
         c = _capi
         sc = self._scratch
+        if self._obs_pad is not None:   # k-input network: zero-padded to the kernels' NIN inputs
+            self._obs_pad[:, :self.obs_dim].copy_(obs)
+            obs = self._obs_pad
         c.call("ppo_policy_step", c.byref(self.cfg), c.ptr(self.model_params), c.ptr(self.obs_rms),
                c.ptr(self.val_rms), c.ptr(obs.contiguous()), 0, c.ptr(sc["obs"]), c.ptr(sc["act"]), c.ptr(sc["nlp"]),
                c.ptr(sc["val"]), c.ptr(sc["mu"]), c.ptr(sc["sigma"]), c.ptr(self._done8), c.ptr(self._dones),

@@ -59,7 +59,9 @@ class USVVirtual:
         self.rl_device = rl_device or device
         self.cfg = build_usv_cfg(task_cfg)
         self._max_episode_length = int(task_cfg["env"]["maxEpisodeLength"])
-        self._num_observations = NOBS
+        # the reference's obs width: 3 + (5 + 5*3) + 2 + priv_dim (USV_core.py:46); the device rows keep
+        # NOBS columns (a priv_dim = 4 row ends in 4 zero columns: the policy's padded input)
+        self._num_observations = DEFINES["USV_NOBS_BASE"] + int(self.cfg.priv_dim)
         self._num_actions = 2
         self._num_states = 0
         self._num_agents = 1
@@ -68,7 +70,7 @@ class USVVirtual:
         self.control_frequency_inv = int(task_cfg["env"].get("controlFrequencyInv", 10))
         self.randomize_actions = False
         self.randomize_observations = False
-        self.observation_space = DictSpace({"state": Box(-np.inf, np.inf, (NOBS,))})
+        self.observation_space = DictSpace({"state": Box(-np.inf, np.inf, (self._num_observations,))})
         self.action_space = Box(np.array([-1.0, -1.0], np.float32), np.array([1.0, 1.0], np.float32))
         self.state_space = Box(-np.inf, np.inf, (0,))
         self._initial_action_bias, self._initial_action_bias_steps = action_bias_cfg(task_cfg)
@@ -140,6 +142,8 @@ class USVVirtual:
         _capi.call("usv_build_lut", _capi.ptr(self._tables[0]), _capi.ptr(self._tables[1]), int(len(tl)),
                    _capi.ptr(self.lut), _capi.stream_ptr())
         self._init_scene_replay()
+        # what step() returns: the reference's obs columns (a strided view of the NOBS-wide rows)
+        self.obs_view = self.obs_buf_t[:, :self._num_observations]
         self._bufs = self._make_bufs()
         self.extras: Dict[str, Any] = {}
 
@@ -248,7 +252,7 @@ class USVVirtual:
 
     @property
     def obs_buf(self) -> Dict[str, torch.Tensor]:
-        return {"state": self.obs_buf_t}
+        return {"state": self.obs_view}
 
     def reset(self) -> None:
         """RLTask.reset: flag every env for reset (rl_task.py:268-270)."""
@@ -291,7 +295,7 @@ class USVVirtual:
             _capi.call("usv_potential_field", cfg, b, s)
         _capi.call("usv_env_step", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
                    self.seed, k, _capi.ptr(u_step), s)
-        return self.obs_buf_t, self.rew_buf, self.dones
+        return self.obs_view, self.rew_buf, self.dones
 
     def _f32(self, actions: torch.Tensor) -> torch.Tensor:
         if actions.dtype != torch.float32 or not actions.is_contiguous():

@@ -758,7 +758,7 @@ static void priv_tail(const usv_cfg_t *c, const oracle_env_t *E, int e, float *o
     mass_o = c->mass_relative ? (E->mass[e] - c->base_mass) / denom : E->mass[e];
     for (int a = 0; a < 3; ++a) com_o[a] = c->com_scaled ? comv[a] / (c->com_scale[a] + 1e-6f) : comv[a];
   }
-  float *pt = obs + USV_NOBS - c->priv_dim;
+  float *pt = obs + USV_NOBS_BASE;   /* priv_dim = 4: columns 29..32 stay 0 (input padding) */
   pt[0] = mass_o; pt[1] = com_o[0]; pt[2] = com_o[1]; pt[3] = com_o[2];
   if (c->priv_dim == 8) {
     float kd, tl, tr, kz;
@@ -873,7 +873,7 @@ void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
     }
     obs[2] = wzn;
     for (int q = 0; q < 5 + 3 * USV_NCLOSE; ++q) obs[3 + q] = task[q];
-    const int pa = USV_NOBS - c->priv_dim - 2;
+    const int pa = USV_NOBS_BASE - 2;
     obs[pa + 0] = E->prev_cmd[0 * n + e];
     obs[pa + 1] = E->prev_cmd[1 * n + e];
     priv_tail(c, E, e, obs);
@@ -1049,7 +1049,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
       obs[0] = vxn; obs[1] = vyn;
     }
     obs[2] = wzn;
-    const int pa = USV_NOBS - c->priv_dim - 2;
+    const int pa = USV_NOBS_BASE - 2;
     obs[pa + 0] = E->prev_cmd[0 * n + e];
     obs[pa + 1] = E->prev_cmd[1 * n + e];
     priv_tail(c, E, e, obs);

@@ -332,6 +332,23 @@ def load_task_cfg(variant: str):
         env["water_current"]["use_water_current"] = True
         env["water_current"]["flow_velocity"] = [0.3, -0.2, 0.0]
         env["maxEpisodeLength"] = 30
+    if variant == "D":
+        # 8f-4 modes: priv_dim 4 (the 29-column obs of every reference yaml but TEST) and a
+        # global observation frame (USV_core.py:103-112)
+        env = cfg["env"]
+        env.pop("mass_dim", None)
+        env["priv_dim"] = 4
+        env["observation_frame"] = "global"
+        env["maxEpisodeLength"] = 30
+    if variant == "E":
+        # privileged tail from the base (nominal) mass / CoM, raw encodings (USV_Virtual.py:455-520)
+        env = cfg["env"]
+        m = env["disturbances"]["mass"]
+        m["masscom_obs_source"] = "base"
+        m["mass_obs_mode"] = "raw"
+        m["com_obs_mode"] = "raw"
+        env["privileged_params"]["mode"] = "raw"
+        env["maxEpisodeLength"] = 30
     if variant == "S":
         # scene replay (8f-2): deterministic scenes from tests/golden/scenes_S.npz
         sr = cfg["env"]["scene_replay"]
@@ -900,6 +917,8 @@ def main():
         "episodeA": lambda: gen_episode(torch, "A", 16, 64, 1234),
         "episodeB": lambda: gen_episode(torch, "B", 12, 56, 99),
         "episodeC": lambda: gen_episode(torch, "C", 12, 64, 77),
+        "episodeD": lambda: gen_episode(torch, "D", 10, 48, 55),
+        "episodeE": lambda: gen_episode(torch, "E", 10, 48, 56),
         "episodeP": lambda: gen_episode(torch, "P", 12, 64, 31),
         "episodeS": lambda: (make_scene_file(), gen_episode(torch, "S", 6, 64, 41)),
         "episodeT": lambda: gen_episode(torch, "T", 12, 64, 32),

@@ -1,0 +1,80 @@
+"""rl_games checkpoint layout with a narrower observation (priv_dim 4 -> obs_dim 29).
+
+The device network always has PPO_NIN inputs; a 29-input reference network maps onto it with
+zero W1 columns (and RMS slots) past column 29, so a checkpoint round trip is exact and the
+padded forward equals the reference's 29-input forward (a2c_common.py:590-621 layout).
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from omniisaacgymenvs_loop_amd.rl_games import checkpoint as C
+
+
+def _reference_shaped(obs_dim, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    sd = {}
+    for k, s in C.PARAM_LAYOUT:
+        shape = (C.NH, obs_dim) if k == C.W1_KEY else s
+        sd[k] = torch.randn(*shape, generator=g)
+    sd["value_mean_std.running_mean"] = torch.randn(1, generator=g).double()
+    sd["value_mean_std.running_var"] = torch.rand(1, generator=g).double() + 0.5
+    sd["value_mean_std.count"] = torch.tensor(123.0, dtype=torch.float64)
+    sd["running_mean_std.running_mean_std.state.running_mean"] = torch.randn(obs_dim, generator=g).double()
+    sd["running_mean_std.running_mean_std.state.running_var"] = torch.rand(obs_dim, generator=g).double() + 0.5
+    sd["running_mean_std.running_mean_std.state.count"] = torch.tensor(456.0, dtype=torch.float64)
+    return sd
+
+
+@pytest.mark.parametrize("obs_dim", [29, C.NIN])
+def test_model_round_trip(obs_dim):
+    sd = _reference_shaped(obs_dim)
+    params = torch.full((C.NPARAM,), 7.0)
+    obs_rms = torch.zeros(2 * C.NIN + 1, dtype=torch.float64)
+    obs_rms[C.NIN:2 * C.NIN] = 1.0
+    val_rms = torch.zeros(3, dtype=torch.float64)
+    C.load_model_state_dict(sd, params, obs_rms, val_rms, obs_dim)
+    w1 = C.split_flat(params)[C.W1_KEY]
+    assert w1.shape == (C.NH, C.NIN)
+    assert float(w1[:, obs_dim:].abs().sum()) == 0.0   # zero pad columns
+    assert float(obs_rms[obs_dim:C.NIN].abs().sum()) == 0.0 and bool((obs_rms[C.NIN + obs_dim:2 * C.NIN] == 1).all())
+    back = C.model_state_dict(params, obs_rms, val_rms, obs_dim)
+    assert set(back) == set(sd)
+    for k, t in sd.items():
+        assert tuple(back[k].shape) == tuple(t.shape), k
+        torch.testing.assert_close(back[k].double(), t.double(), rtol=0, atol=1e-6 if t.dtype == torch.float32 else 0)
+
+
+def test_padded_forward_equals_narrow_forward():
+    sd = _reference_shaped(29, seed=3)
+    params = torch.zeros(C.NPARAM)
+    C.load_model_state_dict(sd, params, torch.zeros(2 * C.NIN + 1, dtype=torch.float64),
+                            torch.zeros(3, dtype=torch.float64), 29)
+    w1 = C.split_flat(params)[C.W1_KEY]
+    x = torch.randn(64, 29, dtype=torch.float64)
+    xp = torch.cat([x, torch.zeros(64, C.NIN - 29, dtype=torch.float64)], 1)
+    np.testing.assert_array_equal((xp @ w1.double().T).numpy(), (x @ sd[C.W1_KEY].double().T).numpy())
+
+
+def test_optimizer_round_trip_narrow():
+    g = torch.Generator().manual_seed(1)
+    m = torch.randn(C.NPARAM, generator=g)
+    v = torch.rand(C.NPARAM, generator=g)
+    # pad columns of a narrow network never receive gradient: zero moments
+    for t in (m, v):
+        C.split_flat(t)[C.W1_KEY][:, 29:] = 0
+    osd = C.optimizer_state_dict(m, v, 17, 3e-4, obs_dim=29)
+    assert osd["state"][1]["exp_avg"].shape == (C.NH, 29)
+    m2, v2 = torch.zeros_like(m), torch.zeros_like(v)
+    step, lr = C.load_optimizer_state_dict(osd, m2, v2, obs_dim=29)
+    assert step == 17 and lr == pytest.approx(3e-4)
+    torch.testing.assert_close(m2, m, rtol=0, atol=0)
+    torch.testing.assert_close(v2, v, rtol=0, atol=0)
+
+
+def test_shape_mismatch_raises():
+    sd = _reference_shaped(29)
+    with pytest.raises(ValueError):
+        C.load_model_state_dict(sd, torch.zeros(C.NPARAM), torch.zeros(2 * C.NIN + 1, dtype=torch.float64),
+                                torch.zeros(3, dtype=torch.float64), C.NIN)

@@ -26,7 +26,7 @@ def _task(cfg_d, n):
     return USVVirtual(cfg_d, num_envs=n, device=DEV, seed=7)
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T", "S"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "T", "S"])
 def test_fixture_replay_on_gpu(golden, variant):
     d = golden(f"episode_{variant}.npz")
     cfg_d = json.loads(bytes(d["config_json"]).decode())
@@ -108,6 +108,31 @@ def test_philox_mode_matches_oracle():
     # per-episode parameters drawn by the reset kernel
     np.testing.assert_allclose(task.params[0].cpu().numpy(), E.mass, rtol=1e-6)
     np.testing.assert_allclose(task.obst.cpu().numpy().reshape(16, 2, n), E.obst, rtol=1e-6, atol=1e-5)
+
+
+@pytest.mark.parametrize("frame", ["local", "global"])
+def test_philox_priv4_matches_oracle(frame):
+    """priv_dim 4 (every reference yaml but TEST): 29-column rows, the slab's 4 pad columns stay 0."""
+    task_cfg = load_yaml(TEST_YAML)
+    task_cfg["env"].pop("mass_dim", None)
+    task_cfg["env"]["priv_dim"] = 4
+    task_cfg["env"]["observation_frame"] = frame
+    n, T = 2048, 16
+    task = _task(task_cfg, n)
+    assert task.num_observations == 29
+    E = _oracle_for(task.cfg, n, task_cfg)
+    rng = np.random.default_rng(3)
+    for t in range(T):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        bias = task.current_action_bias()
+        obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
+        E.full_step(a, bias, t, seed=task.seed)
+        torch.cuda.synchronize()
+        assert obs.shape == (n, 29)
+        assert float(task.obs_buf_t[:, 29:].abs().max()) == 0.0
+        np.testing.assert_array_equal(dones.cpu().numpy(), E.reset_buf, err_msg=f"dones t={t}")
+        np.testing.assert_allclose(obs.cpu().numpy(), E.obs[:, :29], rtol=1e-4, atol=1e-4, err_msg=f"obs t={t}")
+        np.testing.assert_allclose(rew.cpu().numpy(), E.rew, rtol=1e-3, atol=1e-3, err_msg=f"rew t={t}")
 
 
 def test_philox_mode_disturbances_matches_oracle():

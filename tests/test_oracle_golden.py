@@ -176,12 +176,15 @@ def test_episode_c_exercises_disturbances(golden):
     assert (d["dist"][-1][7] < 0).any() and (d["dist"][-1][7] > 0).any()   # torque sign flip
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T", "S"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "T", "S"])
 def test_episode_post_physics(golden, variant):
     """obs / reward / done / DR / spawns given the reference's post-integration state."""
     d = golden(f"episode_{variant}.npz")
+    w = d["obs"].shape[-1]
     for t, (obs, rew, rb, mass, kd, tl, tr, kiz, obst, prog, gc) in enumerate(_replay(d, post_only=True)):
-        np.testing.assert_allclose(obs, d["obs"][t], rtol=2e-6, atol=2e-6, err_msg=f"obs step {t}")
+        # rows are 25 + priv_dim wide in the reference; a priv_dim-4 slab row carries 4 zero pad columns
+        assert (obs[:, w:] == 0).all()
+        np.testing.assert_allclose(obs[:, :w], d["obs"][t], rtol=2e-6, atol=2e-6, err_msg=f"obs step {t}")
         np.testing.assert_allclose(rew, d["rew"][t], rtol=5e-6, atol=5e-6, err_msg=f"rew step {t}")
         np.testing.assert_array_equal(rb, d["reset"][t])
         np.testing.assert_array_equal(prog, d["progress"][t])
@@ -194,13 +197,14 @@ def test_episode_post_physics(golden, variant):
         np.testing.assert_array_equal(obst.transpose(2, 0, 1), d["obst"][t])
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "P", "T", "S"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "T", "S"])
 def test_episode_end_to_end(golden, variant):
     """Full replay incl. this build's integrator; the reference's potential-shaping
     term amplifies ~1e-7 state differences by 100, hence the reward tolerance."""
     d = golden(f"episode_{variant}.npz")
+    w = d["obs"].shape[-1]
     for t, (obs, rew, rb, *_rest) in enumerate(_replay(d, post_only=False)):
-        np.testing.assert_allclose(obs, d["obs"][t], rtol=2e-5, atol=2e-5, err_msg=f"obs step {t}")
+        np.testing.assert_allclose(obs[:, :w], d["obs"][t], rtol=2e-5, atol=2e-5, err_msg=f"obs step {t}")
         np.testing.assert_allclose(rew, d["rew"][t], rtol=1e-4, atol=1e-4, err_msg=f"rew step {t}")
         np.testing.assert_array_equal(rb, d["reset"][t])
 

@@ -69,3 +69,34 @@ def test_graph_replay_matches_eager():
     # episode meters are float atomics across waves (order-dependent last bits): close, not identical
     assert abs(a["meters"] - b["meters"]) <= 1e-5 * max(1.0, abs(a["meters"]))
     assert int(b["clock"][0]) == b["host_step"]
+
+
+def test_priv4_training_keeps_pad_columns_zero(tmp_path):
+    """priv_dim 4 -> 29 observation columns: the device net's W1 pad columns get no gradient and
+    no Adam moment, so training is exactly the 29-input network's; the checkpoint holds [NH, 29]."""
+    from omniisaacgymenvs_loop_amd.scripts import rlgames_train as T
+    from omniisaacgymenvs_loop_amd.rl_games import checkpoint as C
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
+    from omniisaacgymenvs_loop_amd.envs.vec_env_rlgames import VecEnvRLGames
+    from omniisaacgymenvs_loop_amd.utils.task_util import initialize_task
+    cfg = T.build_config({"num_envs": 512, "minibatch_size": 2048, "seed": 5})
+    cfg["task"]["env"].pop("mass_dim", None)
+    cfg["task"]["env"]["priv_dim"] = 4
+    env = VecEnvRLGames(headless=True)
+    task = initialize_task(cfg, env)
+    assert task.num_observations == 29
+    params = cfg["train"]["params"]
+    params["config"].update(vec_env=env, train_dir=str(tmp_path), print_stats=False)
+    ag = A2CAgent("run", params)
+    ag.obs = ag.env_reset()
+    for _ in range(3):
+        ag.train_epoch()
+    torch.cuda.synchronize()
+    for t in (ag.model_params, ag.adam_m, ag.adam_v):
+        w1 = C.split_flat(t.detach().cpu())[C.W1_KEY]
+        assert float(w1[:, 29:].abs().max()) == 0.0
+        assert float(w1[:, :29].abs().max()) > 0.0
+    ag.save(str(tmp_path / "ck"))
+    ck = C.load_checkpoint(str(tmp_path / "ck.pth"))
+    assert tuple(ck["model"][C.W1_KEY].shape) == (C.NH, 29)
+    assert tuple(ck["model"]["running_mean_std.running_mean_std.state.running_mean"].shape) == (29,)
