@@ -240,7 +240,7 @@ typedef struct usv_bufs {
   int32_t *reset_ids;              /* [n] compacted reset list */
   float   *fscratch;               /* [16] float reductions (max_val, jmax) */
   float   *extras;                 /* [USV_NSTAT] extras["episode"] (persistent) */
-  float   *extras_acc;             /* [USV_NSTAT] scratch sums */
+  float   *extras_acc;             /* [ceil(n/256)][USV_NSTAT] reset-kernel per-workgroup sums (scratch) */
   float   *field_old_tgt;          /* [2][n] target used by the field of each reset env */
   float   *slot_stats;             /* [n][USV_FIELD_SLOT_STATS] per-reset-slot field statistics (scratch) */
   float   *sdf;                    /* [n][150*150] per-reset-slot signed distance (scratch) */

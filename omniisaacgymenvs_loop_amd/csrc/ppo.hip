@@ -280,7 +280,8 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
 }
 
 // rewards_shaper + episode meters (a2c_common.py:721-759, tr_helpers.py:33-43)
-__global__ void k_store_reward(ppo_cfg_t c, const float *__restrict__ rew, const int64_t *__restrict__ dones, int t,
+constexpr int kStoreTB = 256;
+__global__ __launch_bounds__(kStoreTB) void k_store_reward(ppo_cfg_t c, const float *__restrict__ rew, const int64_t *__restrict__ dones, int t,
                                float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len, float *meter,
                                uint64_t *step_dev) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -302,11 +303,17 @@ __global__ void k_store_reward(ppo_cfg_t c, const float *__restrict__ rew, const
     cur_len[e] = cl * nd;
   }
   s_rew = wave_sum(s_rew); s_shaped = wave_sum(s_shaped); s_len = wave_sum(s_len); s_cnt = wave_sum(s_cnt);
-  if ((threadIdx.x & 63) == 0 && s_cnt > 0.f) {
-    atomicAdd(&meter[t * 4 + 0], s_rew);
-    atomicAdd(&meter[t * 4 + 1], s_shaped);
-    atomicAdd(&meter[t * 4 + 2], s_len);
-    atomicAdd(&meter[t * 4 + 3], s_cnt);
+  // one set of atomics per workgroup, not per wave: all of them land on the same four
+  // addresses, so their number sets this kernel's time at large env counts
+  __shared__ float red[kStoreTB / 64][4];
+  const int wv = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) { red[wv][0] = s_rew; red[wv][1] = s_shaped; red[wv][2] = s_len; red[wv][3] = s_cnt; }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float a = red[0][threadIdx.x], cnt = red[0][3];
+#pragma unroll
+    for (int w = 1; w < kStoreTB / 64; ++w) { a += red[w][threadIdx.x]; cnt += red[w][3]; }
+    if (cnt > 0.f) atomicAdd(&meter[t * 4 + threadIdx.x], a);
   }
 }
 
@@ -965,7 +972,8 @@ int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *done
                      float *cur_rew, float *cur_shaped, float *cur_len, float *meter, uint64_t *step_dev,
                      void *stream) {
   if (!cfg || !rew || !dones || cfg->n_envs <= 0) return 1;
-  hipLaunchKernelGGL(k_store_reward, dim3((cfg->n_envs + 255) / 256), dim3(256), 0, (hipStream_t)stream, *cfg, rew,
+  hipLaunchKernelGGL(k_store_reward, dim3((cfg->n_envs + kStoreTB - 1) / kStoreTB), dim3(kStoreTB), 0,
+                     (hipStream_t)stream, *cfg, rew,
                      dones, t, exp_rew, cur_rew, cur_shaped, cur_len, meter, step_dev);
   USV_CHECK_LAUNCH();
   return 0;

@@ -90,7 +90,6 @@ __global__ void k_step_begin(usv_bufs_t b) {
   if (t == 1) b.ctl[USV_CTL_ANY_INSIDE] = 0;
   if (t == 2) b.ctl[USV_CTL_ANY_FINITE] = 0;
   if (t < 4) b.fscratch[t] = 0.f;
-  if (t < USV_NSTAT) b.extras_acc[t] = 0.f;
 }
 
 // ------------------------------------------------------------------------
@@ -106,16 +105,20 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = b.n;
   const bool active = (e < n) && (b.reset_buf[e] != 0);
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // episode-extras sums of this workgroup's resetting envs, per wave (fixed order)
+  __shared__ float wsum[kBlock / 64][USV_NSTAT];
   step = step_of(b, step);
   // ---- compaction: reset_buf.nonzero() (USV_Virtual.py:1045) ----
   const uint64_t mask = __ballot(active);
+  if (c.stats_on && mask == 0 && lane < USV_NSTAT) wsum[wid][lane] = 0.f;
   if (mask != 0) {
     const int leader = __ffsll((long long)mask) - 1;
     int base = 0;
     if (lane == leader) base = atomicAdd(&b.ctl[USV_CTL_RESET_COUNT], __popcll(mask));
     base = __shfl(base, leader, 64);
-    // ---- episode extras: sums of the envs being reset (:1591-1612), one atomic per wave ----
+    // ---- episode extras: sums of the envs being reset (:1591-1612): wave sums here, the
+    // workgroup's partial at the end, folded in workgroup order by the last workgroup ----
     if (c.stats_on) {
       // all 28 loads first, then 28 independent wave sums (their shuffles interleave)
       const int ec = min(e, n - 1);
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
       for (int q = 0; q < USV_NSTAT; ++q) v[q] = wave_sum(active ? v[q] : 0.f);
       if (lane == leader) {
 #pragma unroll
-        for (int q = 0; q < USV_NSTAT; ++q) atomicAdd(&b.extras_acc[q], v[q]);
+        for (int q = 0; q < USV_NSTAT; ++q) wsum[wid][q] = v[q];
       }
     }
     float sx = 0.f, sy = 0.f, tx = 0.f, ty = 0.f;
@@ -324,8 +327,20 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
     b.ctl[USV_CTL_H_INJ_HI] = (int32_t)(uint32_t)((uint64_t)(uintptr_t)inj >> 32);
     b.ctl[USV_CTL_PLACE] = b.scene ? 0 : 1;   // scene replay: obstacles come from the scene
   }
-  // ---- the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612) ----
+  // ---- the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612).
+  // Per-workgroup partials (no float atomics: one address per statistic would serialise
+  // every wave of the grid on it, and the sum order would vary run to run) ----
   __shared__ bool last;
+  __shared__ float fold[8][32];
+  __syncthreads();
+  const int qs = threadIdx.x;
+  if (c.stats_on && qs < USV_NSTAT) {
+    float a = wsum[0][qs];
+#pragma unroll
+    for (int w = 1; w < kBlock / 64; ++w) a += wsum[w][qs];
+    b.extras_acc[(size_t)blockIdx.x * USV_NSTAT + qs] = a;
+    __threadfence();
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
@@ -335,11 +350,23 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   __syncthreads();
   if (!last) return;
   const int count = b.ctl[USV_CTL_RESET_COUNT];
-  const int qs = threadIdx.x;
-  if (qs < USV_NSTAT && count > 0) {
-    float m = b.extras_acc[qs] / (float)count;
-    if (qs != ST_SUCCESS && qs != ST_COLLISION) m = m / (float)c.max_episode_length;
-    b.extras[qs] = isnan(m) ? 0.f : m;
+  if (c.stats_on && count > 0) {
+    // 8 interleaved block subsets per statistic, each summed in block order, then combined in order
+    static_assert(USV_NSTAT <= 32 && kBlock == 256, "fold layout");
+    const int q = qs & 31, k = qs >> 5;
+    float a = 0.f;
+    if (q < USV_NSTAT)
+      for (int blk = k; blk < (int)gridDim.x; blk += 8) a += b.extras_acc[(size_t)blk * USV_NSTAT + q];
+    fold[k][q] = a;
+    __syncthreads();
+    if (qs < USV_NSTAT) {
+      float tot = fold[0][qs];
+#pragma unroll
+      for (int kk = 1; kk < 8; ++kk) tot += fold[kk][qs];
+      float m = tot / (float)count;
+      if (qs != ST_SUCCESS && qs != ST_COLLISION) m = m / (float)c.max_episode_length;
+      b.extras[qs] = isnan(m) ? 0.f : m;
+    }
   }
   if (qs == 0) b.ctl[USV_CTL_OBST_DONE] = 0;
 }

@@ -436,10 +436,8 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       pp[SS_JMIN_F_NI] = a[2]; pp[SS_JMAX_F_NI] = a[3]; pp[SS_JMAX_F_ALL] = a[4];
       pp[SS_JRMIN_I_NI] = a[5]; pp[SS_JRMAX_I_NI] = a[6]; pp[SS_JRMAX_I_ALL] = a[7];
       pp[SS_INSIDE] = flags[1] ? 1.f : 0.f;
-      if (isfinite(a[1])) {
-        atomic_max_f32(&b.fscratch[0], a[1]);      // batch max of finite costs (:205-210)
-        atomicOr(&b.ctl[USV_CTL_ANY_FINITE], 1);
-      }
+      // the batch max of finite costs (:205-210) is folded from these chunk maxima by
+      // k_field_batch (one atomic per chunk on a single address serialised this kernel)
     }
     __syncthreads();
   }
@@ -452,10 +450,31 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
 __global__ __launch_bounds__(1024) void k_field_batch(usv_cfg_t c, usv_bufs_t b) {
   __shared__ float red[16];
   __shared__ int ins;
+  __shared__ float fmx[16];
   const int count = b.ctl[USV_CTL_RESET_COUNT];
   const int tid = threadIdx.x;
   if (count <= 0) return;
-  const BatchK k = batch_k(c, b);
+  // batch max of finite costs over every chunk of every slot (d_multi_gemini.py:205-210); a
+  // max is exact in any order.  -inf (no finite cell in a chunk) never wins over a finite one
+  {
+    float m = -INFINITY;
+    for (int q = tid; q < count * kChunks; q += 1024)
+      m = fmaxf(m, b.slot_stats[(size_t)(q / kChunks) * kSlotStride + 16 + 12 * (q % kChunks) + SS_GMAX_F]);
+    m = wave_max(m);
+    if ((tid & 63) == 0) fmx[tid >> 6] = m;
+    __syncthreads();
+    if (tid == 0) {
+      float mm = fmx[0];
+      for (int w = 1; w < 16; ++w) mm = fmaxf(mm, fmx[w]);
+      const bool fin = isfinite(mm);
+      b.fscratch[0] = fin ? mm : 0.f;                    // for k_field_final's batch_k
+      b.ctl[USV_CTL_ANY_FINITE] = fin ? 1 : 0;
+      fmx[0] = fin ? mm : 100.0f;                        // batch_k's max_val, through LDS
+    }
+    __syncthreads();
+  }
+  const float inf_val = fmx[0] * 1.5f;
+  const BatchK k{inf_val, goal_mask(c, inf_val, (float)((double)c.map_size / G))};
   if (tid == 0) ins = 0;
   __syncthreads();
   float jm = 0.f;

@@ -129,7 +129,7 @@ class USVVirtual:
         self.ctl = Z(CTL_N, **i32)
         self.fscratch = Z(16, **f32)
         self.extras_buf = Z(NSTAT, **f32)
-        self.extras_acc = Z(NSTAT, **f32)
+        self.extras_acc = Z(((n + 255) // 256) * NSTAT, **f32)   # per reset-kernel workgroup (256 envs)
         self.slot_stats = Z((n, DEFINES["USV_FIELD_SLOT_STATS"]), **f32)
         # device step clock (next step, next bias call, current step, current bias call): the kernels take
         # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
