@@ -194,6 +194,11 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s) {
 }
 
 // ------------------------------------------------------------------ rollout
+// workgroups of the persistent forward kernels: one 32-row tile each up to 256
+// (one per CU at this LDS size), then tiles loop
+__host__ __device__ constexpr int policy_grid(int n) {
+  return (n + RB - 1) / RB < 256 ? (n + RB - 1) / RB : 256;
+}
 __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms,
                                                     const double *__restrict__ val_rms, const float *__restrict__ obs,
@@ -205,19 +210,23 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   __shared__ MlpSmem s;
   const int n = c.n_envs, H = c.horizon;
   if (step_dev) step = *step_dev + (uint64_t)t;   // the rollout's first step + slot
-  const int row0 = blockIdx.x * RB;
+  // persistent over 32-row tiles: the weights are staged once per workgroup, not once per tile
+  StagedW wr;
+  stage_load(P, wr);
+  const int ntiles = (n + RB - 1) / RB;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  const int row0 = tile * RB;
   const int nrows = min(RB, n - row0);
   // raw obs into the experience buffer (row = env*H + t, swap_and_flatten01 layout)
   for (int i = threadIdx.x; i < nrows * NIN; i += TB) {
     const int r = i / NIN, k = i % NIN;
     exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = obs[(size_t)(row0 + r) * NIN + k];
   }
-  StagedW wr;
-  stage_load(P, wr);
+  // s.x of the previous tile was last read before block_forward's first barrier
   stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
-  stage_store_small(wr, s);
+  if (tile == (int)blockIdx.x) stage_store_small(wr, s);
   __syncthreads();
-  block_forward(wr, s);
+  block_forward(wr, s);   // re-commits the same W2 values on later tiles
   const int r = threadIdx.x;
   if (r < nrows) {
     const int e = row0 + r;
@@ -254,28 +263,34 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
     actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
     actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
   }
+  __syncthreads();   // s.out of this tile is read above before the next tile's forward rewrites it
+  }
 }
 
 __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,
                                               const double *val_rms, const float *__restrict__ obs, float *values) {
   __shared__ MlpSmem s;
   const int n = c.n_envs;
-  const int row0 = blockIdx.x * RB;
-  const int nrows = min(RB, n - row0);
   StagedW wr;
   stage_load(P, wr);
-  stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
-  stage_store_small(wr, s);
-  __syncthreads();
-  block_forward(wr, s);
-  const int r = threadIdx.x;
-  if (r < nrows) {
-    float vd = s.out[r * 4 + 2];
-    if (c.normalize_value) {
-      vd = clampt(vd, -5.0f, 5.0f);
-      vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
+  const int ntiles = (n + RB - 1) / RB;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {   // persistent, as k_policy_step
+    const int row0 = tile * RB;
+    const int nrows = min(RB, n - row0);
+    stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+    if (tile == (int)blockIdx.x) stage_store_small(wr, s);
+    __syncthreads();
+    block_forward(wr, s);
+    const int r = threadIdx.x;
+    if (r < nrows) {
+      float vd = s.out[r * 4 + 2];
+      if (c.normalize_value) {
+        vd = clampt(vd, -5.0f, 5.0f);
+        vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
+      }
+      values[row0 + r] = vd;
     }
-    values[row0 + r] = vd;
+    __syncthreads();
   }
 }
 
@@ -950,7 +965,7 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
                     float *actions_out, uint64_t seed, uint64_t step, const uint64_t *step_dev,
                     const float *eps_inject, void *stream) {
   if (!cfg || !params || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
-  const int grid = (cfg->n_envs + RB - 1) / RB;
+  const int grid = policy_grid(cfg->n_envs);
   hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
                      obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
                      actions_out, seed, step, step_dev, eps_inject);
@@ -961,7 +976,7 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
 int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, const double *val_rms,
               const float *obs, float *values, void *stream) {
   if (!cfg || !params || !obs || !values || cfg->n_envs <= 0) return 1;
-  const int grid = (cfg->n_envs + RB - 1) / RB;
+  const int grid = policy_grid(cfg->n_envs);
   hipLaunchKernelGGL(k_value, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
                      values);
   USV_CHECK_LAUNCH();

@@ -109,14 +109,25 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   // episode-extras sums of this workgroup's resetting envs, per wave (fixed order)
   __shared__ float wsum[kBlock / 64][USV_NSTAT];
   step = step_of(b, step);
-  // ---- compaction: reset_buf.nonzero() (USV_Virtual.py:1045) ----
+  // ---- compaction: reset_buf.nonzero() (USV_Virtual.py:1045): wave ballots, a workgroup
+  // prefix in LDS and one atomic per workgroup (slots are workgroup-contiguous) ----
   const uint64_t mask = __ballot(active);
+  __shared__ int wbase[kBlock / 64];
+  if (lane == 0) wbase[wid] = __popcll(mask);
   if (c.stats_on && mask == 0 && lane < USV_NSTAT) wsum[wid][lane] = 0.f;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) { const int k = wbase[w]; wbase[w] = tot; tot += k; }
+    const int base0 = tot ? atomicAdd(&b.ctl[USV_CTL_RESET_COUNT], tot) : 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; ++w) wbase[w] += base0;
+  }
+  __syncthreads();
   if (mask != 0) {
     const int leader = __ffsll((long long)mask) - 1;
-    int base = 0;
-    if (lane == leader) base = atomicAdd(&b.ctl[USV_CTL_RESET_COUNT], __popcll(mask));
-    base = __shfl(base, leader, 64);
+    const int base = wbase[wid];
     // ---- episode extras: sums of the envs being reset (:1591-1612): wave sums here, the
     // workgroup's partial at the end, folded in workgroup order by the last workgroup ----
     if (c.stats_on) {
@@ -355,8 +366,18 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
     static_assert(USV_NSTAT <= 32 && kBlock == 256, "fold layout");
     const int q = qs & 31, k = qs >> 5;
     float a = 0.f;
-    if (q < USV_NSTAT)
-      for (int blk = k; blk < (int)gridDim.x; blk += 8) a += b.extras_acc[(size_t)blk * USV_NSTAT + q];
+    if (q < USV_NSTAT) {
+      // blocks k, k+8, k+16, ... in that order; 8 loads in flight per batch
+      const int G = (int)gridDim.x;
+      for (int b0 = k; b0 < G; b0 += 64) {
+        float x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = b.extras_acc[(size_t)min(b0 + 8 * u, G - 1) * USV_NSTAT + q];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (b0 + 8 * u < G) a += x[u];
+      }
+    }
     fold[k][q] = a;
     __syncthreads();
     if (qs < USV_NSTAT) {

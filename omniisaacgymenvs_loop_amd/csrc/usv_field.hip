@@ -458,8 +458,17 @@ __global__ __launch_bounds__(1024) void k_field_batch(usv_cfg_t c, usv_bufs_t b)
   // max is exact in any order.  -inf (no finite cell in a chunk) never wins over a finite one
   {
     float m = -INFINITY;
-    for (int q = tid; q < count * kChunks; q += 1024)
-      m = fmaxf(m, b.slot_stats[(size_t)(q / kChunks) * kSlotStride + 16 + 12 * (q % kChunks) + SS_GMAX_F]);
+    const int nq = count * kChunks;
+    for (int q0 = tid; q0 < nq; q0 += 8 * 1024) {   // 8 loads in flight; a max is exact in any order
+      float x[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int q = min(q0 + u * 1024, nq - 1);
+        x[u] = b.slot_stats[(size_t)(q / kChunks) * kSlotStride + 16 + 12 * (q % kChunks) + SS_GMAX_F];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) m = fmaxf(m, x[u]);
+    }
     m = wave_max(m);
     if ((tid & 63) == 0) fmx[tid >> 6] = m;
     __syncthreads();
