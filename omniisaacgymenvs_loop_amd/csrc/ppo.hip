@@ -124,14 +124,32 @@ __device__ __forceinline__ float fast_tanh(float x) {
 
 __device__ __forceinline__ void stage_obs(const float *__restrict__ obs, int row0, int nrows, const double *obs_rms,
                                           bool normalize, float eps, MlpSmem &s) {
-  for (int i = threadIdx.x; i < RB * XS; i += TB) {
+  // compile-time trip count: every obs and statistics load of the thread is in flight
+  // before the first one is waited on
+  constexpr int NU = (RB * XS + TB - 1) / TB;
+  float v[NU];
+  double mu[NU], var[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = threadIdx.x + u * TB;
     const int r = i / XS, k = i % XS;
-    float v = 0.f;
+    const bool ok = i < RB * XS && r < nrows && k < NIN;
+    const int rc = ok ? r : 0, kc = ok ? k : 0;
+    v[u] = obs[(size_t)(row0 + rc) * NIN + kc];
+    mu[u] = normalize ? obs_rms[kc] : 0.0;
+    var[u] = normalize ? obs_rms[NIN + kc] : 1.0;
+  }
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = threadIdx.x + u * TB;
+    if (i >= RB * XS) continue;
+    const int r = i / XS, k = i % XS;
+    float x = 0.f;
     if (r < nrows && k < NIN) {
-      v = obs[(size_t)(row0 + r) * NIN + k];
-      if (normalize) v = rms_norm(v, obs_rms[k], obs_rms[NIN + k], eps);
+      x = v[u];
+      if (normalize) x = rms_norm(x, mu[u], var[u], eps);
     }
-    s.x[i] = v;
+    s.x[i] = x;
   }
 }
 
@@ -450,9 +468,17 @@ __global__ __launch_bounds__(TB) void k_obs_stats(ppo_cfg_t c, const float *__re
   if (lane_r < nl) {
     const int chunk = (rows + gridDim.x - 1) / gridDim.x;
     const int a = blockIdx.x * chunk, bnd = min(rows, a + chunk);
-    for (int r = a + lane_r; r < bnd; r += nl) {
-      const double x = obs[(size_t)(row0 + r) * NIN + col];
-      s += x; s2 += x * x;
+    // rows a + lane_r, + nl, ... in that order; 8 loads in flight per batch
+    for (int r0 = a + lane_r; r0 < bnd; r0 += 8 * nl) {
+      float xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xv[u] = obs[(size_t)(row0 + min(r0 + u * nl, bnd - 1)) * NIN + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r0 + u * nl < bnd) {
+          const double x = xv[u];
+          s += x; s2 += x * x;
+        }
     }
     acc[0][col][lane_r] = s;
     acc[1][col][lane_r] = s2;
