@@ -7,10 +7,10 @@
 //   by clamp(dist_to_goal/3, 0, 1), batch-global max of finite costs and of J,
 //   per-env min/max normalisation, potential = g_norm + 0.5 J_norm.
 //
-// k_field_wave (one 256-thread workgroup per reset env, persistent over the
-// device-side reset count):
+// k_field_wave / k_field_wave_pack (one 256-thread workgroup per reset env,
+// persistent over the device-side reset count; _pack holds two envs per CU):
 //   1. SDF + occupancy of the 150x150 grid (SDF to a per-slot HBM scratch, the
-//      cost grid initialised in LDS, 90 KB);
+//      occupancy as a 2.8 KB bit map in LDS);
 //   2. cost-to-go: 225 threads each own a 10x10 tile in registers and relax it
 //      with a raster forward + backward chamfer sweep against a halo ring read
 //      from LDS; one barrier per iteration with a block-wide "changed" vote.
@@ -42,6 +42,7 @@ constexpr int kMaxIters = 4096;  // safety cap (never reached)
 constexpr int kChunk = 2048;     // cells per k_field_final work item
 constexpr int kChunks = (G2 + kChunk - 1) / kChunk;
 constexpr int kSlotStride = USV_FIELD_SLOT_STATS;   // floats per reset slot: 16 final + 12 per chunk
+constexpr int kFieldPackMinEnvs = 32768;           // k_field_wave_pack (two envs per CU) from this many envs
 
 // slot_stats layout (per reset slot)
 enum {
@@ -101,9 +102,21 @@ constexpr uint32_t kOcc = 0xFFFFFFFFu;          // occupied cell marker (a NaN a
 enum { E_TOP = 0, E_BOT, E_LEFT, E_RIGHT };
 constexpr int kSegRows = 30;                    // SDF work unit: one column x 30 rows
 constexpr int kUnits = G * (G / kSegRows);
+// occupancy (sdf <= 0) bit map, column-major: column cc owns words [cc * kOccColWords, +5)
+constexpr int kOccColWords = (G + 31) / 32;
+__device__ __forceinline__ bool occ_bit(const uint32_t *occ, int r, int cc) {
+  return (occ[cc * kOccColWords + (r >> 5)] >> (r & 31)) & 1u;
+}
 
-__global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) {
-  __shared__ float sdf_l[G2];
+// LDS holds the tile edges and a 2.8 KB occupancy bit map (the SDF itself goes to
+// the per-slot HBM scratch only): 51 KB.  Two launch shapes of the same body:
+// k_field_wave_pack is held to 256 registers (its spills sit in the per-slot
+// prologue, not in the sweep), so two reset envs share a CU -- one wave of each per
+// SIMD -- for batches that fill the chip more than once; k_field_wave keeps the
+// compiler's 256 + 76 registers and one env per CU, for small batches, where the
+// kernel is latency-bound and a shared CU would only slow the slowest env.
+__device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bufs_t &b) {
+  __shared__ uint32_t occ[G * kOccColWords];
   __shared__ float edge[4][NTP * NTP][T];
   __shared__ int lastc[NTP * NTP];
   __shared__ float so[2 * USV_NOBST];
@@ -161,6 +174,7 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
       so[tid] = b.obst[(size_t)tid * n + e];
     }
     if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
+    for (int q = tid; q < G * kOccColWords; q += kWaveThreads) occ[q] = 0u;
     __syncthreads();
 #ifdef USV_PHASE_PROBE
     if (tid == 0 && blockIdx.x < 4096) g_probe_field[blockIdx.x][12] = wall_clock64();
@@ -181,6 +195,7 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
       }
       // three rows at a time (independent chains), each a balanced min tree over
       // the 16 obstacles; squared distances are >= 0: float order == u32 order
+      uint32_t om = 0u;   // occupancy of the unit's 30 rows (bit r - rs)
       for (int r = rs; r < rs + kSegRows; r += 3) {
         float sd[3];
 #pragma unroll
@@ -200,10 +215,15 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
         }
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          sdf_l[(r + k) * G + cc] = sd[k];
+          om |= (sd[k] <= 0.f ? 1u : 0u) << (r + k - rs);
           sdf_s[(r + k) * G + cc] = sd[k];
         }
       }
+      // the unit's 30 bits span at most two words of its column
+      const uint64_t m64 = (uint64_t)om << (rs & 31);
+      uint32_t *oc = occ + cc * kOccColWords + (rs >> 5);
+      if ((uint32_t)m64) atomicOr(oc, (uint32_t)m64);
+      if ((uint32_t)(m64 >> 32)) atomicOr(oc + 1, (uint32_t)(m64 >> 32));
     }
     __syncthreads();
     USV_PHASE(field, 1);
@@ -215,7 +235,7 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
     int ix = (int)((tx + half_map) / cell), iy = (int)((ty + half_map) / cell);
     ix = min(max(ix, 0), G - 1);
     iy = min(max(iy, 0), G - 1);
-    const bool tgt_free = !(sdf_l[iy * G + ix] <= 0.f) && ix > 0 && ix < G - 1 && iy > 0 && iy < G - 1;
+    const bool tgt_free = !occ_bit(occ, iy, ix) && ix > 0 && ix < G - 1 && iy > 0 && iy < G - 1;
     // ---- 2. cost-to-go: tiled chamfer sweeps until nothing changes ----
     // Costs are >= 0, so float order == unsigned order of the bit patterns:
     // the relaxation runs on u32 min (no NaN canonicalisation).  An occupied
@@ -230,7 +250,7 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
         for (int j = 0; j < T; ++j) {
           const int r = r0 + i, cc = c0 + j;
           const bool border = r == 0 || r == G - 1 || cc == 0 || cc == G - 1;
-          const bool o = border || sdf_l[r * G + cc] <= 0.f;
+          const bool o = border || occ_bit(occ, r, cc);
           float init = INFINITY;
           if (o) {
             init = __uint_as_float(kOcc);
@@ -352,6 +372,9 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bu
     USV_PHASE(field, 3);
   }
 }
+
+__global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) { field_wave_body(c, b); }
+__global__ __launch_bounds__(kWaveThreads, 2) void k_field_wave_pack(usv_cfg_t c, usv_bufs_t b) { field_wave_body(c, b); }
 
 // batch constants given every slot's statistics
 struct BatchK {
@@ -575,7 +598,12 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   // the reset count lives on the device: launch persistent grids, blocks loop over slots
   const int grid_b = b->n < 512 ? b->n : 512;
   const int grid_d = b->n * kChunks < 4096 ? b->n * kChunks : 4096;
-  hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
+  // two reset envs per CU only when the batch fills the chip more than once (a few hundred
+  // resets per step); USV_FIELD_PACK=0/1 forces either layout (A/B runs, tests)
+  const char *pack_env = getenv("USV_FIELD_PACK");
+  const bool pack = pack_env ? atoi(pack_env) != 0 : b->n >= kFieldPackMinEnvs;
+  if (pack) hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
+  else hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_stats, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
