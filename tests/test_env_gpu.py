@@ -233,7 +233,9 @@ def _run_field(task, ids, obst, tgt, lin=None):
     return task.field[ids_t.long()].cpu().numpy()
 
 
-def test_potential_field_bit_exact_vs_reference(golden):
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_potential_field_bit_exact_vs_reference(golden, pack, monkeypatch):
+    monkeypatch.setenv("USV_FIELD_PACK", pack)
     g = golden("field.npz")
     task = _task(load_yaml(TEST_YAML), 8)
     for name in ("b1", "b4"):
@@ -244,7 +246,10 @@ def test_potential_field_bit_exact_vs_reference(golden):
         np.testing.assert_array_equal(f, ref)
 
 
-def test_potential_field_random_batches_vs_oracle():
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_potential_field_random_batches_vs_oracle(pack, monkeypatch):
+    """Both launch shapes of the field kernel (one env per CU / two per CU, USV_FIELD_PACK)."""
+    monkeypatch.setenv("USV_FIELD_PACK", pack)
     task_cfg = load_yaml(TEST_YAML)
     task = _task(task_cfg, 64)
     rng = np.random.default_rng(3)
