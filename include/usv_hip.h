@@ -238,7 +238,7 @@ typedef struct usv_bufs {
   /* control block (device) */
   int32_t *ctl;                    /* [16] see USV_CTL_* */
   int32_t *reset_ids;              /* [n] compacted reset list */
-  float   *fscratch;               /* [16] float reductions (max_val, jmax) */
+  float   *fscratch;               /* [16] float reductions (max_val, jmax, J max finite / infinite) */
   float   *extras;                 /* [USV_NSTAT] extras["episode"] (persistent) */
   float   *extras_acc;             /* [ceil(n/256)][USV_NSTAT] reset-kernel per-workgroup sums (scratch) */
   float   *field_old_tgt;          /* [2][n] target used by the field of each reset env */
@@ -292,6 +292,7 @@ typedef struct usv_bufs {
 #define USV_CTL_H_INJ_LO   14
 #define USV_CTL_H_INJ_HI   15
 #define USV_CTL_SCENE_ERR  16   /* scene replay: an index fell outside [0, n_scenes) with cycle off */
+#define USV_CTL_BATCH_DONE 17   /* completion counter of the potential-field batch fold (keep 0) */
 #define USV_CTL_N           20
 
 /* ------------------------------------------------------------------------ */

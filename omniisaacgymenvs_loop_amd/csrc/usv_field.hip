@@ -466,85 +466,70 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   }
 }
 
-// batch constants given every slot's statistics
 // ------------------------------------------------------------- pass C2 ---
-// fold each slot's chunk partials (fixed order), then the batch J max and the
-// any-inside flag (one workgroup)
-__global__ __launch_bounds__(1024) void k_field_batch(usv_cfg_t c, usv_bufs_t b) {
-  __shared__ float red[16];
-  __shared__ int ins;
-  __shared__ float fmx[16];
+// fold each slot's chunk partials (chunk order), then the batch maxima: the max of
+// finite costs (d_multi_gemini.py:205-210), J.max() (:257-260) and the any-inside
+// flag.  One wave per slot (lane q folds statistic q over the chunks: one cache line
+// per chunk row instead of a scattered load per statistic and slot), waves of
+// kBatchBlocks workgroups loop over the slots; the batch maxima leave through max
+// atomics (exact in any order, one set per workgroup) and the last workgroup forms
+// J.max() = max(J over finite cells, mask(inf_val) * raw J over infinite cells) --
+// the multiplication by the non-negative mask is monotone, so the max of the
+// products is the product with the max.
+constexpr int kBatchBlocks = 64;
+__global__ __launch_bounds__(256) void k_field_batch(usv_cfg_t c, usv_bufs_t b) {
+  __shared__ float wred[4][4];
+  __shared__ bool last;
   const int count = b.ctl[USV_CTL_RESET_COUNT];
-  const int tid = threadIdx.x;
   if (count <= 0) return;
-  // batch max of finite costs over every chunk of every slot (d_multi_gemini.py:205-210); a
-  // max is exact in any order.  -inf (no finite cell in a chunk) never wins over a finite one
-  {
-    float m = -INFINITY;
-    const int nq = count * kChunks;
-    for (int q0 = tid; q0 < nq; q0 += 8 * 1024) {   // 8 loads in flight; a max is exact in any order
-      float x[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int q = min(q0 + u * 1024, nq - 1);
-        x[u] = b.slot_stats[(size_t)(q / kChunks) * kSlotStride + 16 + 12 * (q % kChunks) + SS_GMAX_F];
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) m = fmaxf(m, x[u]);
-    }
-    m = wave_max(m);
-    if ((tid & 63) == 0) fmx[tid >> 6] = m;
-    __syncthreads();
-    if (tid == 0) {
-      float mm = fmx[0];
-      for (int w = 1; w < 16; ++w) mm = fmaxf(mm, fmx[w]);
-      const bool fin = isfinite(mm);
-      b.fscratch[0] = fin ? mm : 0.f;                    // for k_field_final's batch_k
-      b.ctl[USV_CTL_ANY_FINITE] = fin ? 1 : 0;
-      fmx[0] = fin ? mm : 100.0f;                        // batch_k's max_val, through LDS
-    }
-    __syncthreads();
-  }
-  const float inf_val = fmx[0] * 1.5f;
-  const BatchK k{inf_val, goal_mask(c, inf_val, (float)((double)c.map_size / G))};
-  if (tid == 0) ins = 0;
-  __syncthreads();
-  float jm = 0.f;
-  int inside = 0;
-  for (int sl = tid; sl < count; sl += 1024) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nw = (int)gridDim.x * 4;
+  float gfin = -INFINITY, jf = 0.f, jr = 0.f, ins = 0.f;
+  const bool is_min = lane == SS_GMIN_F || lane == SS_JMIN_F_NI || lane == SS_JRMIN_I_NI;
+  for (int sl = (int)blockIdx.x * 4 + wid; sl < count; sl += nw) {
     float *st = b.slot_stats + (size_t)sl * kSlotStride;
-    float a[10];
+    float a = 0.f;
+    if (lane < 10) {
+      float x[kChunks];
 #pragma unroll
-    for (int q = 0; q < 10; ++q) a[q] = st[16 + q];
-    for (int ch = 1; ch < kChunks; ++ch) {
-      const float *pp = st + 16 + 12 * ch;
-      a[SS_GMIN_F] = fminf(a[SS_GMIN_F], pp[SS_GMIN_F]);
-      a[SS_GMAX_F] = fmaxf(a[SS_GMAX_F], pp[SS_GMAX_F]);
-      a[SS_ANY_INF] = fmaxf(a[SS_ANY_INF], pp[SS_ANY_INF]);
-      a[SS_JMIN_F_NI] = fminf(a[SS_JMIN_F_NI], pp[SS_JMIN_F_NI]);
-      a[SS_JMAX_F_NI] = fmaxf(a[SS_JMAX_F_NI], pp[SS_JMAX_F_NI]);
-      a[SS_JMAX_F_ALL] = fmaxf(a[SS_JMAX_F_ALL], pp[SS_JMAX_F_ALL]);
-      a[SS_JRMIN_I_NI] = fminf(a[SS_JRMIN_I_NI], pp[SS_JRMIN_I_NI]);
-      a[SS_JRMAX_I_NI] = fmaxf(a[SS_JRMAX_I_NI], pp[SS_JRMAX_I_NI]);
-      a[SS_JRMAX_I_ALL] = fmaxf(a[SS_JRMAX_I_ALL], pp[SS_JRMAX_I_ALL]);
-      a[SS_INSIDE] = fmaxf(a[SS_INSIDE], pp[SS_INSIDE]);
+      for (int ch = 0; ch < kChunks; ++ch) x[ch] = st[16 + 12 * ch + lane];
+      a = x[0];
+#pragma unroll
+      for (int ch = 1; ch < kChunks; ++ch) a = is_min ? fminf(a, x[ch]) : fmaxf(a, x[ch]);
+      st[lane] = a;
     }
-#pragma unroll
-    for (int q = 0; q < 10; ++q) st[q] = a[q];
-    jm = fmaxf(jm, a[SS_JMAX_F_ALL]);
-    if (a[SS_ANY_INF] != 0.f) jm = fmaxf(jm, a[SS_JRMAX_I_ALL] * k.mask_inf);   // monotone in the raw value
-    inside |= a[SS_INSIDE] != 0.f;
+    const float s_gmax = __shfl(a, SS_GMAX_F, 64), s_anyinf = __shfl(a, SS_ANY_INF, 64);
+    const float s_jf = __shfl(a, SS_JMAX_F_ALL, 64), s_jr = __shfl(a, SS_JRMAX_I_ALL, 64);
+    const float s_in = __shfl(a, SS_INSIDE, 64);
+    gfin = fmaxf(gfin, s_gmax);             // -inf: no finite cell in the slot
+    jf = fmaxf(jf, s_jf);
+    if (s_anyinf != 0.f) jr = fmaxf(jr, s_jr);
+    ins = fmaxf(ins, s_in);
   }
-  jm = wave_max(jm);
-  if ((tid & 63) == 0) red[tid >> 6] = jm;
-  if (inside) ins = 1;
+  if (lane == 0) { wred[wid][0] = gfin; wred[wid][1] = jf; wred[wid][2] = jr; wred[wid][3] = ins; }
   __syncthreads();
   if (tid == 0) {
-    float m = 0.f;
-    for (int w = 0; w < 16; ++w) m = fmaxf(m, red[w]);
-    b.fscratch[1] = m;                                   // J.max() over the batch (:257)
-    b.ctl[USV_CTL_ANY_INSIDE] = ins;
+    float g = wred[0][0], f = wred[0][1], r = wred[0][2], in = wred[0][3];
+    for (int w = 1; w < 4; ++w) {
+      g = fmaxf(g, wred[w][0]); f = fmaxf(f, wred[w][1]); r = fmaxf(r, wred[w][2]); in = fmaxf(in, wred[w][3]);
+    }
+    // fscratch[0], [2], [3] and the two flags start at 0 (k_step_begin); costs and J are >= 0
+    if (isfinite(g)) {
+      atomic_max_f32(&b.fscratch[0], g);
+      atomicOr(&b.ctl[USV_CTL_ANY_FINITE], 1);
+    }
+    atomic_max_f32(&b.fscratch[2], f);
+    atomic_max_f32(&b.fscratch[3], r);
+    if (in != 0.f) atomicOr(&b.ctl[USV_CTL_ANY_INSIDE], 1);
+    __threadfence();
+    last = atomicAdd(&b.ctl[USV_CTL_BATCH_DONE], 1) == (int)gridDim.x - 1;
   }
+  __syncthreads();
+  if (!last || tid != 0) return;
+  __threadfence();
+  const BatchK k = batch_k(c, b);
+  b.fscratch[1] = fmaxf(b.fscratch[2], b.fscratch[3] * k.mask_inf);   // J.max() over the batch (:257)
+  b.ctl[USV_CTL_BATCH_DONE] = 0;
 }
 
 // ---------------------------------------------------------------- pass D ---
@@ -607,7 +592,7 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_stats, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_batch, dim3(1), dim3(1024), 0, s, *cfg, *b);
+  hipLaunchKernelGGL(k_field_batch, dim3(kBatchBlocks), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_final, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
