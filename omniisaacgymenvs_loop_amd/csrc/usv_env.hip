@@ -367,14 +367,14 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
     const int q = qs & 31, k = qs >> 5;
     float a = 0.f;
     if (q < USV_NSTAT) {
-      // blocks k, k+8, k+16, ... in that order; 8 loads in flight per batch
+      // blocks k, k+8, k+16, ... in that order; 16 loads in flight per batch
       const int G = (int)gridDim.x;
-      for (int b0 = k; b0 < G; b0 += 64) {
-        float x[8];
+      for (int b0 = k; b0 < G; b0 += 128) {
+        float x[16];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = b.extras_acc[(size_t)min(b0 + 8 * u, G - 1) * USV_NSTAT + q];
+        for (int u = 0; u < 16; ++u) x[u] = b.extras_acc[(size_t)min(b0 + 8 * u, G - 1) * USV_NSTAT + q];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < 16; ++u)
           if (b0 + 8 * u < G) a += x[u];
       }
     }
