@@ -236,7 +236,7 @@ typedef struct usv_bufs {
   float *rew;                      /* [n] */
   int64_t *dones;                  /* [n] reset_buf copy as int64 (rl_games API) */
   /* control block (device) */
-  int32_t *ctl;                    /* [16] see USV_CTL_* */
+  int32_t *ctl;                    /* [USV_CTL_N] see USV_CTL_* */
   int32_t *reset_ids;              /* [n] compacted reset list */
   float   *fscratch;               /* [16] float reductions (max_val, jmax, J max finite / infinite) */
   float   *extras;                 /* [USV_NSTAT] extras["episode"] (persistent) */
