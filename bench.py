@@ -173,8 +173,12 @@ def main():
     env_timer, ppo_timer = KernelTimer(), KernelTimer()
     orig_call, orig_call_rc = _capi.call, _capi.call_rc
 
+    last_env_args = []
+
     def timed_call(name, *a):
         if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
+            if name == "usv_env_step":
+                last_env_args[:] = [a]
             env_timer(lambda: orig_call(name, *a))
         elif timing[0] and name == "ppo_minibatch_grad":
             ppo_timer(lambda: orig_call(name, *a))
@@ -244,6 +248,19 @@ def main():
     torch.cuda.synchronize()
     timing[0] = False
     agent.use_graph = use_graph
+    # the same env-step launch 32 times back to back between one event pair: the per-launch event
+    # pairs above carry ~3 us of event overhead at 4096 envs; this mean (kernel + launch gap) is
+    # what rocprofv3's per-kernel average is compared with
+    env_b2b_ms = float("nan")
+    if last_env_args:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        nb2b = 32
+        e0.record()
+        for _ in range(nb2b):
+            orig_call("usv_env_step", *last_env_args[0])
+        e1.record()
+        torch.cuda.synchronize()
+        env_b2b_ms = e0.elapsed_time(e1) / nb2b
 
     # env + inference only (play_steps) and env only (VecEnv.step with fixed actions), same sizes
     torch.cuda.synchronize()
@@ -261,7 +278,8 @@ def main():
     torch.cuda.synchronize()
     env_fps = args.envs * nenv / (time.perf_counter() - t1)
 
-    env_ms = env_timer.mean_ms()
+    env_ms_events = env_timer.mean_ms()
+    env_ms = env_b2b_ms if env_b2b_ms == env_b2b_ms else env_ms_events
     ppo_ms = ppo_timer.mean_ms()
     achieved = step_bytes * args.envs / (env_ms * 1e-3) / 1e9
     ppo_tfs = PPO_FLOPS_PER_ROW * agent.minibatch_size / (ppo_ms * 1e-3) / 1e12
@@ -319,7 +337,10 @@ def main():
             "roofline": {"bound": "hbm", "kernel": step_kernel,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_env_step": step_bytes, "launch_ms": env_ms,
-                         "envs_per_launch": args.envs},
+                         "launch_ms_event_pairs": env_ms_events, "envs_per_launch": args.envs,
+                         "launch_ms_method": ("32 back-to-back launches between one HIP event pair on the launch "
+                                              "stream" if env_b2b_ms == env_b2b_ms else
+                                              "HIP event pair around each launch")},
             "roofline_ppo": {"bound": "mfma",
                              "kernel": ("k_mb_fused (f32 MFMA fwd+bwd + reduction + Adam, one launch)"
                                         if agent.fused_update else
