@@ -9,8 +9,9 @@
 //
 // k_field_wave / k_field_wave_pack (one 256-thread workgroup per reset env,
 // persistent over the device-side reset count; _pack holds two envs per CU):
-//   1. SDF + occupancy of the 150x150 grid (SDF to a per-slot HBM scratch, the
-//      occupancy as a 2.8 KB bit map in LDS);
+//   1. occupancy of the 150x150 grid as a 2.8 KB bit map in LDS, splatted per
+//      obstacle over its bounding box with the exact per-cell distance test (the
+//      SDF itself is computed by k_field_stats, off this kernel's critical path);
 //   2. cost-to-go: 225 threads each own a 10x10 tile in registers and relax it
 //      with a raster forward + backward chamfer sweep against a halo ring read
 //      from LDS; one barrier per iteration with a block-wide "changed" vote.
@@ -41,7 +42,10 @@ constexpr int kWaveThreads = 256;
 constexpr int kMaxIters = 4096;  // safety cap (never reached)
 constexpr int kChunk = 2048;     // cells per k_field_final work item
 constexpr int kChunks = (G2 + kChunk - 1) / kChunk;
-constexpr int kSlotStride = USV_FIELD_SLOT_STATS;   // floats per reset slot: 16 final + 12 per chunk
+constexpr int kSlotStride = USV_FIELD_SLOT_STATS;   // floats per reset slot: 16 final + 12 per chunk + obstacles
+constexpr int kSlotObst = 160;                      // the slot's 16 obstacle centres (x, y interleaved)
+static_assert(kSlotObst >= 16 + 12 * ((USV_GRID2 + 2047) / 2048) && kSlotObst + 2 * USV_NOBST <= kSlotStride,
+              "slot_stats layout");
 constexpr int kFieldPackMinEnvs = 32768;           // k_field_wave_pack (two envs per CU) from this many envs
 
 // slot_stats layout (per reset slot)
@@ -69,6 +73,24 @@ __device__ __forceinline__ float min_dist(const float *so, float gx, float gy) {
     m2 = fminf(m2, fmaf(dy, dy, dx * dx));
   }
   return sqrtf(m2);   // sqrt is monotone: sqrt(min) == min(sqrt), bit-exact
+}
+
+// compute_occupancy_and_sdf (d_multi_gemini.py:66-104) for one cell: min over the 16
+// obstacles of the squared distance (dx*dx rounded, then fma with dy), sqrt, minus the
+// radius -- the separable SDF's operations per cell, so the bits are the same.
+// Squared distances are >= 0: float order == u32 order (balanced min tree).
+__device__ __forceinline__ float cell_sdf(const float *so, float gx, float gy, float radius) {
+  uint32_t a[USV_NOBST];
+#pragma unroll
+  for (int o = 0; o < USV_NOBST; ++o) {
+    const float dx = gx - so[2 * o], dy = gy - so[2 * o + 1];
+    a[o] = __float_as_uint(fmaf(dy, dy, dx * dx));
+  }
+#pragma unroll
+  for (int w = USV_NOBST / 2; w >= 1; w >>= 1)
+#pragma unroll
+    for (int o = 0; o < w; ++o) a[o] = min(a[o], a[o + w]);
+  return sqrtf(__uint_as_float(a[0])) - radius;   // sqrt(min) == min(sqrt), bit-exact
 }
 
 // +inf for an occupied cell, 0 for a free one (costs are >= 0: max(m, wall) keeps
@@ -100,8 +122,6 @@ constexpr int NTP = NT + 2;                     // padded tile grid edge
 constexpr uint32_t kInfBits = 0x7f800000u;      // +inf
 constexpr uint32_t kOcc = 0xFFFFFFFFu;          // occupied cell marker (a NaN above +inf in u32 order)
 enum { E_TOP = 0, E_BOT, E_LEFT, E_RIGHT };
-constexpr int kSegRows = 30;                    // SDF work unit: one column x 30 rows
-constexpr int kUnits = G * (G / kSegRows);
 // occupancy (sdf <= 0) bit map, column-major: column cc owns words [cc * kOccColWords, +5)
 constexpr int kOccColWords = (G + 31) / 32;
 __device__ __forceinline__ bool occ_bit(const uint32_t *occ, int r, int cc) {
@@ -179,51 +199,26 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
 #ifdef USV_PHASE_PROBE
     if (tid == 0 && blockIdx.x < 4096) g_probe_field[blockIdx.x][12] = wall_clock64();
 #endif
-    // ---- 1. SDF (compute_occupancy_and_sdf :66-104), separable: one column x 30 rows per unit ----
-    float *sdf_s = b.sdf + (size_t)slot * G2;
-    float oy[USV_NOBST];
-#pragma unroll
-    for (int o = 0; o < USV_NOBST; ++o) oy[o] = so[2 * o + 1];
-    for (int u = tid; u < kUnits; u += kWaveThreads) {
-      const int cc = u % G, rs = (u / G) * kSegRows;
-      const float gx = slin[cc];
-      float dx2[USV_NOBST];
-#pragma unroll
-      for (int o = 0; o < USV_NOBST; ++o) {
-        const float dx = gx - so[2 * o];
-        dx2[o] = dx * dx;
+    // ---- 1. occupancy (compute_occupancy_and_sdf :66-104): sdf <= 0 <=> some obstacle has
+    // sqrt(d^2) - r <= 0 (sqrt and the subtraction are monotone), so each obstacle marks the
+    // cells of its bounding box that pass the exact test with its own distance ----
+    if (tid < 2 * USV_NOBST) b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid] = so[tid];
+    {
+      const float half_m = (float)((double)c.map_size / 2);
+      const float cellf = (float)((double)c.map_size / G);
+      const int reach = (int)ceilf(c.obstacle_radius / cellf) + 2;   // cells either side, with margin
+      const int bw = 2 * reach + 1;
+      for (int q = tid; q < USV_NOBST * bw * bw; q += kWaveThreads) {
+        const int o = q / (bw * bw), k = q % (bw * bw);
+        const float ox = so[2 * o], oy = so[2 * o + 1];
+        const float ic = (ox + half_m) / cellf - 0.5f, jc = (oy + half_m) / cellf - 0.5f;
+        if (!(fabsf(ic) < 4.0f * G && fabsf(jc) < 4.0f * G)) continue;   // parked obstacles (999, 999)
+        const int cc = (int)floorf(ic) - reach + k % bw, r = (int)floorf(jc) - reach + k / bw;
+        if (cc < 0 || cc >= G || r < 0 || r >= G) continue;
+        const float dx = slin[cc] - ox, dy = slin[r] - oy;
+        if (sqrtf(fmaf(dy, dy, dx * dx)) - c.obstacle_radius <= 0.f)
+          atomicOr(&occ[cc * kOccColWords + (r >> 5)], 1u << (r & 31));
       }
-      // three rows at a time (independent chains), each a balanced min tree over
-      // the 16 obstacles; squared distances are >= 0: float order == u32 order
-      uint32_t om = 0u;   // occupancy of the unit's 30 rows (bit r - rs)
-      for (int r = rs; r < rs + kSegRows; r += 3) {
-        float sd[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const float gy = slin[r + k];
-          uint32_t a[USV_NOBST];
-#pragma unroll
-          for (int o = 0; o < USV_NOBST; ++o) {
-            const float dy = gy - oy[o];
-            a[o] = __float_as_uint(fmaf(dy, dy, dx2[o]));
-          }
-#pragma unroll
-          for (int w = USV_NOBST / 2; w >= 1; w >>= 1)
-#pragma unroll
-            for (int o = 0; o < w; ++o) a[o] = min(a[o], a[o + w]);
-          sd[k] = sqrtf(__uint_as_float(a[0])) - c.obstacle_radius;   // sqrt(min) == min(sqrt), bit-exact
-        }
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          om |= (sd[k] <= 0.f ? 1u : 0u) << (r + k - rs);
-          sdf_s[(r + k) * G + cc] = sd[k];
-        }
-      }
-      // the unit's 30 bits span at most two words of its column
-      const uint64_t m64 = (uint64_t)om << (rs & 31);
-      uint32_t *oc = occ + cc * kOccColWords + (rs >> 5);
-      if ((uint32_t)m64) atomicOr(oc, (uint32_t)m64);
-      if ((uint32_t)(m64 >> 32)) atomicOr(oc + 1, (uint32_t)(m64 >> 32));
     }
     __syncthreads();
     USV_PHASE(field, 1);
@@ -394,17 +389,22 @@ __device__ __forceinline__ BatchK batch_k(const usv_cfg_t &c, const usv_bufs_t &
 __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
   __shared__ float red[10][4];
   __shared__ int flags[2];
+  __shared__ float slin[G];
+  __shared__ float so[2 * USV_NOBST];
   const int count = b.ctl[USV_CTL_RESET_COUNT];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float cell = (float)((double)c.map_size / G);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
   const int items = count * kChunks;
+  if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
     const int slot = w / kChunks, ch = w % kChunks;
     const int e = b.reset_ids[slot];
     const float *Fe = b.field + (size_t)e * G2;
-    const float *sdf_s = b.sdf + (size_t)slot * G2;
+    float *sdf_s = b.sdf + (size_t)slot * G2;
+    if (tid < 2 * USV_NOBST) so[tid] = b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid];
     if (tid < 2) flags[tid] = 0;
+    __syncthreads();
     float gmin = INFINITY, gmax = -INFINITY, jmin_f = INFINITY, jmax_f = -INFINITY, jall_f = 0.f;
     float jrmin_i = INFINITY, jrmax_i = -INFINITY, jrall_i = 0.f;
     int any_inf = 0, inside = 0;
@@ -415,7 +415,14 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
     for (int k = 0; k < PER; ++k) {
       const int q = ch * kChunk + k * 256 + tid;
       gv[k] = q < q1 ? Fe[q] : 0.f;
-      sv[k] = q < q1 ? sdf_s[q] : INFINITY;
+    }
+    // the SDF of this chunk (k_field_final reads it back)
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int q = ch * kChunk + k * 256 + tid;
+      const int qc = min(q, G2 - 1);
+      sv[k] = cell_sdf(so, slin[qc % G], slin[qc / G], c.obstacle_radius);
+      if (q < q1) sdf_s[q] = sv[k];
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
