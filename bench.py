@@ -252,7 +252,9 @@ def main():
     # pairs above carry ~3 us of event overhead at 4096 envs; this mean (kernel + launch gap) is
     # what rocprofv3's per-kernel average is compared with
     env_b2b_ms = float("nan")
-    if last_env_args:
+    # only where the step's working set is cache-resident in the training loop too (4096 envs: 2.7 MB);
+    # at large env counts back-to-back launches would find the previous launch's state in the MALL
+    if last_env_args and args.envs <= 16384:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         nb2b = 32
         e0.record()
