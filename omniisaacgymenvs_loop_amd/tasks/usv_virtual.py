@@ -281,11 +281,14 @@ class USVVirtual:
         return 0.0
 
     def env_step(self, actions: torch.Tensor, u_step: Optional[torch.Tensor] = None,
-                 u_reset: Optional[torch.Tensor] = None):
+                 u_reset: Optional[torch.Tensor] = None, post_state: Optional[torch.Tensor] = None):
         """pre_physics_step + 10 substeps + post_physics_step (USV_Virtual.py:1042-1652).
 
         Returns the device tensors (obs [n,33], rew [n], dones int64 [n]).  u_step / u_reset replay
-        recorded uniforms (parity tests) instead of the in-kernel Philox draws."""
+        recorded uniforms (parity tests) instead of the in-kernel Philox draws.  post_state ([8][n]:
+        px, py, yaw, vx, vy, wz, fl, fr) replaces the integrator by a recorded post-integration state:
+        the step then runs pre_physics_step and RLTask.post_physics_step (rl_task.py:283-303) on that
+        state, as the reference does on whatever PhysX returned (parity of the post-physics path alone)."""
         actions = self._f32(actions)
         s = _capi.stream_ptr()
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
@@ -293,8 +296,15 @@ class USVVirtual:
         _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
         if self._has_field:   # CaptureXY only (GoToPose / TrackXYOVelocity have no obstacles)
             _capi.call("usv_potential_field", cfg, b, s)
-        _capi.call("usv_env_step", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
-                   self.seed, k, _capi.ptr(u_step), s)
+        substeps = self.cfg.substeps
+        if post_state is not None:
+            self.state.copy_(post_state.to(self._device, torch.float32).reshape(8, self._num_envs))
+            self.cfg.substeps = 0
+        try:
+            _capi.call("usv_env_step", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
+                       self.seed, k, _capi.ptr(u_step), s)
+        finally:
+            self.cfg.substeps = substeps
         return self.obs_view, self.rew_buf, self.dones
 
     def _f32(self, actions: torch.Tensor) -> torch.Tensor:

@@ -52,3 +52,11 @@ def golden():
         return cache[name]
 
     return load
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    from tests import errtab
+    errtab.dump(os.path.join(ROOT, "gpurun_out", "parity_errors.json"))
+    txt = errtab.format_table()
+    if txt:
+        terminalreporter.write_line(txt)
