@@ -4,12 +4,13 @@ One bench "step" = one rl_games train epoch: horizon_length=16 control steps of
 num_envs envs (each = reset path + 10 physics substeps + obs/reward/done, on the
 GPU) interleaved with the policy forward, then GAE + dataset preparation and
 8 mini-epochs of PPO minibatch updates (fwd + bwd + clip + Adam), i.e. the
-reference's "fps total" (rl_games a2c_common.py:46-60).  Workload:
-BASELINE.json configs[1] = USV_Virtual_CaptureXY num_envs=4096 PPO-MLP fp32 per
-GPU; with --gpus N each rank owns 4096 envs (weak scaling) and gradients are
-all-reduced over RCCL every minibatch.
+reference's "fps total" (rl_games a2c_common.py:46-60).  Workload: the north
+star's USV_Virtual_CaptureXY at 2^20 envs over 8 GPUs (BASELINE.json configs[4]),
+i.e. 131072 envs per GPU, PPO-MLP fp32; with --gpus N each rank owns 131072 envs
+(weak scaling) and gradients are all-reduced over RCCL every minibatch.  The
+4096-env BASELINE configs[1] line is reported as a secondary field (extra.c2).
 
-    python bench.py [--gpus N --steps K --warmup W --envs 4096]
+    python bench.py [--gpus N --steps K --warmup W --envs 131072]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -100,11 +101,26 @@ class KernelTimer:
         return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
 
 
-def cpu_baseline(envs=256, budget_s=12.0):
-    """The oracle (C env restatement + numpy PPO) timed on one host core, on a
-    bounded sample of the same workload: repeated train epochs of envs x 16
-    control steps (incl. episode resets + potential fields) + 8 mini-epochs of
-    PPO on that epoch's batch, until ~budget_s of CPU time has been spent."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(shapes=((32, 512, 4.0), (4096, 8192, 20.0))):
+    """The oracle (C env restatement, OpenMP over envs / reset slots, + numpy PPO with threaded BLAS)
+    timed on all host cores, on bounded samples of the same workload at BASELINE's CPU-sized shapes:
+    configs[0] (32 envs, minibatch 512 = the whole 32 x 16 batch) and configs[1] (4096 envs, the real
+    minibatch 8192).  One sample = whole train epochs: 16 control steps (policy forward, Normal sample,
+    env step incl. episode resets + potential fields), GAE on the rewards x 0.01, value / advantage
+    preparation, 8 mini-epochs of minibatch updates (fwd + bwd + clip + Adam + adaptive LR), until the
+    shape's time budget is spent (at least one epoch).  `value` is the configs[1] rate."""
+    os.environ["USV_ORACLE_OMP"] = "1"
     import numpy as np
     from threadpoolctl import threadpool_limits
     from oracle import oracle as O
@@ -113,37 +129,81 @@ def cpu_baseline(envs=256, budget_s=12.0):
     yaml_path = os.path.join(ROOT, "omniisaacgymenvs_loop_amd/cfg/task/USV/IROS2024/USV_Virtual_CaptureXY_SysID-TEST.yaml")
     task_cfg = load_yaml(yaml_path)
     cfg = build_usv_cfg(task_cfg)
+    cores = int(O.lib().oracle_threads())
     H = 16
-    sw = lambda x: np.ascontiguousarray(np.swapaxes(np.stack(x), 0, 1).reshape(envs * H, *np.stack(x).shape[2:]))
-    with threadpool_limits(1):
-        E = O.OracleEnv(cfg, envs, O.make_lut(*thruster_tables(task_cfg)))
-        rng = np.random.default_rng(0)
-        P = PO.unflatten(np.random.default_rng(1).uniform(-0.08, 0.08, PO.NPARAM).astype(np.float32))
-        orms, adam, lr = PO.RMS.zeros(33), PO.Adam.zeros(), 1e-4
-        E.full_step(np.zeros((envs, 2), np.float32), -0.6, 0, seed=1)     # initial reset of every env: untimed
-        obs = E.obs.copy()
-        step, epochs = 1, 0
-        t0 = time.perf_counter()
-        while epochs < 2 or time.perf_counter() - t0 < budget_s:
-            obs_buf, act_buf, nlp_buf, val_buf, mu_buf = [], [], [], [], []
-            for _ in range(H):
-                _, _, mu, v = PO.forward(P, orms.norm(obs).astype(np.float32))
-                a = (mu + rng.standard_normal(mu.shape).astype(np.float32)).astype(np.float32)
-                obs_buf.append(obs.copy()); act_buf.append(a); val_buf.append(v[:, 0]); mu_buf.append(mu)
-                nlp_buf.append(PO.neglogp(a, mu, np.ones_like(mu), np.zeros_like(mu)))
-                E.full_step(np.clip(a, -1, 1), -0.6, step, seed=1)
-                obs = E.obs.copy()
-                step += 1
-            ds = {"obs": sw(obs_buf), "actions": sw(act_buf), "old_logp": sw(nlp_buf), "old_values": sw(val_buf),
-                  "returns": sw(val_buf) + 0.1, "advantages": rng.standard_normal(envs * H).astype(np.float32),
-                  "mu": sw(mu_buf), "sigma": np.ones((envs * H, 2), np.float32)}
-            P, lr, _ = PO.train_epoch_update(P, adam, lr, orms, ds, PO.PPOConfig(minibatch=envs * H))
-            epochs += 1
-        dt = time.perf_counter() - t0
-    return {"value": epochs * envs * H / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{epochs} train epochs of {envs} envs x {H} steps (C oracle env incl. episode resets + "
-                      f"potential fields; initial reset untimed) + 8 mini-epochs numpy PPO per epoch; "
-                      f"1 thread; {dt:.1f} s"}
+    res = {}
+    with threadpool_limits(cores):
+        for envs, mb, budget in shapes:
+            sw = lambda x: np.ascontiguousarray(np.swapaxes(np.stack(x), 0, 1).reshape(envs * H, *np.stack(x).shape[2:]))
+            E = O.OracleEnv(cfg, envs, O.make_lut(*thruster_tables(task_cfg)))
+            rng = np.random.default_rng(0)
+            P = PO.unflatten(np.random.default_rng(1).uniform(-0.08, 0.08, PO.NPARAM).astype(np.float32))
+            orms, vrms, adam, lr = PO.RMS.zeros(33), PO.RMS.zeros(1), PO.Adam.zeros(), 3e-4
+            pcfg = PO.PPOConfig(minibatch=mb)
+            E.full_step(np.zeros((envs, 2), np.float32), -0.6, 0, seed=1)     # initial reset of every env: untimed
+            obs = E.obs.copy()
+            dones = np.ones(envs, np.float32)
+            step, epochs = 1, 0
+            t0 = time.perf_counter()
+            while epochs < 1 or time.perf_counter() - t0 < budget:
+                obs_b, act_b, nlp_b, val_b, mu_b, rew_b, done_b = [], [], [], [], [], [], []
+                for _ in range(H):
+                    _, _, mu, v = PO.forward(P, orms.norm(obs).astype(np.float32))
+                    a = (mu + rng.standard_normal(mu.shape).astype(np.float32)).astype(np.float32)
+                    obs_b.append(obs.copy()); act_b.append(a); val_b.append(v); mu_b.append(mu)
+                    nlp_b.append(PO.neglogp(a, mu, np.ones_like(mu), np.zeros_like(mu)))
+                    done_b.append(dones.copy())
+                    E.full_step(np.clip(a, -1, 1), -0.6, step, seed=1)
+                    obs = E.obs.copy()
+                    rew_b.append((E.rew * np.float32(0.01))[:, None].astype(np.float32))
+                    dones = E.reset_buf.astype(np.float32)
+                    step += 1
+                _, _, _, last_v = PO.forward(P, orms.norm(obs).astype(np.float32))
+                adv = PO.discount_values(0.99, 0.95, dones, last_v, np.stack(done_b), np.stack(val_b), np.stack(rew_b))
+                ret = adv + np.stack(val_b)
+                vals, rets = sw(val_b)[:, 0], sw([r for r in ret])[:, 0]
+                vrms.update(vals[:, None]); vrms.update(rets[:, None])
+                a_flat = rets - vals
+                a_flat = ((a_flat - a_flat.mean()) / (a_flat.std(ddof=1) + 1e-8)).astype(np.float32)
+                ds = {"obs": sw(obs_b), "actions": sw(act_b), "old_logp": sw(nlp_b), "old_values": vals,
+                      "returns": rets, "advantages": a_flat, "mu": sw(mu_b),
+                      "sigma": np.ones((envs * H, 2), np.float32)}
+                P, lr, _ = PO.train_epoch_update(P, adam, lr, orms, ds, pcfg)
+                epochs += 1
+            dt = time.perf_counter() - t0
+            res[envs] = (epochs * envs * H / dt, epochs, dt, mb)
+    (v1, e1, t1, m1), (v2, e2, t2, m2) = res[shapes[0][0]], res[shapes[1][0]]
+    return {"value": v2, "unit": "env-steps/s", "cores": cores, "kind": "port", "cpu_model": _cpu_model(),
+            "value_c1": v1,
+            "sample": f"configs[1] shape: {e2} train epochs of {shapes[1][0]} envs x {H} steps in {t2:.1f} s "
+                      f"(minibatch {m2}); configs[0] shape: {e1} epochs of {shapes[0][0]} envs in {t1:.1f} s "
+                      f"(minibatch {m1}); C oracle env (OpenMP, episode resets + potential fields; initial reset "
+                      f"untimed) + numpy PPO (GAE, 8 mini-epochs, clip + Adam + adaptive LR); {cores} threads"}
+
+
+C2_ENVS = 4096                 # BASELINE configs[1]: secondary line of the same run
+HEADLINE_ENVS = 131072         # BASELINE configs[4] per GPU: 2^20 envs over 8 GPUs
+REWARD_TARGET = 30.0           # BASELINE metric, half 2: wall-clock to rewards/step >= 30
+
+
+def time_epochs(agent, steps, world, local):
+    """`steps` train epochs between barrier + synchronize pairs; max over ranks (seconds)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        agent.train_epoch()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def main():
@@ -151,20 +211,22 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--envs", type=int, default=4096, help="envs per GPU (BASELINE configs[1]: 4096)")
+    ap.add_argument("--envs", type=int, default=HEADLINE_ENVS,
+                    help="envs per GPU (default: BASELINE configs[4]'s per-GPU share, 131072 = 2^20 / 8)")
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph capture)")
     ap.add_argument("--task", default="CaptureXY", choices=sorted(TASKS) + ["multitask"],
                     help="multitask: even ranks GoToPose, odd ranks TrackXYOVelocity, one shared policy (C4)")
-    ap.add_argument("--env-only-envs", type=int, default=131072,
-                    help="extra env-only throughput probe at the C5 per-GPU size (0 = skip)")
+    ap.add_argument("--c2-steps", type=int, default=10,
+                    help="epochs of the secondary BASELINE configs[1] line (4096 envs/GPU; 0 = skip)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
     rank, world, local = _dist_setup(args.gpus)
     task_name = args.task if args.task != "multitask" else ("GoToPose", "TrackXYOVelocity")[rank % 2]
     step_bytes, step_kernel = TASKS[task_name][1], TASKS[task_name][2]
+    t_start = time.perf_counter()
     env, task, agent = build(args.envs, local, world, args.seed + rank, task_name)
     agent.use_graph = not args.no_graph
     from omniisaacgymenvs_loop_amd import _capi
@@ -173,12 +235,8 @@ def main():
     env_timer, ppo_timer = KernelTimer(), KernelTimer()
     orig_call, orig_call_rc = _capi.call, _capi.call_rc
 
-    last_env_args = []
-
     def timed_call(name, *a):
         if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
-            if name == "usv_env_step":
-                last_env_args[:] = [a]
             env_timer(lambda: orig_call(name, *a))
         elif timing[0] and name == "ppo_minibatch_grad":
             ppo_timer(lambda: orig_call(name, *a))
@@ -196,19 +254,30 @@ def main():
     _capi.call = timed_call
     _capi.call_rc = timed_call_rc
 
+    # training from the random init starts here: the wall clock to reward=30 counts from the first
+    # reset (env / agent construction excluded), through warmup and timed epochs alike
+    t_train = time.perf_counter()
+    to_reward = {"target": REWARD_TARGET, "seconds": None, "epochs": None}
+
+    def note_reward():
+        if to_reward["seconds"] is None and agent.game_rewards.current_size > 0 and \
+                agent.game_rewards.get_mean() >= REWARD_TARGET:
+            to_reward["seconds"] = time.perf_counter() - t_train
+            to_reward["epochs"] = agent.epoch_num
+
     agent.obs = agent.env_reset()
     # warmup: the first epoch runs eagerly, the second captures the rollout and update HIP graphs
     for _ in range(max(args.warmup, 2)):
+        agent.update_epoch()
         agent.train_epoch()
+        note_reward()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    step_t = play_t = 0.0
     for _ in range(args.steps):
-        st, pt, ut, tt = agent.train_epoch()
-        step_t += st
-        play_t += pt
+        agent.update_epoch()
+        agent.train_epoch()          # synchronises the stream at its end (meters, adaptive LR)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -217,15 +286,18 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    note_reward()
     frames = world * args.envs * agent.horizon_length * args.steps
     value = frames / elapsed
+    print(f"[bench] rank {rank}: {args.steps} epochs in {elapsed:.3f} s -> {value / 1e6:.2f} M env-steps/s",
+          file=sys.stderr, flush=True)
 
     # phase split of one epoch with graph replays: rollout (+ GAE/prepare) vs minibatch update
     phase = {}
     if agent._graph_play is not None and agent._graph_update is not None:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         tp = tu = 0.0
-        nrep = 5
+        nrep = 3
         for _ in range(nrep):
             ev[0].record()
             agent._graph_play.replay()
@@ -236,100 +308,50 @@ def main():
             agent._advance_host_clocks()
             tp += ev[0].elapsed_time(ev[1])
             tu += ev[1].elapsed_time(ev[2])
-        phase = {"rollout_ms": tp / nrep, "update_ms": tu / nrep}
+        phase = {"rollout_ms": tp / nrep, "update_ms": tu / nrep,
+                 "update_us_per_minibatch": tu / nrep * 1e3 / (agent.mini_epochs_num * agent.num_minibatches)}
 
-    # per-launch kernel times: the same epochs launched eagerly (graph replays carry no per-kernel events),
+    # per-launch kernel times inside real epochs (eager: graph replays carry no per-kernel events),
     # HIP events on the launch stream around each C-ABI call
     use_graph = agent.use_graph
     agent.use_graph = False
     timing[0] = True
-    for _ in range(2):
-        agent.train_epoch()
+    agent.train_epoch()
     torch.cuda.synchronize()
     timing[0] = False
     agent.use_graph = use_graph
-    # the same env-step launch 32 times back to back between one event pair: the per-launch event
-    # pairs above carry ~3 us of event overhead at 4096 envs; this mean (kernel + launch gap) is
-    # what rocprofv3's per-kernel average is compared with
-    env_b2b_ms = float("nan")
-    # only where the step's working set is cache-resident in the training loop too (4096 envs: 2.7 MB);
-    # at large env counts back-to-back launches would find the previous launch's state in the MALL
-    if last_env_args and args.envs <= 16384:
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        nb2b = 32
-        e0.record()
-        for _ in range(nb2b):
-            orig_call("usv_env_step", *last_env_args[0])
-        e1.record()
-        torch.cuda.synchronize()
-        env_b2b_ms = e0.elapsed_time(e1) / nb2b
 
-    # env + inference only (play_steps) and env only (VecEnv.step with fixed actions), same sizes
+    # env + inference only (play_steps) and env only (VecEnv.step with fixed actions), same size
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(max(2, args.steps // 4)):
+    nplay = 2
+    for _ in range(nplay):
         agent.play_steps()
     torch.cuda.synchronize()
-    play_fps = args.envs * agent.horizon_length * max(2, args.steps // 4) / (time.perf_counter() - t1)
+    play_fps = args.envs * agent.horizon_length * nplay / (time.perf_counter() - t1)
     acts = torch.zeros((args.envs, 2), device=f"cuda:{local}")
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    nenv = 64
+    nenv = 32
     for _ in range(nenv):
         env.step(acts)
     torch.cuda.synchronize()
     env_fps = args.envs * nenv / (time.perf_counter() - t1)
 
-    env_ms_events = env_timer.mean_ms()
-    env_ms = env_b2b_ms if env_b2b_ms == env_b2b_ms else env_ms_events
+    env_ms = env_timer.mean_ms()
     ppo_ms = ppo_timer.mean_ms()
     achieved = step_bytes * args.envs / (env_ms * 1e-3) / 1e9
     ppo_tfs = PPO_FLOPS_PER_ROW * agent.minibatch_size / (ppo_ms * 1e-3) / 1e12
-    extra = {}
-    if args.env_only_envs and rank == 0 and world == 1:
-        # C5 per-GPU size: env-only throughput and the env-step kernel roofline at scale
-        from omniisaacgymenvs_loop_amd.tasks.usv_virtual import USVVirtual
-        big = USVVirtual(task._task_cfg, num_envs=args.env_only_envs, device=f"cuda:{local}", seed=5)
-        a = torch.rand((args.env_only_envs, 2), device=f"cuda:{local}") * 2 - 1
-        for _ in range(3):
-            big.env_step(a)
-        big_timer = KernelTimer()
-        timing_big = []
-
-        def big_call(name, *aa):
-            if name == "usv_env_step":
-                big_timer(lambda: orig_call(name, *aa))
-            else:
-                orig_call(name, *aa)
-
-        _capi.call = big_call
-        torch.cuda.synchronize()
-        tb = time.perf_counter()
-        nb = 32
-        for _ in range(nb):
-            big.env_step(a)
-        torch.cuda.synchronize()
-        tb = time.perf_counter() - tb
-        _capi.call = timed_call
-        bms = big_timer.mean_ms()
-        extra = {"env_only_envs": args.env_only_envs, "env_only_fps": args.env_only_envs * nb / tb,
-                 "env_step_kernel_ms": bms,
-                 "env_step_kernel_gbs": step_bytes * args.env_only_envs / (bms * 1e-3) / 1e9,
-                 "env_step_kernel_frac": step_bytes * args.env_only_envs / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS}
-        tf = os.path.join(ROOT, "profiles", f"env_step_traffic_{args.env_only_envs}.json")
-        if os.path.exists(tf) and task_name == "CaptureXY":
-            with open(tf) as f:
-                tr = json.load(f)
-            extra["env_step_kernel_traffic"] = tr.get("bytes_per_launch")
-            extra["env_step_kernel_traffic_gbs"] = tr.get("bytes_per_launch") / (bms * 1e-3) / 1e9
-        del big
+    out = None
     if rank == 0:
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init policy, "
             "randomised spawns/obstacles/DR from the reset path)",
-            "config": {"workload": (f"USV_Virtual_CaptureXY num_envs={args.envs}/GPU PPO-MLP fp32 (BASELINE configs[1])"
+            "config": {"workload": (f"USV_Virtual_CaptureXY num_envs={args.envs}/GPU PPO-MLP fp32"
+                                    + (" (BASELINE configs[4] per GPU: 2^20 envs over 8 GPUs)"
+                                       if args.envs == HEADLINE_ENVS else "")
                                     if args.task == "CaptureXY" else
                                     f"USV_Virtual_{args.task} num_envs={args.envs}/GPU PPO-MLP fp32"),
                        "num_envs_per_gpu": args.envs, "horizon_length": agent.horizon_length,
@@ -339,10 +361,9 @@ def main():
             "roofline": {"bound": "hbm", "kernel": step_kernel,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_env_step": step_bytes, "launch_ms": env_ms,
-                         "launch_ms_event_pairs": env_ms_events, "envs_per_launch": args.envs,
-                         "launch_ms_method": ("32 back-to-back launches between one HIP event pair on the launch "
-                                              "stream" if env_b2b_ms == env_b2b_ms else
-                                              "HIP event pair around each launch")},
+                         "envs_per_launch": args.envs,
+                         "launch_ms_method": f"HIP event pair around each of the {len(env_timer.pairs)} env-step "
+                                             "launches of one eager training epoch, on the launch stream"},
             "roofline_ppo": {"bound": "mfma",
                              "kernel": ("k_mb_fused (f32 MFMA fwd+bwd + reduction + Adam, one launch)"
                                         if agent.fused_update else
@@ -350,18 +371,41 @@ def main():
                              "achieved": ppo_tfs,
                              "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},
-            "extra": dict(extra, **phase),
+            "wall_clock_to_reward": dict(to_reward, unit="s", since="first env reset of this run (random-init policy)",
+                                         last100_mean_at_end=float(agent.game_rewards.get_mean())),
+            "extra": dict(phase),
         }
-        traffic_file = os.path.join(ROOT, "profiles", "env_step_traffic.json")
-        if os.path.exists(traffic_file):
-            with open(traffic_file) as f:
+        tf = os.path.join(ROOT, "profiles", f"env_step_traffic_{args.envs}.json")
+        if not os.path.exists(tf) and args.envs == C2_ENVS:
+            tf = os.path.join(ROOT, "profiles", "env_step_traffic.json")
+        if os.path.exists(tf) and task_name == "CaptureXY":
+            with open(tf) as f:
                 tr = json.load(f)
-            if tr.get("envs") == args.envs and task_name == "CaptureXY":
+            if tr.get("envs") == args.envs:
                 out["roofline"]["traffic"] = tr.get("bytes_per_launch")
                 out["roofline"]["traffic_source"] = tr.get("source")
+    # secondary line: BASELINE configs[1] (4096 envs/GPU), same code path, graph-replayed epochs
+    if args.c2_steps and args.envs != C2_ENVS and task_name == "CaptureXY":
+        del agent, env, task
+        torch.cuda.empty_cache()
+        env2, task2, agent2 = build(C2_ENVS, local, world, args.seed + rank, task_name)
+        agent2.use_graph = not args.no_graph
+        agent2.obs = agent2.env_reset()
+        for _ in range(3):
+            agent2.train_epoch()
+        el2 = time_epochs(agent2, args.c2_steps, world, local)
+        if out is not None:
+            out["extra"]["c2"] = {"workload": f"USV_Virtual_CaptureXY num_envs={C2_ENVS}/GPU PPO-MLP fp32 "
+                                              "(BASELINE configs[1])",
+                                  "value": world * C2_ENVS * agent2.horizon_length * args.c2_steps / el2,
+                                  "unit": "env-steps/s", "ms_per_step": el2 / args.c2_steps * 1e3,
+                                  "steps": args.c2_steps}
+    if rank == 0:
         if not args.no_cpu_baseline and world == 1 and args.task == "CaptureXY":
+            print("[bench] cpu baseline ...", file=sys.stderr, flush=True)
             out["cpu_baseline"] = cpu_baseline()
-        print(json.dumps(out))
+        out["extra"]["bench_wall_s"] = time.perf_counter() - t_start
+        print(json.dumps(out, default=float))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

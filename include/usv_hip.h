@@ -293,6 +293,7 @@ typedef struct usv_bufs {
 #define USV_CTL_H_INJ_HI   15
 #define USV_CTL_SCENE_ERR  16   /* scene replay: an index fell outside [0, n_scenes) with cycle off */
 #define USV_CTL_BATCH_DONE 17   /* completion counter of the potential-field batch fold (keep 0) */
+#define USV_CTL_FIELD_EXACT 18  /* count of reset envs whose cost field took the reference's 225 literal sweeps */
 #define USV_CTL_N           20
 
 /* ------------------------------------------------------------------------ */

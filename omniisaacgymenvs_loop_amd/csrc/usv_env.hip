@@ -90,6 +90,11 @@ __global__ void k_step_begin(usv_bufs_t b) {
   if (t == 1) b.ctl[USV_CTL_ANY_INSIDE] = 0;
   if (t == 2) b.ctl[USV_CTL_ANY_FINITE] = 0;
   if (t < 4) b.fscratch[t] = 0.f;
+  // completion counters of this step's kernels: their last workgroup also returns them to 0,
+  // but a step never depends on that (a counter left non-zero by an aborted launch would
+  // otherwise make every later "last workgroup" test fail silently)
+  if (t == 4) b.ctl[USV_CTL_OBST_DONE] = 0;
+  if (t == 5) b.ctl[USV_CTL_BATCH_DONE] = 0;
 }
 
 // ------------------------------------------------------------------------

@@ -53,7 +53,7 @@ enum {
   SS_GMIN_F = 0, SS_GMAX_F, SS_ANY_INF,        // finite-cost extrema, any infinite cell
   SS_JMIN_F_NI, SS_JMAX_F_NI, SS_JMAX_F_ALL,   // J over finite cells: non-inside min/max, max of all
   SS_JRMIN_I_NI, SS_JRMAX_I_NI, SS_JRMAX_I_ALL,  // eta (1/d - 1/r0)^2 over infinite cells (mask applied later)
-  SS_INSIDE, SS_ITERS
+  SS_INSIDE, SS_ITERS, SS_EXACT
 };
 
 __device__ __forceinline__ float grid_coord(const float *lin, float map_size, int i) {
@@ -128,6 +128,39 @@ __device__ __forceinline__ bool occ_bit(const uint32_t *occ, int r, int cc) {
   return (occ[cc * kOccColWords + (r >> 5)] >> (r & 31)) & 1u;
 }
 
+// compute_cost_field_wavefront (d_multi_gemini.py:135-192) as written: int(1.5 G) = 225
+// synchronous sweeps of min(self, 8 rolled neighbours + move cost) with the rolled-in edge at
+// +inf, occupied cells forced to +inf after every sweep, the target cell seeded with 0.  Run
+// only for an env whose tile-sweep fixed point is not certified equal to it (see below):
+// ping-pong through the env's field row and the slot's SDF scratch (k_field_stats writes the
+// SDF later), one block barrier per sweep; all waves of the block share the CU's L1, so plain
+// global loads see the other waves' stores after the barrier.
+constexpr int kRefSweeps = (G * 3) / 2;
+__device__ __forceinline__ void cost_sweeps_exact(const uint32_t *occ, int ix, int iy, float *A, float *B) {
+  const int tid = threadIdx.x;
+  for (int q = tid; q < G2; q += kWaveThreads) A[q] = (q == iy * G + ix) ? 0.f : INFINITY;
+  __syncthreads();
+  for (int it = 0; it < kRefSweeps; ++it) {
+    for (int q = tid; q < G2; q += kWaveThreads) {
+      const int r = q / G, cc = q % G;
+      float m = A[q];
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy)
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (!dx && !dy) continue;
+          const int rr = r - dy, c2 = cc - dx;   // torch.roll(shifts=(dy, dx)): shifted[r][c] = A[r-dy][c-dx]
+          if (rr < 0 || rr >= G || c2 < 0 || c2 >= G) continue;
+          m = fminf(m, A[rr * G + c2] + ((dx && dy) ? 1.414f : 1.0f));
+        }
+      const bool o = r == 0 || r == G - 1 || cc == 0 || cc == G - 1 || occ_bit(occ, r, cc);
+      B[q] = o ? INFINITY : m;
+    }
+    __syncthreads();
+    float *t = A; A = B; B = t;
+  }
+}
+
 // LDS holds the tile edges and a 2.8 KB occupancy bit map (the SDF itself goes to
 // the per-slot HBM scratch only): 51 KB.  Two launch shapes of the same body:
 // k_field_wave_pack is held to 256 registers (its spills sit in the per-slot
@@ -143,7 +176,7 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
   __shared__ float slin[G];
   __shared__ float red[12][kWaveThreads / 64];
   const int n = b.n;
-  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);   // slots index reset_ids[0, n)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
   // obstacle placement handed over by usv_reset (keys of its draws)
@@ -345,6 +378,23 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
 #ifdef USV_PHASE_PROBE
     if (tid == 0 && blockIdx.x < 4096) g_probe_field[blockIdx.x][14] = clock64();
 #endif
+    // ---- certificate: the reference stops after 225 Jacobi sweeps, whose result at a cell is the
+    // minimum over paths of at most 225 hops.  Every hop adds >= 1 to an fp32 path sum, so a cell
+    // whose fixed-point cost is <= kPinnedCost has an optimal path of <= 225 hops and the two agree.
+    // If some finite cost exceeds it (long detours; never for the packaged spawn ranges, possible
+    // for replayed scenes) or the sweep cap was reached, the env takes the reference's sweeps. ----
+    constexpr float kPinnedCost = 224.0f;
+    float hmax = 0.f;
+    if (tile_ok) {
+#pragma unroll
+      for (int i = 0; i < T; ++i)
+#pragma unroll
+        for (int j = 0; j < T; ++j) {
+          const uint32_t hb = __float_as_uint(h[i + 1][j + 1]);
+          if (hb < kInfBits) hmax = fmaxf(hmax, h[i + 1][j + 1]);
+        }
+    }
+    const bool exact = __syncthreads_or((hmax > kPinnedCost) || (it >= kMaxIters)) != 0;
     // ---- 3. raw cost out (occupied marker -> +inf); statistics in k_field_stats ----
     float *Fe = b.field + (size_t)e * G2;
     if (tile_ok) {
@@ -359,6 +409,7 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
     }
     if (tid == 0) {
       b.slot_stats[(size_t)slot * kSlotStride + SS_ITERS] = (float)it;   // iterations (diagnostic)
+      b.slot_stats[(size_t)slot * kSlotStride + SS_EXACT] = exact ? 1.f : 0.f;   // k_field_exact redoes it
 #ifdef USV_PHASE_PROBE
       if (blockIdx.x < 4096) g_probe_field[blockIdx.x][15] = (unsigned long long)it;
 #endif
@@ -370,6 +421,54 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
 
 __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) { field_wave_body(c, b); }
 __global__ __launch_bounds__(kWaveThreads, 2) void k_field_wave_pack(usv_cfg_t c, usv_bufs_t b) { field_wave_body(c, b); }
+
+// The reference's literal sweeps for the slots k_field_wave could not certify (SS_EXACT):
+// one workgroup per such slot, the occupancy bit map rebuilt from the slot's obstacles
+// exactly as k_field_wave builds it.  A separate launch keeps the sweep kernel's registers
+// untouched; with nothing flagged every workgroup exits after one load per slot.
+__global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_bufs_t b) {
+  __shared__ uint32_t occ[G * kOccColWords];
+  __shared__ float so[2 * USV_NOBST];
+  __shared__ float slin[G];
+  const int n = b.n;
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);
+  const int tid = threadIdx.x;
+  for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
+    const float *st = b.slot_stats + (size_t)slot * kSlotStride;
+    if (st[SS_EXACT] == 0.f) continue;   // uniform per workgroup
+    const int e = b.reset_ids[slot];
+    if (tid < 2 * USV_NOBST) so[tid] = st[kSlotObst + tid];
+    if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
+    for (int q = tid; q < G * kOccColWords; q += kWaveThreads) occ[q] = 0u;
+    __syncthreads();
+    const float half_m = (float)((double)c.map_size / 2);
+    const float cellf = (float)((double)c.map_size / G);
+    const int reach = (int)ceilf(c.obstacle_radius / cellf) + 2;
+    const int bw = 2 * reach + 1;
+    for (int q = tid; q < USV_NOBST * bw * bw; q += kWaveThreads) {
+      const int o = q / (bw * bw), k = q % (bw * bw);
+      const float ox = so[2 * o], oy = so[2 * o + 1];
+      const float ic = (ox + half_m) / cellf - 0.5f, jc = (oy + half_m) / cellf - 0.5f;
+      if (!(fabsf(ic) < 4.0f * G && fabsf(jc) < 4.0f * G)) continue;
+      const int cc = (int)floorf(ic) - reach + k % bw, r = (int)floorf(jc) - reach + k / bw;
+      if (cc < 0 || cc >= G || r < 0 || r >= G) continue;
+      const float dx = slin[cc] - ox, dy = slin[r] - oy;
+      if (sqrtf(fmaf(dy, dy, dx * dx)) - c.obstacle_radius <= 0.f)
+        atomicOr(&occ[cc * kOccColWords + (r >> 5)], 1u << (r & 31));
+    }
+    const float tx = b.field_old_tgt[e], ty = b.field_old_tgt[n + e];
+    int ix = (int)((tx + half_m) / cellf), iy = (int)((ty + half_m) / cellf);
+    ix = min(max(ix, 0), G - 1);
+    iy = min(max(iy, 0), G - 1);
+    __syncthreads();
+    float *Fe = b.field + (size_t)e * G2;
+    float *scratch = b.sdf + (size_t)slot * G2;   // k_field_stats writes the SDF there afterwards
+    cost_sweeps_exact(occ, ix, iy, Fe, scratch);  // 225 (odd) sweeps: the result is in scratch
+    for (int q = tid; q < G2; q += kWaveThreads) Fe[q] = scratch[q];
+    if (tid == 0) atomicAdd(&b.ctl[USV_CTL_FIELD_EXACT], 1);
+    __syncthreads();
+  }
+}
 
 // batch constants given every slot's statistics
 struct BatchK {
@@ -391,7 +490,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   __shared__ int flags[2];
   __shared__ float slin[G];
   __shared__ float so[2 * USV_NOBST];
-  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const float cell = (float)((double)c.map_size / G);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
@@ -487,7 +586,7 @@ constexpr int kBatchBlocks = 64;
 __global__ __launch_bounds__(256) void k_field_batch(usv_cfg_t c, usv_bufs_t b) {
   __shared__ float wred[4][4];
   __shared__ bool last;
-  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
   if (count <= 0) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nw = (int)gridDim.x * 4;
@@ -541,7 +640,7 @@ __global__ __launch_bounds__(256) void k_field_batch(usv_cfg_t c, usv_bufs_t b) 
 
 // ---------------------------------------------------------------- pass D ---
 __global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) {
-  const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
   const BatchK k = batch_k(c, b);
   const float cell = (float)((double)c.map_size / G);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
@@ -596,6 +695,8 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   const bool pack = pack_env ? atoi(pack_env) != 0 : b->n >= kFieldPackMinEnvs;
   if (pack) hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   else hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
+  USV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_stats, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();

@@ -14,7 +14,10 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "libusv_oracle.so")
+# USV_ORACLE_OMP=1: the OpenMP build of the same source (bench.py's cpu_baseline on all host cores;
+# bit-identical results, every parallel loop is over independent envs / reset slots)
+LIB_PATH = os.path.join(HERE, "build", "libusv_oracle_omp.so" if os.environ.get("USV_ORACLE_OMP") == "1"
+                        else "libusv_oracle.so")
 
 NOBS, NOBST, GRID, NSTAT = 33, 16, 150, 28
 NU_RESET, NU_STEP = 712, 8
@@ -53,6 +56,7 @@ def lib():
         _lib.oracle_philox.argtypes = [P, P, P]
         _lib.oracle_sample_field.argtypes = [P, ctypes.c_float, ctypes.c_float, ctypes.c_float]
         _lib.oracle_sample_field.restype = ctypes.c_float
+        _lib.oracle_threads.restype = ctypes.c_int
     return _lib
 
 

@@ -20,6 +20,9 @@
  * (Hydrodynamics.py:176-245, ThrusterDynamics.py:129-234).
  */
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -27,6 +30,29 @@
 #include "oracle_philox.h"
 
 #define OPI 3.14159265358979323846
+
+/* OpenMP (bench.py's cpu_baseline build, libusv_oracle_omp.so): every parallel loop is over
+ * independent envs / reset slots, the two batch maxima are exact max reductions, so the
+ * results are the single-threaded build's bit for bit */
+#ifdef _OPENMP
+#define OMP_PRAGMA(x) _Pragma(#x)
+#define OMP_FOR OMP_PRAGMA(omp parallel for schedule(static))
+#define OMP_FOR_DYN OMP_PRAGMA(omp parallel for schedule(dynamic, 1))
+#define OMP_REDUCE_MAX(m, f) OMP_PRAGMA(omp parallel for schedule(static) reduction(max : m) reduction(| : f))
+#else
+#define OMP_FOR
+#define OMP_FOR_DYN
+#define OMP_REDUCE_MAX(m, f)
+#endif
+int oracle_threads(void) {
+#ifdef _OPENMP
+  int t = 1;
+  _Pragma("omp parallel") { _Pragma("omp single") t = omp_get_num_threads(); }
+  return t;
+#else
+  return 1;
+#endif
+}
 
 static inline float clampf_(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
 static inline float maxf_(float a, float b) { return a > b ? a : b; }
@@ -53,6 +79,7 @@ static float philox_u(uint64_t seed, uint32_t env, uint64_t step, uint32_t site,
 
 /* uniforms one env consumes in one step (layout SU_* in usv_hip.h) */
 void oracle_step_uniforms(uint64_t seed, uint64_t step, int n, float *u /*[n][USV_NU_STEP]*/) {
+  OMP_FOR
   for (int e = 0; e < n; ++e)
     for (int i = 0; i < USV_NU_STEP; ++i) u[(size_t)e * USV_NU_STEP + i] = philox_u(seed, (uint32_t)e, step, 0u, i);
 }
@@ -220,8 +247,8 @@ void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][1
   float *sdf = (float *)malloc(sizeof(float) * (size_t)K * G2);
   uint8_t *freec = (uint8_t *)malloc((size_t)K * G2);
   float *cost = (float *)malloc(sizeof(float) * (size_t)K * G2);
-  float *nxt = (float *)malloc(sizeof(float) * (size_t)G2);
   /* compute_occupancy_and_sdf (:66-104) */
+  OMP_FOR_DYN
   for (int k = 0; k < K; ++k) {
     for (int i = 0; i < G; ++i)
       for (int j = 0; j < G; ++j) {
@@ -242,7 +269,9 @@ void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][1
   }
   /* compute_cost_field_wavefront (:135-192): Jacobi relaxation, fixed iterations */
   const float diag = 1.414f;
+  OMP_FOR_DYN
   for (int k = 0; k < K; ++k) {
+    float *nxt = (float *)malloc(sizeof(float) * (size_t)G2);
     float *C = cost + (size_t)k * G2;
     const uint8_t *F = freec + (size_t)k * G2;
     for (int q = 0; q < G2; ++q) C[q] = INFINITY;
@@ -273,11 +302,13 @@ void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][1
       memcpy(C, nxt, sizeof(float) * G2);
       if (!changed) break;   /* a Jacobi fixed point stays fixed: exact early exit */
     }
+    free(nxt);
   }
   if (cost_out) memcpy(cost_out, cost, sizeof(float) * (size_t)K * G2);
   /* compute_potential_field (:194-271) */
   float max_val = -INFINITY;
   int any_finite = 0;
+  OMP_REDUCE_MAX(max_val, any_finite)
   for (size_t q = 0; q < (size_t)K * G2; ++q)
     if (isfinite(cost[q])) { any_finite = 1; if (cost[q] > max_val) max_val = cost[q]; }
   if (!any_finite) max_val = 100.0f;
@@ -286,6 +317,7 @@ void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][1
   float jmax = -INFINITY;
   int any_inside = 0;
   const float inv_r = (float)(1.0 / (double)c->influence_radius);
+  OMP_REDUCE_MAX(jmax, any_inside)
   for (int k = 0; k < K; ++k)
     for (int q = 0; q < G2; ++q) {
       const size_t p = (size_t)k * G2 + q;
@@ -311,6 +343,7 @@ void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][1
         if (sdf[p] - c->obstacle_radius <= 0.f) J[p] = high;
       }
   }
+  OMP_FOR_DYN
   for (int k = 0; k < K; ++k) {
     float gmin = INFINITY, gmax = -INFINITY, jmn = INFINITY, jmx = -INFINITY;
     for (int q = 0; q < G2; ++q) {
@@ -329,7 +362,7 @@ void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][1
       field[p] = gn + c->field_alpha * jn;
     }
   }
-  free(sdf); free(freec); free(cost); free(nxt); free(J);
+  free(sdf); free(freec); free(cost); free(J);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -424,6 +457,7 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
     E->extras[q] = isnan(m) ? 0.f : m;
   }
   E->ctl[USV_CTL_POT_VALID] = 0;  /* CaptureXYTask.reset: prev_potential = None (:773) */
+  OMP_FOR_DYN
   for (int s = 0; s < k; ++s) {
     const int e = ids[s];
     const float *u = U + (size_t)s * USV_NU_RESET;
@@ -679,6 +713,7 @@ void oracle_step(const usv_cfg_t *c, oracle_env_t *E, const float *actions, cons
 void oracle_step_pre(const usv_cfg_t *c, oracle_env_t *E, const float *actions, const float *lut,
                      float action_bias, const float *U) {
   const int n = E->n;
+  OMP_FOR
   for (int e = 0; e < n; ++e) {
     const float *u = U + (size_t)e * USV_NU_STEP;
     const int was_reset = E->just_reset[e];
@@ -715,6 +750,7 @@ void oracle_step_pre(const usv_cfg_t *c, oracle_env_t *E, const float *actions, 
 
 void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E) {
   const float PI_F = (float)OPI, TWO_PI_F = (float)(2.0 * OPI);
+  OMP_FOR
   for (int e = 0; e < E->n; ++e) {
     const float *tmp = E->tmp + (size_t)e * 8;
     const float tgt[2] = {tmp[6], tmp[7]};
@@ -797,6 +833,7 @@ void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
   const int pen_valid = E->ctl[USV_CTL_PEN_VALID];
   const int rew_valid = E->ctl[USV_CTL_REW_VALID];
   const float PI_F = (float)OPI, TWO_PI_F = (float)(2.0 * OPI);
+  OMP_FOR
   for (int e = 0; e < n; ++e) {
     const float *u = U + (size_t)e * USV_NU_STEP;
     const int was_reset = E->just_reset[e];

@@ -364,6 +364,29 @@ def test_potential_field_random_batches_vs_oracle(pack, monkeypatch):
         np.testing.assert_array_equal(f, ref)
 
 
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_potential_field_long_detour_takes_reference_sweeps(pack, monkeypatch):
+    """A wall of 16 obstacles across the diagonal from a corner target: finite costs reach 235 > 224,
+    so the tile-sweep fixed point is not certified equal to the reference's 225 sweeps
+    (d_multi_gemini.py:171) and k_field_exact recomputes that env with them; the ordinary env of the
+    same batch keeps the fast path.  Both bit-exact against the oracle (which runs the 225 sweeps)."""
+    from omniisaacgymenvs_loop_amd._abi import DEFINES
+    monkeypatch.setenv("USV_FIELD_PACK", pack)
+    task_cfg = load_yaml(TEST_YAML)
+    task = _task(task_cfg, 16)
+    k = np.arange(16) - 7.5
+    wall = np.stack([-8.0 - k * 0.9 / np.sqrt(2), -8.0 + k * 0.9 / np.sqrt(2)], 1)
+    rng = np.random.default_rng(11)
+    obst = np.stack([wall, rng.uniform(-12, 12, (16, 2))]).astype(np.float32)
+    tgt = np.array([[-14.3, -14.3], [0.4, -0.3]], np.float32)
+    ids = np.array([9, 2], np.int32)
+    f = _run_field(task, ids, obst, tgt)
+    ref, cost = O.potential_field(task.cfg, obst, tgt, want_cost=True)
+    assert np.nanmax(np.where(np.isfinite(cost[0]), cost[0], np.nan)) > 224.0
+    np.testing.assert_array_equal(f, ref)
+    assert int(task.ctl[DEFINES["USV_CTL_FIELD_EXACT"]].item()) == 1
+
+
 def test_forces_vs_reference_drag(golden):
     g = golden("forces.npz")
     task_cfg = load_yaml(TEST_YAML)
