@@ -233,7 +233,7 @@ def main():
 
     # live per-launch timing of the fused env-step kernel and the PPO gradient kernel
     env_timer, ppo_timer = KernelTimer(), KernelTimer()
-    orig_call, orig_call_rc = _capi.call, _capi.call_rc
+    orig_call = _capi.call
 
     def timed_call(name, *a):
         if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
@@ -243,16 +243,8 @@ def main():
         else:
             orig_call(name, *a)
 
-    def timed_call_rc(name, *a):
-        if timing[0] and name == "ppo_minibatch_fused":
-            rc = [0]
-            ppo_timer(lambda: rc.__setitem__(0, orig_call_rc(name, *a)))
-            return rc[0]
-        return orig_call_rc(name, *a)
-
     timing = [False]
     _capi.call = timed_call
-    _capi.call_rc = timed_call_rc
 
     # training from the random init starts here: the wall clock to reward=30 counts from the first
     # reset (env / agent construction excluded), through warmup and timed epochs alike
@@ -365,9 +357,8 @@ def main():
                          "launch_ms_method": f"HIP event pair around each of the {len(env_timer.pairs)} env-step "
                                              "launches of one eager training epoch, on the launch stream"},
             "roofline_ppo": {"bound": "mfma",
-                             "kernel": ("k_mb_fused (f32 MFMA fwd+bwd + reduction + Adam, one launch)"
-                                        if agent.fused_update else
-                                        "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, fixed-order reduction)"),
+                             "kernel": "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, 64 rows per "
+                                       "workgroup, fixed-order reduction)",
                              "achieved": ppo_tfs,
                              "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},

@@ -441,10 +441,9 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
  * Split in two so the flat gradient can be all-reduced in between:
  *   ppo_minibatch_grad  -> grad[PPO_NPARAM] (+ kl sum in grad[PPO_NPARAM])
  *   ppo_minibatch_apply -> clip + Adam + lr update.
- * opt: device floats [0]=lr [1]=step [2]=last kl [3]=last grad norm [4]=barrier timeout
- *      flag, [5..6]=grid barrier of ppo_minibatch_fused (uint bits, keep 0),
+ * opt: device floats [0]=lr [1]=step [2]=last kl [3]=last grad norm [4..6] unused (0),
  *      [7]=completion counter of the multi-workgroup Adam kernel (uint bits, keep 0);
- * m, v: [PPO_NPARAM].  minibatch must be a multiple of 32 (workgroup row block).
+ * m, v: [PPO_NPARAM].  minibatch must be a multiple of 32 (one 512-thread workgroup per 32 rows).
  * grad must be 16-byte aligned.  losses (nullable) receives the minibatch means
  * (a_loss, c_loss, entropy, b_loss, kl) of this rank; kl_out (nullable) the KL
  * the LR schedule used (after the all-reduce), as kls[] of the reference log.
@@ -460,22 +459,6 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m,
                         float *adam_v, float *opt, float grad_scale, float *kl_out,
                         int norm_from_partials, void *stream);
-
-/* ppo_minibatch_grad (+ ppo_minibatch_apply when apply != 0) in ONE launch: the
- * partial-gradient reduction and the Adam step run behind grid barriers among the
- * co-resident workgroups (opt[5..6] hold the barrier; opt[4] becomes nonzero if a
- * barrier ever timed out).  apply = 0 stops after the reduction (multi-GPU: the
- * caller all-reduces grad, then calls ppo_minibatch_apply).  Returns 4 when the
- * device cannot hold every workgroup at once or the minibatch is below 5,344
- * rows (each workgroup reduces at most two 64-parameter chunks) -- use the split
- * calls then. */
-int ppo_minibatch_fused(const ppo_cfg_t *cfg, float *params, double *obs_rms,
-                        const double *val_rms, int update_obs_rms, int mb_index,
-                        const float *exp_obs, const float *exp_act, const float *exp_nlp,
-                        const float *exp_val, const float *exp_ret, const float *exp_adv,
-                        float *exp_mu, float *exp_sigma, float *grad, float *losses,
-                        float *partials, double *work, float *adam_m, float *adam_v,
-                        float *opt, float *kl_out, int apply, void *stream);
 
 /* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad */
 int ppo_partials_floats(int minibatch);

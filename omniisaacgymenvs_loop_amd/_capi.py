@@ -61,7 +61,6 @@ def _declare(lib):
         "ppo_prepare": [P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_grad": [P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_apply": [P, P, P, P, P, P, F, P, I, P],
-        "ppo_minibatch_fused": [P, P, P, P, I, I] + [P] * 16 + [I, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
         "usv_hip_version": [],

@@ -523,26 +523,195 @@ __global__ __launch_bounds__(TB) void k_obs_stats(ppo_cfg_t c, const float *__re
 }
 
 // ------------------------------------------------------ minibatch grad ----
-__device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__restrict__ P,
-                                             const double *__restrict__ obs_rms, int row0,
-                                             const float *__restrict__ e_obs, const float *__restrict__ e_act,
-                                             const float *__restrict__ e_nlp, const float *__restrict__ e_val,
-                                             const float *__restrict__ e_ret, const float *__restrict__ e_adv,
-                                             float *e_mu, float *e_sigma, float *partials, MlpSmem &s) {
+// One 512-thread workgroup (8 waves, two per SIMD) per 32 minibatch rows, 256
+// workgroups for a 8192-row minibatch (every CU).  The second wave of each SIMD
+// takes the upper half of K of the long matrix-core chains (layer 2 and dh1:
+// K = 128) and the halves meet in LDS in a fixed order (lower + upper); the
+// 16 dW2 tiles go two per wave; the row inputs of the losses are loaded with the
+// weights, so nothing in the loss phase waits on memory.
+constexpr int GTB = 512;          // threads per workgroup
+struct GradSmem {
+  float w2[NH * HS];              // W2[j][k]
+  float w1[NH * XS];              // W1[j][k], k 33..35 = 0
+  float x[RB * XS];               // normalised obs (dW1 operand)
+  float h1[RB * HS];              // tanh layer 1, later dz1
+  float h2[RB * HS];              // tanh layer 2, later dz2
+  float xch[4][16][64];           // upper-K partial accumulators of layer 2 / dh1 (per wave, register, lane)
+  float out[RB * 4];              // mu0, mu1, value
+  float g[RB * 4];                // dmu0, dmu1, dv, dnlp per row
+  float hg[4][4][NH];             // head-gradient / b2 quarter sums
+  float b1[NH];
+  float tail[TAIL + 1];
+};
+
+// per-row inputs of the losses (wave 0: lane = row), loaded with the weights
+struct RowIn {
+  float act0, act1, nlp, val, ret, adv, mu0, mu1, sg0, sg1;
+};
+
+// Partial-gradient stores write through to the MALL (sc1): the 85 KB per workgroup leave
+// during the kernel instead of as dirty L2 lines at the kernel boundary (MI355X_MICROARCH.md,
+// publish-large / boundary rows)
+struct PartOut {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ void operator()(int idx, float v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (uint32_t)idx * 4u, 0, 16);
+  }
+};
+
+__device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__restrict__ P,
+                                          const double *__restrict__ obs_rms, int row0,
+                                          const float *__restrict__ e_obs, const float *__restrict__ e_act,
+                                          const float *__restrict__ e_nlp, const float *__restrict__ e_val,
+                                          const float *__restrict__ e_ret, const float *__restrict__ e_adv,
+                                          float *e_mu, float *e_sigma, float *partials, GradSmem &s) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
-  const int rb0 = row0 + blockIdx.x * RB;             // global row of this block
+  const int kh = w >> 2, cb = w & 3, n0 = 32 * cb;      // K half, column block
+  const int rb0 = row0 + blockIdx.x * RB;               // first row of this workgroup
   const float invB = 1.0f / (float)c.minibatch;
   USV_PHASE(ppo, 0);
-  StagedW wr;
-  stage_load(P, wr);
-  stage_obs(e_obs, rb0, RB, obs_rms, c.normalize_input != 0, c.rms_eps, s);
-  stage_store_small(wr, s);
+  // ---- every global load issued up front (compile-time trip counts) ----
+  constexpr int NW2H = NH * NH / 2 / GTB, NW1G = NH * XS / GTB, NTLG = (TAIL + GTB - 1) / GTB;
+  static_assert(NH * NH / 2 % GTB == 0 && NH * XS % GTB == 0, "staging trip counts");
+  float2 w2r[NW2H];
+  float w1r[NW1G], tlr[NTLG];
+  {
+    const float2 *W2 = reinterpret_cast<const float2 *>(P + PPO_OFF_W2);   // PPO_OFF_W2 is even
+#pragma unroll
+    for (int u = 0; u < NW1G; ++u) {
+      const int q = tid + u * GTB, j = q / XS, k = q % XS;
+      w1r[u] = k < NIN ? P[PPO_OFF_W1 + j * NIN + k] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < NTLG; ++u) tlr[u] = (tid + u * GTB < TAIL) ? P[PPO_OFF_B2 + tid + u * GTB] : 0.f;
+#pragma unroll
+    for (int u = 0; u < NW2H; ++u) w2r[u] = W2[tid + u * GTB];
+  }
+  const float b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
+  const float lsig0 = P[PPO_OFF_SIGMA], lsig1 = P[PPO_OFF_SIGMA + 1];
+  RowIn ri = {};
+  if (tid < RB) {
+    const size_t row = (size_t)rb0 + tid;
+    ri.act0 = e_act[row * 2]; ri.act1 = e_act[row * 2 + 1];
+    ri.nlp = e_nlp[row]; ri.val = e_val[row]; ri.ret = e_ret[row]; ri.adv = e_adv[row];
+    ri.mu0 = e_mu[row * 2]; ri.mu1 = e_mu[row * 2 + 1];
+    ri.sg0 = e_sigma[row * 2]; ri.sg1 = e_sigma[row * 2 + 1];
+  }
+  {   // obs rows, normalised on the way into LDS
+    constexpr int NU = (RB * XS + GTB - 1) / GTB;
+    float v[NU];
+    double mu[NU], var[NU];
+    const bool norm = c.normalize_input != 0;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int q = tid + u * GTB, r = q / XS, k = q % XS;
+      const bool ok = q < RB * XS && k < NIN;
+      const int rc = ok ? r : 0, kc = ok ? k : 0;
+      v[u] = e_obs[(size_t)(rb0 + rc) * NIN + kc];
+      mu[u] = norm ? obs_rms[kc] : 0.0;
+      var[u] = norm ? obs_rms[NIN + kc] : 1.0;
+    }
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int q = tid + u * GTB;
+      if (q >= RB * XS) continue;
+      const int k = q % XS;
+      float xv = 0.f;
+      if (k < NIN) {
+        xv = v[u];
+        if (norm) xv = rms_norm(xv, mu[u], var[u], c.rms_eps);
+      }
+      s.x[q] = xv;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < NW1G; ++u) s.w1[tid + u * GTB] = w1r[u];
+#pragma unroll
+  for (int u = 0; u < NTLG; ++u)
+    if (tid + u * GTB < TAIL) s.tail[tid + u * GTB] = tlr[u];
+  if (tid < NH) s.b1[tid] = b1r;
   __syncthreads();
   USV_PHASE(ppo, 1);
-  block_forward(wr, s);
+  if (kh == 0) {
+    // ---- layer 1 (waves 0-3): h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero) ----
+    f32x16 acc = {};
+#pragma unroll
+    for (int st = 0; st < 17; ++st) {
+      const int k = 2 * st + h;
+      acc = mfma32(s.x[i * XS + k], s.w1[(n0 + i) * XS + k], acc);
+    }
+    const float bj = s.b1[n0 + i];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
+  }
+  USV_PHASE(ppo, 9);
+  // W2 into LDS (waves 4-7 do it while 0-3 run layer 1; each thread commits its own loads)
+#pragma unroll
+  for (int u = 0; u < NW2H; ++u) {
+    const int q = tid + u * GTB, j = q / (NH / 2), k2 = q % (NH / 2);
+    *reinterpret_cast<float2 *>(&s.w2[j * HS + 2 * k2]) = w2r[u];
+  }
+  __syncthreads();
+  USV_PHASE(ppo, 10);
+  // ---- layer 2: h2 = tanh(h1 W2^T + b2); wave (kh, cb) sums k in [64 kh, 64 kh + 64) ----
+  {
+    f32x16 acc = {};
+#pragma unroll 16
+    for (int st = 0; st < NH / 4; ++st) {
+      const int k = 64 * kh + 2 * st + h;
+      acc = mfma32(s.h1[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
+    }
+    USV_PHASE(ppo, 11);
+    // the two K halves meet in LDS: each wave of the pair finishes 8 of the 16 accumulator rows,
+    // always as (lower half + upper half) + bias
+    // (kh is wave-uniform: both branches index the accumulator with constants)
+    if (kh == 0) {
+#pragma unroll
+      for (int r = 8; r < 16; ++r) s.xch[cb][r][lane] = acc[r];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s.xch[cb][r][lane] = acc[r];
+    }
+    __syncthreads();
+    const float bj = s.tail[T_B2 + n0 + i];
+    if (kh == 0) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh((acc[r] + s.xch[cb][r][lane]) + bj);
+    } else {
+#pragma unroll
+      for (int r = 8; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh((s.xch[cb][r][lane] + acc[r]) + bj);
+    }
+  }
+  __syncthreads();
+  USV_PHASE(ppo, 12);
+  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (16 threads per row, 8 k each) ----
+  {
+    const int r = tid / 16, part = tid % 16;
+    float a0 = 0.f, a1 = 0.f, av = 0.f;
+#pragma unroll
+    for (int k = part * 8; k < part * 8 + 8; ++k) {
+      const float hv = s.h2[r * HS + k];
+      a0 = fmaf(s.tail[T_WMU + k], hv, a0);
+      a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
+      av = fmaf(s.tail[T_WV + k], hv, av);
+    }
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) {
+      a0 += __shfl_xor(a0, m, 64);
+      a1 += __shfl_xor(a1, m, 64);
+      av += __shfl_xor(av, m, 64);
+    }
+    if (part == 0) {
+      s.out[r * 4 + 0] = a0 + s.tail[T_BMU];
+      s.out[r * 4 + 1] = a1 + s.tail[T_BMU + 1];
+      s.out[r * 4 + 2] = av + s.tail[T_BV];
+    }
+  }
+  __syncthreads();
   USV_PHASE(ppo, 2);
-  float *part = partials + (size_t)blockIdx.x * NPART;
+  const PartOut part_st{__builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART, 0, NPART * 4,
+                                                          0x00020000)};
   // ---- per-row losses and output gradients (wave 0, lanes < RB) ----
   if (tid < 64) {
     float la = 0.f, lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f, gs0 = 0.f, gs1 = 0.f;
@@ -550,14 +719,13 @@ __device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__
       const int r = tid;
       const size_t row = (size_t)rb0 + r;
       const float mu0 = s.out[r * 4], mu1 = s.out[r * 4 + 1], v = s.out[r * 4 + 2];
-      const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
+      const float ls0 = mu0 * 0.f + lsig0, ls1 = mu1 * 0.f + lsig1;
       const float sg0 = expf(ls0), sg1 = expf(ls1);
-      const float x0 = e_act[row * 2], x1 = e_act[row * 2 + 1];
-      const float z0 = (x0 - mu0) / sg0, z1 = (x1 - mu1) / sg1;
+      const float z0 = (ri.act0 - mu0) / sg0, z1 = (ri.act1 - mu1) / sg1;
       const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
-      const float A = e_adv[row];
+      const float A = ri.adv;
       // actor_loss (common_losses.py:36-46)
-      const float ratio = expf(e_nlp[row] - nlp);
+      const float ratio = expf(ri.nlp - nlp);
       const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
       const float rc = clampt(ratio, lo, hi);
       const float s1 = -(A * ratio), s2 = -(A * rc);
@@ -567,7 +735,7 @@ __device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__
       const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
       const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
       // critic_loss (common_losses.py:10-19)
-      const float vo = e_val[row], R = e_ret[row];
+      const float vo = ri.val, R = ri.ret;
       float dv, c_loss;
       if (c.clip_value) {
         const float dvr = v - vo;
@@ -590,15 +758,13 @@ __device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__
       const float bc = c.bounds_loss_coef * invB;
       const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
       const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
-      // d nlp / d logstd = 1 - z^2 (through sigma = exp(logstd) and the sum of logstd)
-      // - entropy_coef * mean(entropy): d entropy / d logstd = 1 per row (Normal.entropy, fixed sigma)
+      // d nlp / d logstd = 1 - z^2; - entropy_coef * mean(entropy): d entropy / d logstd = 1 per row
       const float dent = -c.entropy_coef * invB;
       gs0 = dnlp * (1.f - z0 * z0) + dent;
       gs1 = dnlp * (1.f - z1 * z1) + dent;
       const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
       // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
-      const float om0 = e_mu[row * 2], om1 = e_mu[row * 2 + 1];
-      const float os0 = e_sigma[row * 2], os1 = e_sigma[row * 2 + 1];
+      const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
       const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
       const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
       e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
@@ -612,21 +778,21 @@ __device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__
     la = wave_sum(la); lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
     gs0 = wave_sum(gs0); gs1 = wave_sum(gs1);
     if (tid == 0) {
-      part[P_LOSS + 0] = la; part[P_LOSS + 1] = lc; part[P_LOSS + 2] = le; part[P_LOSS + 3] = lb;
-      part[P_LOSS + 4] = lkl;
-      part[PPO_OFF_SIGMA] = gs0; part[PPO_OFF_SIGMA + 1] = gs1;
+      part_st(P_LOSS + 0, la); part_st(P_LOSS + 1, lc); part_st(P_LOSS + 2, le); part_st(P_LOSS + 3, lb);
+      part_st(P_LOSS + 4, lkl);
+      part_st(PPO_OFF_SIGMA, gs0); part_st(PPO_OFF_SIGMA + 1, gs1);
     }
   }
   __syncthreads();
   USV_PHASE(ppo, 3);
-  // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 ----
+  // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 (quarter qq: 8 rows) ----
   {
-    const int j = tid & (NH - 1), half = tid >> 7;     // rows 16*half .. 16*half+15
+    const int j = tid & (NH - 1), qq = tid >> 7;
     const float wm0 = s.tail[T_WMU + j], wm1 = s.tail[T_WMU + NH + j], wv = s.tail[T_WV + j];
     float gw0 = 0.f, gw1 = 0.f, gwv = 0.f, db = 0.f;
 #pragma unroll
-    for (int q = 0; q < RB / 2; ++q) {
-      const int rr = half * (RB / 2) + q;
+    for (int q = 0; q < RB / 4; ++q) {
+      const int rr = qq * (RB / 4) + q;
       const float hv = s.h2[rr * HS + j];
       const float d0 = s.g[rr * 4], d1 = s.g[rr * 4 + 1], dvv = s.g[rr * 4 + 2];
       gw0 = fmaf(d0, hv, gw0); gw1 = fmaf(d1, hv, gw1); gwv = fmaf(dvv, hv, gwv);
@@ -634,88 +800,103 @@ __device__ __forceinline__ void mb_grad_body(const ppo_cfg_t &c, const float *__
       s.h2[rr * HS + j] = dz;
       db += dz;
     }
-    s.hg[half][0][j] = gw0; s.hg[half][1][j] = gw1; s.hg[half][2][j] = gwv; s.hg[half][3][j] = db;
+    s.hg[qq][0][j] = gw0; s.hg[qq][1][j] = gw1; s.hg[qq][2][j] = gwv; s.hg[qq][3][j] = db;
   }
   __syncthreads();
   if (tid < NH) {
     const int j = tid;
-    part[PPO_OFF_WMU + j] = s.hg[0][0][j] + s.hg[1][0][j];
-    part[PPO_OFF_WMU + NH + j] = s.hg[0][1][j] + s.hg[1][1][j];
-    part[PPO_OFF_WV + j] = s.hg[0][2][j] + s.hg[1][2][j];
-    part[PPO_OFF_B2 + j] = s.hg[0][3][j] + s.hg[1][3][j];
+    part_st(PPO_OFF_WMU + j, ((s.hg[0][0][j] + s.hg[1][0][j]) + s.hg[2][0][j]) + s.hg[3][0][j]);
+    part_st(PPO_OFF_WMU + NH + j, ((s.hg[0][1][j] + s.hg[1][1][j]) + s.hg[2][1][j]) + s.hg[3][1][j]);
+    part_st(PPO_OFF_WV + j, ((s.hg[0][2][j] + s.hg[1][2][j]) + s.hg[2][2][j]) + s.hg[3][2][j]);
+    part_st(PPO_OFF_B2 + j, ((s.hg[0][3][j] + s.hg[1][3][j]) + s.hg[2][3][j]) + s.hg[3][3][j]);
   } else if (tid < NH + 3) {
     const int q = tid - NH;
     float sacc = 0.f;
     for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
-    part[q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV] = sacc;
+    part_st(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV, sacc);
   }
   USV_PHASE(ppo, 4);
-  // ---- dW2[j][k] = sum_r dz2[r][j] h1[r][k]: wave w owns rows j in [32w, 32w+32), 4 k tiles ----
+  // ---- dW2[n][k] = sum_r dz2[r][n] h1[r][k]: wave (kh, cb) owns n block cb, k blocks 2 kh, 2 kh + 1 ----
+  f32x16 acc[2] = {};
   {
-    f32x16 acc[4] = {};
 #pragma unroll 4
     for (int st = 0; st < RB / 2; ++st) {
       const int r = st + (RB / 2) * h;
-      const float a = s.h2[r * HS + 32 * w + i];
+      const float a = s.h2[r * HS + n0 + i];
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) acc[kt] = mfma32(a, s.h1[r * HS + 32 * kt + i], acc[kt]);
+      for (int kt = 0; kt < 2; ++kt) acc[kt] = mfma32(a, s.h1[r * HS + 32 * (2 * kh + kt) + i], acc[kt]);
     }
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int q = 0; q < 16; ++q) part[PPO_OFF_W2 + (32 * w + crow(q, h)) * NH + 32 * kt + i] = acc[kt][q];
+    USV_PHASE(ppo, 13);
   }
   USV_PHASE(ppo, 5);
-  // ---- dh1[r][k] = sum_j dz2[r][j] W2[j][k]: wave w owns columns k in [32w, 32w+32) ----
-  f32x16 dh = {};
-#pragma unroll 16
-  for (int st = 0; st < NH / 2; ++st) {
-    const int j = 2 * st + h;
-    dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + 32 * w + i], dh);
-  }
-  USV_PHASE(ppo, 6);
-  __syncthreads();   // every read of h1 (dW2 operand) is done
+  // ---- dh1[r][k] = sum_n dz2[r][n] W2[n][k]: wave (kh, cb) owns columns k in block cb, n in half kh.
+  // The dW2 partial (32 stores per lane, memory-bandwidth bound) is stored one value per step of
+  // this chain, so the stores drain under the matrix-core work instead of stalling the issue ----
+  {
+    f32x16 dh = {};
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int idx = crow(q, h) * HS + 32 * w + i;
-    const float hv = s.h1[idx];
-    s.h1[idx] = dh[q] * (1.f - hv * hv);   // h1 := dz1
+    for (int st = 0; st < NH / 4; ++st) {
+      const int j = 64 * kh + 2 * st + h;
+      dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + n0 + i], dh);
+      const int kt = st >> 4, q = st & 15;
+      part_st(PPO_OFF_W2 + (n0 + crow(q, h)) * NH + 32 * (2 * kh + kt) + i, acc[kt][q]);
+    }
+    USV_PHASE(ppo, 6);
+    if (kh == 0) {
+#pragma unroll
+      for (int q = 8; q < 16; ++q) s.xch[cb][q][lane] = dh[q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) s.xch[cb][q][lane] = dh[q];
+    }
+    __syncthreads();   // every read of h1 (dW2 operand) is done; the halves are published
+    const int q0 = 8 * kh;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int idx = crow(q0 + q, h) * HS + n0 + i;
+      const float hv = s.h1[idx];
+      const float lo_hi = kh == 0 ? dh[q] + s.xch[cb][q][lane] : s.xch[cb][8 + q][lane] + dh[8 + q];
+      s.h1[idx] = lo_hi * (1.f - hv * hv);   // h1 := dz1
+    }
   }
   __syncthreads();
   USV_PHASE(ppo, 7);
-  // ---- dW1[j][k] = sum_r dz1[r][j] x[r][k] (k < 32 on the matrix cores), db1 ----
-  {
+  // ---- dW1[j][k] = sum_r dz1[r][j] x[r][k]: waves 0-3 on the matrix cores (k < 32); waves 4-7 the
+  // last column (k = 32) and db1 ----
+  if (kh == 0) {
     f32x16 acc = {};
 #pragma unroll
     for (int st = 0; st < RB / 2; ++st) {
       const int r = st + (RB / 2) * h;
-      acc = mfma32(s.h1[r * HS + 32 * w + i], s.x[r * XS + i], acc);
+      acc = mfma32(s.h1[r * HS + n0 + i], s.x[r * XS + i], acc);
     }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) part[PPO_OFF_W1 + (32 * w + crow(q, h)) * NIN + i] = acc[q];
-  }
-  if (tid < NH) {
-    const int j = tid;
-    float a = 0.f;
-    for (int r = 0; r < RB; ++r) a = fmaf(s.h1[r * HS + j], s.x[r * XS + NIN - 1], a);
-    part[PPO_OFF_W1 + j * NIN + NIN - 1] = a;
+    for (int q = 0; q < 16; ++q) part_st(PPO_OFF_W1 + (n0 + crow(q, h)) * NIN + i, acc[q]);
   } else {
-    const int j = tid - NH;
-    float a = 0.f;
-    for (int r = 0; r < RB; ++r) a += s.h1[r * HS + j];
-    part[PPO_OFF_B1 + j] = a;
+    const int t = tid - 256;
+    if (t < NH) {
+      const int j = t;
+      float a = 0.f;
+      for (int r = 0; r < RB; ++r) a = fmaf(s.h1[r * HS + j], s.x[r * XS + NIN - 1], a);
+      part_st(PPO_OFF_W1 + j * NIN + NIN - 1, a);
+    } else {
+      const int j = t - NH;
+      float a = 0.f;
+      for (int r = 0; r < RB; ++r) a += s.h1[r * HS + j];
+      part_st(PPO_OFF_B1 + j, a);
+    }
   }
   USV_PHASE(ppo, 8);
 }
 
-__global__ __launch_bounds__(TB) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
-                                                const double *__restrict__ obs_rms, int row0,
-                                                const float *__restrict__ e_obs, const float *__restrict__ e_act,
-                                                const float *__restrict__ e_nlp, const float *__restrict__ e_val,
-                                                const float *__restrict__ e_ret, const float *__restrict__ e_adv,
-                                                float *e_mu, float *e_sigma, float *partials) {
-  __shared__ MlpSmem s;
-  mb_grad_body(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
+__global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
+                                                    const double *__restrict__ obs_rms, int row0,
+                                                    const float *__restrict__ e_obs, const float *__restrict__ e_act,
+                                                    const float *__restrict__ e_nlp, const float *__restrict__ e_val,
+                                                    const float *__restrict__ e_ret, const float *__restrict__ e_adv,
+                                                    float *e_mu, float *e_sigma, float *partials) {
+  __shared__ GradSmem s;
+  mb_grad8w(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
 }
 
 // sum the per-block partials (fixed order => deterministic) into grad[]:
@@ -871,116 +1052,6 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   }
 }
 
-// ------------------------------------------------- fused minibatch kernel --
-// Sense-reversing grid barrier for co-resident workgroups (the host checks
-// that every workgroup of the launch fits the device at once): bar[0] arrival
-// count, bar[1] sense.  The spin is bounded: on timeout it raises *err instead
-// of hanging the device.
-__device__ __forceinline__ void grid_barrier(unsigned *bar, unsigned nblk, unsigned *err) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned s0 = atomicAdd(bar + 1, 0u);
-    __threadfence();
-    if (atomicAdd(bar, 1u) == nblk - 1) {
-      atomicExch(bar, 0u);
-      __threadfence();
-      atomicExch(bar + 1, s0 ^ 1u);
-    } else {
-      unsigned spins = 0;
-      while (atomicAdd(bar + 1, 0u) == s0) {
-        __builtin_amdgcn_s_sleep(2);
-        if (++spins > (1u << 24)) { atomicExch(err, 1u); break; }
-      }
-    }
-    __threadfence();
-  }
-  __syncthreads();
-}
-
-// One PPO minibatch in one launch: forward/backward partials (as k_mb_grad) ->
-// barrier -> fixed-order reduction, chunk by chunk -> [kApply: barrier -> clip
-// norm from the chunk squares -> Adam on the chunks this workgroup reduced ->
-// the last workgroup advances step / lr / kl].  Saves the two kernel
-// boundaries of the split path (their drain + dispatch dominate at 8192 rows).
-template <bool kApply>
-__global__ __launch_bounds__(TB) void k_mb_fused(ppo_cfg_t c, float *P, const double *__restrict__ obs_rms, int row0,
-                                                 const float *__restrict__ e_obs, const float *__restrict__ e_act,
-                                                 const float *__restrict__ e_nlp, const float *__restrict__ e_val,
-                                                 const float *__restrict__ e_ret, const float *__restrict__ e_adv,
-                                                 float *e_mu, float *e_sigma, float *partials, float *grad,
-                                                 float *losses, float *m, float *v, float *opt, float *kl_out) {
-  __shared__ MlpSmem s;
-  __shared__ float red[4][64];
-  __shared__ float nred[4];
-  __shared__ bool last;
-  unsigned *bar = reinterpret_cast<unsigned *>(opt + 5);
-  unsigned *err = reinterpret_cast<unsigned *>(opt + 4);
-  mb_grad_body(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
-  const unsigned nblk = gridDim.x;
-  grid_barrier(bar, nblk, err);
-  const float inv_b = 1.0f / (float)c.minibatch;
-  constexpr int MAXC = 2;   // chunks per workgroup (RED_BLOCKS <= 2 * 256)
-  float gk[MAXC];
-  int nck = 0;
-  for (int ch = blockIdx.x; ch < RED_BLOCKS; ch += nblk) gk[nck++] = reduce_chunk(partials, (int)nblk, grad, losses, inv_b, ch, red);
-  if (!kApply) return;
-  grid_barrier(bar, nblk, err);
-  // clip_grad_norm_ from the chunk squares (same order in every workgroup)
-  const int tid = threadIdx.x;
-  float sq = 0.f;
-  for (int q = tid; q < RED_BLOCKS; q += TB) sq += grad[PPO_NPARAM + 8 + q];
-  sq = wave_sum(sq);
-  if ((tid & 63) == 0) nred[tid >> 6] = sq;
-  __syncthreads();
-  const float total_norm = sqrtf(((nred[0] + nred[1]) + nred[2]) + nred[3]);
-  float coef = 1.0f;
-  if (c.truncate_grads) coef = fminf(c.grad_norm / (total_norm + 1e-6f), 1.0f);
-  const float lr = opt[0];
-  const float step = opt[1] + 1.0f;
-  const double bc1 = 1.0 - pow((double)c.adam_b1, (double)step);
-  const double bc2 = 1.0 - pow((double)c.adam_b2, (double)step);
-  const float step_size = (float)((double)lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
-  if (tid < 64) {
-    int k = 0;
-    for (int ch = blockIdx.x; ch < RED_BLOCKS; ch += nblk, ++k) {
-      const int q = ch * 64 + tid;
-      if (q >= PPO_NPARAM) continue;
-      float g = gk[k] * coef;
-      if (c.weight_decay != 0.f) g = g + c.weight_decay * P[q];
-      float mi = m[q], vi = v[q];
-      mi = mi + (1.0f - c.adam_b1) * (g - mi);          // exp_avg.lerp_(grad, 1 - beta1)
-      vi = vi * c.adam_b2 + (1.0f - c.adam_b2) * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
-      const float denom = sqrtf(vi) / bc2s + c.adam_eps;
-      P[q] = P[q] - step_size * (mi / denom);
-      m[q] = mi;
-      v[q] = vi;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    last = atomicAdd(reinterpret_cast<unsigned *>(opt + 7), 1u) == nblk - 1;
-    __threadfence();
-  }
-  __syncthreads();
-  if (last && tid == 0) {
-    opt[1] = step;
-    opt[3] = total_norm;
-    if (c.lr_adaptive) {   // AdaptiveScheduler.update on this minibatch's KL (schedulers.py:26-32)
-      const float kl = grad[PPO_NPARAM];
-      float nl = lr;
-      if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
-      if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
-      opt[0] = nl;
-      opt[2] = kl;
-      if (kl_out) *kl_out = kl;
-    }
-    __threadfence();
-    atomicExch(reinterpret_cast<unsigned *>(opt + 7), 0u);
-  }
-}
-
 }  // namespace
 
 extern "C" {
@@ -1061,7 +1132,7 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
     USV_CHECK_LAUNCH();
   }
   const int nblk = cfg->minibatch / RB;
-  hipLaunchKernelGGL(k_mb_grad, dim3(nblk), dim3(TB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
+  hipLaunchKernelGGL(k_mb_grad, dim3(nblk), dim3(GTB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
                      exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_reduce_partials, dim3((PPO_NPARAM + 5 + 63) / 64), dim3(256), 0, s, partials, nblk, grad, losses,
@@ -1076,51 +1147,6 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
   if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
   hipLaunchKernelGGL(norm_from_partials ? k_apply<true> : k_apply<false>, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB),
                      dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params, grad, adam_m, adam_v, opt, grad_scale, kl_out);
-  USV_CHECK_LAUNCH();
-  return 0;
-}
-
-int ppo_minibatch_fused(const ppo_cfg_t *cfg, float *params, double *obs_rms, const double *val_rms,
-                        int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
-                        const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
-                        float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
-                        float *adam_m, float *adam_v, float *opt, float *kl_out, int apply, void *stream) {
-  (void)val_rms;
-  if (!cfg || !params || !grad || !partials || !work || !opt) return 1;
-  if (apply && (!adam_m || !adam_v)) return 1;
-  if (cfg->minibatch % RB != 0) return 2;
-  const int nblk = cfg->minibatch / RB;
-  if (nblk * 2 < RED_BLOCKS) return 4;   // each workgroup reduces at most two chunks: use the split path
-  // every workgroup must be resident at once (grid barrier): 1 per CU at this LDS size
-  static int checked_dev = -1, capacity = 0;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return 5;
-  if (dev != checked_dev) {
-    int cus = 0, per_cu = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 5;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(k_mb_fused<true>), TB,
-                                                     0) != hipSuccess)
-      return 5;
-    capacity = cus * per_cu;
-    checked_dev = dev;
-  }
-  if (nblk > capacity) return 4;         // caller falls back to ppo_minibatch_grad + ppo_minibatch_apply
-  hipStream_t s = (hipStream_t)stream;
-  const int row0 = mb_index * cfg->minibatch;
-  if (update_obs_rms && cfg->normalize_input) {
-    const int nb = 64;
-    hipLaunchKernelGGL(k_obs_stats, dim3(nb), dim3(TB), 0, s, *cfg, exp_obs, row0, cfg->minibatch, work + 8, obs_rms,
-                       reinterpret_cast<unsigned *>(work + 7));
-    USV_CHECK_LAUNCH();
-  }
-  if (apply)
-    hipLaunchKernelGGL(k_mb_fused<true>, dim3(nblk), dim3(TB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act,
-                       exp_nlp, exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials, grad, losses, adam_m, adam_v,
-                       opt, kl_out);
-  else
-    hipLaunchKernelGGL(k_mb_fused<false>, dim3(nblk), dim3(TB), 0, s, *cfg, params, obs_rms, row0, exp_obs,
-                       exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials, grad, losses, adam_m,
-                       adam_v, opt, kl_out);
   USV_CHECK_LAUNCH();
   return 0;
 }

@@ -215,10 +215,6 @@ class A2CAgent:
         # minibatch update are captured once and replayed every epoch (the step / Philox counters live on
         # the device, so a replay continues exactly where the eager loop would)
         self.use_graph = bool(config.get("hip_graph", True))
-        # one kernel per minibatch with grid barriers (ppo_minibatch_fused): bit-identical to the split
-        # kernels but slower on MI355X (256 cross-XCD arrivals per barrier cost more than the two kernel
-        # boundaries it removes), so off by default
-        self.fused_update = bool(config.get("fused_update", False))
         self._graph_play = None
         self._graph_update = None
         self._eager_epochs = 0
@@ -322,8 +318,7 @@ class A2CAgent:
     def update_epoch_minibatches(self) -> None:
         """The mini-epoch / minibatch loop (a2c_common.py:1190-1245): per minibatch the gradient kernel
         (+ fixed-order partial reduction), [RCCL all-reduce of the flat gradient + KL with several
-        ranks], then the clip + Adam + LR kernel.  `fused_update` runs the first and last in one launch
-        behind grid barriers instead (stopping after the reduction when ranks > 1)."""
+        ranks], then the clip + Adam + LR kernel."""
         c = _capi
         cfg = c.byref(self.cfg)
         s = c.stream_ptr()
@@ -335,23 +330,11 @@ class A2CAgent:
                         c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp), c.ptr(self.exp_val),
                         c.ptr(self.exp_ret), c.ptr(self.exp_adv), c.ptr(self.exp_mu), c.ptr(self.exp_sigma),
                         c.ptr(self.grad), c.ptr(self.loss_log[k]), c.ptr(self.partials), c.ptr(self.work))
-                fused = False
-                if self.fused_update:
-                    rc = c.call_rc("ppo_minibatch_fused", *args, c.ptr(self.adam_m), c.ptr(self.adam_v),
-                                   c.ptr(self.opt), c.ptr(self.kls[k:k + 1]), int(not dp), s)
-                    if rc == 4:
-                        self.fused_update = False      # the device cannot hold every workgroup at once
-                    elif rc != 0:
-                        raise RuntimeError(f"ppo_minibatch_fused failed with status {rc}")
-                    else:
-                        fused = True
-                if not fused:
-                    c.call("ppo_minibatch_grad", *args, s)
-                if not fused or dp:
-                    scale = self._allreduce_grad()
-                    c.call("ppo_minibatch_apply", cfg, c.ptr(self.model_params), c.ptr(self.grad),
-                           c.ptr(self.adam_m), c.ptr(self.adam_v), c.ptr(self.opt), float(scale),
-                           c.ptr(self.kls[k:k + 1]), int(not dp), s)
+                c.call("ppo_minibatch_grad", *args, s)
+                scale = self._allreduce_grad()
+                c.call("ppo_minibatch_apply", cfg, c.ptr(self.model_params), c.ptr(self.grad),
+                       c.ptr(self.adam_m), c.ptr(self.adam_v), c.ptr(self.opt), float(scale),
+                       c.ptr(self.kls[k:k + 1]), int(not dp), s)
                 k += 1
 
     def _graph_capture(self, fn):
@@ -400,10 +383,7 @@ class A2CAgent:
         update_time_end = time.time()
         self._eager_epochs += 1
         self._replay_meters()
-        opt = self.opt.cpu()
-        if opt[4].item() != 0.0:
-            raise RuntimeError("a grid barrier of the fused minibatch kernel timed out")
-        self.last_lr = float(opt[0].item())
+        self.last_lr = float(self.opt[0].item())
         step_time = batch["step_time"]
         if step_time != step_time:   # graph replay: no per-step host timing
             step_time = play_time_end - play_time_start

@@ -207,27 +207,3 @@ def test_checkpoint_roundtrip(tmp_path):
     assert torch.equal(ag2.model_params, ag.model_params)
     assert torch.equal(ag2.obs_rms, ag.obs_rms)
     assert ag2.epoch_num == 7 and ag2.frame == 1024
-
-
-def test_fused_minibatch_matches_split_path():
-    """ppo_minibatch_fused (one launch, grid barriers) == ppo_minibatch_grad + ppo_minibatch_apply, bit for bit."""
-    N, H = 1024, 16
-    rng = np.random.default_rng(5)
-    B = N * H
-    data = {"exp_obs": rng.normal(0, 2, (B, 33)), "exp_act": rng.normal(0, 1, (B, 2)),
-            "exp_nlp": rng.uniform(1.5, 3.5, B), "exp_val": rng.normal(0, 1, B), "exp_ret": rng.normal(0, 1, B),
-            "exp_adv": rng.normal(0, 1, B), "exp_mu": rng.normal(0, 0.3, (B, 2)), "exp_sigma": np.ones((B, 2))}
-    outs = []
-    for fused in (True, False):
-        ag = _agent(N, 8192, mini_epochs=3)
-        ag.fused_update = fused
-        for k, v in data.items():
-            getattr(ag, k).copy_(torch.tensor(v.astype(np.float32), device=DEV))
-        ag.update_epoch_minibatches()
-        torch.cuda.synchronize()
-        assert ag.fused_update == fused
-        outs.append([t.cpu().numpy().copy() for t in (ag.model_params, ag.adam_m, ag.adam_v, ag.opt[:4], ag.kls,
-                                                      ag.loss_log, ag.obs_rms, ag.exp_mu)])
-    for a, b in zip(*outs):
-        np.testing.assert_array_equal(a, b)
-    assert float(outs[0][3][0]) > 0

@@ -52,7 +52,13 @@ def main():
     for _ in range(4):
         agent.train_epoch()
     torch.cuda.synchronize()
-    report("k_mb_grad (last launch)", read("ppo"), agent.minibatch_size // 32, 9)
+    pb = read("ppo")
+    report("k_mb_grad (last launch)", pb, agent.minibatch_size // 32, 9)
+    b = pb[:agent.minibatch_size // 32]
+    b = b[b[:, 0] > 0]
+    for k, what in ((9, "layer 1 done"), (10, "W2 committed"), (11, "layer-2 MFMA loop done"),
+                    (12, "layer 2 done"), (2, "heads done"), (13, "dW2 MFMA loop done"), (5, "dW2 stored")):
+        print(f"  slot {k:2d} {what:24s} t = {np.mean(b[:, k] - b[:, 0]) / 100:7.2f} us")
     cnt = int(task.ctl[0].item())
     print("reset count of the last step:", cnt)
     report("k_field_wave (last launch)", read("field"), min(cnt, 512), 4, extra_col=15)
