@@ -417,7 +417,9 @@ int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms,
 
 /* Store rewards of slot t shaped by DefaultRewardsShaper (tr_helpers.py:33-43)
  * and accumulate the episode meters (a2c_common.py:738-759).
- * meter: device [H][4] per-step (sum reward of done envs, sum shaped, sum length, count).
+ * meter: device [ppo_meter_floats(n_envs, H)]: [H][4] per-step sums (reward of done envs,
+ * shaped reward, length, count), complete after slot H - 1 (a fixed-order fold of the
+ * per-workgroup partials that follow them: deterministic, no float atomics).
  * step_dev (nullable): advanced by the horizon when t == horizon - 1. */
 int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *dones, int t,
                      float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len,
@@ -464,6 +466,8 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
 int ppo_partials_floats(int minibatch);
 /* size (floats) of the grad buffer of ppo_minibatch_grad / ppo_minibatch_apply */
 int ppo_grad_floats(void);
+/* size (floats) of the meter buffer of ppo_store_reward */
+int ppo_meter_floats(int n_envs, int horizon);
 /* library version */
 int usv_hip_version(void);
 

@@ -63,6 +63,7 @@ def _declare(lib):
         "ppo_minibatch_apply": [P, P, P, P, P, P, F, P, I, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
+        "ppo_meter_floats": [I, I],
         "usv_hip_version": [],
     }
     for name, args in sig.items():

@@ -312,7 +312,11 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
   }
 }
 
-// rewards_shaper + episode meters (a2c_common.py:721-759, tr_helpers.py:33-43)
+// rewards_shaper + episode meters (a2c_common.py:721-759, tr_helpers.py:33-43).
+// meter = [H][4] per-slot sums (reward of done envs, shaped reward, length, count),
+// then [H][nblk][4] per-workgroup partials: every workgroup stores its sums (no
+// float atomics), k_meter_fold adds them in workgroup order after the last slot,
+// so the meters are bit-identical run to run (graph replay == eager).
 constexpr int kStoreTB = 256;
 __global__ __launch_bounds__(kStoreTB) void k_store_reward(ppo_cfg_t c, const float *__restrict__ rew, const int64_t *__restrict__ dones, int t,
                                float *exp_rew, float *cur_rew, float *cur_shaped, float *cur_len, float *meter,
@@ -336,18 +340,35 @@ __global__ __launch_bounds__(kStoreTB) void k_store_reward(ppo_cfg_t c, const fl
     cur_len[e] = cl * nd;
   }
   s_rew = wave_sum(s_rew); s_shaped = wave_sum(s_shaped); s_len = wave_sum(s_len); s_cnt = wave_sum(s_cnt);
-  // one set of atomics per workgroup, not per wave: all of them land on the same four
-  // addresses, so their number sets this kernel's time at large env counts
   __shared__ float red[kStoreTB / 64][4];
   const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) { red[wv][0] = s_rew; red[wv][1] = s_shaped; red[wv][2] = s_len; red[wv][3] = s_cnt; }
   __syncthreads();
   if (threadIdx.x < 4) {
-    float a = red[0][threadIdx.x], cnt = red[0][3];
+    float a = red[0][threadIdx.x];
 #pragma unroll
-    for (int w = 1; w < kStoreTB / 64; ++w) { a += red[w][threadIdx.x]; cnt += red[w][3]; }
-    if (cnt > 0.f) atomicAdd(&meter[t * 4 + threadIdx.x], a);
+    for (int w = 1; w < kStoreTB / 64; ++w) a += red[w][threadIdx.x];
+    meter[c.horizon * 4 + ((size_t)t * gridDim.x + blockIdx.x) * 4 + threadIdx.x] = a;
   }
+}
+
+// meter[t][q] = sum over workgroups (in order) of the slot's partials; 64 threads = 16 slots x 4
+__global__ void k_meter_fold(ppo_cfg_t c, float *meter, int nblk) {
+  const int tq = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tq >= c.horizon * 4) return;
+  const int t = tq >> 2, q = tq & 3;
+  const float *part = meter + c.horizon * 4 + (size_t)t * nblk * 4 + q;
+  float a = 0.f;
+  constexpr int U = 16;   // loads in flight, added in workgroup order
+  for (int b0 = 0; b0 < nblk; b0 += U) {
+    float x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x[u] = part[(size_t)min(b0 + u, nblk - 1) * 4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (b0 + u < nblk) a += x[u];
+  }
+  meter[tq] = a;
 }
 
 // ---------------------------------------------------------- GAE + stats ---
@@ -1084,10 +1105,15 @@ int ppo_store_reward(const ppo_cfg_t *cfg, const float *rew, const int64_t *done
                      float *cur_rew, float *cur_shaped, float *cur_len, float *meter, uint64_t *step_dev,
                      void *stream) {
   if (!cfg || !rew || !dones || cfg->n_envs <= 0) return 1;
-  hipLaunchKernelGGL(k_store_reward, dim3((cfg->n_envs + kStoreTB - 1) / kStoreTB), dim3(kStoreTB), 0,
-                     (hipStream_t)stream, *cfg, rew,
+  const int nblk = (cfg->n_envs + kStoreTB - 1) / kStoreTB;
+  hipLaunchKernelGGL(k_store_reward, dim3(nblk), dim3(kStoreTB), 0, (hipStream_t)stream, *cfg, rew,
                      dones, t, exp_rew, cur_rew, cur_shaped, cur_len, meter, step_dev);
   USV_CHECK_LAUNCH();
+  if (t == cfg->horizon - 1) {
+    hipLaunchKernelGGL(k_meter_fold, dim3((cfg->horizon * 4 + 63) / 64), dim3(64), 0, (hipStream_t)stream, *cfg,
+                       meter, nblk);
+    USV_CHECK_LAUNCH();
+  }
   return 0;
 }
 
@@ -1153,5 +1179,8 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
 
 int ppo_partials_floats(int minibatch) { return (minibatch / RB) * NPART; }
 int ppo_grad_floats(void) { return PPO_NPARAM + 8 + RED_BLOCKS; }
+int ppo_meter_floats(int n_envs, int horizon) {
+  return horizon * 4 + horizon * ((n_envs + kStoreTB - 1) / kStoreTB) * 4;
+}
 
 }  // extern "C"

@@ -265,7 +265,9 @@ class A2CAgent:
         self.cur_rew = torch.zeros(N, **f32)
         self.cur_shaped = torch.zeros(N, **f32)
         self.cur_len = torch.zeros(N, **f32)
-        self.meter = torch.zeros((H, 4), **f32)
+        # [H][4] per-slot meter sums, then the per-workgroup partials they are folded from
+        self.meter_buf = torch.zeros(_capi.lib().ppo_meter_floats(N, H), **f32)
+        self.meter = self.meter_buf[:H * 4].view(H, 4)
         self.step_dev = torch.zeros(1, device=dev, dtype=torch.int64)   # rollout Philox step (device clock)
         self.kls = torch.zeros(self.mini_epochs_num * self.num_minibatches, **f32)
         # per minibatch: a_loss, c_loss, entropy, b_loss, kl (this rank), written by the reduce kernel
@@ -294,7 +296,7 @@ class A2CAgent:
             self.obs, rewards, self.dones, infos = self.vec_env.step(self.actions)
             step_time += time.time() - t0
             c.call("ppo_store_reward", cfg, c.ptr(rewards), c.ptr(self.dones), n, c.ptr(self.exp_rew),
-                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter),
+                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter_buf),
                    c.ptr(self.step_dev), s)
             self.algo_observer.process_infos(infos, None)
             self._step_counter += 1
@@ -337,6 +339,16 @@ class A2CAgent:
                        c.ptr(self.kls[k:k + 1]), int(not dp), s)
                 k += 1
 
+    def _update_capturable(self) -> bool:
+        """The minibatch update goes into a HIP graph on one GPU and, with several ranks, when the
+        gradient all-reduces are RCCL collectives (capturable on the launch stream; gloo's host-staged
+        collectives are not).  USV_GRAPH_COLLECTIVES=0 keeps the multi-rank update eager."""
+        if getattr(self, "_graph_update_failed", False):
+            return False
+        if not self.multi_gpu or self.rank_size == 1:
+            return True
+        return dist_util.backend() == "nccl" and os.getenv("USV_GRAPH_COLLECTIVES", "1") != "0"
+
     def _graph_capture(self, fn):
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
@@ -373,10 +385,21 @@ class A2CAgent:
         play_time_end = time.time()
         self.curr_frames = batch["played_frames"]
         self.algo_observer.after_steps()
-        if graphs and not self.multi_gpu:
+        if graphs and self._update_capturable():
             if self._graph_update is None:
-                self._graph_update = self._graph_capture(self.update_epoch_minibatches)
-            self._graph_update.replay()
+                try:
+                    self._graph_update = self._graph_capture(self.update_epoch_minibatches)
+                except RuntimeError as err:   # a collective the backend cannot capture: eager from now on
+                    self._graph_update_failed = True
+                    self._graph_update = None
+                    if self.rank == 0:
+                        print(f"update graph capture failed ({err}); the update runs eagerly")
+                    torch.cuda.synchronize()
+                    self.update_epoch_minibatches()
+                else:
+                    self._graph_update.replay()
+            else:
+                self._graph_update.replay()
         else:
             self.update_epoch_minibatches()
         torch.cuda.current_stream().synchronize()

@@ -893,6 +893,48 @@ def gen_ppo(torch, n=32, horizon=16, minibatch=128, seed=5):
     print("ppo: lr", recorded["lr"][:6], "... kl", recorded["kl"][:4])
 
 
+CKPT811 = os.path.join(REF, "811_3.5刹车_____（复件）", "last_USV_ep_5450_rew_38.54975.pth")
+
+
+def gen_ckpt811(torch, rows=64, seed=8):
+    """The reference's only checkpoint (rl_games, 13-input network of the Aug-11 task): its
+    state_dict tensors and metadata, and the reference ModelA2CContinuousLogStd (built from the USV
+    train yaml's network section, normalize_input / normalize_value as trained) evaluated on fixed
+    13-dim observations: mus, sigmas, denormalised values, the sampled actions and their neglogp."""
+    import codecs
+    import yaml
+    from rl_games.algos_torch import model_builder
+    torch.serialization.add_safe_globals([(np._core.multiarray.scalar, "numpy.core.multiarray.scalar"), np.dtype,
+                                          codecs.encode, np.dtypes.Float64DType, np.dtypes.Float32DType])
+    ck = torch.load(CKPT811, weights_only=True, map_location="cpu")
+    with open(os.path.join(REF, "omniisaacgymenvs/cfg/train/USV/USV_PPOcontinuous_MLP.yaml")) as f:
+        params = yaml.safe_load(f)["params"]
+    net = model_builder.ModelBuilder().load(params).build(
+        {"actions_num": 2, "input_shape": {"state": (13,)}, "num_seqs": 1, "value_size": 1,
+         "normalize_value": True, "normalize_input": True, "normalize_input_keys": ["state"]})
+    net.load_state_dict(ck["model"])
+    net.eval()
+    g = torch.Generator().manual_seed(seed)
+    obs = (torch.randn(rows, 13, generator=g) * 2.0).float()
+    torch.manual_seed(seed)
+    with torch.no_grad():
+        res = net({"is_train": False, "obs": {"state": obs.clone()}, "prev_actions": None})
+    out = {"obs": obs.numpy(), "mus": res["mus"].numpy(), "sigmas": res["sigmas"].numpy(),
+           "values": res["values"].numpy(), "actions": res["actions"].numpy(),
+           "neglogpacs": res["neglogpacs"].numpy(), "epoch": np.int64(ck["epoch"]), "frame": np.int64(ck["frame"]),
+           "last_mean_rewards": np.float32(ck["last_mean_rewards"]),
+           "opt_lr": np.float64(ck["optimizer"]["param_groups"][0]["lr"]),
+           "opt_step": np.float64(ck["optimizer"]["state"][0]["step"]),
+           "keys": np.array(list(ck["model"].keys())), "top_keys": np.array(list(ck.keys()))}
+    for k, v in ck["model"].items():
+        out["sd__" + k] = v.numpy()
+    for i, st in ck["optimizer"]["state"].items():
+        out[f"opt_m_{i}"] = st["exp_avg"].numpy()
+        out[f"opt_v_{i}"] = st["exp_avg_sq"].numpy()
+    np.savez_compressed(os.path.join(OUT, "ckpt811.npz"), **out)
+    print("ckpt811: mus[0]", out["mus"][0], "values[0]", out["values"][0])
+
+
 STAT_NAMES = [
     "total_reward", "distance_reward", "alignment_reward", "heading_improve_reward",
     "potential_shaping_reward", "speed_reward", "angular_reward", "turn_hazard_penalty",
@@ -923,6 +965,7 @@ def main():
         "episodeS": lambda: (make_scene_file(), gen_episode(torch, "S", 6, 64, 41)),
         "episodeT": lambda: gen_episode(torch, "T", 12, 64, 32),
         "ppo": lambda: gen_ppo(torch),
+        "ckpt811": lambda: gen_ckpt811(torch),
     }
     for name, fn in jobs.items():
         if args.only and name not in args.only.split(","):

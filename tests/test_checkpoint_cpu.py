@@ -78,3 +78,71 @@ def test_shape_mismatch_raises():
     with pytest.raises(ValueError):
         C.load_model_state_dict(sd, torch.zeros(C.NPARAM), torch.zeros(2 * C.NIN + 1, dtype=torch.float64),
                                 torch.zeros(3, dtype=torch.float64), C.NIN)
+
+
+# ---- the reference's own checkpoint (811_3.5.../last_USV_ep_5450_rew_38.54975.pth, 13-input net) ----
+import os  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+REF_CKPT = "/root/reference/811_3.5刹车_____（复件）/last_USV_ep_5450_rew_38.54975.pth"
+
+
+def ckpt811_dict(d):
+    """The reference's checkpoint dict rebuilt from the fixture arrays (a2c_common.py:590-606 layout)."""
+    from collections import OrderedDict
+    model = OrderedDict((str(k), torch.from_numpy(np.array(d["sd__" + str(k)]))) for k in d["keys"])
+    state = {i: {"step": torch.tensor(float(d["opt_step"])), "exp_avg": torch.from_numpy(d[f"opt_m_{i}"]),
+                 "exp_avg_sq": torch.from_numpy(d[f"opt_v_{i}"])} for i in range(len(C.PARAM_LAYOUT))}
+    group = {"lr": float(d["opt_lr"]), "betas": (0.9, 0.999), "eps": 1e-08, "weight_decay": 0.0, "amsgrad": False,
+             "maximize": False, "foreach": None, "capturable": False, "differentiable": False, "fused": None,
+             "params": list(range(len(C.PARAM_LAYOUT)))}
+    return {"model": model, "epoch": int(d["epoch"]), "optimizer": {"state": state, "param_groups": [group]},
+            "frame": int(d["frame"]), "last_mean_rewards": np.float32(d["last_mean_rewards"]), "env_state": None}
+
+
+def test_reference_checkpoint_key_set_and_dtypes(golden):
+    """The 811 checkpoint's key set, shapes and dtypes (pinned in the fixture), read by load_checkpoint with
+    weights_only=True when the reference tree is present; its model maps onto the padded device vector and back
+    bit for bit."""
+    d = golden("ckpt811.npz")
+    assert [str(k) for k in d["top_keys"]] == ["model", "epoch", "optimizer", "frame", "last_mean_rewards",
+                                               "env_state"]
+    keys = [str(k) for k in d["keys"]]
+    assert keys[:6] == ["value_mean_std.running_mean", "value_mean_std.running_var", "value_mean_std.count",
+                        "running_mean_std.running_mean_std.state.running_mean",
+                        "running_mean_std.running_mean_std.state.running_var",
+                        "running_mean_std.running_mean_std.state.count"]
+    assert keys[6:] == [k for k, _ in C.PARAM_LAYOUT]
+    assert d["sd__" + C.W1_KEY].shape == (C.NH, 13) and d["sd__" + C.W1_KEY].dtype == np.float32
+    assert d["sd__value_mean_std.count"].dtype == np.float64 and d["sd__value_mean_std.count"].shape == ()
+    if os.path.exists(REF_CKPT):
+        ck = C.load_checkpoint(REF_CKPT)
+        assert list(ck.keys()) == [str(k) for k in d["top_keys"]]
+        assert list(ck["model"].keys()) == keys
+        for k in keys:
+            t = ck["model"][k]
+            assert t.dtype == torch.from_numpy(np.array(d["sd__" + k])).dtype, k
+            np.testing.assert_array_equal(t.numpy(), d["sd__" + k])
+    sd = ckpt811_dict(d)["model"]
+    params = torch.zeros(C.NPARAM)
+    obs_rms = torch.zeros(2 * C.NIN + 1, dtype=torch.float64)
+    obs_rms[C.NIN:2 * C.NIN] = 1.0
+    val_rms = torch.zeros(3, dtype=torch.float64)
+    C.load_model_state_dict(sd, params, obs_rms, val_rms, 13)
+    back = C.model_state_dict(params, obs_rms, val_rms, 13)
+    assert list(back.keys()) == keys
+    for k in keys:
+        assert back[k].dtype == sd[k].dtype and tuple(back[k].shape) == tuple(sd[k].shape), k
+        torch.testing.assert_close(back[k], sd[k], rtol=0, atol=0)
+
+
+def test_reference_checkpoint_optimizer_round_trip(golden):
+    d = golden("ckpt811.npz")
+    osd = ckpt811_dict(d)["optimizer"]
+    m, v = torch.zeros(C.NPARAM), torch.zeros(C.NPARAM)
+    step, lr = C.load_optimizer_state_dict(osd, m, v, 13)
+    assert step == float(d["opt_step"]) and lr == pytest.approx(float(d["opt_lr"]))
+    back = C.optimizer_state_dict(m, v, step, lr, 0.0, 13)
+    for i in range(len(C.PARAM_LAYOUT)):
+        torch.testing.assert_close(back["state"][i]["exp_avg"], osd["state"][i]["exp_avg"], rtol=0, atol=0)
+        torch.testing.assert_close(back["state"][i]["exp_avg_sq"], osd["state"][i]["exp_avg_sq"], rtol=0, atol=0)

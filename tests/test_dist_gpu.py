@@ -1,0 +1,123 @@
+"""Two ranks on ONE GPU (gloo over the device tensors, USV_RANKS_SHARE_DEVICE): A2CAgent's multi-GPU
+branch end to end -- the initial weight broadcast (a2c_common.py:1354), the per-minibatch flat
+gradient + KL all-reduce and the 1/world scale inside the Adam kernel (a2c_common.py:308-323,
+1218-1222), the LR schedule following the all-reduced KL -- against a single rank that trains on
+both ranks' rows; and the per-rank env streams (torch_runner.py:74-75 seeds every rank with
+seed + LOCAL_RANK before any env draw).
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+N, H, MB, EPOCHS = 256, 16, 1024, 2     # per rank: 4096 rows, 4 minibatches of 1024
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _dataset(rows, seed=5):
+    rng = np.random.default_rng(seed)
+    f = np.float32
+    return {"exp_obs": rng.normal(0, 2, (rows, 33)).astype(f), "exp_act": rng.normal(0, 1, (rows, 2)).astype(f),
+            "exp_nlp": rng.uniform(1.5, 3.5, rows).astype(f), "exp_val": rng.normal(0, 1, rows).astype(f),
+            "exp_ret": rng.normal(0, 1, rows).astype(f), "exp_adv": rng.normal(0, 1, rows).astype(f),
+            "exp_mu": rng.normal(0, 0.3, (rows, 2)).astype(f), "exp_sigma": np.ones((rows, 2), f)}
+
+
+def _rank_rows(rank, world):
+    """Rank r's local batch: minibatch i of rank r = rows [i*MB + r*MB/2 .. ) of the union layout
+    the single-rank run sees (each union minibatch = rank 0's half, then rank 1's half)."""
+    half = MB // world
+    idx = [np.arange(i * MB + rank * half, i * MB + (rank + 1) * half) for i in range(N * H * world // MB)]
+    return np.concatenate(idx)
+
+
+def _agent(n_envs, minibatch, multi_gpu, params_seed=11):
+    import yaml
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
+    from tests.test_ppo_gpu import FakeVecEnv
+    with open(os.path.join(ROOT, "omniisaacgymenvs_loop_amd/cfg/train/USV/USV_PPOcontinuous_MLP.yaml")) as f:
+        params = yaml.safe_load(f)["params"]
+    params["seed"] = params_seed
+    # obs RMS is per rank in the reference (never synchronised): off, so the union run is comparable
+    params["config"].update(num_actors=n_envs, minibatch_size=minibatch, mini_epochs=EPOCHS, device="cuda:0",
+                            vec_env=FakeVecEnv(n_envs), train_dir="/tmp/dist_gpu_runs", multi_gpu=multi_gpu,
+                            normalize_input=False, print_stats=False)
+    return A2CAgent("run", params)
+
+
+def _load(ag, data, rows):
+    for k, v in data.items():
+        getattr(ag, k).copy_(torch.tensor(np.ascontiguousarray(v[rows]), device="cuda:0"))
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
+                      WORLD_SIZE=str(world), USV_RANKS_SHARE_DEVICE="0", USV_DIST_BACKEND="gloo")
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    try:
+        # different init seeds per rank: the broadcast must make rank 0's weights everyone's
+        ag = _agent(N, MB // world, True, params_seed=11 + 100 * rank)
+        assert ag.multi_gpu and ag.rank_size == world
+        _load(ag, _dataset(N * H * world), _rank_rows(rank, world))
+        p0 = ag.model_params.cpu().numpy().copy()
+        ag.update_epoch_minibatches()
+        torch.cuda.synchronize()
+        # env streams: the same config on every rank, seeds offset by LOCAL_RANK
+        from omniisaacgymenvs_loop_amd.envs.vec_env_rlgames import VecEnvRLGames
+        from omniisaacgymenvs_loop_amd.scripts.rlgames_train import build_config
+        from omniisaacgymenvs_loop_amd.utils.task_util import initialize_task
+        cfg = build_config({"num_envs": 64, "seed": 42, "multi_gpu": True})
+        task = initialize_task(cfg, VecEnvRLGames(headless=True))
+        obs, _, _ = task.env_step(torch.zeros((64, 2), device="cuda:0"))
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), p0=p0, p=ag.model_params.cpu().numpy(),
+                 lr=float(ag.opt[0].item()), kls=ag.kls.cpu().numpy(), env_seed=task.seed, obs=obs.cpu().numpy(),
+                 mass=task.params[0].cpu().numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def two_ranks(tmp_path_factory):
+    import torch.multiprocessing as mp
+    out = tmp_path_factory.mktemp("dist_gpu")
+    mp.spawn(_worker, args=(2, _port(), str(out)), nprocs=2, join=True)
+    return [np.load(out / f"r{r}.npz") for r in range(2)]
+
+
+def test_two_ranks_equal_single_rank_on_the_union(two_ranks):
+    r0, r1 = two_ranks
+    np.testing.assert_array_equal(r0["p0"], r1["p0"])              # broadcast from rank 0
+    np.testing.assert_array_equal(r0["p"], r1["p"])                # identical updates on both ranks
+    assert r0["lr"] == r1["lr"]
+    single = _agent(2 * N, MB, False, params_seed=11)
+    np.testing.assert_array_equal(single.model_params.cpu().numpy(), r0["p0"])
+    _load(single, _dataset(N * H * 2), np.arange(2 * N * H))
+    single.update_epoch_minibatches()
+    torch.cuda.synchronize()
+    from tests import errtab as ET
+    # the mean of two half-minibatch gradients == the union minibatch's gradient up to summation order
+    ET.check("dist_2ranks", "params", r0["p"], single.model_params.cpu().numpy(), 1e-5, 1e-5)
+    ET.check("dist_2ranks", "kl", r0["kls"], single.kls.cpu().numpy(), 1e-4, 1e-7)
+    assert r0["lr"] == pytest.approx(float(single.opt[0].item()), rel=1e-6)
+
+
+def test_ranks_draw_different_env_streams(two_ranks):
+    r0, r1 = two_ranks
+    assert int(r0["env_seed"]) == 42 and int(r1["env_seed"]) == 43
+    assert not np.array_equal(r0["mass"], r1["mass"])              # SysID domain randomisation
+    assert not np.array_equal(r0["obs"], r1["obs"])                # spawns, obstacles, noise

@@ -207,3 +207,96 @@ def test_checkpoint_roundtrip(tmp_path):
     assert torch.equal(ag2.model_params, ag.model_params)
     assert torch.equal(ag2.obs_rms, ag.obs_rms)
     assert ag2.epoch_num == 7 and ag2.frame == 1024
+
+
+
+def test_reward_shaper_and_meters_vs_reference(ppo):
+    """DefaultRewardsShaper x0.01 (tr_helpers.py:33-43) into the experience buffer and the
+    episode meters (a2c_common.py:738-759, AverageMeter torch_ext.py:281-307) replayed from the reference
+    epoch's env rewards / dones: game_rewards mean and size as the reference left them."""
+    from omniisaacgymenvs_loop_amd import _capi as c
+    H, N = ppo["exp_rewards"].shape[:2]
+    ag = _agent(N, 128)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a), device=DEV)
+    ag.meter.zero_()
+    for t in range(H):
+        c.call("ppo_store_reward", c.byref(ag.cfg), c.ptr(T(ppo["env_rew"][t])), c.ptr(T(ppo["env_dones"][t])), t,
+               c.ptr(ag.exp_rew), c.ptr(ag.cur_rew), c.ptr(ag.cur_shaped), c.ptr(ag.cur_len), c.ptr(ag.meter_buf),
+               None, c.stream_ptr())
+    torch.cuda.synchronize()
+    ET.check("ppo_meters", "exp_rew", ag.exp_rew.cpu().numpy(), _swap(ppo["exp_rewards"])[:, 0], 1e-5, 1e-5)
+    ag._replay_meters()
+    assert ag.game_rewards.current_size == int(ppo["game_rewards_size"])
+    ET.check("ppo_meters", "game_rewards", np.float32(ag.game_rewards.get_mean()), ppo["game_rewards_mean"][0],
+             1e-5, 1e-5)
+
+
+class _Env13(FakeVecEnv):
+    """The 13-dim observation space of the Aug-11 task the 811 checkpoint was trained on."""
+
+    def __init__(self, n):
+        super().__init__(n)
+        from omniisaacgymenvs_loop_amd.utils.spaces import Box, DictSpace
+        self.info["observation_space"] = DictSpace({"state": Box(-np.inf, np.inf, (13,))})
+
+
+def test_reference_checkpoint_player_forward(golden, tmp_path):
+    """The reference's 811 checkpoint (13-input net, zero-padded to the kernels' 33 inputs) restored by
+    PpoPlayerContinuous (players.py:107-182) through torch.load(weights_only=True): the HIP forward equals the
+    reference ModelA2CContinuousLogStd's mus / sigmas / denormalised values / neglogp on the same inputs, and the
+    deterministic action is clamp(mu) (players.py:139-150)."""
+    import yaml
+    from omniisaacgymenvs_loop_amd import _capi as c
+    from omniisaacgymenvs_loop_amd.rl_games.players import PpoPlayerContinuous
+    from tests.test_checkpoint_cpu import ckpt811_dict
+    d = golden("ckpt811.npz")
+    n = d["obs"].shape[0]
+    torch.save(ckpt811_dict(d), str(tmp_path / "811.pth"))
+    with open(os.path.join(ROOT, "omniisaacgymenvs_loop_amd/cfg/train/USV/USV_PPOcontinuous_MLP.yaml")) as f:
+        params = yaml.safe_load(f)["params"]
+    params["config"].update(num_actors=n, device=DEV, vec_env=_Env13(n))
+    pl = PpoPlayerContinuous(params)
+    assert pl.obs_dim == 13
+    pl.restore(str(tmp_path / "811.pth"))
+    obs = torch.tensor(d["obs"], device=DEV)
+    act = pl.get_action(obs, is_deterministic=True)
+    torch.cuda.synchronize()
+    tn = "ckpt811_player"
+    mus = pl._scratch["mu"].cpu().numpy()
+    ET.check(tn, "mu", mus, d["mus"], 1e-5, 1e-5, ["mu0", "mu1"])
+    ET.check(tn, "sigma", pl._scratch["sigma"].cpu().numpy(), d["sigmas"], 1e-5, 1e-5, ["s0", "s1"])
+    ET.check(tn, "value", pl._scratch["val"].cpu().numpy(), d["values"][:, 0], 1e-5, 1e-5)
+    np.testing.assert_array_equal(act.cpu().numpy(), np.clip(mus, -1, 1))
+    # the reference's sampled actions replayed through the same kernel: its neglogp
+    eps = torch.tensor((d["actions"] - d["mus"]) / d["sigmas"], device=DEV)
+    obs_pad = torch.zeros((n, 33), device=DEV)
+    obs_pad[:, :13] = obs
+    sc = pl._scratch
+    c.call("ppo_policy_step", c.byref(pl.cfg), c.ptr(pl.model_params), c.ptr(pl.obs_rms), c.ptr(pl.val_rms),
+           c.ptr(obs_pad), 0, c.ptr(sc["obs"]), c.ptr(sc["act"]), c.ptr(sc["nlp"]), c.ptr(sc["val"]), c.ptr(sc["mu"]),
+           c.ptr(sc["sigma"]), c.ptr(pl._done8), c.ptr(pl._dones), c.ptr(pl._actions), 0, 0, None, c.ptr(eps),
+           c.stream_ptr())
+    torch.cuda.synchronize()
+    ET.check(tn, "action", sc["act"].cpu().numpy(), d["actions"], 1e-5, 1e-5, ["a0", "a1"])
+    ET.check(tn, "neglogp", sc["nlp"].cpu().numpy(), d["neglogpacs"], 1e-5, 1e-5)
+
+
+def test_player_runs_the_usv_task(tmp_path):
+    """test=True path: a trained-then-saved checkpoint restored into PpoPlayerContinuous plays the USV task
+    (common/player.py:319-423) through VecEnvRLGames; finished games are counted and rewards are finite."""
+    from omniisaacgymenvs_loop_amd.rl_games.players import PpoPlayerContinuous
+    from tests.test_train_gpu import _agent_env
+    env, task, ag = _agent_env(256, 2048, True, seed=3)
+    ag.obs = ag.env_reset()
+    for _ in range(2):
+        ag.train_epoch()
+    ag.save(str(tmp_path / "ck"))
+    params = copy.deepcopy({k: v for k, v in ag.params.items() if k != "config"})
+    params["config"] = {k: v for k, v in ag.config.items() if k != "vec_env"}
+    params["config"]["vec_env"] = env
+    params["player"] = {"deterministic": True, "games_num": 64, "max_steps": 400}
+    pl = PpoPlayerContinuous(params)
+    pl.restore(str(tmp_path / "ck.pth"))
+    torch.testing.assert_close(pl.model_params, ag.model_params, rtol=0, atol=0)
+    mean_reward = pl.run()
+    assert np.isfinite(mean_reward)

@@ -47,7 +47,8 @@ def _agent_env(n, minibatch, use_graph, seed=11):
 
 def test_graph_replay_matches_eager():
     """The captured rollout + update graphs replay exactly what the eager loop launches: after 4 epochs
-    (1 eager, 1 capture, 2 replays) parameters, optimiser state, env state and meters are bit-identical."""
+    (1 eager, 1 capture, 2 replays) parameters, optimiser state, env state and episode meters are
+    bit-identical."""
     runs = []
     for use_graph in (False, True):
         env, task, ag = _agent_env(512, 2048, use_graph)
@@ -66,8 +67,8 @@ def test_graph_replay_matches_eager():
     for k in ("params", "m", "obs_rms", "state", "obs", "clock", "step_dev"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     assert a["lr"] == b["lr"] and a["host_step"] == b["host_step"]
-    # episode meters are float atomics across waves (order-dependent last bits): close, not identical
-    assert abs(a["meters"] - b["meters"]) <= 1e-5 * max(1.0, abs(a["meters"]))
+    # episode meters: per-workgroup partials folded in a fixed order, so identical too
+    assert a["meters"] == b["meters"]
     assert int(b["clock"][0]) == b["host_step"]
 
 
