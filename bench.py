@@ -81,15 +81,21 @@ def build(envs, local, world, seed, task_name="CaptureXY"):
 
 
 class KernelTimer:
-    """HIP events around one C-ABI launch on torch's current stream (the launch stream)."""
+    """HIP events around one C-ABI launch on torch's current stream (the launch stream).  A spin
+    kernel (torch.cuda._sleep) keeps the GPU busy while the host enqueues event / launch / event, so
+    the pair brackets the launch's own execution, not the host's launch latency (eager epochs are
+    host-bound at this size)."""
 
-    def __init__(self):
+    def __init__(self, spin_cycles=200_000):
         self.pairs = []
+        self.spin = spin_cycles
 
     def __call__(self, fn):
         import torch
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
+        if self.spin:
+            torch.cuda._sleep(self.spin)
         a.record()
         fn()
         b.record()
@@ -355,7 +361,8 @@ def main():
                          "traffic": None, "bytes_per_env_step": step_bytes, "launch_ms": env_ms,
                          "envs_per_launch": args.envs,
                          "launch_ms_method": f"HIP event pair around each of the {len(env_timer.pairs)} env-step "
-                                             "launches of one eager training epoch, on the launch stream"},
+                                             "launches of one eager training epoch, on the launch stream, behind a "
+                                             "spin kernel (host launch latency excluded)"},
             "roofline_ppo": {"bound": "mfma",
                              "kernel": "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, 64 rows per "
                                        "workgroup, fixed-order reduction)",

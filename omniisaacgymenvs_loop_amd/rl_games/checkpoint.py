@@ -145,7 +145,8 @@ def save_checkpoint(filename: str, state: Dict[str, Any]) -> None:
 def _allow_numpy_globals():
     import codecs
     allow = [np.dtype, codecs.encode]
-    try:
+    try:   # numpy 2 writes numpy._core.multiarray.scalar, numpy 1 wrote numpy.core.multiarray.scalar
+        allow.append(np._core.multiarray.scalar)
         allow.append((np._core.multiarray.scalar, "numpy.core.multiarray.scalar"))
     except AttributeError:  # numpy < 2
         allow.append(np.core.multiarray.scalar)

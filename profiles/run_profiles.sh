@@ -1,18 +1,19 @@
 #!/bin/bash
-# GPU-box profiling recipe for the round's bench: kernel trace + stats, then
-# two separate PMC passes (FETCH_SIZE, WRITE_SIZE) on the env-step kernel.
+# GPU-box profiling recipe for the round's bench: kernel trace + stats, then two separate PMC
+# passes (FETCH_SIZE, WRITE_SIZE) on the env-step kernel (MI355X_MICROARCH.md HBM section: one
+# counter group per pass, FETCH_SIZE doubled for wide streaming reads on gfx950).
 # Usage (on the GPU box, from the repo root):  bash profiles/run_profiles.sh <tag> [envs]
 set -euo pipefail
-TAG=${1:-r01}
-ENVS=${2:-4096}
+TAG=${1:-r02}
+ENVS=${2:-131072}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 5 --warmup 2 --envs $ENVS --no-cpu-baseline --env-only-envs 0"
+B="$R/bench.py --steps 5 --warmup 2 --envs $ENVS --no-cpu-baseline --c2-steps 0"
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o trace -- python3 $B > "$OUT/trace.log" 2>&1
 echo "trace done"
-timeout -k 10 420 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_env_step --output-format csv -d "$OUT" -o pmc_fetch -- python3 $B > "$OUT/pmc_fetch.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_env_step --output-format csv -d "$OUT" -o pmc_fetch -- python3 $B > "$OUT/pmc_fetch.log" 2>&1
 echo "fetch done"
-timeout -k 10 420 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_env_step --output-format csv -d "$OUT" -o pmc_write -- python3 $B > "$OUT/pmc_write.log" 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_env_step --output-format csv -d "$OUT" -o pmc_write -- python3 $B > "$OUT/pmc_write.log" 2>&1
 echo "write done"

@@ -220,9 +220,10 @@ def test_reward_shaper_and_meters_vs_reference(ppo):
     T = lambda a: torch.tensor(np.ascontiguousarray(a), device=DEV)
     ag.meter.zero_()
     for t in range(H):
-        c.call("ppo_store_reward", c.byref(ag.cfg), c.ptr(T(ppo["env_rew"][t])), c.ptr(T(ppo["env_dones"][t])), t,
-               c.ptr(ag.exp_rew), c.ptr(ag.cur_rew), c.ptr(ag.cur_shaped), c.ptr(ag.cur_len), c.ptr(ag.meter_buf),
-               None, c.stream_ptr())
+        rew, dones = T(ppo["env_rew"][t]), T(ppo["env_dones"][t])     # alive until the launch has run
+        c.call("ppo_store_reward", c.byref(ag.cfg), c.ptr(rew), c.ptr(dones), t, c.ptr(ag.exp_rew), c.ptr(ag.cur_rew),
+               c.ptr(ag.cur_shaped), c.ptr(ag.cur_len), c.ptr(ag.meter_buf), None, c.stream_ptr())
+        torch.cuda.synchronize()
     torch.cuda.synchronize()
     ET.check("ppo_meters", "exp_rew", ag.exp_rew.cpu().numpy(), _swap(ppo["exp_rewards"])[:, 0], 1e-5, 1e-5)
     ag._replay_meters()
