@@ -88,23 +88,38 @@ class KernelTimer:
 
     def __init__(self, spin_cycles=200_000):
         self.pairs = []
+        self.empty = []
         self.spin = spin_cycles
 
-    def __call__(self, fn):
+    def _pair(self, fn, into):
         import torch
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
         if self.spin:
             torch.cuda._sleep(self.spin)
         a.record()
-        fn()
+        if fn is not None:
+            fn()
         b.record()
-        self.pairs.append((a, b))
+        into.append((a, b))
 
-    def mean_ms(self):
+    def __call__(self, fn):
+        self._pair(fn, self.pairs)
+        self._pair(None, self.empty)    # the same pair around nothing: the event overhead
+
+    def raw_ms(self):
         if not self.pairs:
             return float("nan")
         return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
+
+    def overhead_ms(self):
+        if not self.empty:
+            return 0.0
+        return sum(a.elapsed_time(b) for a, b in self.empty) / len(self.empty)
+
+    def mean_ms(self):
+        """Mean launch time, the empty pair's time (event overhead) subtracted."""
+        return self.raw_ms() - self.overhead_ms()
 
 
 def _cpu_model() -> str:
@@ -359,12 +374,14 @@ def main():
             "roofline": {"bound": "hbm", "kernel": step_kernel,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_env_step": step_bytes, "launch_ms": env_ms,
+                         "launch_ms_raw": env_timer.raw_ms(), "event_overhead_ms": env_timer.overhead_ms(),
                          "envs_per_launch": args.envs,
                          "launch_ms_method": f"HIP event pair around each of the {len(env_timer.pairs)} env-step "
                                              "launches of one eager training epoch, on the launch stream, behind a "
-                                             "spin kernel (host launch latency excluded)"},
+                                             "spin kernel (host launch latency excluded), minus the same pair around "
+                                             "no launch (event overhead)"},
             "roofline_ppo": {"bound": "mfma",
-                             "kernel": "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, 64 rows per "
+                             "kernel": "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, 8 waves per 32-row "
                                        "workgroup, fixed-order reduction)",
                              "achieved": ppo_tfs,
                              "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
