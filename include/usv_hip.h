@@ -443,8 +443,9 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
  * Split in two so the flat gradient can be all-reduced in between:
  *   ppo_minibatch_grad  -> grad[PPO_NPARAM] (+ kl sum in grad[PPO_NPARAM])
  *   ppo_minibatch_apply -> clip + Adam + lr update.
- * opt: device floats [0]=lr [1]=step [2]=last kl [3]=last grad norm [4..6] unused (0),
- *      [7]=completion counter of the multi-workgroup Adam kernel (uint bits, keep 0);
+ * opt: device floats [2][8], two slots of [0]=lr [1]=step [2]=last kl [3]=last grad norm
+ *      [4..7] unused; ppo_minibatch_apply reads slot opt_slot (0 or 1) and writes the
+ *      next values to the other slot (callers alternate; no in-kernel completion counter);
  * m, v: [PPO_NPARAM].  minibatch must be a multiple of 32 (one 512-thread workgroup per 32 rows).
  * grad must be 16-byte aligned.  losses (nullable) receives the minibatch means
  * (a_loss, c_loss, entropy, b_loss, kl) of this rank; kl_out (nullable) the KL
@@ -459,10 +460,10 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        float *exp_mu, float *exp_sigma, float *grad, float *losses,
                        float *partials, double *work, void *stream);
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m,
-                        float *adam_v, float *opt, float grad_scale, float *kl_out,
-                        int norm_from_partials, void *stream);
+                        float *adam_v, float *opt, int opt_slot, float grad_scale,
+                        float *kl_out, int norm_from_partials, void *stream);
 
-/* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad */
+/* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad (16-byte aligned) */
 int ppo_partials_floats(int minibatch);
 /* size (floats) of the grad buffer of ppo_minibatch_grad / ppo_minibatch_apply */
 int ppo_grad_floats(void);

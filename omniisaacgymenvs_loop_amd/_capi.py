@@ -60,7 +60,7 @@ def _declare(lib):
         "ppo_store_reward": [P, P, P, I, P, P, P, P, P, P, P],
         "ppo_prepare": [P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_grad": [P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
-        "ppo_minibatch_apply": [P, P, P, P, P, P, F, P, I, P],
+        "ppo_minibatch_apply": [P, P, P, P, P, P, I, F, P, I, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
         "ppo_meter_floats": [I, I],

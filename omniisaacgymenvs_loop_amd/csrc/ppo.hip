@@ -32,6 +32,7 @@ constexpr int TB = 256;         // threads per block (4 waves; wave w owns outpu
 constexpr int XS = 36;          // row stride of x / W1 in LDS (k 33..35 zero)
 constexpr int HS = 130;         // row stride of h1 / h2 / W2 in LDS
 constexpr int NPART = PPO_NPARAM + 8;   // partial row: params + loss sums
+constexpr int NPART_PAD = (NPART + 3) & ~3;   // partial row stride (16-B aligned rows)
 constexpr int P_LOSS = PPO_NPARAM;      // a, c, entropy, b, kl sums
 constexpr float kLog2Pi = 1.8378770664093453f;  // 0.5*log(2*pi)*2 (models.py:400)
 
@@ -593,12 +594,16 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   const float invB = 1.0f / (float)c.minibatch;
   USV_PHASE(ppo, 0);
   // ---- every global load issued up front (compile-time trip counts) ----
-  constexpr int NW2H = NH * NH / 2 / GTB, NW1G = NH * XS / GTB, NTLG = (TAIL + GTB - 1) / GTB;
-  static_assert(NH * NH / 2 % GTB == 0 && NH * XS % GTB == 0, "staging trip counts");
-  float2 w2r[NW2H];
+  // W2 as 16-byte loads from the 16-byte aligned parameter base (checked on the host): the
+  // float4s q = W2Q0 .. W2Q0 + NW2Q - 1 cover W2; each is two (even k, k + 1) pairs of one row
+  constexpr int NW1G = NH * XS / GTB, NTLG = (TAIL + GTB - 1) / GTB;
+  constexpr int W2Q0 = PPO_OFF_W2 / 4, W2E0 = 4 * W2Q0 - PPO_OFF_W2;
+  constexpr int NW2Q = (PPO_OFF_W2 + NH * NH - 1) / 4 - W2Q0 + 1, NW2U = NW2Q / GTB, NW2X = NW2Q % GTB;
+  static_assert(NH * XS % GTB == 0 && PPO_OFF_W2 % 2 == 0 && NW2X <= GTB, "staging trip counts");
+  float4 w2q[NW2U], w2x = make_float4(0.f, 0.f, 0.f, 0.f);
   float w1r[NW1G], tlr[NTLG];
   {
-    const float2 *W2 = reinterpret_cast<const float2 *>(P + PPO_OFF_W2);   // PPO_OFF_W2 is even
+    const float4 *P4 = reinterpret_cast<const float4 *>(P);
 #pragma unroll
     for (int u = 0; u < NW1G; ++u) {
       const int q = tid + u * GTB, j = q / XS, k = q % XS;
@@ -607,7 +612,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
 #pragma unroll
     for (int u = 0; u < NTLG; ++u) tlr[u] = (tid + u * GTB < TAIL) ? P[PPO_OFF_B2 + tid + u * GTB] : 0.f;
 #pragma unroll
-    for (int u = 0; u < NW2H; ++u) w2r[u] = W2[tid + u * GTB];
+    for (int u = 0; u < NW2U; ++u) w2q[u] = P4[W2Q0 + tid + u * GTB];
+    if (NW2X > 0 && tid < NW2X) w2x = P4[W2Q0 + NW2U * GTB + tid];
   }
   const float b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
   const float lsig0 = P[PPO_OFF_SIGMA], lsig1 = P[PPO_OFF_SIGMA + 1];
@@ -668,10 +674,15 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   }
   USV_PHASE(ppo, 9);
   // W2 into LDS (waves 4-7 do it while 0-3 run layer 1; each thread commits its own loads)
+  {
+    auto put_w2 = [&](int qrel, float4 v) {
+      const int e0 = 4 * qrel + W2E0, e1 = e0 + 2;     // both even: a pair never crosses a row
+      if (e0 >= 0) *reinterpret_cast<float2 *>(&s.w2[(e0 >> 7) * HS + (e0 & (NH - 1))]) = make_float2(v.x, v.y);
+      if (e1 < NH * NH) *reinterpret_cast<float2 *>(&s.w2[(e1 >> 7) * HS + (e1 & (NH - 1))]) = make_float2(v.z, v.w);
+    };
 #pragma unroll
-  for (int u = 0; u < NW2H; ++u) {
-    const int q = tid + u * GTB, j = q / (NH / 2), k2 = q % (NH / 2);
-    *reinterpret_cast<float2 *>(&s.w2[j * HS + 2 * k2]) = w2r[u];
+    for (int u = 0; u < NW2U; ++u) put_w2(tid + u * GTB, w2q[u]);
+    if (NW2X > 0 && tid < NW2X) put_w2(NW2U * GTB + tid, w2x);
   }
   __syncthreads();
   USV_PHASE(ppo, 10);
@@ -731,7 +742,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   }
   __syncthreads();
   USV_PHASE(ppo, 2);
-  const PartOut part_st{__builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART, 0, NPART * 4,
+  const PartOut part_st{__builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4,
                                                           0x00020000)};
   // ---- per-row losses and output gradients (wave 0, lanes < RB) ----
   if (tid < 64) {
@@ -920,70 +931,71 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__
   mb_grad8w(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
 }
 
-// sum the per-block partials (fixed order => deterministic) into grad[]:
-// 64 params x 4 block-strided groups per workgroup, combined in LDS.
-// chunk `chunk` = params [64 chunk, 64 chunk + 64), summed over the per-workgroup
-// partials in a fixed order (deterministic); writes grad, the kl / loss means and the
-// chunk's squared norm; returns the summed gradient in the g == 0 threads (0 elsewhere)
-__device__ __forceinline__ float reduce_chunk(const float *__restrict__ partials, int nblk, float *grad, float *losses,
-                                              float inv_b, int chunk, float (&red)[4][64]) {
-  const int cidx = threadIdx.x & 63, g = threadIdx.x >> 6;
-  const int p = chunk * 64 + cidx;
-  float acc = 0.f;
-  if (p < PPO_NPARAM + 5) {
-    // 32 loads in flight per thread, then added in block order (the order of the sum
-    // is b = g, g + 4, g + 8, ... whatever the batching)
-    constexpr int kB = 32;
-    for (int b0 = g; b0 < nblk; b0 += 4 * kB) {
-      float x[kB];
+// k_reduce_partials: the per-workgroup partial rows (stride NPART_PAD floats, 16-B aligned)
+// summed in a fixed order (deterministic, independent of the launch) into grad[].
+// One 512-thread workgroup per 128 consecutive entries: each half-wave loads a 512-B
+// row segment as float4s (32 lanes x 4 params), 16 row groups (wave w, half h: group
+// 2w + h takes rows g, g + 16, g + 32, ...) with all 16 loads of a lane in flight,
+// then the 16 group sums are added in group order through LDS.  Also writes the KL /
+// loss means and the chunk's squared norm (k_apply's clip norm on one rank).
+constexpr int RD_TB = 512, RD_P = 128, RD_G = 16, RD_KB = 16;
+constexpr int RED_BLOCKS = (PPO_NPARAM + 5 + RD_P - 1) / RD_P;
+static_assert(RD_G == 2 * (RD_TB / 64) && RD_P == 4 * 32, "reduce geometry");
+__global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
+                                                           float *losses, float inv_b) {
+  __shared__ float4 red[RD_G][RD_P / 4];
+  __shared__ float sq2[2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int col = lane & 31, grp = 2 * w + (lane >> 5);
+  const int p4 = blockIdx.x * (RD_P / 4) + col;                 // float4 column of the partial rows
+  const bool ok = p4 < NPART_PAD / 4;
+  const float4 *P4 = reinterpret_cast<const float4 *>(partials);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int b0 = grp; b0 < nblk; b0 += RD_G * RD_KB) {
+    float4 x[RD_KB];
 #pragma unroll
-      for (int k = 0; k < kB; ++k) x[k] = partials[(size_t)min(b0 + 4 * k, nblk - 1) * NPART + p];
+    for (int k = 0; k < RD_KB; ++k)
+      x[k] = ok ? P4[(size_t)min(b0 + RD_G * k, nblk - 1) * (NPART_PAD / 4) + p4] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int k = 0; k < kB; ++k)
-        if (b0 + 4 * k < nblk) acc += x[k];
-    }
-  }
-  red[g][cidx] = acc;
-  __syncthreads();
-  float gsum = 0.f;
-  if (g == 0) {
-    float sq = 0.f;
-    if (p < PPO_NPARAM + 5) {
-      const float sum = ((red[0][cidx] + red[1][cidx]) + red[2][cidx]) + red[3][cidx];
-      if (p < PPO_NPARAM) {
-        grad[p] = sum;
-        gsum = sum;
-        sq = sum * sum;
-      } else {
-        const int q = p - PPO_NPARAM;
-        if (q == 4) grad[PPO_NPARAM] = sum * inv_b;      // kl mean rides with the gradient (all-reduce)
-        if (losses) losses[q] = sum * inv_b;
+    for (int k = 0; k < RD_KB; ++k)
+      if (b0 + RD_G * k < nblk) {
+        acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w;
       }
-    }
-    // this chunk's share of the squared norm (single-process runs take the norm from these)
-    sq = wave_sum(sq);
-    if (cidx == 0) grad[PPO_NPARAM + 8 + chunk] = sq;
   }
-  __syncthreads();   // red[] is reused by the next chunk
-  return gsum;
-}
-
-__global__ __launch_bounds__(256) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
-                                                         float *losses, float inv_b) {
-  __shared__ float red[4][64];
-  reduce_chunk(partials, nblk, grad, losses, inv_b, blockIdx.x, red);
+  red[grp][col] = acc;
+  __syncthreads();
+  if (tid < RD_P) {
+    const int p = blockIdx.x * RD_P + tid;
+    float s = 0.f;
+#pragma unroll
+    for (int g = 0; g < RD_G; ++g) s += reinterpret_cast<const float *>(red[g])[tid];
+    float sq = 0.f;
+    if (p < PPO_NPARAM) {
+      grad[p] = s;
+      sq = s * s;
+    } else if (p < PPO_NPARAM + 5) {
+      const int q = p - PPO_NPARAM;
+      if (q == 4) grad[PPO_NPARAM] = s * inv_b;      // kl mean rides with the gradient (all-reduce)
+      if (losses) losses[q] = s * inv_b;
+    }
+    sq = wave_sum(sq);
+    if (lane == 0) sq2[w] = sq;
+  }
+  __syncthreads();
+  if (tid == 0) grad[PPO_NPARAM + 8 + blockIdx.x] = sq2[0] + sq2[1];
 }
 
 // clip_grad_norm_ + Adam + AdaptiveScheduler.  Every workgroup forms the same
-// total norm (same order), updates its 256 parameters; the last workgroup to
-// finish (completion counter in opt[7]) advances step / lr / kl / norm.
+// total norm (same order) and the same next learning rate, and updates its 256
+// parameters.  The optimiser scalars are double-buffered: the launch reads slot
+// opt_in and workgroup 0 writes the next values to slot opt_out, so no workgroup
+// waits for another (no completion counter, no device-scope fence).
 constexpr int AP_TB = 256;
-constexpr int RED_BLOCKS = (PPO_NPARAM + 5 + 63) / 64;
 template <bool kNormFromPartials>
 __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const float *__restrict__ grad_in,
-                                                 float *m, float *v, float *opt, float grad_scale, float *kl_out) {
+                                                 float *m, float *v, const float *__restrict__ opt_in,
+                                                 float *__restrict__ opt_out, float grad_scale, float *kl_out) {
   __shared__ float red[AP_TB / 64];
-  __shared__ bool last;
   const int tid = threadIdx.x;
   const int q = blockIdx.x * AP_TB + tid;
   const int qc = min(q, PPO_NPARAM - 1);
@@ -992,11 +1004,11 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   // corrections below are computed while they are in flight
   const float g_raw = grad_in[qc], p_old = P[qc], m_old = m[qc], v_old = v[qc];
   // the reduce kernel's per-chunk squares (fixed order; loaded unconditionally: no branch)
-  static_assert(RED_BLOCKS <= 2 * AP_TB, "two chunk squares per thread");
+  static_assert(RED_BLOCKS <= AP_TB, "one chunk square per thread");
   const float s0 = grad_in[PPO_NPARAM + 8 + min(tid, RED_BLOCKS - 1)];
-  const float s1 = grad_in[PPO_NPARAM + 8 + min(tid + AP_TB, RED_BLOCKS - 1)];
-  const float lr = opt[0];
-  const float step = opt[1] + 1.0f;
+  const float lr = opt_in[0];
+  const float step = opt_in[1] + 1.0f;
+  const float kl = grad_in[PPO_NPARAM] * grad_scale;
   __builtin_amdgcn_sched_barrier(0);   // the loads above issue first
   // torch.optim.Adam forms the bias corrections in Python doubles
   const double bc1 = 1.0 - pow((double)c.adam_b1, (double)step);
@@ -1008,7 +1020,7 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   __asm__ volatile("" : : "v"(step_size), "v"(bc2s));
   float ss = 0.f;
   if (kNormFromPartials) {
-    ss = (tid < RED_BLOCKS ? s0 : 0.f) + (tid + AP_TB < RED_BLOCKS ? s1 : 0.f);
+    ss = tid < RED_BLOCKS ? s0 : 0.f;
   } else {
     // total norm of the (all-reduced) gradient: 16-byte aligned, checked on the host
     constexpr int N4 = PPO_NPARAM / 4, U = (N4 + AP_TB - 1) / AP_TB;
@@ -1048,28 +1060,21 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
     m[q] = mi;
     v[q] = vi;
   }
-  __syncthreads();
-  if (tid == 0) {
-    __threadfence();
-    unsigned *cnt = reinterpret_cast<unsigned *>(opt + 7);
-    last = atomicAdd(cnt, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && tid == 0) {
-    opt[1] = step;
-    opt[3] = total_norm;
+  if (blockIdx.x == 0 && tid == 0) {
     // AdaptiveScheduler.update on this minibatch's KL (schedulers.py:26-32)
+    float nl = lr, kl_keep = opt_in[2];
     if (c.lr_adaptive) {
-      const float kl = grad_in[PPO_NPARAM] * grad_scale;
-      float nl = lr;
       if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
       if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
-      opt[0] = nl;
-      opt[2] = kl;
+      kl_keep = kl;
       if (kl_out) *kl_out = kl;
     }
-    __threadfence();
-    atomicExch(reinterpret_cast<unsigned *>(opt + 7), 0u);
+    opt_out[0] = nl;
+    opt_out[1] = step;
+    opt_out[2] = kl_keep;
+    opt_out[3] = total_norm;
+#pragma unroll
+    for (int i = 4; i < 8; ++i) opt_out[i] = opt_in[i];
   }
 }
 
@@ -1147,6 +1152,7 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
   (void)val_rms;
   if (!cfg || !params || !grad || !partials || !work) return 1;
   if (cfg->minibatch % RB != 0) return 2;
+  if (reinterpret_cast<uintptr_t>(params) & 15u) return 4;   // 16-byte weight staging loads
   hipStream_t s = (hipStream_t)stream;
   const int row0 = mb_index * cfg->minibatch;
   if (update_obs_rms && cfg->normalize_input) {
@@ -1161,23 +1167,26 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
   hipLaunchKernelGGL(k_mb_grad, dim3(nblk), dim3(GTB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
                      exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_reduce_partials, dim3((PPO_NPARAM + 5 + 63) / 64), dim3(256), 0, s, partials, nblk, grad, losses,
+  if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
+  hipLaunchKernelGGL(k_reduce_partials, dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad, losses,
                      1.0f / (float)cfg->minibatch);
   USV_CHECK_LAUNCH();
   return 0;
 }
 
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m, float *adam_v, float *opt,
-                        float grad_scale, float *kl_out, int norm_from_partials, void *stream) {
+                        int opt_slot, float grad_scale, float *kl_out, int norm_from_partials, void *stream) {
   if (!cfg || !params || !grad || !adam_m || !adam_v || !opt) return 1;
   if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
+  if (opt_slot != 0 && opt_slot != 1) return 3;
   hipLaunchKernelGGL(norm_from_partials ? k_apply<true> : k_apply<false>, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB),
-                     dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params, grad, adam_m, adam_v, opt, grad_scale, kl_out);
+                     dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params, grad, adam_m, adam_v, opt + 8 * opt_slot,
+                     opt + 8 * (1 - opt_slot), grad_scale, kl_out);
   USV_CHECK_LAUNCH();
   return 0;
 }
 
-int ppo_partials_floats(int minibatch) { return (minibatch / RB) * NPART; }
+int ppo_partials_floats(int minibatch) { return (minibatch / RB) * NPART_PAD; }
 int ppo_grad_floats(void) { return PPO_NPARAM + 8 + RED_BLOCKS; }
 int ppo_meter_floats(int n_envs, int horizon) {
   return horizon * 4 + horizon * ((n_envs + kStoreTB - 1) / kStoreTB) * 4;

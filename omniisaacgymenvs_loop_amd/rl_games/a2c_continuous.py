@@ -239,7 +239,8 @@ class A2CAgent:
             dist_util.broadcast_params(self.model_params, 0)   # a2c_common.py:1354 (initial weights from rank 0)
         self.adam_m = torch.zeros(NPARAM, **f32)
         self.adam_v = torch.zeros(NPARAM, **f32)
-        self.opt = torch.zeros(8, **f32)
+        # optimiser scalars, two slots (lr, step, kl, norm): minibatch k reads slot k % 2 and writes the other
+        self.opt = torch.zeros(16, **f32)
         self.opt[0] = self.last_lr
         self.obs_rms = torch.zeros(2 * NIN + 1, **f64)
         self.obs_rms[NIN:2 * NIN] = 1.0
@@ -335,9 +336,11 @@ class A2CAgent:
                 c.call("ppo_minibatch_grad", *args, s)
                 scale = self._allreduce_grad()
                 c.call("ppo_minibatch_apply", cfg, c.ptr(self.model_params), c.ptr(self.grad),
-                       c.ptr(self.adam_m), c.ptr(self.adam_v), c.ptr(self.opt), float(scale),
+                       c.ptr(self.adam_m), c.ptr(self.adam_v), c.ptr(self.opt), k % 2, float(scale),
                        c.ptr(self.kls[k:k + 1]), int(not dp), s)
                 k += 1
+        if k % 2:   # the last minibatch wrote slot 1: the epoch ends with the state in slot 0
+            self.opt[:8].copy_(self.opt[8:])
 
     def _update_capturable(self) -> bool:
         """The minibatch update goes into a HIP graph on one GPU and, with several ranks, when the
