@@ -37,6 +37,7 @@ constexpr int P_LOSS = PPO_NPARAM;      // a, c, entropy, b, kl sums
 constexpr float kLog2Pi = 1.8378770664093453f;  // 0.5*log(2*pi)*2 (models.py:400)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
@@ -566,6 +567,36 @@ struct GradSmem {
   float tail[TAIL + 1];
 };
 
+// Partial-gradient slot layout (a permutation of the parameters, then the loss sums): the
+// matrix-core accumulators of dW2 and dW1[:, :32] are stored in their register order, so each
+// lane writes 4 consecutive values of one tile with one 16-byte store ([tile][a][lane][4],
+// value r = 4a + r4 of the lane's 16); the remaining parameters follow in parameter order
+// (sigma, b1, b2..bmu, the last W1 column).  k_reduce_partials maps slots back to parameters.
+constexpr int S_W2 = 0, S_W1 = NH * NH, S_SIG = S_W1 + NH * 32, S_B1 = S_SIG + 2, S_TAIL = S_B1 + NH,
+              S_W1C = S_TAIL + TAIL, S_END = S_W1C + NH;
+static_assert(S_END == PPO_NPARAM && S_W1 % 4 == 0 && NIN == 33, "partial slot layout");
+__device__ __forceinline__ int tail_slot(int param) { return S_TAIL + param - PPO_OFF_B2; }
+// tile t of a 32x32 accumulator: slot of the lane's values 4a..4a+3
+__device__ __forceinline__ int acc_slot(int base, int tile, int a, int lane) { return base + ((tile * 4 + a) * 64 + lane) * 4; }
+// parameter index of a partial slot (-1: a loss sum)
+__device__ __forceinline__ int param_of_slot(int s) {
+  if (s < S_W1) {             // W2 tiles: tile = 4 cb + k block
+    const int tile = s >> 10, a = (s >> 8) & 3, lane = (s >> 2) & 63, q = 4 * a + (s & 3);
+    const int n = 32 * (tile >> 2) + crow(q, lane >> 5), k = 32 * (tile & 3) + (lane & 31);
+    return PPO_OFF_W2 + n * NH + k;
+  }
+  if (s < S_SIG) {            // W1[:, :32] tiles: tile = cb
+    const int t = s - S_W1, tile = t >> 10, a = (t >> 8) & 3, lane = (t >> 2) & 63, q = 4 * a + (t & 3);
+    const int n = 32 * tile + crow(q, lane >> 5), k = lane & 31;
+    return PPO_OFF_W1 + n * NIN + k;
+  }
+  if (s < S_B1) return PPO_OFF_SIGMA + (s - S_SIG);
+  if (s < S_TAIL) return PPO_OFF_B1 + (s - S_B1);
+  if (s < S_W1C) return PPO_OFF_B2 + (s - S_TAIL);
+  if (s < S_END) return PPO_OFF_W1 + (s - S_W1C) * NIN + (NIN - 1);
+  return -1;
+}
+
 // per-row inputs of the losses (wave 0: lane = row), loaded with the weights
 struct RowIn {
   float act0, act1, nlp, val, ret, adv, mu0, mu1, sg0, sg1;
@@ -578,6 +609,11 @@ struct PartOut {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ void operator()(int idx, float v) const {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (uint32_t)idx * 4u, 0, 16);
+  }
+  __device__ __forceinline__ void x4(int idx, float a, float b, float c, float d) const {
+    const u32x4_t v = {__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c),
+                       __builtin_bit_cast(uint32_t, d)};
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)idx * 4u, 0, 16);
   }
 };
 
@@ -812,7 +848,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
     if (tid == 0) {
       part_st(P_LOSS + 0, la); part_st(P_LOSS + 1, lc); part_st(P_LOSS + 2, le); part_st(P_LOSS + 3, lb);
       part_st(P_LOSS + 4, lkl);
-      part_st(PPO_OFF_SIGMA, gs0); part_st(PPO_OFF_SIGMA + 1, gs1);
+      part_st(S_SIG, gs0); part_st(S_SIG + 1, gs1);
     }
   }
   __syncthreads();
@@ -837,15 +873,15 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   __syncthreads();
   if (tid < NH) {
     const int j = tid;
-    part_st(PPO_OFF_WMU + j, ((s.hg[0][0][j] + s.hg[1][0][j]) + s.hg[2][0][j]) + s.hg[3][0][j]);
-    part_st(PPO_OFF_WMU + NH + j, ((s.hg[0][1][j] + s.hg[1][1][j]) + s.hg[2][1][j]) + s.hg[3][1][j]);
-    part_st(PPO_OFF_WV + j, ((s.hg[0][2][j] + s.hg[1][2][j]) + s.hg[2][2][j]) + s.hg[3][2][j]);
-    part_st(PPO_OFF_B2 + j, ((s.hg[0][3][j] + s.hg[1][3][j]) + s.hg[2][3][j]) + s.hg[3][3][j]);
+    part_st(tail_slot(PPO_OFF_WMU + j), ((s.hg[0][0][j] + s.hg[1][0][j]) + s.hg[2][0][j]) + s.hg[3][0][j]);
+    part_st(tail_slot(PPO_OFF_WMU + NH + j), ((s.hg[0][1][j] + s.hg[1][1][j]) + s.hg[2][1][j]) + s.hg[3][1][j]);
+    part_st(tail_slot(PPO_OFF_WV + j), ((s.hg[0][2][j] + s.hg[1][2][j]) + s.hg[2][2][j]) + s.hg[3][2][j]);
+    part_st(tail_slot(PPO_OFF_B2 + j), ((s.hg[0][3][j] + s.hg[1][3][j]) + s.hg[2][3][j]) + s.hg[3][3][j]);
   } else if (tid < NH + 3) {
     const int q = tid - NH;
     float sacc = 0.f;
     for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
-    part_st(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV, sacc);
+    part_st(tail_slot(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV), sacc);
   }
   USV_PHASE(ppo, 4);
   // ---- dW2[n][k] = sum_r dz2[r][n] h1[r][k]: wave (kh, cb) owns n block cb, k blocks 2 kh, 2 kh + 1 ----
@@ -870,8 +906,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
     for (int st = 0; st < NH / 4; ++st) {
       const int j = 64 * kh + 2 * st + h;
       dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + n0 + i], dh);
-      const int kt = st >> 4, q = st & 15;
-      part_st(PPO_OFF_W2 + (n0 + crow(q, h)) * NH + 32 * (2 * kh + kt) + i, acc[kt][q]);
+      if ((st & 3) == 0) {   // one 16-byte store of the lane's dW2 values every 4 steps
+        const int kt = st >> 4, a = (st >> 2) & 3;
+        part_st.x4(acc_slot(S_W2, 4 * cb + 2 * kh + kt, a, lane), acc[kt][4 * a], acc[kt][4 * a + 1],
+                   acc[kt][4 * a + 2], acc[kt][4 * a + 3]);
+      }
     }
     USV_PHASE(ppo, 6);
     if (kh == 0) {
@@ -903,19 +942,20 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
       acc = mfma32(s.h1[r * HS + n0 + i], s.x[r * XS + i], acc);
     }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) part_st(PPO_OFF_W1 + (n0 + crow(q, h)) * NIN + i, acc[q]);
+    for (int a = 0; a < 4; ++a)
+      part_st.x4(acc_slot(S_W1, cb, a, lane), acc[4 * a], acc[4 * a + 1], acc[4 * a + 2], acc[4 * a + 3]);
   } else {
     const int t = tid - 256;
     if (t < NH) {
       const int j = t;
       float a = 0.f;
       for (int r = 0; r < RB; ++r) a = fmaf(s.h1[r * HS + j], s.x[r * XS + NIN - 1], a);
-      part_st(PPO_OFF_W1 + j * NIN + NIN - 1, a);
+      part_st(S_W1C + j, a);
     } else {
       const int j = t - NH;
       float a = 0.f;
       for (int r = 0; r < RB; ++r) a += s.h1[r * HS + j];
-      part_st(PPO_OFF_B1 + j, a);
+      part_st(S_B1 + j, a);
     }
   }
   USV_PHASE(ppo, 8);
@@ -933,7 +973,8 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__
 
 // k_reduce_partials: the per-workgroup partial rows (stride NPART_PAD floats, 16-B aligned)
 // summed in a fixed order (deterministic, independent of the launch) into grad[].
-// One 512-thread workgroup per 128 consecutive entries: each half-wave loads a 512-B
+// One 512-thread workgroup per 128 consecutive slots (param_of_slot maps them back to the
+// parameter order of grad[]): each half-wave loads a 512-B
 // row segment as float4s (32 lanes x 4 params), 16 row groups (wave w, half h: group
 // 2w + h takes rows g, g + 16, g + 32, ...) with all 16 loads of a lane in flight,
 // then the 16 group sums are added in group order through LDS.  Also writes the KL /
@@ -965,16 +1006,16 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
   red[grp][col] = acc;
   __syncthreads();
   if (tid < RD_P) {
-    const int p = blockIdx.x * RD_P + tid;
+    const int slot = blockIdx.x * RD_P + tid;
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < RD_G; ++g) s += reinterpret_cast<const float *>(red[g])[tid];
     float sq = 0.f;
-    if (p < PPO_NPARAM) {
-      grad[p] = s;
+    if (slot < S_END) {
+      grad[param_of_slot(slot)] = s;
       sq = s * s;
-    } else if (p < PPO_NPARAM + 5) {
-      const int q = p - PPO_NPARAM;
+    } else if (slot < PPO_NPARAM + 5) {
+      const int q = slot - PPO_NPARAM;
       if (q == 4) grad[PPO_NPARAM] = s * inv_b;      // kl mean rides with the gradient (all-reduce)
       if (losses) losses[q] = s * inv_b;
     }
