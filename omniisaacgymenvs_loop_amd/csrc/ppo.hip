@@ -722,34 +722,28 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   }
   __syncthreads();
   USV_PHASE(ppo, 10);
-  // ---- layer 2: h2 = tanh(h1 W2^T + b2); wave (kh, cb) sums k in [64 kh, 64 kh + 64) ----
+  // ---- layer 2: h2 = tanh(h1 W2^T + b2); wave (kh, cb) sums k in [64 kh, 64 kh + 64).  The K-half
+  // kh = 1 wave feeds its A-operand rows rotated by 16 (ra), so in BOTH waves of a pair the rows it
+  // finishes sit in accumulator registers 0-7 and the rows it hands over in 8-15: every register
+  // index is a constant (no per-wave select, no dynamic register indexing) ----
+  const int ra = (i + 16 * kh) & (RB - 1);
   {
     f32x16 acc = {};
 #pragma unroll 16
     for (int st = 0; st < NH / 4; ++st) {
       const int k = 64 * kh + 2 * st + h;
-      acc = mfma32(s.h1[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
+      acc = mfma32(s.h1[ra * HS + k], s.w2[(n0 + i) * HS + k], acc);
     }
     USV_PHASE(ppo, 11);
-    // the two K halves meet in LDS: each wave of the pair finishes 8 of the 16 accumulator rows,
-    // always as (lower half + upper half) + bias
-    // (kh is wave-uniform: both branches index the accumulator with constants)
-    if (kh == 0) {
+    // the two K halves meet in LDS as (lower half + upper half) + bias (fp32 addition commutes,
+    // so own + other is that sum in both waves)
 #pragma unroll
-      for (int r = 8; r < 16; ++r) s.xch[cb][r][lane] = acc[r];
-    } else {
-#pragma unroll
-      for (int r = 0; r < 8; ++r) s.xch[cb][r][lane] = acc[r];
-    }
+    for (int q = 0; q < 8; ++q) s.xch[cb][8 * kh + q][lane] = acc[8 + q];
     __syncthreads();
     const float bj = s.tail[T_B2 + n0 + i];
-    if (kh == 0) {
 #pragma unroll
-      for (int r = 0; r < 8; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh((acc[r] + s.xch[cb][r][lane]) + bj);
-    } else {
-#pragma unroll
-      for (int r = 8; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh((s.xch[cb][r][lane] + acc[r]) + bj);
-    }
+    for (int q = 0; q < 8; ++q)
+      s.h2[(crow(q, h) + 16 * kh) * HS + n0 + i] = fast_tanh((acc[q] + s.xch[cb][8 - 8 * kh + q][lane]) + bj);
   }
   __syncthreads();
   USV_PHASE(ppo, 12);
@@ -884,50 +878,52 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
     part_st(tail_slot(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV), sacc);
   }
   USV_PHASE(ppo, 4);
-  // ---- dW2[n][k] = sum_r dz2[r][n] h1[r][k]: wave (kh, cb) owns n block cb, k blocks 2 kh, 2 kh + 1 ----
-  f32x16 acc[2] = {};
-  {
-#pragma unroll 4
-    for (int st = 0; st < RB / 2; ++st) {
-      const int r = st + (RB / 2) * h;
-      const float a = s.h2[r * HS + n0 + i];
+  // ---- dW2[n][k] = sum_r dz2[r][n] h1[r][k]: wave (kh, cb) owns n block cb, k blocks 2 kh, 2 kh + 1.
+  // The dW2 partial (64 KB per workgroup) is bound by the chip's write bandwidth, so its 16-byte
+  // stores are spread over the matrix-core chains that follow (the k block 2 kh tile's during the
+  // second tile's chain, the second tile's during dh1); sched_barrier keeps them there ----
+  const int tile0 = 4 * cb + 2 * kh;
+  f32x16 dw0 = {}, dw1 = {};
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) acc[kt] = mfma32(a, s.h1[r * HS + 32 * (2 * kh + kt) + i], acc[kt]);
-    }
-    USV_PHASE(ppo, 13);
+  for (int st = 0; st < RB / 2; ++st) {
+    const int r = st + (RB / 2) * h;
+    dw0 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh) + i], dw0);
   }
+#pragma unroll
+  for (int st = 0; st < RB / 2; ++st) {
+    const int r = st + (RB / 2) * h;
+    dw1 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh + 1) + i], dw1);
+    if ((st & 3) == 1) {
+      const int a = st >> 2;
+      part_st.x4(acc_slot(S_W2, tile0, a, lane), dw0[4 * a], dw0[4 * a + 1], dw0[4 * a + 2], dw0[4 * a + 3]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  USV_PHASE(ppo, 13);
   USV_PHASE(ppo, 5);
-  // ---- dh1[r][k] = sum_n dz2[r][n] W2[n][k]: wave (kh, cb) owns columns k in block cb, n in half kh.
-  // The dW2 partial (32 stores per lane, memory-bandwidth bound) is stored one value per step of
-  // this chain, so the stores drain under the matrix-core work instead of stalling the issue ----
+  // ---- dh1[r][k] = sum_n dz2[r][n] W2[n][k]: wave (kh, cb) owns columns k in block cb, n in half kh
+  // (A-operand rows rotated as in layer 2) ----
   {
     f32x16 dh = {};
 #pragma unroll
     for (int st = 0; st < NH / 4; ++st) {
       const int j = 64 * kh + 2 * st + h;
-      dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + n0 + i], dh);
-      if ((st & 3) == 0) {   // one 16-byte store of the lane's dW2 values every 4 steps
-        const int kt = st >> 4, a = (st >> 2) & 3;
-        part_st.x4(acc_slot(S_W2, 4 * cb + 2 * kh + kt, a, lane), acc[kt][4 * a], acc[kt][4 * a + 1],
-                   acc[kt][4 * a + 2], acc[kt][4 * a + 3]);
+      dh = mfma32(s.h2[ra * HS + j], s.w2[j * HS + n0 + i], dh);
+      if ((st & 3) == 1 && st < 16) {
+        const int a = st >> 2;
+        part_st.x4(acc_slot(S_W2, tile0 + 1, a, lane), dw1[4 * a], dw1[4 * a + 1], dw1[4 * a + 2], dw1[4 * a + 3]);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     USV_PHASE(ppo, 6);
-    if (kh == 0) {
 #pragma unroll
-      for (int q = 8; q < 16; ++q) s.xch[cb][q][lane] = dh[q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) s.xch[cb][q][lane] = dh[q];
-    }
+    for (int q = 0; q < 8; ++q) s.xch[cb][8 * kh + q][lane] = dh[8 + q];
     __syncthreads();   // every read of h1 (dW2 operand) is done; the halves are published
-    const int q0 = 8 * kh;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      const int idx = crow(q0 + q, h) * HS + n0 + i;
+      const int idx = (crow(q, h) + 16 * kh) * HS + n0 + i;
       const float hv = s.h1[idx];
-      const float lo_hi = kh == 0 ? dh[q] + s.xch[cb][q][lane] : s.xch[cb][8 + q][lane] + dh[8 + q];
-      s.h1[idx] = lo_hi * (1.f - hv * hv);   // h1 := dz1
+      s.h1[idx] = (dh[q] + s.xch[cb][8 - 8 * kh + q][lane]) * (1.f - hv * hv);   // h1 := dz1
     }
   }
   __syncthreads();
