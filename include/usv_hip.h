@@ -352,6 +352,31 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
  * and the thruster lever arms.  out: [n][3] body X, Y, N. */
 int usv_forces(const usv_cfg_t *cfg, const usv_bufs_t *b, float *out, void *stream);
 
+/* Hydrostatics constants (task yaml dynamics.hydrostatics + sim.gravity), USV_Virtual.py:441-456,
+ * 724-736: metacentric width / length = box_width / 2, box_length / 2; max_volume =
+ * box_width * box_length * (heron_zero_height + 20). */
+typedef struct usv_hydro {
+  float water_density;
+  float gravity;              /* sim.gravity[2] (-9.81) */
+  float metacentric_width;
+  float metacentric_length;
+  float avg_force;            /* average_hydrostatics_force_value (275) */
+  float amplify_torque;
+  float waterplane_area;
+  float zero_height;          /* heron_zero_height */
+  float max_volume;
+} usv_hydro_t;
+
+/* 6-DoF hydrostatic wrench of the hull (buoyancy + metacentric restoring torques), body frame:
+ * submerged volume from the root height (USVVirtual.update_state, USV_Virtual.py:791-798), euler
+ * angles (get_euler_angles :815-835), HydrostaticsObject.compute_archimedes_metacentric_local
+ * (Hydrostatics.py:63-133; force rotated by R^T, torque not rotated, x amplify_torque).
+ * quat [n][4] (w, x, y, z), root_z [n] -> volume [n], euler [n][3], wrench [n][6].
+ * On the planar model (roll = pitch = 0) the surge, sway and yaw components are exactly 0, which is
+ * why usv_env_step does not add them (tests/test_env_gpu.py::test_hydrostatics_vs_reference). */
+int usv_hydrostatics(const usv_hydro_t *h, int n, const float *quat, const float *root_z, float *volume,
+                     float *euler, float *wrench, void *stream);
+
 /* ------------------------------------------------------------------------ */
 /* PPO entry points (rl_games a2c_continuous / a2c_common)                   */
 /* ------------------------------------------------------------------------ */

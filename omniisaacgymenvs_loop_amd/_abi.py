@@ -84,6 +84,10 @@ class UsvBufs(ctypes.Structure):
     _fields_ = _struct_fields(_TXT, "usv_bufs", DEFINES)
 
 
+class UsvHydro(ctypes.Structure):
+    _fields_ = _struct_fields(_TXT, "usv_hydro", DEFINES)
+
+
 class PpoCfg(ctypes.Structure):
     _fields_ = _struct_fields(_TXT, "ppo_cfg", DEFINES)
 

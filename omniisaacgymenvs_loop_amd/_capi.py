@@ -55,6 +55,7 @@ def _declare(lib):
         "usv_env_step": [P, P, P, P, F, U64, U64, P, P],
         "usv_env_step_part": [P, P, P, P, F, U64, U64, P, I, P],
         "usv_forces": [P, P, P, P],
+        "usv_hydrostatics": [P, I, P, P, P, P, P, P],
         "ppo_policy_step": [P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, U64, U64, P, P, P],
         "ppo_value": [P, P, P, P, P, P, P],
         "ppo_store_reward": [P, P, P, I, P, P, P, P, P, P, P],

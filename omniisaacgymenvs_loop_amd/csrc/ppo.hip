@@ -975,16 +975,22 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__
 // 2w + h takes rows g, g + 16, g + 32, ...) with all 16 loads of a lane in flight,
 // then the 16 group sums are added in group order through LDS.  Also writes the KL /
 // loss means and the chunk's squared norm (k_apply's clip norm on one rank).
-constexpr int RD_TB = 512, RD_P = 128, RD_G = 16, RD_KB = 16;
+#ifndef USV_RD_P
+#define USV_RD_P 128
+#endif
+constexpr int RD_TB = 512, RD_P = USV_RD_P;            // threads, slots per workgroup
+constexpr int RD_L = RD_P / 4;                          // lanes per row segment (float4 each)
+constexpr int RD_G = (RD_TB / RD_L);                    // row groups
+constexpr int RD_KB = 16;                               // loads in flight per lane
 constexpr int RED_BLOCKS = (PPO_NPARAM + 5 + RD_P - 1) / RD_P;
-static_assert(RD_G == 2 * (RD_TB / 64) && RD_P == 4 * 32, "reduce geometry");
+static_assert(RD_P % 4 == 0 && 64 % RD_L == 0 && RD_P <= RD_TB, "reduce geometry");
 __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
                                                            float *losses, float inv_b) {
-  __shared__ float4 red[RD_G][RD_P / 4];
-  __shared__ float sq2[2];
+  __shared__ float4 red[RD_G][RD_L];
+  __shared__ float sqw[RD_TB / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int col = lane & 31, grp = 2 * w + (lane >> 5);
-  const int p4 = blockIdx.x * (RD_P / 4) + col;                 // float4 column of the partial rows
+  const int col = tid % RD_L, grp = tid / RD_L;
+  const int p4 = blockIdx.x * RD_L + col;                 // float4 column of the partial rows
   const bool ok = p4 < NPART_PAD / 4;
   const float4 *P4 = reinterpret_cast<const float4 *>(partials);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -992,21 +998,21 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     float4 x[RD_KB];
 #pragma unroll
     for (int k = 0; k < RD_KB; ++k)
-      x[k] = ok ? P4[(size_t)min(b0 + RD_G * k, nblk - 1) * (NPART_PAD / 4) + p4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[k] = (ok && b0 + RD_G * k < nblk) ? P4[(size_t)(b0 + RD_G * k) * (NPART_PAD / 4) + p4]
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int k = 0; k < RD_KB; ++k)
-      if (b0 + RD_G * k < nblk) {
-        acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w;
-      }
+    for (int k = 0; k < RD_KB; ++k) {
+      acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w;
+    }
   }
   red[grp][col] = acc;
   __syncthreads();
+  float sq = 0.f;
   if (tid < RD_P) {
     const int slot = blockIdx.x * RD_P + tid;
     float s = 0.f;
 #pragma unroll
     for (int g = 0; g < RD_G; ++g) s += reinterpret_cast<const float *>(red[g])[tid];
-    float sq = 0.f;
     if (slot < S_END) {
       grad[param_of_slot(slot)] = s;
       sq = s * s;
@@ -1015,11 +1021,18 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
       if (q == 4) grad[PPO_NPARAM] = s * inv_b;      // kl mean rides with the gradient (all-reduce)
       if (losses) losses[q] = s * inv_b;
     }
+  }
+  if (w < (RD_P + 63) / 64) {
     sq = wave_sum(sq);
-    if (lane == 0) sq2[w] = sq;
+    if (lane == 0) sqw[w] = sq;
   }
   __syncthreads();
-  if (tid == 0) grad[PPO_NPARAM + 8 + blockIdx.x] = sq2[0] + sq2[1];
+  if (tid == 0) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < (RD_P + 63) / 64; ++q) t += sqw[q];
+    grad[PPO_NPARAM + 8 + blockIdx.x] = t;
+  }
 }
 
 // clip_grad_norm_ + Adam + AdaptiveScheduler.  Every workgroup forms the same
@@ -1041,8 +1054,9 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   // corrections below are computed while they are in flight
   const float g_raw = grad_in[qc], p_old = P[qc], m_old = m[qc], v_old = v[qc];
   // the reduce kernel's per-chunk squares (fixed order; loaded unconditionally: no branch)
-  static_assert(RED_BLOCKS <= AP_TB, "one chunk square per thread");
+  static_assert(RED_BLOCKS <= 2 * AP_TB, "two chunk squares per thread");
   const float s0 = grad_in[PPO_NPARAM + 8 + min(tid, RED_BLOCKS - 1)];
+  const float s1 = grad_in[PPO_NPARAM + 8 + min(tid + AP_TB, RED_BLOCKS - 1)];
   const float lr = opt_in[0];
   const float step = opt_in[1] + 1.0f;
   const float kl = grad_in[PPO_NPARAM] * grad_scale;
@@ -1057,7 +1071,7 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   __asm__ volatile("" : : "v"(step_size), "v"(bc2s));
   float ss = 0.f;
   if (kNormFromPartials) {
-    ss = tid < RED_BLOCKS ? s0 : 0.f;
+    ss = (tid < RED_BLOCKS ? s0 : 0.f) + (tid + AP_TB < RED_BLOCKS ? s1 : 0.f);
   } else {
     // total norm of the (all-reduced) gradient: 16-byte aligned, checked on the host
     constexpr int N4 = PPO_NPARAM / 4, U = (N4 + AP_TB - 1) / AP_TB;

@@ -1319,6 +1319,43 @@ __global__ __launch_bounds__(kBlock) void k_track_finish(usv_cfg_t c, usv_bufs_t
 }
 
 // planar forces only (parity with Hydrodynamics.ComputeHydrodynamicsEffects)
+// Hydrostatic wrench (usv_hydrostatics): one thread per env, the reference's operation order.
+__global__ void k_hydrostatics(usv_hydro_t h, int n, const float *__restrict__ quat, const float *__restrict__ root_z,
+                               float *__restrict__ volume, float *__restrict__ euler, float *__restrict__ wrench) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const float4 q = reinterpret_cast<const float4 *>(quat)[e];
+  const float w = q.x, x = q.y, y = q.z, z = q.w;
+  // USVVirtual.update_state (USV_Virtual.py:791-798)
+  const float high = clampt(h.zero_height - root_z[e], 0.f, h.zero_height + 20.0f);
+  const float vol = clampt(high * h.waterplane_area, 0.f, h.max_volume);
+  // get_euler_angles (:815-835): the rotation-matrix entries as the reference forms them
+  const float r00 = 1.0f - 2.0f * (y * y) - 2.0f * (z * z);
+  const float r10 = 2.0f * x * y + 2.0f * w * z;
+  const float r20 = 2.0f * x * z - 2.0f * w * y;
+  const float r21 = 2.0f * y * z + 2.0f * w * x;
+  const float r22 = 1.0f - 2.0f * (x * x) - 2.0f * (y * y);
+  const float roll = atan2f(r21, r22), pitch = asinf(-r20), yaw = atan2f(r10, r00);
+  // compute_archimedes_metacentric_global (Hydrostatics.py:63-98); the Python scalars fold first
+  const float fz = (-h.water_density * h.gravity) * vol;
+  const float tx = (-1.0f * h.metacentric_width) * (sinf(roll) * h.avg_force);
+  const float ty = (-1.0f * h.metacentric_length) * (sinf(pitch) * h.avg_force);
+  // _local (:100-133): R = quaternion_to_matrix(q) (pytorch3d, real first); F_local = R^T (0, 0, fz)
+  const float two_s = 2.0f / (((w * w + x * x) + y * y) + z * z);
+  const float R20 = two_s * (x * z - y * w), R21 = two_s * (y * z + x * w), R22 = 1.0f - two_s * (x * x + y * y);
+  float *out = wrench + (size_t)e * 6;
+  out[0] = R20 * fz;
+  out[1] = R21 * fz;
+  out[2] = R22 * fz;
+  out[3] = tx * h.amplify_torque;   // torque not rotated (:123)
+  out[4] = ty * h.amplify_torque;
+  out[5] = 0.0f * h.amplify_torque;
+  volume[e] = vol;
+  euler[(size_t)e * 3 + 0] = roll;
+  euler[(size_t)e * 3 + 1] = pitch;
+  euler[(size_t)e * 3 + 2] = yaw;
+}
+
 __global__ void k_forces(usv_cfg_t c, usv_bufs_t b, float *__restrict__ out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = b.n;
@@ -1552,6 +1589,15 @@ int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions
 int usv_forces(const usv_cfg_t *cfg, const usv_bufs_t *b, float *out, void *stream) {
   if (!cfg || !b || !out || b->n <= 0) return 1;
   hipLaunchKernelGGL(k_forces, dim3((b->n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *cfg, *b, out);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int usv_hydrostatics(const usv_hydro_t *h, int n, const float *quat, const float *root_z, float *volume,
+                     float *euler, float *wrench, void *stream) {
+  if (!h || !quat || !root_z || !volume || !euler || !wrench || n <= 0) return 1;
+  hipLaunchKernelGGL(k_hydrostatics, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, *h, n, quat, root_z,
+                     volume, euler, wrench);
   USV_CHECK_LAUNCH();
   return 0;
 }

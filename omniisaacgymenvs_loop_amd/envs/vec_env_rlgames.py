@@ -54,6 +54,14 @@ class VecEnvRLGames:
         obs_dict, _, _, _ = self.step(actions)
         return obs_dict
 
+    def check_errors(self) -> None:
+        """Raise the errors the device path flags instead of raising mid-step (a host sync; called
+        by the trainer after each epoch, outside graph capture): scene replay past its last scene
+        with cycle off -> IndexError, as USV_Virtual.py:1386-1390."""
+        chk = getattr(self._task, "check_scene_replay", None)
+        if chk is not None:
+            chk()
+
     def advance_host_clock(self, steps: int) -> None:
         """A captured rollout graph was replayed: the device step clock advanced by `steps`."""
         self._task.advance_host_clock(steps)

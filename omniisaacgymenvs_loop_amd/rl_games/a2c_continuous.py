@@ -407,6 +407,9 @@ class A2CAgent:
             self.update_epoch_minibatches()
         torch.cuda.current_stream().synchronize()
         update_time_end = time.time()
+        chk = getattr(self.vec_env, "check_errors", None)   # device-flagged env errors (scene replay)
+        if chk is not None:
+            chk()
         self._eager_epochs += 1
         self._replay_meters()
         self.last_lr = float(self.opt[0].item())

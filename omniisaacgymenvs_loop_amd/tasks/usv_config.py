@@ -20,7 +20,7 @@ from typing import Any, Dict
 
 import numpy as np
 
-from .._abi import PEN, UsvCfg
+from .._abi import PEN, UsvCfg, UsvHydro
 
 # heron.usd rigid-body constants (decoded offline)
 HERON_THRUSTER_Y = 0.37765
@@ -376,6 +376,22 @@ def _pose_task_cfg(c: UsvCfg, name: str, env: Dict[str, Any]) -> Dict[str, Any]:
         c.tk_goal_rand[1] = tp["goal_random_angular_velocity"]
         tp.setdefault("position_tolerance", 0.0)   # read by the common parser, unused by this task
     return tp
+
+
+def build_hydro_cfg(task_cfg: Dict[str, Any]) -> UsvHydro:
+    """dynamics.hydrostatics + sim.gravity as USVVirtual reads them (USV_Virtual.py:441-456, 724-736)."""
+    hs = task_cfg["dynamics"]["hydrostatics"]
+    h = UsvHydro()
+    h.water_density = float(hs["water_density"])
+    h.gravity = float(task_cfg.get("sim", {}).get("gravity", [0.0, 0.0, -9.81])[2])
+    h.metacentric_width = float(hs["box_width"]) / 2
+    h.metacentric_length = float(hs["box_length"]) / 2
+    h.avg_force = float(hs["average_hydrostatics_force_value"])
+    h.amplify_torque = float(hs["amplify_torque"])
+    h.waterplane_area = float(hs["waterplane_area"])
+    h.zero_height = float(hs["heron_zero_height"])
+    h.max_volume = float(hs["box_width"]) * float(hs["box_length"]) * (float(hs["heron_zero_height"]) + 20)
+    return h
 
 
 def stat_names(c: UsvCfg):

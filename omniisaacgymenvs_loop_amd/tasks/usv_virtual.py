@@ -21,7 +21,8 @@ import torch
 from .. import _capi
 from .._abi import DEFINES, UsvBufs, enum_values
 from ..utils.spaces import Box, DictSpace
-from .usv_config import action_bias_cfg, build_usv_cfg, env_origins, has_disturbance, stat_names, thruster_tables
+from .usv_config import (action_bias_cfg, build_hydro_cfg, build_usv_cfg, env_origins, has_disturbance, stat_names,
+                         thruster_tables)
 
 NOBS = DEFINES["USV_NOBS"]
 NOBST = DEFINES["USV_NOBST"]
@@ -137,6 +138,7 @@ class USVVirtual:
         self.states_buf = Z((n, 0), **f32)
         self.sdf = torch.empty((n if self._has_field else 1, GRID2), **f32)   # per-reset-slot SDF scratch
         self.lut = Z((2, 1000), **f32)
+        self.hydro = build_hydro_cfg(self._task_cfg)
         tl, tr = thruster_tables(self._task_cfg)
         self._tables = torch.tensor(np.stack([tl, tr]), **f32)
         _capi.call("usv_build_lut", _capi.ptr(self._tables[0]), _capi.ptr(self._tables[1]), int(len(tl)),
@@ -323,6 +325,22 @@ class USVVirtual:
             # extras["episode"]: 0-d views of the device buffer written at every reset (USV_Virtual.py:1591-1612)
             self.extras = {"episode": {name: self.extras_buf[i] for name, i in stat_names(self.cfg)}}
         return bias, k
+
+    def hydrostatics(self, quat: torch.Tensor, root_z: torch.Tensor):
+        """HydrostaticsObject.compute_archimedes_metacentric_local fed as update_state feeds it
+        (USV_Virtual.py:785-798, 1105-1109): quat [n][4] (w, x, y, z), root heights [n] ->
+        (submerged volume [n], euler [n][3], body-frame wrench [n][6])."""
+        quat = quat.to(self._device, torch.float32).contiguous()
+        root_z = root_z.to(self._device, torch.float32).contiguous()
+        n = int(root_z.shape[0])
+        if tuple(quat.shape) != (n, 4):
+            raise ValueError(f"quat must be [{n}, 4], got {tuple(quat.shape)}")
+        vol = torch.empty(n, device=self._device, dtype=torch.float32)
+        eul = torch.empty((n, 3), device=self._device, dtype=torch.float32)
+        wr = torch.empty((n, 6), device=self._device, dtype=torch.float32)
+        _capi.call("usv_hydrostatics", _capi.byref(self.hydro), n, _capi.ptr(quat), _capi.ptr(root_z),
+                   _capi.ptr(vol), _capi.ptr(eul), _capi.ptr(wr), _capi.stream_ptr())
+        return vol, eul, wr
 
     def forces(self) -> torch.Tensor:
         out = torch.empty((self._num_envs, 3), device=self._device, dtype=torch.float32)

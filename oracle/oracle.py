@@ -49,6 +49,7 @@ def lib():
         _lib.oracle_grid_lin.argtypes = [ctypes.c_float, P]
         _lib.oracle_lut.argtypes = [P, ctypes.c_int, ctypes.c_int, P]
         _lib.oracle_forces.argtypes = [P, P, P]
+        _lib.oracle_hydrostatics.argtypes = [P, ctypes.c_int, P, P, P, P, P]
         _lib.oracle_compact.argtypes = [P, P]
         _lib.oracle_compact.restype = ctypes.c_int
         _lib.oracle_step_uniforms.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, P]
@@ -208,6 +209,16 @@ class OracleEnv:
         out = np.zeros((self.n, 3), np.float32)
         lib().oracle_forces(ctypes.byref(self.cfg), ctypes.byref(self.c), _p(out))
         return out
+
+
+def hydrostatics(h, quat: np.ndarray, z: np.ndarray):
+    """Hydrostatic wrench per env (oracle_hydrostatics): h is a usv_config.UsvHydro."""
+    n = len(z)
+    quat = np.ascontiguousarray(quat, np.float32)
+    z = np.ascontiguousarray(z, np.float32)
+    vol, eul, wr = np.zeros(n, np.float32), np.zeros((n, 3), np.float32), np.zeros((n, 6), np.float32)
+    lib().oracle_hydrostatics(ctypes.byref(h), n, _p(quat), _p(z), _p(vol), _p(eul), _p(wr))
+    return vol, eul, wr
 
 
 def has_dist(cfg) -> bool:

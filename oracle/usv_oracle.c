@@ -219,6 +219,36 @@ void oracle_forces(const usv_cfg_t *c, oracle_env_t *E, float *out /*[n][3]*/) {
   }
 }
 
+/* Hydrostatic wrench: USVVirtual.update_state volume (USV_Virtual.py:791-798), get_euler_angles
+ * (:815-835), HydrostaticsObject.compute_archimedes_metacentric_local (Hydrostatics.py:63-133) */
+void oracle_hydrostatics(const usv_hydro_t *h, int n, const float *quat, const float *root_z, float *volume,
+                         float *euler, float *wrench) {
+  for (int e = 0; e < n; ++e) {
+    const float w = quat[4 * e], x = quat[4 * e + 1], y = quat[4 * e + 2], z = quat[4 * e + 3];
+    float high = h->zero_height - root_z[e];
+    high = high < 0.f ? 0.f : (high > h->zero_height + 20.0f ? h->zero_height + 20.0f : high);
+    float vol = high * h->waterplane_area;
+    vol = vol < 0.f ? 0.f : (vol > h->max_volume ? h->max_volume : vol);
+    const float r00 = 1.0f - 2.0f * (y * y) - 2.0f * (z * z), r10 = 2.0f * x * y + 2.0f * w * z;
+    const float r20 = 2.0f * x * z - 2.0f * w * y, r21 = 2.0f * y * z + 2.0f * w * x;
+    const float r22 = 1.0f - 2.0f * (x * x) - 2.0f * (y * y);
+    const float roll = atan2f(r21, r22), pitch = asinf(-r20), yaw = atan2f(r10, r00);
+    const float fz = (-h->water_density * h->gravity) * vol;
+    const float tx = (-1.0f * h->metacentric_width) * (sinf(roll) * h->avg_force);
+    const float ty = (-1.0f * h->metacentric_length) * (sinf(pitch) * h->avg_force);
+    const float two_s = 2.0f / (((w * w + x * x) + y * y) + z * z);
+    float *o = wrench + 6 * e;
+    o[0] = two_s * (x * z - y * w) * fz;
+    o[1] = two_s * (y * z + x * w) * fz;
+    o[2] = (1.0f - two_s * (x * x + y * y)) * fz;
+    o[3] = tx * h->amplify_torque;
+    o[4] = ty * h->amplify_torque;
+    o[5] = 0.0f * h->amplify_torque;
+    volume[e] = vol;
+    euler[3 * e] = roll; euler[3 * e + 1] = pitch; euler[3 * e + 2] = yaw;
+  }
+}
+
 /* ------------------------------------------------------------------------ */
 /* Potential field: BatchedMapGPU (tasks/USV/d_multi_gemini.py:7-271)        */
 /* K envs, obstacles [K][16][2], targets [K][2] -> field [K][150][150]       */

@@ -587,6 +587,41 @@ def gen_forces(torch):
                         local_vel=h.local_velocities.numpy())
 
 
+def gen_hydrostatics(torch):
+    """HydrostaticsObject.compute_archimedes_metacentric_local (Hydrostatics.py:63-133) on the TEST
+    config's constants, fed as USVVirtual.update_state feeds it (USV_Virtual.py:785-798): submerged
+    volume from the root height, euler angles from USVVirtual.get_euler_angles (:815-835).  Rows
+    0..127: random attitudes; rows 128..255: level attitudes (roll = pitch = 0, the planar model)."""
+    import types as _types
+    from omniisaacgymenvs.envs.USV.Hydrostatics import HydrostaticsObject
+    from omniisaacgymenvs.tasks.USV_Virtual import USVVirtual
+    cfg = load_task_cfg("A")
+    hs = cfg["dynamics"]["hydrostatics"]
+    grav = float(cfg["sim"]["gravity"][2])
+    n = 256
+    g = torch.Generator().manual_seed(23)
+    h = HydrostaticsObject(n, "cpu", hs["water_density"], grav, hs["box_width"] / 2, hs["box_length"] / 2,
+                           hs["average_hydrostatics_force_value"], hs["amplify_torque"], 0.0, 1.0, 0.3, -10.0)
+    q = torch.randn((n, 4), generator=g)
+    yaw = (torch.rand(n // 2, generator=g) * 2 - 1) * math.pi
+    q[n // 2:, 0] = torch.cos(yaw * 0.5)
+    q[n // 2:, 1] = 0.0
+    q[n // 2:, 2] = 0.0
+    q[n // 2:, 3] = torch.sin(yaw * 0.5)
+    q[:n // 2] = q[:n // 2] / q[:n // 2].norm(dim=1, keepdim=True)
+    z = (torch.rand(n, generator=g) * 2 - 1) * 0.6
+    zero_h = float(hs["heron_zero_height"])
+    max_volume = hs["box_width"] * hs["box_length"] * (zero_h + 20)
+    high = torch.clamp(zero_h - z, 0, zero_h + 20)
+    vol = torch.clamp(high * hs["waterplane_area"], 0, max_volume)
+    ns = _types.SimpleNamespace(euler_angles=torch.zeros((n, 3)))
+    USVVirtual.get_euler_angles(ns, q)
+    w = h.compute_archimedes_metacentric_local(vol, ns.euler_angles, q)
+    np.savez_compressed(os.path.join(OUT, "hydrostatics.npz"), quat=q.numpy(), z=z.numpy(),
+                        volume=vol.numpy(), euler=ns.euler_angles.numpy(), wrench=w.numpy(),
+                        gravity=np.float32(grav))
+
+
 def gen_field(torch):
     from omniisaacgymenvs.tasks.USV.d_multi_gemini import BatchedMapGPU
     res = {}
@@ -955,6 +990,7 @@ def main():
     jobs = {
         "lut": lambda: gen_lut(torch),
         "forces": lambda: gen_forces(torch),
+        "hydrostatics": lambda: gen_hydrostatics(torch),
         "field": lambda: gen_field(torch),
         "episodeA": lambda: gen_episode(torch, "A", 16, 64, 1234),
         "episodeB": lambda: gen_episode(torch, "B", 12, 56, 99),

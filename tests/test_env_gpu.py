@@ -403,6 +403,27 @@ def test_forces_vs_reference_drag(golden):
     ET.check("forces", "drag", F, g["drag"][:, [0, 1, 5]], 1e-5, 1e-5, ["X", "Y", "N"])
 
 
+def test_hydrostatics_vs_reference(golden):
+    """usv_hydrostatics (buoyancy + metacentric restoring torques, Hydrostatics.py:63-133, volume and
+    euler angles as USV_Virtual.py:791-798, 815-835) against the reference at random and level
+    attitudes, 1e-5; on level attitudes -- every state of the planar model -- the surge, sway and yaw
+    components are exactly 0, so the planar integrator's force sum does not change by omitting them."""
+    g = golden("hydrostatics.npz")
+    task = _task(load_yaml(TEST_YAML), 64)
+    vol, eul, wr = (t.cpu().numpy() for t in task.hydrostatics(torch.tensor(g["quat"]), torch.tensor(g["z"])))
+    ET.check("hydrostatics", "volume", vol[:, None], g["volume"][:, None], 1e-5, 1e-5, ["V"])
+    ET.check("hydrostatics", "euler", eul, g["euler"], 1e-5, 1e-5, ["roll", "pitch", "yaw"])
+    scale = float(np.abs(g["wrench"]).max())
+    ET.check("hydrostatics", "wrench", wr / scale, g["wrench"] / scale, 1e-5, 1e-5, ["Fx", "Fy", "Fz", "Tx", "Ty", "Tz"])
+    level = slice(len(g["z"]) // 2, None)
+    assert np.all(wr[level][:, [0, 1, 5]] == 0)
+    # the planar model's own attitudes: yaw-only quaternions from the state, any root height
+    yaw = task.state[2]
+    q = torch.stack([torch.cos(yaw * 0.5), torch.zeros_like(yaw), torch.zeros_like(yaw), torch.sin(yaw * 0.5)], 1)
+    _, _, wr2 = task.hydrostatics(q, torch.linspace(-0.3, 0.5, len(yaw), device=DEV))
+    assert torch.all(wr2[:, [0, 1, 5]] == 0)
+
+
 @pytest.mark.parametrize("n", [65536, 131072])
 def test_full_size_properties(n):
     """BASELINE sizes (C3 65536/GPU, C5 131072/GPU): determinism, finiteness, resets, field range."""
