@@ -494,6 +494,71 @@ int ppo_partials_floats(int minibatch);
 int ppo_grad_floats(void);
 /* size (floats) of the meter buffer of ppo_store_reward */
 int ppo_meter_floats(int n_envs, int horizon);
+/* ------------------------------------------------------------------------
+ * loopz trainer (the reference's default trainer, scripts/rlgames_train.py:273-328 with
+ * algo/ppo/{ppo,storage,module}.py): MLPEncode actor / critic (mass encoder 8-64-16-8, main
+ * MLP (obs_dim - 8 + 8)-128-128-{2 tanh, 1}, LeakyReLU 0.01), tanh-squashed diagonal
+ * Gaussian, time-major rollout storage [T][N], GAE, in-order minibatches, clip_grad_norm_ +
+ * Adam.  Flat parameters (optimizer order): actor net | std[2] | critic net, each net
+ * mass_encoder.{0,2,4}.{weight,bias} then action_mlp.{0,2,4}.{weight,bias}.
+ * ------------------------------------------------------------------------ */
+#define LZ_MASS 8
+#define LZ_LAT  8
+#define LZ_E1   64
+#define LZ_E2   16
+#define LZ_NH   128
+#define LZ_NA   2
+#define LZ_MAX_OBS 36
+typedef struct lz_cfg {
+  int   n_envs;
+  int   horizon;             /* num_transitions_per_env: floor(max_time / control_dt) */
+  int   obs_dim;             /* 33 (priv_dim 8) or 29 (priv_dim 4); <= LZ_MAX_OBS */
+  int   mini_batches;        /* 4 */
+  int   epochs;              /* num_learning_epochs 4 */
+  int   use_clipped_value_loss;
+  float gamma, lam;          /* 0.997, 0.95 */
+  float clip;                /* clip_param 0.2 */
+  float value_loss_coef;     /* 0.5 */
+  float entropy_coef;        /* 0.0 */
+  float max_grad_norm;       /* 0.5 */
+  float lr, adam_b1, adam_b2, adam_eps;
+  float min_std;             /* enforce_minimum_std 0.05 */
+  float action_scale[LZ_NA]; /* clipActions */
+} lz_cfg_t;
+
+/* size (floats) of the flat loopz parameter vector (actor | std | critic) for obs_dim */
+int lz_nparam(int obs_dim);
+/* rollout step t: actor forward + squashed-Gaussian sample (u = mu + std eps, a = tanh(u) scale,
+ * log_prob of module.py:555-583) and critic forward on obs [N][obs_dim] (nan_to_num'd, as
+ * storage.add_transitions does); writes actions_out [N][2] and the storage rows
+ * st_obs[t], st_act[t], st_logp[t], st_val[t].  eps_inject [N][2] (nullable): the N(0,1) draws;
+ * otherwise Philox(seed, env, step, site 0x300). */
+int lz_act(const lz_cfg_t *cfg, const float *params, const float *obs, int t, float *st_obs, float *st_act,
+           float *st_logp, float *st_val, float *actions_out, uint64_t seed, uint64_t step,
+           const float *eps_inject, void *stream);
+/* critic forward only: values [N] (ppo.update's last_values) */
+int lz_value(const lz_cfg_t *cfg, const float *params, const float *obs, float *values, void *stream);
+/* storage.add_transitions' rewards / dones at step t (nan_to_num on the reward) */
+int lz_store(const lz_cfg_t *cfg, const float *rew, const int64_t *dones, int t, float *st_rew, uint8_t *st_done,
+             void *stream);
+/* RolloutStorage.compute_returns (storage.py:92-121): returns, normalised advantages [T][N].
+ * work: >= 8 + 4 * ceil(N / 256) doubles of device scratch. */
+int lz_returns(const lz_cfg_t *cfg, const float *last_values, const float *st_rew, const uint8_t *st_done,
+               const float *st_val, float *st_ret, float *st_adv, double *work, void *stream);
+/* One PPO minibatch of _train_step (ppo.py:242-305): actor and critic gradients of rows
+ * [mb * M, (mb + 1) * M) of the time-major batch (M = N T / mini_batches), fixed-order
+ * reduction into grad (lz_grad_floats()), then clip_grad_norm_ + Adam, skipped when the loss
+ * is not finite.  opt: [2][8] floats, slot opt_slot read, the other written ([0] lr, [1] step,
+ * [2] value loss, [3] surrogate loss, [4] total norm, [5] 1 if the step was applied).
+ * partials: lz_partials_floats(cfg) floats. */
+int lz_minibatch(const lz_cfg_t *cfg, float *params, float *adam_m, float *adam_v, float *opt, int opt_slot, int mb,
+                 const float *st_obs, const float *st_act, const float *st_logp, const float *st_val,
+                 const float *st_ret, const float *st_adv, float *partials, float *grad, void *stream);
+/* enforce_minimum_std (module.py:649-659): std = max(finite(std) ? std : min_std, min_std) */
+int lz_enforce_min_std(const lz_cfg_t *cfg, float *params, void *stream);
+int lz_partials_floats(const lz_cfg_t *cfg);
+int lz_grad_floats(int obs_dim);
+
 /* library version */
 int usv_hip_version(void);
 

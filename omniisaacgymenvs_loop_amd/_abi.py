@@ -88,6 +88,10 @@ class UsvHydro(ctypes.Structure):
     _fields_ = _struct_fields(_TXT, "usv_hydro", DEFINES)
 
 
+class LzCfg(ctypes.Structure):
+    _fields_ = _struct_fields(_TXT, "lz_cfg", DEFINES)
+
+
 class PpoCfg(ctypes.Structure):
     _fields_ = _struct_fields(_TXT, "ppo_cfg", DEFINES)
 

@@ -21,7 +21,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libusv_hip.so")
 # instrumented build (per-workgroup phase timestamps, tools/phase_probe.py); selected with USV_HIP_PROBE=1
 PROBE_LIB_PATH = os.path.join(LIB_DIR, "libusv_hip_probe.so")
-SOURCES = [os.path.join(HERE, "csrc", f) for f in ("usv_env.hip", "usv_field.hip", "ppo.hip")]
+SOURCES = [os.path.join(HERE, "csrc", f) for f in ("usv_env.hip", "usv_field.hip", "ppo.hip", "loopz.hip")]
 DEPS = SOURCES + [os.path.join(HERE, "csrc", "usv_device.h"), os.path.join(ROOT, "include", "usv_hip.h")]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
@@ -56,6 +56,12 @@ def _declare(lib):
         "usv_env_step_part": [P, P, P, P, F, U64, U64, P, I, P],
         "usv_forces": [P, P, P, P],
         "usv_hydrostatics": [P, I, P, P, P, P, P, P],
+        "lz_act": [P, P, P, I, P, P, P, P, P, U64, U64, P, P],
+        "lz_value": [P, P, P, P, P],
+        "lz_store": [P, P, P, I, P, P, P],
+        "lz_returns": [P, P, P, P, P, P, P, P, P],
+        "lz_minibatch": [P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P],
+        "lz_enforce_min_std": [P, P, P],
         "ppo_policy_step": [P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, U64, U64, P, P, P],
         "ppo_value": [P, P, P, P, P, P, P],
         "ppo_store_reward": [P, P, P, I, P, P, P, P, P, P, P],
@@ -64,6 +70,9 @@ def _declare(lib):
         "ppo_minibatch_apply": [P, P, P, P, P, P, I, F, P, I, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
+        "lz_nparam": [I],
+        "lz_grad_floats": [I],
+        "lz_partials_floats": [P],
         "ppo_meter_floats": [I, I],
         "usv_hip_version": [],
     }

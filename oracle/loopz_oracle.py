@@ -1,0 +1,277 @@
+"""ORACLE / TEST INFRASTRUCTURE ONLY.
+
+numpy restatement of the loopz trainer's PPO (the reference's own default trainer,
+omniisaacgymenvs/scripts/rlgames_train.py) with explicit backprop: the MLPEncode actor /
+critic (algo/ppo/module.py:184-361), the tanh-squashed diagonal Gaussian
+(module.py:517-659), RolloutStorage.compute_returns (algo/ppo/storage.py:92-121) and
+PPO._train_step (algo/ppo/ppo.py:237-321) with torch.optim.Adam and clip_grad_norm_.
+Checker for the HIP loopz kernels (omniisaacgymenvs_loop_amd/csrc/loopz.hip), pinned
+against tests/golden/loopz_update.npz, recorded from the reference PPO class.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import numpy as np
+
+F = np.float32
+SPEED, MASS, LAT, NH = 3, 8, 8, 128
+ENC = (64, 16)
+SLOPE = F(0.01)                    # nn.LeakyReLU default negative_slope
+EPS_SQ = F(1e-6)                   # SquashedGaussianDiagonalCovariance eps (module.py:519)
+HALF_LOG_2PI = F(math.log(math.sqrt(2 * math.pi)))
+
+
+def net_shapes(obs_dim: int, n_out: int):
+    """MLPEncode parameters in module (= optimizer) order: mass_encoder, then action_mlp."""
+    main_in = obs_dim - MASS + LAT
+    return [("enc0.w", (ENC[0], MASS)), ("enc0.b", (ENC[0],)), ("enc2.w", (ENC[1], ENC[0])), ("enc2.b", (ENC[1],)),
+            ("enc4.w", (LAT, ENC[1])), ("enc4.b", (LAT,)), ("mlp0.w", (NH, main_in)), ("mlp0.b", (NH,)),
+            ("mlp2.w", (NH, NH)), ("mlp2.b", (NH,)), ("mlp4.w", (n_out, NH)), ("mlp4.b", (n_out,))]
+
+
+STATE_KEY = {"enc0": "architecture.mass_encoder.0", "enc2": "architecture.mass_encoder.2",
+             "enc4": "architecture.mass_encoder.4", "mlp0": "architecture.action_mlp.0",
+             "mlp2": "architecture.action_mlp.2", "mlp4": "architecture.action_mlp.4"}
+
+
+def layout(obs_dim: int, n_act: int = 2):
+    """Flat parameter vector: actor net, actor std, critic net (the optimizer's param order,
+    scripts/rlgames_train.py:314 -> ppo.py:59)."""
+    out, o = [], 0
+    for k, s in net_shapes(obs_dim, n_act):
+        out.append(("actor." + k, s, o)); o += int(np.prod(s))
+    out.append(("std", (n_act,), o)); o += n_act
+    for k, s in net_shapes(obs_dim, 1):
+        out.append(("critic." + k, s, o)); o += int(np.prod(s))
+    return out, o
+
+
+def unflatten(v, obs_dim, n_act=2):
+    lay, _ = layout(obs_dim, n_act)
+    return {k: np.asarray(v[o:o + int(np.prod(s))], F).reshape(s) for k, s, o in lay}
+
+
+def flatten(p: dict, obs_dim, n_act=2):
+    lay, n = layout(obs_dim, n_act)
+    out = np.zeros(n, F)
+    for k, s, o in lay:
+        out[o:o + int(np.prod(s))] = np.asarray(p[k], F).reshape(-1)
+    return out
+
+
+def from_state_dicts(actor_sd: dict, dist_sd: dict, critic_sd: dict, obs_dim: int, n_act: int = 2) -> np.ndarray:
+    p = {}
+    for pre, sd in (("actor.", actor_sd), ("critic.", critic_sd)):
+        for k, key in STATE_KEY.items():
+            p[f"{pre}{k}.w"] = sd[key + ".weight"]
+            p[f"{pre}{k}.b"] = sd[key + ".bias"]
+    p["std"] = dist_sd["std"]
+    return flatten(p, obs_dim, n_act)
+
+
+def lrelu(x):
+    return np.where(x > 0, x, x * SLOPE).astype(F)
+
+
+def lin(x, w, b):
+    return (x @ w.T + b).astype(F)
+
+
+def net_forward(p: dict, pre: str, x: np.ndarray, out_tanh: bool):
+    """MLPEncode.forward (module.py:340-361): speed | task | mass split, mass encoder, main MLP."""
+    obs_dim = x.shape[1]
+    mass = x[:, obs_dim - MASS:]
+    e1 = lrelu(lin(mass, p[pre + "enc0.w"], p[pre + "enc0.b"]))
+    e2 = lrelu(lin(e1, p[pre + "enc2.w"], p[pre + "enc2.b"]))
+    lat = lrelu(lin(e2, p[pre + "enc4.w"], p[pre + "enc4.b"]))
+    z = np.concatenate([x[:, :obs_dim - MASS], lat], 1).astype(F)
+    h1 = lrelu(lin(z, p[pre + "mlp0.w"], p[pre + "mlp0.b"]))
+    h2 = lrelu(lin(h1, p[pre + "mlp2.w"], p[pre + "mlp2.b"]))
+    o = lin(h2, p[pre + "mlp4.w"], p[pre + "mlp4.b"])
+    out = np.tanh(o).astype(F) if out_tanh else o
+    return out, (mass, e1, e2, lat, z, h1, h2)
+
+
+def log_prob_u(u, mu, std, scale):
+    """_log_prob_from_u (module.py:555-565): Normal(mu, std).log_prob(u).sum - log|det|."""
+    var = (std * std).astype(F)
+    lp = (-((u - mu) ** 2) / (F(2) * var) - np.log(std).astype(F) - HALF_LOG_2PI).astype(F).sum(1)
+    log_det = np.log(scale + EPS_SQ).astype(F).sum() + np.log(F(1) - np.tanh(u) ** 2 + EPS_SQ).astype(F).sum(1)
+    return (lp - log_det).astype(F)
+
+
+def sample(p: dict, x: np.ndarray, eps: np.ndarray, scale):
+    """Actor.sample (module.py:67-70) + SquashedGaussian.sample (:568-583) with u = mu + std * eps."""
+    mu, _ = net_forward(p, "actor.", x, True)
+    u = (mu + p["std"] * eps).astype(F)
+    a = (np.tanh(u) * scale).astype(F)
+    return a, log_prob_u(u, mu, p["std"], scale), mu
+
+
+def value(p: dict, x: np.ndarray):
+    v, _ = net_forward(p, "critic.", x, False)
+    return v[:, 0]
+
+
+def u_of_action(a, scale):
+    """SquashedGaussian.evaluate's inverse (module.py:623-627)."""
+    a_s = np.clip((a / (scale + EPS_SQ)).astype(F), F(-1) + EPS_SQ, F(1) - EPS_SQ)
+    return (F(0.5) * (np.log1p(a_s) - np.log1p(-a_s))).astype(F)
+
+
+def compute_returns(rew, values, dones, last_values, gamma=0.997, lam=0.95):
+    """RolloutStorage.compute_returns (storage.py:92-121), time-major [T][N]."""
+    T = rew.shape[0]
+    g, gl = F(gamma), F(gamma) * F(lam)
+    ret = np.zeros_like(values)
+    adv = np.zeros(values.shape[1], F)
+    for t in reversed(range(T)):
+        nv = last_values if t == T - 1 else values[t + 1]
+        nnt = (F(1) - dones[t].astype(F)).astype(F)
+        delta = (rew[t] + (nnt * g) * nv - values[t]).astype(F)
+        adv = (delta + ((nnt * g) * F(lam)) * adv).astype(F)
+        ret[t] = adv + values[t]
+    a = (ret - values).astype(F)
+    a = ((a - a.mean(dtype=np.float64)) / (a.std(ddof=1, dtype=np.float64) + 1e-8)).astype(F)
+    return ret, a
+
+
+@dataclass
+class Config:
+    clip: float = 0.2
+    value_loss_coef: float = 0.5
+    entropy_coef: float = 0.0
+    max_grad_norm: float = 0.5
+    lr: float = 5e-4
+    b1: float = 0.9
+    b2: float = 0.999
+    eps: float = 1e-8
+    epochs: int = 4
+    mini_batches: int = 4
+    use_clipped_value_loss: bool = True
+
+
+def _net_backward(p, pre, cache, dout, G):
+    mass, e1, e2, lat, z, h1, h2 = cache
+    G[pre + "mlp4.w"] = dout.T @ h2
+    G[pre + "mlp4.b"] = dout.sum(0)
+    dz2 = (dout @ p[pre + "mlp4.w"]) * np.where(h2 > 0, F(1), SLOPE)
+    G[pre + "mlp2.w"] = dz2.T @ h1
+    G[pre + "mlp2.b"] = dz2.sum(0)
+    dz1 = (dz2 @ p[pre + "mlp2.w"]) * np.where(h1 > 0, F(1), SLOPE)
+    G[pre + "mlp0.w"] = dz1.T @ z
+    G[pre + "mlp0.b"] = dz1.sum(0)
+    dlat = (dz1 @ p[pre + "mlp0.w"])[:, z.shape[1] - LAT:] * np.where(lat > 0, F(1), SLOPE)
+    G[pre + "enc4.w"] = dlat.T @ e2
+    G[pre + "enc4.b"] = dlat.sum(0)
+    de2 = (dlat @ p[pre + "enc4.w"]) * np.where(e2 > 0, F(1), SLOPE)
+    G[pre + "enc2.w"] = de2.T @ e1
+    G[pre + "enc2.b"] = de2.sum(0)
+    de1 = (de2 @ p[pre + "enc2.w"]) * np.where(e1 > 0, F(1), SLOPE)
+    G[pre + "enc0.w"] = de1.T @ mass
+    G[pre + "enc0.b"] = de1.sum(0)
+
+
+def minibatch_grad(p: dict, obs, act, old_logp, old_val, ret, adv, scale, cfg: Config):
+    """PPO._train_step's loss (ppo.py:252-288) and its gradient."""
+    B = obs.shape[0]
+    mu, ca = net_forward(p, "actor.", obs, True)
+    v_out, cc = net_forward(p, "critic.", obs, False)
+    v = v_out[:, 0]
+    std = p["std"]
+    u = u_of_action(act, scale)
+    lp = log_prob_u(u, mu, std, scale)
+    ratio = np.exp(lp - old_logp).astype(F)
+    lo, hi = F(1 - cfg.clip), F(1 + cfg.clip)
+    s1, s2 = -adv * ratio, -adv * np.clip(ratio, lo, hi)
+    surr = np.maximum(s1, s2)
+    inr = ((ratio >= lo) & (ratio <= hi)).astype(F)
+    g1, g2 = -adv, -adv * inr
+    g_r = np.where(s1 > s2, g1, np.where(s1 < s2, g2, F(0.5) * (g1 + g2)))
+    # loss = mean(surr + c_v * vl - c_e * entropy), entropy = -lp
+    dlp = ((g_r * ratio + F(cfg.entropy_coef)) / F(B)).astype(F)
+    if cfg.use_clipped_value_loss:
+        dvr = v - old_val
+        vc = old_val + np.clip(dvr, F(-cfg.clip), F(cfg.clip))
+        l1, l2 = (v - ret) ** 2, (vc - ret) ** 2
+        vl = np.maximum(l1, l2)
+        d1 = F(2) * (v - ret)
+        d2 = F(2) * (vc - ret) * ((dvr >= -cfg.clip) & (dvr <= cfg.clip)).astype(F)
+        dv = np.where(l1 > l2, d1, np.where(l1 < l2, d2, F(0.5) * (d1 + d2)))
+    else:
+        vl = (ret - v) ** 2
+        dv = F(2) * (v - ret)
+    dv = (dv * F(cfg.value_loss_coef) / F(B)).astype(F)
+    var = (std * std).astype(F)
+    dmu = (dlp[:, None] * (u - mu) / var).astype(F)
+    dstd = (dlp[:, None] * (((u - mu) ** 2) / (var * std) - F(1) / std)).sum(0).astype(F)
+    G = {"std": dstd}
+    _net_backward(p, "actor.", ca, (dmu * (F(1) - mu * mu)).astype(F), G)
+    _net_backward(p, "critic.", cc, dv[:, None], G)
+    loss = float((surr + F(cfg.value_loss_coef) * vl - F(cfg.entropy_coef) * (-lp)).mean())
+    return G, float(vl.mean()), float(surr.mean()), loss
+
+
+@dataclass
+class Adam:
+    m: np.ndarray
+    v: np.ndarray
+    step: int = 0
+
+    @classmethod
+    def zeros(cls, n):
+        return cls(np.zeros(n, F), np.zeros(n, F), 0)
+
+    def apply(self, pv, g, cfg: Config):
+        """torch.optim.Adam (non-amsgrad, no weight decay)."""
+        self.step += 1
+        self.m = (self.m + F(1 - cfg.b1) * (g - self.m)).astype(F)
+        self.v = (self.v * F(cfg.b2) + F(1 - cfg.b2) * g * g).astype(F)
+        step_size = cfg.lr / (1 - cfg.b1 ** self.step)
+        denom = np.sqrt(self.v) / F(math.sqrt(1 - cfg.b2 ** self.step)) + F(cfg.eps)
+        return (pv - F(step_size) * (self.m / denom)).astype(F)
+
+
+def clip_grad(G: dict, obs_dim, max_norm, n_act=2):
+    """nn.utils.clip_grad_norm_ over actor + critic parameters (ppo.py:304)."""
+    g = flatten(G, obs_dim, n_act)
+    lay, _ = layout(obs_dim, n_act)
+    norms = np.array([np.linalg.norm(g[o:o + int(np.prod(s))].astype(np.float64)) for _, s, o in lay])
+    total = float(np.linalg.norm(norms))
+    coef = min(max_norm / (total + 1e-6), 1.0)
+    return (g * F(coef)).astype(F), total
+
+
+def train_step(pv, adam: Adam, data: dict, scale, cfg: Config):
+    """PPO._train_step (ppo.py:237-321): epochs x in-order minibatches of the time-major batch."""
+    obs_dim = data["obs"].shape[-1]
+    flat = {k: np.asarray(v).reshape((-1,) + np.asarray(v).shape[2:]) for k, v in data.items()}
+    B = flat["obs"].shape[0]
+    M = B // cfg.mini_batches
+    vls, sls = [], []
+    for _ in range(cfg.epochs):
+        for i in range(cfg.mini_batches):
+            sl = slice(i * M, (i + 1) * M)
+            G, vl, sloss, loss = minibatch_grad(unflatten(pv, obs_dim), flat["obs"][sl], flat["actions"][sl],
+                                                flat["logp"][sl], flat["values"][sl], flat["returns"][sl],
+                                                flat["advantages"][sl], scale, cfg)
+            if not math.isfinite(loss):
+                continue
+            g, _ = clip_grad(G, obs_dim, cfg.max_grad_norm)
+            pv = adam.apply(pv, g, cfg)
+            vls.append(vl)
+            sls.append(sloss)
+    return pv, float(np.mean(vls)), float(np.mean(sls))
+
+
+def enforce_minimum_std(pv, obs_dim, min_std=0.05, n_act=2):
+    """SquashedGaussian.enforce_minimum_std (module.py:649-659), as rlgames_train.py:526-528 calls it."""
+    lay, _ = layout(obs_dim, n_act)
+    o = [o for k, _, o in lay if k == "std"][0]
+    s = pv[o:o + n_act]
+    s = np.where(np.isfinite(s), s, F(min_std))
+    pv = pv.copy()
+    pv[o:o + n_act] = np.maximum(s, F(min_std))
+    return pv

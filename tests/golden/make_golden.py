@@ -622,6 +622,88 @@ def gen_hydrostatics(torch):
                         gravity=np.float32(grav))
 
 
+def gen_loopz(torch, n=16, T=24, seed=7):
+    """The loopz trainer's PPO (omniisaacgymenvs/algo/ppo/{ppo,storage,module}.py) as
+    scripts/rlgames_train.py:273-328 builds it (MLPEncode_wrap actor / critic, LeakyReLU, tanh actor
+    output, squashed Gaussian init std 0.3, gamma 0.997, lambda 0.95, 4 x 4 in-order minibatches,
+    lr 5e-4, max grad norm 0.5), fed a scripted rollout: T steps of observe() / step() on recorded
+    observations, rewards and dones, then update().  Every Normal.sample draw is recorded (eps) and
+    formed as loc + scale * eps; the squashed actions, log-probs, values, GAE returns / advantages,
+    the parameters before and after the update, the Adam state and the mean losses are stored."""
+    import torch.nn as nn
+    tb = types.ModuleType("torch.utils.tensorboard")
+
+    class _Writer:
+        def __init__(self, *a, **k):
+            pass
+
+        def add_scalar(self, *a, **k):
+            pass
+
+    tb.SummaryWriter = _Writer
+    sys.modules["torch.utils.tensorboard"] = tb
+    import omniisaacgymenvs.algo.ppo.module as M
+    import omniisaacgymenvs.algo.ppo.ppo as P
+    gen = torch.Generator().manual_seed(seed + 100)
+    draws = []
+
+    class RecNormal(torch.distributions.Normal):
+        def sample(self, sample_shape=torch.Size()):
+            eps = torch.randn(self.loc.shape, generator=gen)
+            draws.append(eps.numpy().copy())
+            return self.loc + self.scale * eps
+
+    M.Normal = RecNormal
+    torch.manual_seed(seed)
+    ob_dim, act_dim = 33, 2
+    kw = dict(speed_dim=3, mass_dim=8, mass_latent_dim=8, mass_encoder_shape=(64, 16))
+    actor = M.Actor(M.MLPEncode_wrap([128, 128], nn.LeakyReLU, ob_dim, act_dim, nn.Tanh, False, **kw),
+                    M.SquashedGaussianDiagonalCovariance(act_dim, 0.3, action_scale=1.0), "cpu")
+    critic = M.Critic(M.MLPEncode_wrap([128, 128], nn.LeakyReLU, ob_dim, 1, **kw), "cpu")
+    ppo = P.PPO(actor=actor, critic=critic, num_envs=n, num_transitions_per_env=T, num_learning_epochs=4,
+                gamma=0.997, lam=0.95, num_mini_batches=4, device="cpu", log_dir="/tmp/loopz_golden",
+                mini_batch_sampling="in_order", learning_rate=5e-4)
+    sd = lambda m: {k: v.detach().clone().numpy() for k, v in m.state_dict().items()}
+    init = {"actor": sd(actor.architecture), "dist": sd(actor.distribution), "critic": sd(critic.architecture)}
+    rng = np.random.default_rng(seed)
+    obs = rng.uniform(-2.5, 2.5, (T + 1, n, ob_dim)).astype(np.float32)
+    obs[..., 25:] = rng.uniform(-1, 1, (T + 1, n, 8)).astype(np.float32)
+    rew = rng.normal(0.0, 1.0, (T, n)).astype(np.float32)
+    done = rng.uniform(0, 1, (T, n)) < 0.06
+    acts = []
+    for t in range(T):
+        acts.append(ppo.observe(obs[t]))
+        ppo.step(value_obs=obs[t], rews=rew[t], dones=done[t], infos=[])
+    losses = {}
+    orig = ppo._train_step
+
+    def train_step():
+        mv, ms, inf = orig()
+        losses["value"], losses["surrogate"] = mv, ms
+        return mv, ms, inf
+
+    ppo._train_step = train_step
+    ppo.update(actor_obs=obs[T], value_obs=obs[T], log_this_iteration=False, update=0)
+    st = ppo.storage
+    after = {"actor": sd(actor.architecture), "dist": sd(actor.distribution), "critic": sd(critic.architecture)}
+    opt = ppo.optimizer.state_dict()
+    actor.distribution.enforce_minimum_std(torch.ones(act_dim) * 0.05)
+    out = {"obs": obs, "rew": rew, "done": done.astype(np.uint8), "eps": np.stack(draws[:T]),
+           "actions": np.stack(acts), "logp": st.actions_log_prob.numpy()[..., 0], "values": st.values.numpy()[..., 0],
+           "returns": st.returns.numpy()[..., 0], "advantages": st.advantages.numpy()[..., 0],
+           "loss_value": np.float64(losses["value"]), "loss_surrogate": np.float64(losses["surrogate"]),
+           "std_enforced": actor.distribution.std.detach().numpy().copy(),
+           "adam_step": np.float64(opt["state"][0]["step"])}
+    for tag, d in (("init", init), ("after", after)):
+        for net, sdict in d.items():
+            for k, v in sdict.items():
+                out[f"{tag}/{net}/{k}"] = v
+    for i, s_ in opt["state"].items():
+        out[f"adam_m_{i}"] = s_["exp_avg"].numpy()
+        out[f"adam_v_{i}"] = s_["exp_avg_sq"].numpy()
+    np.savez_compressed(os.path.join(OUT, "loopz_update.npz"), **out)
+
+
 def gen_field(torch):
     from omniisaacgymenvs.tasks.USV.d_multi_gemini import BatchedMapGPU
     res = {}
@@ -1001,6 +1083,7 @@ def main():
         "episodeS": lambda: (make_scene_file(), gen_episode(torch, "S", 6, 64, 41)),
         "episodeT": lambda: gen_episode(torch, "T", 12, 64, 32),
         "ppo": lambda: gen_ppo(torch),
+        "loopz": lambda: gen_loopz(torch),
         "ckpt811": lambda: gen_ckpt811(torch),
     }
     for name, fn in jobs.items():

@@ -1,0 +1,164 @@
+"""The loopz trainer's HIP path (csrc/loopz.hip through the C ABI) against the reference's own
+PPO class (tests/golden/loopz_update.npz) and the oracle (oracle/loopz_oracle.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import loopz_oracle as L
+from omniisaacgymenvs_loop_amd.loopz import PPO, Actor, Critic, MLPEncode_wrap, SquashedGaussianDiagonalCovariance
+
+from tests import errtab as ET
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+OBS = 33
+
+
+class _Leaky:   # stands in for nn.LeakyReLU / nn.Tanh: only the name is read
+    __name__ = "LeakyReLU"
+
+
+class _Tanh:
+    __name__ = "Tanh"
+
+
+def _build(n, T, d=None, seed=0):
+    kw = dict(speed_dim=3, mass_dim=8, mass_latent_dim=8, mass_encoder_shape=(64, 16))
+    actor = Actor(MLPEncode_wrap([128, 128], _Leaky, OBS, 2, _Tanh, False, seed=seed, **kw),
+                  SquashedGaussianDiagonalCovariance(2, 0.3, action_scale=1.0), DEV)
+    critic = Critic(MLPEncode_wrap([128, 128], _Leaky, OBS, 1, seed=seed + 1, **kw), DEV)
+    if d is not None:
+        sd = lambda net: {k.split("/", 2)[2]: torch.tensor(d[k]) for k in d if k.startswith(f"init/{net}/")}
+        actor.architecture.load_state_dict(sd("actor"))
+        actor.distribution.load_state_dict(sd("dist"))
+        critic.architecture.load_state_dict(sd("critic"))
+    return PPO(actor, critic, n, T, 4, 4, gamma=0.997, lam=0.95, device=DEV, mini_batch_sampling="in_order",
+               learning_rate=5e-4, log_dir="/tmp/loopz_test")
+
+
+def _params(d, tag):
+    sd = lambda net: {k.split("/", 2)[2]: d[k] for k in d if k.startswith(f"{tag}/{net}/")}
+    return L.from_state_dicts(sd("actor"), sd("dist"), sd("critic"), OBS)
+
+
+def _rollout(ppo, d):
+    T = d["rew"].shape[0]
+    for t in range(T):
+        a = ppo.observe_device(torch.tensor(d["obs"][t], device=DEV), torch.tensor(d["eps"][t], device=DEV))
+        ET.check("loopz_rollout", "actions", a.cpu().numpy(), d["actions"][t], 1e-5, 1e-5, ["a0", "a1"])
+        ppo.step_device(torch.tensor(d["rew"][t]), torch.tensor(d["done"][t].astype(np.int64)))
+    st = ppo.storage
+    ET.check("loopz_rollout", "logp", st.actions_log_prob.cpu().numpy(), d["logp"], 1e-5, 1e-5)
+    ET.check("loopz_rollout", "values", st.values.cpu().numpy(), d["values"], 1e-5, 1e-5)
+
+
+def test_rollout_and_update_vs_reference(golden):
+    d = golden("loopz_update.npz")
+    T, n = d["rew"].shape
+    ppo = _build(n, T, d)
+    np.testing.assert_array_equal(ppo.params.cpu().numpy(), _params(d, "init"))
+    _rollout(ppo, d)
+    ppo.update(actor_obs=None, value_obs=torch.tensor(d["obs"][T]), log_this_iteration=False, update=0)
+    st = ppo.storage
+    ET.check("loopz_update", "returns", st.returns.cpu().numpy(), d["returns"], 1e-5, 1e-5)
+    ET.check("loopz_update", "advantages", st.advantages.cpu().numpy(), d["advantages"], 1e-5, 1e-5)
+    assert ppo.adam_step() == int(d["adam_step"]) == 16
+    got, want, p0 = ppo.params.cpu().numpy(), _params(d, "after"), _params(d, "init")
+    # 16 Adam steps of lr 5e-4: parameters at 1e-5 relative to their size (absolute 1e-6)
+    ET.check("loopz_update", "params", got, want, 1e-5, 1e-6)
+    ET.record("loopz_update", "param_delta", got - p0, want - p0)
+    np.testing.assert_allclose(ppo.mean_value_loss, float(d["loss_value"]), rtol=1e-5)
+    np.testing.assert_allclose(ppo.mean_surrogate_loss, float(d["loss_surrogate"]), rtol=1e-4, atol=1e-6)
+    ppo.actor.distribution.enforce_minimum_std(0.05)
+    np.testing.assert_allclose(ppo.actor.distribution.std.cpu().numpy(), d["std_enforced"], rtol=1e-6)
+    # state dicts come back in the reference's key set and shapes
+    sd = ppo.actor.architecture.state_dict()
+    ref_keys = {k.split("/", 2)[2] for k in d if k.startswith("after/actor/")}
+    assert set(sd) == ref_keys
+    osd = ppo.optimizer_state_dict()
+    for i in range(len(osd["param_groups"][0]["params"])):
+        np.testing.assert_allclose(osd["state"][i]["exp_avg"].numpy(), d[f"adam_m_{i}"], rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.parametrize("n,T", [(512, 600), (37, 24)])
+def test_minibatch_vs_oracle(n, T):
+    """One full-size in-order minibatch (76800 rows at the loopz default of 512 envs x 600 steps;
+    and a ragged size) through lz_minibatch against the oracle's gradient + clip + Adam."""
+    rng = np.random.default_rng(3)
+    ppo = _build(n, T, seed=5)
+    st = ppo.storage
+    obs = rng.uniform(-2.5, 2.5, (T, n, OBS)).astype(np.float32)
+    obs[..., 25:] = rng.uniform(-1, 1, (T, n, 8))
+    act = np.tanh(rng.normal(0, 1, (T, n, 2))).astype(np.float32)
+    data = {"obs": obs, "actions": act, "logp": rng.normal(-1, 0.5, (T, n)).astype(np.float32),
+            "values": rng.normal(0, 1, (T, n)).astype(np.float32), "returns": rng.normal(0, 1.5, (T, n)).astype(np.float32),
+            "advantages": rng.normal(0, 1, (T, n)).astype(np.float32)}
+    for k, buf in (("obs", st.actor_obs), ("actions", st.actions), ("logp", st.actions_log_prob), ("values", st.values),
+                   ("returns", st.returns), ("advantages", st.advantages)):
+        buf.copy_(torch.tensor(data[k]))
+    p0 = ppo.params.cpu().numpy()
+    mb = 1
+    from omniisaacgymenvs_loop_amd import _capi
+    _capi.call("lz_minibatch", _capi.byref(ppo.cfg), _capi.ptr(ppo.params), _capi.ptr(ppo.adam_m),
+               _capi.ptr(ppo.adam_v), _capi.ptr(ppo.opt), 0, mb, _capi.ptr(st.actor_obs), _capi.ptr(st.actions),
+               _capi.ptr(st.actions_log_prob), _capi.ptr(st.values), _capi.ptr(st.returns), _capi.ptr(st.advantages),
+               _capi.ptr(ppo.partials), _capi.ptr(ppo.grad), _capi.stream_ptr())
+    torch.cuda.synchronize()
+    B = n * T
+    M = B // 4
+    flat = {k: v.reshape((B,) + v.shape[2:]) for k, v in data.items()}
+    sl = slice(mb * M, (mb + 1) * M)
+    G, vl, sl_loss, loss = L.minibatch_grad(L.unflatten(p0, OBS), flat["obs"][sl], flat["actions"][sl],
+                                            flat["logp"][sl], flat["values"][sl], flat["returns"][sl],
+                                            flat["advantages"][sl], np.float32(1.0), L.Config())
+    g_ref = L.flatten(G, OBS)
+    np_ = ppo.nparam
+    g = ppo.grad[:np_].cpu().numpy()
+    scale = float(np.abs(g_ref).max())
+    ET.check(f"loopz_grad_{n}x{T}", "grad/max", g / scale, g_ref / scale, 1e-5, 1e-5)
+    gc, _ = L.clip_grad(G, OBS, 0.5)
+    adam = L.Adam.zeros(np_)
+    want = adam.apply(p0, gc, L.Config())
+    ET.check(f"loopz_grad_{n}x{T}", "params", ppo.params.cpu().numpy(), want, 1e-5, 1e-6)
+    np.testing.assert_allclose(float(ppo.opt[8 + 2].item()), vl, rtol=1e-5)
+
+
+def test_nonfinite_loss_skips_the_step():
+    n, T = 32, 8
+    ppo = _build(n, T, seed=9)
+    st = ppo.storage
+    st.actor_obs.uniform_(-1, 1)
+    st.advantages.fill_(float("nan"))
+    p0 = ppo.params.clone()
+    from omniisaacgymenvs_loop_amd import _capi
+    _capi.call("lz_minibatch", _capi.byref(ppo.cfg), _capi.ptr(ppo.params), _capi.ptr(ppo.adam_m),
+               _capi.ptr(ppo.adam_v), _capi.ptr(ppo.opt), 0, 0, _capi.ptr(st.actor_obs), _capi.ptr(st.actions),
+               _capi.ptr(st.actions_log_prob), _capi.ptr(st.values), _capi.ptr(st.returns), _capi.ptr(st.advantages),
+               _capi.ptr(ppo.partials), _capi.ptr(ppo.grad), _capi.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(ppo.params, p0)
+    assert float(ppo.opt[8 + 1].item()) == 0.0 and float(ppo.opt[8 + 5].item()) == 0.0
+
+
+def test_loopz_trainer_runs_on_the_usv_task(tmp_path, monkeypatch):
+    """scripts/loopz_train.py's loop on the USV env (64 envs, 16 transitions per update), two updates,
+    then a resume from the written full_0.pt checkpoint (reference key set)."""
+    from omniisaacgymenvs_loop_amd.scripts import loopz_train as LT
+    monkeypatch.chdir(tmp_path)
+    cfg = LT.build_config({"num_envs": 64, "seed": 3, "train": "USV/USV_MLP"})
+    cfg = LT.merge_loopz_overrides(cfg, LT.os.path.join(LT.os.path.dirname(LT.os.path.dirname(LT.os.path.abspath(LT.__file__))), "cfg"))
+    cfg["environment"]["max_time"] = 0.16
+    cfg["environment"]["eval_every_n"] = 1
+    hist, ppo = LT.train(cfg, max_updates=1, log=lambda *a: None)
+    assert len(hist) == 2 and all(np.isfinite(h["average_ll_reward"]) for h in hist)
+    assert ppo.adam_step() == 2 * 16
+    assert np.all(np.isfinite(ppo.params.cpu().numpy()))
+    ck = tmp_path / "runs" / "USV" / "nn" / "full_1.pt"
+    sd = torch.load(ck, map_location="cpu", weights_only=True)
+    assert set(sd) == {"actor_architecture_state_dict", "actor_distribution_state_dict", "critic_architecture_state_dict",
+                       "optimizer_state_dict", "update"} and sd["update"] == 1
+    assert "architecture.mass_encoder.0.weight" in sd["actor_architecture_state_dict"]
+    env, actor, critic, ppo2, _ = LT.build(cfg)
+    assert LT.load_full(str(ck), actor, critic, ppo2) == 2
+    p_saved = np.concatenate([v.numpy().reshape(-1) for v in sd["actor_architecture_state_dict"].values()])
+    np.testing.assert_array_equal(actor.architecture.flat().numpy(), p_saved)

@@ -1,0 +1,56 @@
+"""The loopz PPO oracle (oracle/loopz_oracle.py) against the reference's own PPO class
+(tests/golden/loopz_update.npz, recorded by tests/golden/make_golden.py::gen_loopz): rollout
+actions / log-probs / values, GAE returns and normalised advantages, and one update (4 epochs x 4
+in-order minibatches, clip 0.5, Adam 5e-4) of every actor / critic parameter and the Adam state."""
+import numpy as np
+
+from oracle import loopz_oracle as L
+
+OBS = 33
+
+
+def _params(d, tag):
+    sd = lambda net: {k.split("/", 2)[2]: d[k] for k in d if k.startswith(f"{tag}/{net}/")}
+    return L.from_state_dicts(sd("actor"), sd("dist"), sd("critic"), OBS)
+
+
+def test_rollout_matches_reference(golden):
+    d = golden("loopz_update.npz")
+    p = L.unflatten(_params(d, "init"), OBS)
+    T = d["rew"].shape[0]
+    for t in range(T):
+        a, lp, _ = L.sample(p, d["obs"][t], d["eps"][t], np.float32(1.0))
+        np.testing.assert_allclose(a, d["actions"][t], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(lp, d["logp"][t], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(L.value(p, d["obs"][t]), d["values"][t], rtol=1e-5, atol=1e-5)
+
+
+def test_gae_matches_reference(golden):
+    d = golden("loopz_update.npz")
+    p = L.unflatten(_params(d, "init"), OBS)
+    last = L.value(p, d["obs"][-1])
+    ret, adv = L.compute_returns(d["rew"], d["values"], d["done"], last)
+    np.testing.assert_allclose(ret, d["returns"], rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(adv, d["advantages"], rtol=1e-5, atol=1e-5)
+
+
+def test_update_matches_reference(golden):
+    d = golden("loopz_update.npz")
+    pv0 = _params(d, "init")
+    data = {k: d[k] for k in ("obs", "actions", "logp", "values", "returns", "advantages")}
+    data["obs"] = data["obs"][:-1]
+    adam = L.Adam.zeros(len(pv0))
+    pv, vl, sl = L.train_step(pv0, adam, data, np.float32(1.0), L.Config())
+    want = _params(d, "after")
+    assert adam.step == int(d["adam_step"]) == 16
+    np.testing.assert_allclose(vl, float(d["loss_value"]), rtol=1e-5)
+    np.testing.assert_allclose(sl, float(d["loss_surrogate"]), rtol=1e-4, atol=1e-7)
+    # parameter deltas (lr 5e-4 per step) at 1e-5 of their size: absolute 1e-7 on the weights
+    np.testing.assert_allclose(pv - pv0, want - pv0, rtol=1e-3, atol=2e-7)
+    lay, _ = L.layout(OBS)
+    for i, (k, s, o) in enumerate(lay):
+        n = int(np.prod(s))
+        np.testing.assert_allclose(adam.m[o:o + n], d[f"adam_m_{i}"].reshape(-1), rtol=1e-3, atol=1e-7, err_msg=k)
+        np.testing.assert_allclose(adam.v[o:o + n], d[f"adam_v_{i}"].reshape(-1), rtol=1e-3, atol=1e-10, err_msg=k)
+    std = L.enforce_minimum_std(pv, OBS)[[o for k, _, o in lay if k == "std"][0]:][:2]
+    np.testing.assert_allclose(std, d["std_enforced"], rtol=1e-6)
