@@ -26,12 +26,9 @@ from .rlgames_train import build_config, parse_overrides
 from ..utils.hydra_cfg import load_yaml
 
 
-class _LeakyReLU:   # nn.LeakyReLU's name: the kernels implement LeakyReLU(0.01)
-    __name__ = "LeakyReLU"
-
-
-class _Tanh:
-    __name__ = "Tanh"
+# the activation constructors the reference passes (rlgames_train.py:161, 281); the kernels
+# implement LeakyReLU(0.01) hidden layers and a tanh / identity output
+_LeakyReLU, _Tanh = torch.nn.LeakyReLU, torch.nn.Tanh
 
 
 def merge_loopz_overrides(cfg, cfg_dir):

