@@ -484,6 +484,15 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        const float *exp_val, const float *exp_ret, const float *exp_adv,
                        float *exp_mu, float *exp_sigma, float *grad, float *losses,
                        float *partials, double *work, void *stream);
+/* RunningMeanStd.train of mini-epoch 0 for the whole epoch at once (it depends only on the
+ * rollout's observations): merges the rows / minibatch minibatches of exp_obs in order into
+ * obs_rms (final state) and writes the running (mean[33], var[33]) after merge k to
+ * rms_seq[k * 66]; minibatch k of mini-epoch 0 then calls ppo_minibatch_grad with
+ * obs_rms = rms_seq + 66 k and update_obs_rms = 0 (same normalisation as update_obs_rms = 1).
+ * rms_seq: ppo_rms_seq_doubles(cfg, rows) doubles (the tail is scratch). */
+int ppo_obs_rms_epoch(const ppo_cfg_t *cfg, const float *exp_obs, int rows, double *obs_rms, double *rms_seq,
+                      void *stream);
+int ppo_rms_seq_doubles(const ppo_cfg_t *cfg, int rows);
 int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float *adam_m,
                         float *adam_v, float *opt, int opt_slot, float grad_scale,
                         float *kl_out, int norm_from_partials, void *stream);

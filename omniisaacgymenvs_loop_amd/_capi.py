@@ -70,6 +70,8 @@ def _declare(lib):
         "ppo_minibatch_apply": [P, P, P, P, P, P, I, F, P, I, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
+        "ppo_obs_rms_epoch": [P, P, I, P, P, P],
+        "ppo_rms_seq_doubles": [P, I],
         "lz_nparam": [I],
         "lz_grad_floats": [I],
         "lz_partials_floats": [P],

@@ -545,6 +545,75 @@ __global__ __launch_bounds__(TB) void k_obs_stats(ppo_cfg_t c, const float *__re
   }
 }
 
+// ---------------------------------------------- obs RMS over one epoch ----
+// RunningMeanStd.train in mini-epoch 0 (a2c_common.py:1243-1244, running_mean_std.py:44-111)
+// depends only on the rollout's observations, so the whole sequence of running statistics is
+// formed once per epoch: k_obs_moments sums each minibatch's columns (fp64, OM_CH row chunks per
+// minibatch), k_obs_rms_seq merges them in minibatch order (Chan's formula as k_obs_stats) and
+// writes the statistics after merge k to seq[k] -- what minibatch k normalises with -- and the
+// final state to obs_rms.  Two launches per epoch instead of one per minibatch.
+constexpr int OM_CH = 8;
+__global__ __launch_bounds__(TB) void k_obs_moments(ppo_cfg_t c, const float *__restrict__ obs, double *part) {
+  __shared__ double acc[2][NIN][TB / NIN + 1];
+  const int tid = threadIdx.x, mb = blockIdx.x, ch = blockIdx.y;
+  const int col = tid % NIN, lane_r = tid / NIN, nl = TB / NIN;
+  const int M = c.minibatch, chunk = (M + OM_CH - 1) / OM_CH;
+  const int a = mb * M + ch * chunk, bnd = mb * M + min(M, (ch + 1) * chunk);
+  double s = 0, s2 = 0;
+  if (lane_r < nl) {
+    for (int r0 = a + lane_r; r0 < bnd; r0 += 8 * nl) {
+      float xv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) xv[u] = obs[(size_t)min(r0 + u * nl, bnd - 1) * NIN + col];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r0 + u * nl < bnd) {
+          const double x = xv[u];
+          s += x; s2 += x * x;
+        }
+    }
+    acc[0][col][lane_r] = s;
+    acc[1][col][lane_r] = s2;
+  }
+  __syncthreads();
+  if (tid < NIN) {
+    double t = 0, t2 = 0;
+    for (int l = 0; l < nl; ++l) { t += acc[0][tid][l]; t2 += acc[1][tid][l]; }
+    double *o = part + ((size_t)mb * OM_CH + ch) * 2 * NIN;
+    o[tid] = t;
+    o[NIN + tid] = t2;
+  }
+}
+
+__global__ void k_obs_rms_seq(ppo_cfg_t c, const double *__restrict__ part, int nmb, double *obs_rms, double *seq) {
+  const int k = threadIdx.x;
+  if (k >= NIN) return;
+  const double rows = (double)c.minibatch;
+  double mean = obs_rms[k], var = obs_rms[NIN + k], count = obs_rms[2 * NIN];
+  for (int mb = 0; mb < nmb; ++mb) {
+    double sa = 0, sb = 0;
+    for (int ch = 0; ch < OM_CH; ++ch) {
+      const double *o = part + ((size_t)mb * OM_CH + ch) * 2 * NIN;
+      sa += o[k];
+      sb += o[NIN + k];
+    }
+    const double bmean = sa / rows;
+    const double bvar = (sb - rows * bmean * bmean) / (rows - 1.0);
+    const double tot = count + rows;
+    const double delta = bmean - mean;
+    const double M2 = var * count + bvar * rows + delta * delta * count * rows / tot;
+    mean = mean + delta * rows / tot;
+    var = M2 / tot;
+    count = tot;
+    seq[(size_t)mb * 2 * NIN + k] = mean;
+    seq[(size_t)mb * 2 * NIN + NIN + k] = var;
+  }
+  obs_rms[k] = mean;
+  obs_rms[NIN + k] = var;
+  __syncthreads();
+  if (k == 0) obs_rms[2 * NIN] = count;
+}
+
 // ------------------------------------------------------ minibatch grad ----
 // One 512-thread workgroup (8 waves, two per SIMD) per 32 minibatch rows, 256
 // workgroups for a 8192-row minibatch (every CU).  The second wave of each SIMD
@@ -1221,6 +1290,25 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
   hipLaunchKernelGGL(k_reduce_partials, dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad, losses,
                      1.0f / (float)cfg->minibatch);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_rms_seq_doubles(const ppo_cfg_t *cfg, int rows) {
+  if (!cfg || cfg->minibatch <= 0 || rows < cfg->minibatch) return -1;
+  const int nmb = rows / cfg->minibatch;
+  return nmb * 2 * NIN + nmb * OM_CH * 2 * NIN;
+}
+
+int ppo_obs_rms_epoch(const ppo_cfg_t *cfg, const float *exp_obs, int rows, double *obs_rms, double *rms_seq,
+                      void *stream) {
+  if (!cfg || !exp_obs || !obs_rms || !rms_seq || cfg->minibatch <= 1 || rows < cfg->minibatch) return 1;
+  const int nmb = rows / cfg->minibatch;
+  hipStream_t s = (hipStream_t)stream;
+  double *part = rms_seq + (size_t)nmb * 2 * NIN;
+  hipLaunchKernelGGL(k_obs_moments, dim3(nmb, OM_CH), dim3(TB), 0, s, *cfg, exp_obs, part);
+  USV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_obs_rms_seq, dim3(1), dim3(64), 0, s, *cfg, part, nmb, obs_rms, rms_seq);
   USV_CHECK_LAUNCH();
   return 0;
 }

@@ -270,6 +270,9 @@ class A2CAgent:
         self.meter_buf = torch.zeros(_capi.lib().ppo_meter_floats(N, H), **f32)
         self.meter = self.meter_buf[:H * 4].view(H, 4)
         self.step_dev = torch.zeros(1, device=dev, dtype=torch.int64)   # rollout Philox step (device clock)
+        # running obs statistics after each minibatch of mini-epoch 0 (ppo_obs_rms_epoch)
+        nrs = _capi.lib().ppo_rms_seq_doubles(_capi.byref(self.cfg), B) if self.normalize_input else -1
+        self.rms_seq = torch.zeros(max(nrs, 1), **f64)
         self.kls = torch.zeros(self.mini_epochs_num * self.num_minibatches, **f32)
         # per minibatch: a_loss, c_loss, entropy, b_loss, kl (this rank), written by the reduce kernel
         self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 8), **f32)
@@ -327,9 +330,14 @@ class A2CAgent:
         s = c.stream_ptr()
         dp = self.multi_gpu and self.rank_size > 1
         k = 0
+        seq = self.normalize_input and self.rms_seq.numel() > 1
+        if seq:   # RunningMeanStd.train of mini-epoch 0, all minibatches in two launches
+            c.call("ppo_obs_rms_epoch", cfg, c.ptr(self.exp_obs), self.batch_size, c.ptr(self.obs_rms),
+                   c.ptr(self.rms_seq), s)
         for mini_ep in range(self.mini_epochs_num):
             for i in range(self.num_minibatches):
-                args = (cfg, c.ptr(self.model_params), c.ptr(self.obs_rms), c.ptr(self.val_rms), int(mini_ep == 0), i,
+                rms = self.rms_seq[2 * NIN * i:] if seq and mini_ep == 0 else self.obs_rms
+                args = (cfg, c.ptr(self.model_params), c.ptr(rms), c.ptr(self.val_rms), int(mini_ep == 0 and not seq), i,
                         c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp), c.ptr(self.exp_val),
                         c.ptr(self.exp_ret), c.ptr(self.exp_adv), c.ptr(self.exp_mu), c.ptr(self.exp_sigma),
                         c.ptr(self.grad), c.ptr(self.loss_log[k]), c.ptr(self.partials), c.ptr(self.work))
