@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 METRIC = "env-steps/sec USV_CaptureXY at 1/2/4/8 MI355X; wall-clock to reward=30"
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 FP32_PEAK_TFS = 157.3          # MI355X fp32 vector / f32-MFMA peak (same table)
+BF16_PEAK_TFS = 2500.0         # MI355X dense bf16 MFMA peak (same table, no sparsity)
 # Algorithmic bytes of the fused env-step kernel per env-step:
 # SURVEY §8(d) fused figure (476 B: state, lag, DR params, target, obstacles,
 # reward history, 4 field texels, obs row, reward, done) + the episode_sums
@@ -61,7 +62,7 @@ def _dist_setup(gpus):
     return rank, world, local
 
 
-def build(envs, local, world, seed, task_name="CaptureXY"):
+def build(envs, local, world, seed, task_name="CaptureXY", mixed_precision=False):
     from omniisaacgymenvs_loop_amd.envs.vec_env_rlgames import VecEnvRLGames
     from omniisaacgymenvs_loop_amd.rl_games import vecenv
     from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
@@ -70,6 +71,7 @@ def build(envs, local, world, seed, task_name="CaptureXY"):
     cfg = build_config({"num_envs": envs, "seed": seed, "multi_gpu": world > 1, "rl_device": f"cuda:{local}",
                         "task": TASKS[task_name][0]})
     cfg["train"]["params"]["config"]["train_dir"] = "/tmp/bench_runs"
+    cfg["train"]["params"]["config"]["mixed_precision"] = bool(mixed_precision)
     env = VecEnvRLGames(headless=True)
     task = initialize_task(cfg, env)
     vecenv.register("RLGPU", lambda name, n, **kw: vecenv.RLGPUEnv(name, n, **kw))
@@ -239,6 +241,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph capture)")
     ap.add_argument("--task", default="CaptureXY", choices=sorted(TASKS) + ["multitask"],
                     help="multitask: even ranks GoToPose, odd ranks TrackXYOVelocity, one shared policy (C4)")
+    ap.add_argument("--mixed-precision", action="store_true",
+                    help="bf16 GEMM operands / fp32 accumulation for the policy's 128x128 products (train config "
+                         "mixed_precision; BASELINE configs[2] at --envs 65536); physics stays fp32")
     ap.add_argument("--c2-steps", type=int, default=10,
                     help="epochs of the secondary BASELINE configs[1] line (4096 envs/GPU; 0 = skip)")
     args = ap.parse_args()
@@ -248,7 +253,7 @@ def main():
     task_name = args.task if args.task != "multitask" else ("GoToPose", "TrackXYOVelocity")[rank % 2]
     step_bytes, step_kernel = TASKS[task_name][1], TASKS[task_name][2]
     t_start = time.perf_counter()
-    env, task, agent = build(args.envs, local, world, args.seed + rank, task_name)
+    env, task, agent = build(args.envs, local, world, args.seed + rank, task_name, args.mixed_precision)
     agent.use_graph = not args.no_graph
     from omniisaacgymenvs_loop_amd import _capi
 
@@ -360,13 +365,16 @@ def main():
         out = {
             "metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (random-init policy, "
+            "scaling": "weak", "vs_baseline": None,
+            "dtype": "fp32 physics, bf16 GEMM operands / fp32 accumulate" if args.mixed_precision else "fp32",
+            "data": "synthetic (random-init policy, "
             "randomised spawns/obstacles/DR from the reset path)",
             "config": {"workload": (f"USV_Virtual_CaptureXY num_envs={args.envs}/GPU PPO-MLP fp32"
                                     + (" (BASELINE configs[4] per GPU: 2^20 envs over 8 GPUs)"
                                        if args.envs == HEADLINE_ENVS else "")
                                     if args.task == "CaptureXY" else
-                                    f"USV_Virtual_{args.task} num_envs={args.envs}/GPU PPO-MLP fp32"),
+                                    f"USV_Virtual_{args.task} num_envs={args.envs}/GPU PPO-MLP fp32")
+                       + (" [mixed_precision: bf16 GEMMs]" if args.mixed_precision else ""),
                        "num_envs_per_gpu": args.envs, "horizon_length": agent.horizon_length,
                        "minibatch_size": agent.minibatch_size, "mini_epochs": agent.mini_epochs_num,
                        "parallelism": f"dp{world}"},
@@ -384,7 +392,8 @@ def main():
                              "kernel": "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, 8 waves per 32-row "
                                        "workgroup, fixed-order reduction)",
                              "achieved": ppo_tfs,
-                             "peak": FP32_PEAK_TFS, "unit": "TFLOP/s", "frac": ppo_tfs / FP32_PEAK_TFS,
+                             "peak": BF16_PEAK_TFS if args.mixed_precision else FP32_PEAK_TFS, "unit": "TFLOP/s",
+                             "frac": ppo_tfs / (BF16_PEAK_TFS if args.mixed_precision else FP32_PEAK_TFS),
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},
             "wall_clock_to_reward": dict(to_reward, unit="s", since="first env reset of this run (random-init policy)",
                                          last100_mean_at_end=float(agent.game_rewards.get_mean())),

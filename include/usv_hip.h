@@ -414,7 +414,8 @@ typedef struct ppo_cfg {
   int   lr_adaptive;  float kl_threshold, lr_min, lr_max;
   float reward_scale, reward_shift;
   float rms_eps;            /* 1e-5 */
-  int   pad_;
+  int   bf16_gemm;          /* 0: fp32 (the reference); 1: bf16 operands / fp32 accumulation for the
+                               128x128 products (layer 2, dW2, dh1) -- BASELINE configs[2] */
 } ppo_cfg_t;
 
 /* Rollout: obs RMS normalise (eval) -> MLP -> mu, value (denormalised),

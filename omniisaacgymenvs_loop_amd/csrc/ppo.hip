@@ -42,6 +42,26 @@ typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
+// bf16 GEMM mode (ppo_cfg_t.bf16_gemm, BASELINE configs[2]): the three 128 x 128 products (layer 2,
+// dW2, dh1) take bf16 operands (round to nearest even from the fp32 values in LDS) on
+// v_mfma_f32_32x32x16_bf16 with fp32 accumulation: lane l supplies row / column l & 31 and the 8
+// consecutive k of group l >> 5.  Everything else stays fp32.
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x16 mfma_bf16(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ bf16x8 ld8(const float *p) {          // 8 consecutive floats
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (__bf16)p[j];
+  return v;
+}
+__device__ __forceinline__ bf16x8 ld8s(const float *p, int stride) {   // 8 floats, stride apart
+  bf16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (__bf16)p[j * stride];
+  return v;
+}
 // C/D layout of a 32x32 tile: lane l holds column l&31, rows (r&3) + 8(r>>2) + 4(l>>5), r = 0..15
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
@@ -157,6 +177,7 @@ __device__ __forceinline__ void stage_obs(const float *__restrict__ obs, int row
 
 // Forward of the RB rows staged in s.x (W1, biases, heads staged; W2 still in
 // registers, committed after layer 1); leaves h1, h2, out.
+template <bool kBf>
 __device__ void block_forward(const StagedW &wr, MlpSmem &s) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
@@ -177,10 +198,18 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s) {
   // ---- layer 2: h2 = tanh(h1 W2^T + b2) ----
   {
     f32x16 acc = {};
+    if constexpr (kBf) {
+#pragma unroll
+      for (int st = 0; st < NH / 16; ++st) {
+        const int k0 = 16 * st + 8 * h;
+        acc = mfma_bf16(ld8(&s.h1[i * HS + k0]), ld8(&s.w2[(n0 + i) * HS + k0]), acc);
+      }
+    } else {
 #pragma unroll 16
-    for (int st = 0; st < NH / 2; ++st) {
-      const int k = 2 * st + h;
-      acc = mfma32(s.h1[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
+      for (int st = 0; st < NH / 2; ++st) {
+        const int k = 2 * st + h;
+        acc = mfma32(s.h1[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
+      }
     }
     const float bj = s.tail[T_B2 + n0 + i];
 #pragma unroll
@@ -219,6 +248,7 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s) {
 __host__ __device__ constexpr int policy_grid(int n) {
   return (n + RB - 1) / RB < 256 ? (n + RB - 1) / RB : 256;
 }
+template <bool kBf>
 __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms,
                                                     const double *__restrict__ val_rms, const float *__restrict__ obs,
@@ -246,7 +276,7 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
   if (tile == (int)blockIdx.x) stage_store_small(wr, s);
   __syncthreads();
-  block_forward(wr, s);   // re-commits the same W2 values on later tiles
+  block_forward<kBf>(wr, s);   // re-commits the same W2 values on later tiles
   const int r = threadIdx.x;
   if (r < nrows) {
     const int e = row0 + r;
@@ -287,6 +317,7 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   }
 }
 
+template <bool kBf>
 __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,
                                               const double *val_rms, const float *__restrict__ obs, float *values) {
   __shared__ MlpSmem s;
@@ -300,7 +331,7 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
     stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
     if (tile == (int)blockIdx.x) stage_store_small(wr, s);
     __syncthreads();
-    block_forward(wr, s);
+    block_forward<kBf>(wr, s);
     const int r = threadIdx.x;
     if (r < nrows) {
       float vd = s.out[r * 4 + 2];
@@ -686,6 +717,7 @@ struct PartOut {
   }
 };
 
+template <bool kBf>
 __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__restrict__ P,
                                           const double *__restrict__ obs_rms, int row0,
                                           const float *__restrict__ e_obs, const float *__restrict__ e_act,
@@ -798,10 +830,18 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   const int ra = (i + 16 * kh) & (RB - 1);
   {
     f32x16 acc = {};
+    if constexpr (kBf) {
+#pragma unroll
+      for (int st = 0; st < NH / 32; ++st) {
+        const int k0 = 64 * kh + 16 * st + 8 * h;
+        acc = mfma_bf16(ld8(&s.h1[ra * HS + k0]), ld8(&s.w2[(n0 + i) * HS + k0]), acc);
+      }
+    } else {
 #pragma unroll 16
-    for (int st = 0; st < NH / 4; ++st) {
-      const int k = 64 * kh + 2 * st + h;
-      acc = mfma32(s.h1[ra * HS + k], s.w2[(n0 + i) * HS + k], acc);
+      for (int st = 0; st < NH / 4; ++st) {
+        const int k = 64 * kh + 2 * st + h;
+        acc = mfma32(s.h1[ra * HS + k], s.w2[(n0 + i) * HS + k], acc);
+      }
     }
     USV_PHASE(ppo, 11);
     // the two K halves meet in LDS as (lower half + upper half) + bias (fp32 addition commutes,
@@ -953,19 +993,35 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   // second tile's chain, the second tile's during dh1); sched_barrier keeps them there ----
   const int tile0 = 4 * cb + 2 * kh;
   f32x16 dw0 = {}, dw1 = {};
+  if constexpr (kBf) {   // K = the 32 rows: r = 16 st + 8 h + j
 #pragma unroll
-  for (int st = 0; st < RB / 2; ++st) {
-    const int r = st + (RB / 2) * h;
-    dw0 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh) + i], dw0);
-  }
+    for (int st = 0; st < RB / 16; ++st) {
+      const int r0 = 16 * st + 8 * h;
+      dw0 = mfma_bf16(ld8s(&s.h2[r0 * HS + n0 + i], HS), ld8s(&s.h1[r0 * HS + 32 * (2 * kh) + i], HS), dw0);
+    }
 #pragma unroll
-  for (int st = 0; st < RB / 2; ++st) {
-    const int r = st + (RB / 2) * h;
-    dw1 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh + 1) + i], dw1);
-    if ((st & 3) == 1) {
-      const int a = st >> 2;
+    for (int st = 0; st < RB / 16; ++st) {
+      const int r0 = 16 * st + 8 * h;
+      dw1 = mfma_bf16(ld8s(&s.h2[r0 * HS + n0 + i], HS), ld8s(&s.h1[r0 * HS + 32 * (2 * kh + 1) + i], HS), dw1);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
       part_st.x4(acc_slot(S_W2, tile0, a, lane), dw0[4 * a], dw0[4 * a + 1], dw0[4 * a + 2], dw0[4 * a + 3]);
-      __builtin_amdgcn_sched_barrier(0);
+  } else {
+#pragma unroll
+    for (int st = 0; st < RB / 2; ++st) {
+      const int r = st + (RB / 2) * h;
+      dw0 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh) + i], dw0);
+    }
+#pragma unroll
+    for (int st = 0; st < RB / 2; ++st) {
+      const int r = st + (RB / 2) * h;
+      dw1 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh + 1) + i], dw1);
+      if ((st & 3) == 1) {
+        const int a = st >> 2;
+        part_st.x4(acc_slot(S_W2, tile0, a, lane), dw0[4 * a], dw0[4 * a + 1], dw0[4 * a + 2], dw0[4 * a + 3]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
   }
   USV_PHASE(ppo, 13);
@@ -974,14 +1030,25 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   // (A-operand rows rotated as in layer 2) ----
   {
     f32x16 dh = {};
+    if constexpr (kBf) {
 #pragma unroll
-    for (int st = 0; st < NH / 4; ++st) {
-      const int j = 64 * kh + 2 * st + h;
-      dh = mfma32(s.h2[ra * HS + j], s.w2[j * HS + n0 + i], dh);
-      if ((st & 3) == 1 && st < 16) {
-        const int a = st >> 2;
-        part_st.x4(acc_slot(S_W2, tile0 + 1, a, lane), dw1[4 * a], dw1[4 * a + 1], dw1[4 * a + 2], dw1[4 * a + 3]);
+      for (int st = 0; st < NH / 32; ++st) {
+        const int j0 = 64 * kh + 16 * st + 8 * h;
+        dh = mfma_bf16(ld8(&s.h2[ra * HS + j0]), ld8s(&s.w2[j0 * HS + n0 + i], HS), dh);
+        part_st.x4(acc_slot(S_W2, tile0 + 1, st, lane), dw1[4 * st], dw1[4 * st + 1], dw1[4 * st + 2],
+                   dw1[4 * st + 3]);
         __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int st = 0; st < NH / 4; ++st) {
+        const int j = 64 * kh + 2 * st + h;
+        dh = mfma32(s.h2[ra * HS + j], s.w2[j * HS + n0 + i], dh);
+        if ((st & 3) == 1 && st < 16) {
+          const int a = st >> 2;
+          part_st.x4(acc_slot(S_W2, tile0 + 1, a, lane), dw1[4 * a], dw1[4 * a + 1], dw1[4 * a + 2], dw1[4 * a + 3]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
     USV_PHASE(ppo, 6);
@@ -1026,6 +1093,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   USV_PHASE(ppo, 8);
 }
 
+template <bool kBf>
 __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms, int row0,
                                                     const float *__restrict__ e_obs, const float *__restrict__ e_act,
@@ -1033,7 +1101,7 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__
                                                     const float *__restrict__ e_ret, const float *__restrict__ e_adv,
                                                     float *e_mu, float *e_sigma, float *partials) {
   __shared__ GradSmem s;
-  mb_grad8w(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
+  mb_grad8w<kBf>(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
 }
 
 // k_reduce_partials: the per-workgroup partial rows (stride NPART_PAD floats, 16-B aligned)
@@ -1209,7 +1277,7 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
                     const float *eps_inject, void *stream) {
   if (!cfg || !params || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
   const int grid = policy_grid(cfg->n_envs);
-  hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
+  hipLaunchKernelGGL(cfg->bf16_gemm ? k_policy_step<true> : k_policy_step<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
                      obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
                      actions_out, seed, step, step_dev, eps_inject);
   USV_CHECK_LAUNCH();
@@ -1220,7 +1288,7 @@ int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, 
               const float *obs, float *values, void *stream) {
   if (!cfg || !params || !obs || !values || cfg->n_envs <= 0) return 1;
   const int grid = policy_grid(cfg->n_envs);
-  hipLaunchKernelGGL(k_value, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
+  hipLaunchKernelGGL(cfg->bf16_gemm ? k_value<true> : k_value<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
                      values);
   USV_CHECK_LAUNCH();
   return 0;
@@ -1284,7 +1352,7 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
     USV_CHECK_LAUNCH();
   }
   const int nblk = cfg->minibatch / RB;
-  hipLaunchKernelGGL(k_mb_grad, dim3(nblk), dim3(GTB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
+  hipLaunchKernelGGL(cfg->bf16_gemm ? k_mb_grad<true> : k_mb_grad<false>, dim3(nblk), dim3(GTB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
                      exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials);
   USV_CHECK_LAUNCH();
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;

@@ -199,6 +199,11 @@ class A2CAgent:
         c.reward_scale = float(rs.get("scale_value", 1.0))
         c.reward_shift = float(rs.get("shift_value", 0.0))
         c.rms_eps = 1e-5
+        # mixed_precision (a2c_common.py:242-243: torch.cuda.amp autocast + GradScaler in the reference) maps to
+        # the MI355X bf16 GEMM mode: bf16 operands / fp32 accumulation for the 128x128 products, fp32
+        # elsewhere (no loss scaling needed with bf16's exponent range) -- BASELINE configs[2]
+        self.mixed_precision = bool(config.get("mixed_precision", False))
+        c.bf16_gemm = int(self.mixed_precision)
         self._alloc()
         self.frame = 0
         self.epoch_num = 0

@@ -73,10 +73,24 @@ class RMS:
         return (np.sqrt(self.var.astype(F) + F(self.eps)) * y + self.mean.astype(F)).astype(F)
 
 
-def forward(P: dict, x: np.ndarray):
+def bf16(a: np.ndarray) -> np.ndarray:
+    """fp32 -> bf16 (round to nearest even) -> fp32: the operand rounding of the bf16 GEMM mode
+    (ppo_cfg_t.bf16_gemm: the 128x128 products -- layer 2, dW2, dh1 -- take bf16 operands with fp32
+    accumulation on v_mfma_f32_32x32x16_bf16; everything else stays fp32)."""
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    out = r.astype(np.uint32).view(np.float32)
+    return np.where(np.isnan(a), a, out).astype(F)
+
+
+def _mm(a, b, lowp):
+    return (bf16(a) @ bf16(b)).astype(F) if lowp else (a @ b).astype(F)
+
+
+def forward(P: dict, x: np.ndarray, lowp: bool = False):
     z1 = x @ P["W1"].T + P["b1"]
     h1 = np.tanh(z1).astype(F)
-    z2 = h1 @ P["W2"].T + P["b2"]
+    z2 = _mm(h1, P["W2"].T, lowp) + P["b2"]
     h2 = np.tanh(z2).astype(F)
     mu = (h2 @ P["Wmu"].T + P["bmu"]).astype(F)
     v = (h2 @ P["Wv"].T + P["bv"]).astype(F)
@@ -145,10 +159,12 @@ class Adam:
         return (p - F(step_size) * (self.m / denom)).astype(F)
 
 
-def minibatch_grad(P: dict, xn, act, old_nlp, old_val, ret, adv, old_mu, old_sigma, cfg: PPOConfig):
-    """Forward + losses + explicit backward of A2CAgent.calc_gradients (a2c_continuous.py:78-196)."""
+def minibatch_grad(P: dict, xn, act, old_nlp, old_val, ret, adv, old_mu, old_sigma, cfg: PPOConfig,
+                   lowp: bool = False):
+    """Forward + losses + explicit backward of A2CAgent.calc_gradients (a2c_continuous.py:78-196);
+    lowp: the bf16 GEMM mode's operand rounding (see bf16())."""
     B = xn.shape[0]
-    h1, h2, mu, v = forward(P, xn)
+    h1, h2, mu, v = forward(P, xn, lowp)
     v = v[:, 0]
     logstd = mu * F(0) + P["sigma"]
     sigma = np.exp(logstd).astype(F)
@@ -190,9 +206,9 @@ def minibatch_grad(P: dict, xn, act, old_nlp, old_val, ret, adv, old_mu, old_sig
     G["bv"] = np.array([dv.sum()], F)
     dh2 = dmu @ P["Wmu"] + dv[:, None] @ P["Wv"]
     dz2 = dh2 * (F(1) - h2 * h2)
-    G["W2"] = dz2.T @ h1
+    G["W2"] = _mm(dz2.T, h1, lowp)
     G["b2"] = dz2.sum(0)
-    dh1 = dz2 @ P["W2"]
+    dh1 = _mm(dz2, P["W2"], lowp)
     dz1 = dh1 * (F(1) - h1 * h1)
     G["W1"] = dz1.T @ xn
     G["b1"] = dz1.sum(0)
