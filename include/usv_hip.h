@@ -498,6 +498,34 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
                         float *adam_v, float *opt, int opt_slot, float grad_scale,
                         float *kl_out, int norm_from_partials, void *stream);
 
+/* The single-GPU minibatch chain in two launches per minibatch instead of three (the same
+ * training step as ppo_minibatch_grad + ppo_minibatch_apply(norm_from_partials = 1), bit for
+ * bit).  The parameters and Adam moments live in two banks; minibatch seq (0-based position in
+ * the update's chain: mini-epoch x num_minibatches + minibatch) trains on bank seq % 2, and its
+ * reduce kernel takes the Adam step with clip coefficient 1 into bank (seq + 1) % 2.  The clip
+ * norm needs the whole gradient, so the next launch (minibatch seq + 1's gradient kernel, or
+ * ppo_minibatch_finish after the last minibatch) checks it: when clipping was due it redoes
+ * the step from bank seq % 2 and writes the result over bank (seq + 1) % 2.  The optimiser
+ * scalars advance as with ppo_minibatch_apply (slot seq % 2 -> (seq + 1) % 2); kl_prev_out
+ * receives minibatch seq - 1's KL (seq > 0), ppo_minibatch_finish's kl_out the last one's.
+ * After a chain of count minibatches the state is in bank count % 2 (the caller copies it
+ * back to bank 0 when count is odd).  Not for several ranks (the gradient is all-reduced
+ * between the reduction and the step there: ppo_minibatch_grad / ppo_minibatch_apply).
+ * Status 4: a bank pointer is NULL or params[i] is not 16-byte aligned. */
+typedef struct ppo_adam_banks {
+  float *params[2];
+  float *m[2];
+  float *v[2];
+  float *opt;                          /* [2][8], as ppo_minibatch_apply */
+} ppo_adam_banks_t;
+int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int seq, double *obs_rms,
+                        int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+                        const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
+                        float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
+                        float *kl_prev_out, void *stream);
+int ppo_minibatch_finish(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int count, const float *grad,
+                         float *kl_out, void *stream);
+
 /* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad (16-byte aligned) */
 int ppo_partials_floats(int minibatch);
 /* size (floats) of the grad buffer of ppo_minibatch_grad / ppo_minibatch_apply */

@@ -96,6 +96,10 @@ class PpoCfg(ctypes.Structure):
     _fields_ = _struct_fields(_TXT, "ppo_cfg", DEFINES)
 
 
+class PpoAdamBanks(ctypes.Structure):
+    _fields_ = _struct_fields(_TXT, "ppo_adam_banks", DEFINES)
+
+
 def enum_values(enum_name: str) -> dict:
     m = re.search(r"enum\s+%s\s*\{(.*?)\}" % enum_name, _TXT, flags=re.S)
     vals, cur = {}, -1

@@ -68,6 +68,8 @@ def _declare(lib):
         "ppo_prepare": [P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_grad": [P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_apply": [P, P, P, P, P, P, I, F, P, I, P],
+        "ppo_minibatch_fused": [P, P, I, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+        "ppo_minibatch_finish": [P, P, I, P, P, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
         "ppo_obs_rms_epoch": [P, P, I, P, P, P],

@@ -653,6 +653,85 @@ __global__ void k_obs_rms_seq(ppo_cfg_t c, const double *__restrict__ part, int 
 // 16 dW2 tiles go two per wave; the row inputs of the losses are loaded with the
 // weights, so nothing in the loss phase waits on memory.
 constexpr int GTB = 512;          // threads per workgroup
+
+// k_reduce_partials geometry (RED_BLOCKS chunk squares follow the gradient in grad[])
+#ifndef USV_RD_P
+#define USV_RD_P 128
+#endif
+constexpr int RD_TB = 512, RD_P = USV_RD_P;            // threads, slots per workgroup
+constexpr int RD_L = RD_P / 4;                          // lanes per row segment (float4 each)
+constexpr int RD_G = (RD_TB / RD_L);                    // row groups
+constexpr int RD_KB = 16;                               // loads in flight per lane
+constexpr int RED_BLOCKS = (PPO_NPARAM + 5 + RD_P - 1) / RD_P;
+static_assert(RD_P % 4 == 0 && 64 % RD_L == 0 && RD_P <= RD_TB, "reduce geometry");
+static_assert(RED_BLOCKS <= 256, "chunk squares: one per thread of waves 0-3");
+
+// ---- Adam (torch.optim.Adam, amsgrad off), shared by k_apply, the speculative step of
+// k_reduce_partials and the redo of a clipped step in the chained gradient kernel ----
+struct AdamBanks {                 // state before ([0]) and after ([1]) one step
+  const float *P0, *m0, *v0;
+  float *P1, *m1, *v1;
+};
+struct AdamK {
+  float step_size, bc2s;
+};
+__device__ __forceinline__ AdamK adam_consts(const ppo_cfg_t &c, float lr, float step) {
+  // torch.optim.Adam forms the bias corrections in Python doubles
+  const double bc1 = 1.0 - pow((double)c.adam_b1, (double)step);
+  const double bc2 = 1.0 - pow((double)c.adam_b2, (double)step);
+  return {(float)((double)lr / bc1), (float)sqrt(bc2)};
+}
+__device__ __forceinline__ void adam_one(const ppo_cfg_t &c, const AdamK &k, float g, float p_old, float m_old,
+                                         float v_old, float &pn, float &mn, float &vn) {
+  if (c.weight_decay != 0.f) g = g + c.weight_decay * p_old;
+  mn = m_old + (1.0f - c.adam_b1) * (g - m_old);          // exp_avg.lerp_(grad, 1 - beta1)
+  vn = v_old * c.adam_b2 + (1.0f - c.adam_b2) * g * g;    // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+  const float denom = sqrtf(vn) / k.bc2s + c.adam_eps;
+  pn = p_old - k.step_size * (mn / denom);
+}
+// clip_grad_norm_'s coefficient (1 without truncate_grads)
+__device__ __forceinline__ float clip_coef(const ppo_cfg_t &c, float total_norm) {
+  float coef = 1.0f;
+  if (c.truncate_grads) {
+    coef = c.grad_norm / (total_norm + 1e-6f);
+    coef = fminf(coef, 1.0f);
+  }
+  return coef;
+}
+// AdaptiveScheduler.update on a minibatch's KL (schedulers.py:26-32) and the optimiser
+// scalars after its step: opt_in -> opt_out = (lr, step, kl, norm, ...)
+template <class OptIn>
+__device__ __forceinline__ void opt_advance(const ppo_cfg_t &c, const OptIn &opt_in, float *opt_out, float kl,
+                                            float total_norm, float *kl_out) {
+  const float lr = opt_in[0];
+  float nl = lr, kl_keep = opt_in[2];
+  if (c.lr_adaptive) {
+    if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
+    if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
+    kl_keep = kl;
+    if (kl_out) *kl_out = kl;
+  }
+  opt_out[0] = nl;
+  opt_out[1] = opt_in[1] + 1.0f;
+  opt_out[2] = kl_keep;
+  opt_out[3] = total_norm;
+#pragma unroll
+  for (int i = 4; i < 8; ++i) opt_out[i] = opt_in[i];
+}
+
+// The chained single-GPU update (ppo_minibatch_fused): minibatch k's gradient kernel stages
+// the parameters minibatch k-1's reduce kernel stepped speculatively (bank cur), checks that
+// step's clip norm and, when clipping was due, redoes it from bank prev (and writes the redone
+// state over bank cur); workgroup 0 advances the optimiser scalars of minibatch k-1.
+struct ChainIn {
+  const float *P_prev, *m_prev, *v_prev;   // state before minibatch k-1's step
+  float *P_cur, *m_cur, *v_cur;            // its speculative result (the kernel's P)
+  const float *grad;                       // minibatch k-1: gradient, KL, chunk squares
+  const float *opt_prev;                   // optimiser scalars read by minibatch k-1's step
+  float *opt_cur;                          // ... and the ones after it (read by minibatch k's)
+  float *kl_out;                           // minibatch k-1's KL (log)
+};
+
 struct GradSmem {
   float w2[NH * HS];              // W2[j][k]
   float w1[NH * XS];              // W1[j][k], k 33..35 = 0
@@ -665,6 +744,7 @@ struct GradSmem {
   float hg[4][4][NH];             // head-gradient / b2 quarter sums
   float b1[NH];
   float tail[TAIL + 1];
+  float nrm[4];                   // chained update: wave sums of the chunk squares
 };
 
 // Partial-gradient slot layout (a permutation of the parameters, then the loss sums): the
@@ -717,8 +797,42 @@ struct PartOut {
   }
 };
 
-template <bool kBf>
-__device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__restrict__ P,
+// chained update, clipping due: minibatch k-1's step redone from bank prev with the clip
+// coefficient, straight into this workgroup's LDS weights (and sigma into ls0 / ls1);
+// workgroup (q / GTB) % grid writes parameter chunk q / GTB of the redone state over bank cur
+// (no workgroup of this launch reads bank cur after its first barrier)
+__device__ __forceinline__ void redo_step(const ppo_cfg_t &c, const ChainIn &ch, const float (&op)[8], float coef,
+                                          GradSmem &s, float &ls0, float &ls1) {
+  const AdamK ak = adam_consts(c, op[0], op[1] + 1.0f);
+  for (int q = threadIdx.x; q < PPO_NPARAM; q += GTB) {
+    float pn, mn, vn;
+    adam_one(c, ak, ch.grad[q] * 1.0f * coef, ch.P_prev[q], ch.m_prev[q], ch.v_prev[q], pn, mn, vn);
+    if ((q / GTB) % gridDim.x == blockIdx.x) {
+      ch.P_cur[q] = pn; ch.m_cur[q] = mn; ch.v_cur[q] = vn;
+    }
+    if (q >= PPO_OFF_B2) {
+      s.tail[q - PPO_OFF_B2] = pn;
+    } else if (q >= PPO_OFF_W2) {
+      const int e = q - PPO_OFF_W2;
+      s.w2[(e / NH) * HS + e % NH] = pn;
+    } else if (q >= PPO_OFF_B1) {
+      s.b1[q - PPO_OFF_B1] = pn;
+    } else if (q >= PPO_OFF_W1) {
+      const int e = q - PPO_OFF_W1;
+      s.w1[(e / NIN) * XS + e % NIN] = pn;
+    }
+  }
+  float pn, mn, vn;
+  adam_one(c, ak, ch.grad[PPO_OFF_SIGMA] * 1.0f * coef, ch.P_prev[PPO_OFF_SIGMA], ch.m_prev[PPO_OFF_SIGMA],
+           ch.v_prev[PPO_OFF_SIGMA], pn, mn, vn);
+  ls0 = pn;
+  adam_one(c, ak, ch.grad[PPO_OFF_SIGMA + 1] * 1.0f * coef, ch.P_prev[PPO_OFF_SIGMA + 1],
+           ch.m_prev[PPO_OFF_SIGMA + 1], ch.v_prev[PPO_OFF_SIGMA + 1], pn, mn, vn);
+  ls1 = pn;
+}
+
+template <bool kBf, bool kChain>
+__device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch, const float *__restrict__ P,
                                           const double *__restrict__ obs_rms, int row0,
                                           const float *__restrict__ e_obs, const float *__restrict__ e_act,
                                           const float *__restrict__ e_nlp, const float *__restrict__ e_val,
@@ -753,7 +867,16 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
     if (NW2X > 0 && tid < NW2X) w2x = P4[W2Q0 + NW2U * GTB + tid];
   }
   const float b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
-  const float lsig0 = P[PPO_OFF_SIGMA], lsig1 = P[PPO_OFF_SIGMA + 1];
+  float lsig0 = P[PPO_OFF_SIGMA], lsig1 = P[PPO_OFF_SIGMA + 1];
+  // chained update: minibatch k-1's chunk squares (its clip norm)
+  const float csq = (kChain && tid < RED_BLOCKS) ? ch.grad[PPO_NPARAM + 8 + tid] : 0.f;
+  // ... and its optimiser scalars and KL (uniform: scalar loads, in flight with the rest)
+  float op[8] = {}, kl_prev = 0.f;
+  if constexpr (kChain) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) op[q] = ch.opt_prev[q];
+    kl_prev = ch.grad[PPO_NPARAM];
+  }
   RowIn ri = {};
   if (tid < RB) {
     const size_t row = (size_t)rb0 + tid;
@@ -795,7 +918,23 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   for (int u = 0; u < NTLG; ++u)
     if (tid + u * GTB < TAIL) s.tail[tid + u * GTB] = tlr[u];
   if (tid < NH) s.b1[tid] = b1r;
+  if (kChain && w < 4) {   // k_apply's norm: the same lanes, the same order
+    const float t = wave_sum(csq);
+    if (lane == 0) s.nrm[w] = t;
+  }
   __syncthreads();
+  bool slow = false;
+  if constexpr (kChain) {
+    const float total_norm = sqrtf(((s.nrm[0] + s.nrm[1]) + s.nrm[2]) + s.nrm[3]);
+    const float coef = clip_coef(c, total_norm);
+    if (blockIdx.x == 0 && tid == 0)
+      opt_advance(c, op, ch.opt_cur, kl_prev, total_norm, ch.kl_out);
+    if (coef < 1.0f) {   // uniform over the launch
+      slow = true;
+      redo_step(c, ch, op, coef, s, lsig0, lsig1);
+      __syncthreads();
+    }
+  }
   USV_PHASE(ppo, 1);
   if (kh == 0) {
     // ---- layer 1 (waves 0-3): h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero) ----
@@ -817,9 +956,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
       if (e0 >= 0) *reinterpret_cast<float2 *>(&s.w2[(e0 >> 7) * HS + (e0 & (NH - 1))]) = make_float2(v.x, v.y);
       if (e1 < NH * NH) *reinterpret_cast<float2 *>(&s.w2[(e1 >> 7) * HS + (e1 & (NH - 1))]) = make_float2(v.z, v.w);
     };
+    if (!slow) {
 #pragma unroll
-    for (int u = 0; u < NW2U; ++u) put_w2(tid + u * GTB, w2q[u]);
-    if (NW2X > 0 && tid < NW2X) put_w2(NW2U * GTB + tid, w2x);
+      for (int u = 0; u < NW2U; ++u) put_w2(tid + u * GTB, w2q[u]);
+      if (NW2X > 0 && tid < NW2X) put_w2(NW2U * GTB + tid, w2x);
+    }
   }
   __syncthreads();
   USV_PHASE(ppo, 10);
@@ -1093,15 +1234,15 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const float *__res
   USV_PHASE(ppo, 8);
 }
 
-template <bool kBf>
-__global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__restrict__ P,
+template <bool kBf, bool kChain>
+__global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, ChainIn ch, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms, int row0,
                                                     const float *__restrict__ e_obs, const float *__restrict__ e_act,
                                                     const float *__restrict__ e_nlp, const float *__restrict__ e_val,
                                                     const float *__restrict__ e_ret, const float *__restrict__ e_adv,
                                                     float *e_mu, float *e_sigma, float *partials) {
   __shared__ GradSmem s;
-  mb_grad8w<kBf>(c, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
+  mb_grad8w<kBf, kChain>(c, ch, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
 }
 
 // k_reduce_partials: the per-workgroup partial rows (stride NPART_PAD floats, 16-B aligned)
@@ -1112,17 +1253,15 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, const float *__
 // 2w + h takes rows g, g + 16, g + 32, ...) with all 16 loads of a lane in flight,
 // then the 16 group sums are added in group order through LDS.  Also writes the KL /
 // loss means and the chunk's squared norm (k_apply's clip norm on one rank).
-#ifndef USV_RD_P
-#define USV_RD_P 128
-#endif
-constexpr int RD_TB = 512, RD_P = USV_RD_P;            // threads, slots per workgroup
-constexpr int RD_L = RD_P / 4;                          // lanes per row segment (float4 each)
-constexpr int RD_G = (RD_TB / RD_L);                    // row groups
-constexpr int RD_KB = 16;                               // loads in flight per lane
-constexpr int RED_BLOCKS = (PPO_NPARAM + 5 + RD_P - 1) / RD_P;
-static_assert(RD_P % 4 == 0 && 64 % RD_L == 0 && RD_P <= RD_TB, "reduce geometry");
+//
+// With kSpec (the chained single-GPU update, ppo_minibatch_fused) the workgroup also takes the
+// Adam step of its parameters speculatively, with clip coefficient 1 (a.from -> a.to): the clip
+// norm needs every chunk, and the next kernel (the next minibatch's gradient kernel or
+// k_apply<.., true>) checks it and redoes the step when clipping was due.
+template <bool kSpec>
 __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
-                                                           float *losses, float inv_b) {
+                                                           float *losses, float inv_b, ppo_cfg_t c, AdamBanks a,
+                                                           const float *__restrict__ opt_in) {
   __shared__ float4 red[RD_G][RD_L];
   __shared__ float sqw[RD_TB / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1130,18 +1269,36 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
   const int p4 = blockIdx.x * RD_L + col;                 // float4 column of the partial rows
   const bool ok = p4 < NPART_PAD / 4;
   const float4 *P4 = reinterpret_cast<const float4 *>(partials);
+  // the speculative step's inputs, loaded before the partial rows
+  const int myslot = blockIdx.x * RD_P + tid;
+  const bool mine = kSpec && tid < RD_P && myslot < S_END;
+  const int pq = mine ? param_of_slot(myslot) : 0;
+  float p_old = 0.f, m_old = 0.f, v_old = 0.f, lr = 0.f, step = 0.f;
+  if (mine) {
+    p_old = a.P0[pq]; m_old = a.m0[pq]; v_old = a.v0[pq];
+    lr = opt_in[0]; step = opt_in[1] + 1.0f;
+  }
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  AdamK ak = {0.f, 1.f};
+  const int p4c = min(p4, NPART_PAD / 4 - 1);
   for (int b0 = grp; b0 < nblk; b0 += RD_G * RD_KB) {
+    // branch-free: clamped rows / columns loaded, masked in the sum (every load in flight at once)
     float4 x[RD_KB];
 #pragma unroll
-    for (int k = 0; k < RD_KB; ++k)
-      x[k] = (ok && b0 + RD_G * k < nblk) ? P4[(size_t)(b0 + RD_G * k) * (NPART_PAD / 4) + p4]
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < RD_KB; ++k) x[k] = P4[(size_t)min(b0 + RD_G * k, nblk - 1) * (NPART_PAD / 4) + p4c];
+    // the bias corrections in the shadow of the row loads (they wait on opt_in only)
+    if (kSpec && mine) {
+      ak = adam_consts(c, lr, step);
+      __asm__ volatile("" : : "v"(ak.step_size), "v"(ak.bc2s));
+    }
 #pragma unroll
     for (int k = 0; k < RD_KB; ++k) {
-      acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w;
+      if (ok && b0 + RD_G * k < nblk) {
+        acc.x += x[k].x; acc.y += x[k].y; acc.z += x[k].z; acc.w += x[k].w;
+      }
     }
   }
+  if (kSpec && mine && grp >= nblk) ak = adam_consts(c, lr, step);   // (row group without rows)
   red[grp][col] = acc;
   __syncthreads();
   float sq = 0.f;
@@ -1153,6 +1310,11 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     if (slot < S_END) {
       grad[param_of_slot(slot)] = s;
       sq = s * s;
+      if (mine) {   // k_apply's step with grad_scale = coef = 1 (g * 1 * 1 == g)
+        float pn, mn, vn;
+        adam_one(c, ak, s, p_old, m_old, v_old, pn, mn, vn);
+        a.P1[pq] = pn; a.m1[pq] = mn; a.v1[pq] = vn;
+      }
     } else if (slot < PPO_NPARAM + 5) {
       const int q = slot - PPO_NPARAM;
       if (q == 4) grad[PPO_NPARAM] = s * inv_b;      // kl mean rides with the gradient (all-reduce)
@@ -1174,14 +1336,17 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
 
 // clip_grad_norm_ + Adam + AdaptiveScheduler.  Every workgroup forms the same
 // total norm (same order) and the same next learning rate, and updates its 256
-// parameters.  The optimiser scalars are double-buffered: the launch reads slot
-// opt_in and workgroup 0 writes the next values to slot opt_out, so no workgroup
-// waits for another (no completion counter, no device-scope fence).
+// parameters (bank a.*0 -> a.*1; the same buffers for an in-place step).  The optimiser
+// scalars are double-buffered: the launch reads slot opt_in and workgroup 0 writes the next
+// values to slot opt_out, so no workgroup waits for another (no completion counter, no
+// device-scope fence).  kFinish closes a chain of ppo_minibatch_fused launches: the last
+// reduce kernel already took the unclipped step into bank 1, so parameters are written only
+// when clipping was due.
 constexpr int AP_TB = 256;
-template <bool kNormFromPartials>
-__global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const float *__restrict__ grad_in,
-                                                 float *m, float *v, const float *__restrict__ opt_in,
-                                                 float *__restrict__ opt_out, float grad_scale, float *kl_out) {
+template <bool kNormFromPartials, bool kFinish>
+__global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, AdamBanks a, const float *__restrict__ grad_in,
+                                                 const float *__restrict__ opt_in, float *__restrict__ opt_out,
+                                                 float grad_scale, float *kl_out) {
   __shared__ float red[AP_TB / 64];
   const int tid = threadIdx.x;
   const int q = blockIdx.x * AP_TB + tid;
@@ -1189,26 +1354,20 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   // every load this thread needs is issued before anything waits: its parameter,
   // moments and gradient, then the norm inputs; the double-precision bias
   // corrections below are computed while they are in flight
-  const float g_raw = grad_in[qc], p_old = P[qc], m_old = m[qc], v_old = v[qc];
+  const float g_raw = grad_in[qc], p_old = a.P0[qc], m_old = a.m0[qc], v_old = a.v0[qc];
   // the reduce kernel's per-chunk squares (fixed order; loaded unconditionally: no branch)
-  static_assert(RED_BLOCKS <= 2 * AP_TB, "two chunk squares per thread");
   const float s0 = grad_in[PPO_NPARAM + 8 + min(tid, RED_BLOCKS - 1)];
-  const float s1 = grad_in[PPO_NPARAM + 8 + min(tid + AP_TB, RED_BLOCKS - 1)];
   const float lr = opt_in[0];
   const float step = opt_in[1] + 1.0f;
   const float kl = grad_in[PPO_NPARAM] * grad_scale;
   __builtin_amdgcn_sched_barrier(0);   // the loads above issue first
-  // torch.optim.Adam forms the bias corrections in Python doubles
-  const double bc1 = 1.0 - pow((double)c.adam_b1, (double)step);
-  const double bc2 = 1.0 - pow((double)c.adam_b2, (double)step);
-  const float step_size = (float)((double)lr / bc1);
-  const float bc2s = (float)sqrt(bc2);
+  const AdamK ak = adam_consts(c, lr, step);
   // pin the bias corrections here, in the shadow of the loads above (the scheduler
   // would otherwise sink them past the norm's barrier onto the critical path)
-  __asm__ volatile("" : : "v"(step_size), "v"(bc2s));
+  __asm__ volatile("" : : "v"(ak.step_size), "v"(ak.bc2s));
   float ss = 0.f;
   if (kNormFromPartials) {
-    ss = (tid < RED_BLOCKS ? s0 : 0.f) + (tid + AP_TB < RED_BLOCKS ? s1 : 0.f);
+    ss = tid < RED_BLOCKS ? s0 : 0.f;
   } else {
     // total norm of the (all-reduced) gradient: 16-byte aligned, checked on the host
     constexpr int N4 = PPO_NPARAM / 4, U = (N4 + AP_TB - 1) / AP_TB;
@@ -1232,38 +1391,15 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, float *P, const fl
   if ((tid & 63) == 0) red[tid >> 6] = ss;
   __syncthreads();
   const float total_norm = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
-  float coef = 1.0f;
-  if (c.truncate_grads) {
-    coef = c.grad_norm / (total_norm + 1e-6f);
-    coef = fminf(coef, 1.0f);
+  const float coef = clip_coef(c, total_norm);
+  if (q < PPO_NPARAM && (!kFinish || coef < 1.0f)) {
+    float pn, mn, vn;
+    adam_one(c, ak, g_raw * grad_scale * coef, p_old, m_old, v_old, pn, mn, vn);
+    a.P1[q] = pn;
+    a.m1[q] = mn;
+    a.v1[q] = vn;
   }
-  if (q < PPO_NPARAM) {
-    float g = g_raw * grad_scale * coef;
-    if (c.weight_decay != 0.f) g = g + c.weight_decay * p_old;
-    float mi = m_old, vi = v_old;
-    mi = mi + (1.0f - c.adam_b1) * (g - mi);          // exp_avg.lerp_(grad, 1 - beta1)
-    vi = vi * c.adam_b2 + (1.0f - c.adam_b2) * g * g;  // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
-    const float denom = sqrtf(vi) / bc2s + c.adam_eps;
-    P[q] = p_old - step_size * (mi / denom);
-    m[q] = mi;
-    v[q] = vi;
-  }
-  if (blockIdx.x == 0 && tid == 0) {
-    // AdaptiveScheduler.update on this minibatch's KL (schedulers.py:26-32)
-    float nl = lr, kl_keep = opt_in[2];
-    if (c.lr_adaptive) {
-      if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
-      if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
-      kl_keep = kl;
-      if (kl_out) *kl_out = kl;
-    }
-    opt_out[0] = nl;
-    opt_out[1] = step;
-    opt_out[2] = kl_keep;
-    opt_out[3] = total_norm;
-#pragma unroll
-    for (int i = 4; i < 8; ++i) opt_out[i] = opt_in[i];
-  }
+  if (blockIdx.x == 0 && tid == 0) opt_advance(c, opt_in, opt_out, kl, total_norm, kl_out);
 }
 
 }  // namespace
@@ -1351,13 +1487,74 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        reinterpret_cast<unsigned *>(work + 7));
     USV_CHECK_LAUNCH();
   }
-  const int nblk = cfg->minibatch / RB;
-  hipLaunchKernelGGL(cfg->bf16_gemm ? k_mb_grad<true> : k_mb_grad<false>, dim3(nblk), dim3(GTB), 0, s, *cfg, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
-                     exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials);
-  USV_CHECK_LAUNCH();
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
-  hipLaunchKernelGGL(k_reduce_partials, dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad, losses,
-                     1.0f / (float)cfg->minibatch);
+  const int nblk = cfg->minibatch / RB;
+  hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, false> : k_mb_grad<false, false>), dim3(nblk), dim3(GTB), 0, s,
+                     *cfg, ChainIn{}, params, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv,
+                     exp_mu, exp_sigma, partials);
+  USV_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_reduce_partials<false>, dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad, losses,
+                     1.0f / (float)cfg->minibatch, *cfg, AdamBanks{}, nullptr);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+static bool banks_ok(const ppo_adam_banks_t *b) {
+  if (!b || !b->opt) return false;
+  for (int i = 0; i < 2; ++i) {
+    if (!b->params[i] || !b->m[i] || !b->v[i]) return false;
+    if (reinterpret_cast<uintptr_t>(b->params[i]) & 15u) return false;   // 16-byte weight staging loads
+  }
+  return true;
+}
+
+int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int seq, double *obs_rms,
+                        int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+                        const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
+                        float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
+                        float *kl_prev_out, void *stream) {
+  if (!cfg || !grad || !partials || !work || seq < 0) return 1;
+  if (!banks_ok(banks)) return 4;
+  if (cfg->minibatch % RB != 0) return 2;
+  if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
+  hipStream_t s = (hipStream_t)stream;
+  const int cur = seq & 1, prv = cur ^ 1, nblk = cfg->minibatch / RB, row0 = mb_index * cfg->minibatch;
+  if (update_obs_rms && cfg->normalize_input) {
+    hipLaunchKernelGGL(k_obs_stats, dim3(64), dim3(TB), 0, s, *cfg, exp_obs, row0, cfg->minibatch, work + 8, obs_rms,
+                       reinterpret_cast<unsigned *>(work + 7));
+    USV_CHECK_LAUNCH();
+  }
+  const float *P = banks->params[cur];
+  const dim3 gg(nblk), gb(GTB);
+  if (seq == 0) {
+    hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, false> : k_mb_grad<false, false>), gg, gb, 0, s, *cfg,
+                       ChainIn{}, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu,
+                       exp_sigma, partials);
+  } else {
+    const ChainIn ch{banks->params[prv], banks->m[prv], banks->v[prv], banks->params[cur], banks->m[cur],
+                     banks->v[cur], grad, banks->opt + 8 * prv, banks->opt + 8 * cur, kl_prev_out};
+    hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, true> : k_mb_grad<false, true>), gg, gb, 0, s, *cfg, ch, P,
+                       obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu, exp_sigma,
+                       partials);
+  }
+  USV_CHECK_LAUNCH();
+  const AdamBanks a{banks->params[cur], banks->m[cur], banks->v[cur], banks->params[prv], banks->m[prv],
+                    banks->v[prv]};
+  hipLaunchKernelGGL(k_reduce_partials<true>, dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad, losses,
+                     1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_minibatch_finish(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int count, const float *grad,
+                         float *kl_out, void *stream) {
+  if (!cfg || !grad || count <= 0) return 1;
+  if (!banks_ok(banks)) return 4;
+  const int last = (count - 1) & 1, nxt = last ^ 1;
+  const AdamBanks a{banks->params[last], banks->m[last], banks->v[last], banks->params[nxt], banks->m[nxt],
+                    banks->v[nxt]};
+  hipLaunchKernelGGL((k_apply<true, true>), dim3((PPO_NPARAM + AP_TB - 1) / AP_TB), dim3(AP_TB), 0,
+                     (hipStream_t)stream, *cfg, a, grad, banks->opt + 8 * last, banks->opt + 8 * nxt, 1.0f, kl_out);
   USV_CHECK_LAUNCH();
   return 0;
 }
@@ -1386,9 +1583,10 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
   if (!cfg || !params || !grad || !adam_m || !adam_v || !opt) return 1;
   if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
   if (opt_slot != 0 && opt_slot != 1) return 3;
-  hipLaunchKernelGGL(norm_from_partials ? k_apply<true> : k_apply<false>, dim3((PPO_NPARAM + AP_TB - 1) / AP_TB),
-                     dim3(AP_TB), 0, (hipStream_t)stream, *cfg, params, grad, adam_m, adam_v, opt + 8 * opt_slot,
-                     opt + 8 * (1 - opt_slot), grad_scale, kl_out);
+  const AdamBanks a{params, adam_m, adam_v, params, adam_m, adam_v};
+  hipLaunchKernelGGL((norm_from_partials ? k_apply<true, false> : k_apply<false, false>),
+                     dim3((PPO_NPARAM + AP_TB - 1) / AP_TB), dim3(AP_TB), 0, (hipStream_t)stream, *cfg, a, grad,
+                     opt + 8 * opt_slot, opt + 8 * (1 - opt_slot), grad_scale, kl_out);
   USV_CHECK_LAUNCH();
   return 0;
 }

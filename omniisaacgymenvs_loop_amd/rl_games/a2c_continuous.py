@@ -27,7 +27,7 @@ import torch
 import torch.distributed as dist
 
 from .. import _capi
-from .._abi import DEFINES, PpoCfg
+from .._abi import DEFINES, PpoAdamBanks, PpoCfg
 from . import checkpoint as ckpt
 from . import dist_util
 from . import vecenv
@@ -244,6 +244,9 @@ class A2CAgent:
             dist_util.broadcast_params(self.model_params, 0)   # a2c_common.py:1354 (initial weights from rank 0)
         self.adam_m = torch.zeros(NPARAM, **f32)
         self.adam_v = torch.zeros(NPARAM, **f32)
+        # second bank of (params, m, v) for the chained single-GPU update (ppo_minibatch_fused)
+        self._bank1 = torch.zeros((3, NPARAM), **f32)
+        self._banks = None
         # optimiser scalars, two slots (lr, step, kl, norm): minibatch k reads slot k % 2 and writes the other
         self.opt = torch.zeros(16, **f32)
         self.opt[0] = self.last_lr
@@ -326,10 +329,26 @@ class A2CAgent:
             return 1.0
         return dist_util.allreduce_grad(self.grad[:NPARAM + 1])
 
+    def _adam_banks(self) -> PpoAdamBanks:
+        """ppo_adam_banks_t over (model_params, adam_m, adam_v) and the second bank."""
+        ptrs = (self.model_params.data_ptr(), self.adam_m.data_ptr(), self.adam_v.data_ptr(), self.opt.data_ptr())
+        if self._banks is None or self._banks[0] != ptrs:
+            b = PpoAdamBanks()
+            b.params[0], b.m[0], b.v[0], b.opt = ptrs
+            b.params[1], b.m[1], b.v[1] = (t.data_ptr() for t in self._bank1)
+            self._banks = (ptrs, b)
+        return self._banks[1]
+
+    def _fused_update(self) -> bool:
+        """One rank: two launches per minibatch (ppo_minibatch_fused); USV_PPO_FUSED=0 keeps the
+        three-launch split (grad, reduce, apply)."""
+        return not (self.multi_gpu and self.rank_size > 1) and os.environ.get("USV_PPO_FUSED", "1") != "0"
+
     def update_epoch_minibatches(self) -> None:
         """The mini-epoch / minibatch loop (a2c_common.py:1190-1245): per minibatch the gradient kernel
         (+ fixed-order partial reduction), [RCCL all-reduce of the flat gradient + KL with several
-        ranks], then the clip + Adam + LR kernel."""
+        ranks], then the clip + Adam + LR kernel.  On one rank the step is taken inside the reduction
+        and checked by the next launch (ppo_minibatch_fused / ppo_minibatch_finish)."""
         c = _capi
         cfg = c.byref(self.cfg)
         s = c.stream_ptr()
@@ -339,6 +358,24 @@ class A2CAgent:
         if seq:   # RunningMeanStd.train of mini-epoch 0, all minibatches in two launches
             c.call("ppo_obs_rms_epoch", cfg, c.ptr(self.exp_obs), self.batch_size, c.ptr(self.obs_rms),
                    c.ptr(self.rms_seq), s)
+        if self._fused_update():
+            banks = c.byref(self._adam_banks())
+            for mini_ep in range(self.mini_epochs_num):
+                for i in range(self.num_minibatches):
+                    rms = self.rms_seq[2 * NIN * i:] if seq and mini_ep == 0 else self.obs_rms
+                    c.call("ppo_minibatch_fused", cfg, banks, k, c.ptr(rms), int(mini_ep == 0 and not seq), i,
+                           c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp), c.ptr(self.exp_val),
+                           c.ptr(self.exp_ret), c.ptr(self.exp_adv), c.ptr(self.exp_mu), c.ptr(self.exp_sigma),
+                           c.ptr(self.grad), c.ptr(self.loss_log[k]), c.ptr(self.partials), c.ptr(self.work),
+                           c.ptr(self.kls[k - 1:k]) if k else None, s)
+                    k += 1
+            c.call("ppo_minibatch_finish", cfg, banks, k, c.ptr(self.grad), c.ptr(self.kls[k - 1:k]), s)
+            if k % 2:   # the chain ended in bank 1 / slot 1
+                self.model_params.copy_(self._bank1[0])
+                self.adam_m.copy_(self._bank1[1])
+                self.adam_v.copy_(self._bank1[2])
+                self.opt[:8].copy_(self.opt[8:])
+            return
         for mini_ep in range(self.mini_epochs_num):
             for i in range(self.num_minibatches):
                 rms = self.rms_seq[2 * NIN * i:] if seq and mini_ep == 0 else self.obs_rms

@@ -112,10 +112,7 @@ def test_prepare_kernel_vs_reference(ppo):
     assert vr[2] == float(ppo["final_value_mean_std__count"])
 
 
-def test_minibatch_epoch_vs_reference(ppo):
-    """32 optimizer steps: per-minibatch KL / losses, adaptive LR, obs RMS and final weights."""
-    H, N = ppo["exp_rewards"].shape[:2]
-    ag = _agent(N, int(ppo["hyper"][2]))
+def _load_dataset(ag, ppo):
     ag.model_params.copy_(_flat_params(_params(ppo, "init")))
     T = lambda a: torch.tensor(np.ascontiguousarray(a), device=DEV)
     ag.exp_obs.copy_(T(ppo["ds_obs_state"]))
@@ -126,6 +123,46 @@ def test_minibatch_epoch_vs_reference(ppo):
     ag.exp_adv.copy_(T(ppo["ds_advantages"]))
     ag.exp_mu.copy_(T(ppo["batch_mus"]))
     ag.exp_sigma.copy_(T(ppo["batch_sigmas"]))
+
+
+def _run_update(ppo, monkeypatch, fused, minibatch, mini_epochs, grad_norm=None):
+    monkeypatch.setenv("USV_PPO_FUSED", "1" if fused else "0")
+    H, N = ppo["exp_rewards"].shape[:2]
+    ag = _agent(N, minibatch, mini_epochs)
+    if grad_norm is not None:
+        ag.cfg.truncate_grads, ag.cfg.grad_norm = 1, grad_norm
+    _load_dataset(ag, ppo)
+    ag.update_epoch_minibatches()
+    torch.cuda.synchronize()
+    return {k: getattr(ag, k).cpu().numpy().copy()
+            for k in ("model_params", "adam_m", "adam_v", "opt", "kls", "loss_log", "obs_rms")}
+
+
+@pytest.mark.parametrize("mb_div,mini_epochs", [(4, 8), (1, 3)])
+def test_fused_chain_matches_split_path(ppo, monkeypatch, mb_div, mini_epochs):
+    """ppo_minibatch_fused / ppo_minibatch_finish (Adam step speculated inside the reduction, checked by
+    the next launch) vs ppo_minibatch_grad + ppo_minibatch_apply: bit-identical parameters, moments,
+    optimiser scalars, KLs and losses -- without clipping, with clipping at every step (the redo path),
+    with clipping at some steps, and for an odd chain (state copied back from bank 1)."""
+    H, N = ppo["exp_rewards"].shape[:2]
+    mb = N * H // mb_div
+    ref = _run_update(ppo, monkeypatch, False, mb, mini_epochs)
+    last_norm = float(ref["opt"][3])   # the last minibatch's gradient norm: some steps above, some below
+    assert last_norm > 0
+    for gn in (None, 1e-4, last_norm):
+        a = ref if gn is None else _run_update(ppo, monkeypatch, False, mb, mini_epochs, gn)
+        b = _run_update(ppo, monkeypatch, True, mb, mini_epochs, gn)
+        for k in a:
+            np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} grad_norm={gn}")
+        if gn == 1e-4:
+            assert not np.array_equal(a["model_params"], ref["model_params"])   # clipping happened
+
+
+def test_minibatch_epoch_vs_reference(ppo):
+    """32 optimizer steps: per-minibatch KL / losses, adaptive LR, obs RMS and final weights."""
+    H, N = ppo["exp_rewards"].shape[:2]
+    ag = _agent(N, int(ppo["hyper"][2]))
+    _load_dataset(ag, ppo)
     ag.update_epoch_minibatches()
     torch.cuda.synchronize()
     tn = "ppo_epoch"

@@ -15,6 +15,7 @@ from omniisaacgymenvs_loop_amd import _capi  # noqa: E402
 
 
 def main():
+    os.environ["USV_PPO_FUSED"] = "0"   # the split path: the norm is read back after each ppo_minibatch_apply
     envs = int(sys.argv[1]) if len(sys.argv) > 1 else 131072
     epochs = int(sys.argv[2]) if len(sys.argv) > 2 else 12
     env, task, agent = bench.build(envs, 0, 1, 42)
