@@ -877,13 +877,17 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     for (int q = 0; q < 8; ++q) op[q] = ch.opt_prev[q];
     kl_prev = ch.grad[PPO_NPARAM];
   }
-  RowIn ri = {};
-  if (tid < RB) {
-    const size_t row = (size_t)rb0 + tid;
-    ri.act0 = e_act[row * 2]; ri.act1 = e_act[row * 2 + 1];
-    ri.nlp = e_nlp[row]; ri.val = e_val[row]; ri.ret = e_ret[row]; ri.adv = e_adv[row];
-    ri.mu0 = e_mu[row * 2]; ri.mu1 = e_mu[row * 2 + 1];
-    ri.sg0 = e_sigma[row * 2]; ri.sg1 = e_sigma[row * 2 + 1];
+  RowIn ri = {};   // wave 0: the actor side's row inputs, wave 1: the critic / KL side's (lane = row)
+  if (lane < RB && w < 2) {
+    const size_t row = (size_t)rb0 + lane;
+    if (w == 0) {
+      ri.act0 = e_act[row * 2]; ri.act1 = e_act[row * 2 + 1];
+      ri.nlp = e_nlp[row]; ri.adv = e_adv[row];
+    } else {
+      ri.val = e_val[row]; ri.ret = e_ret[row];
+      ri.mu0 = e_mu[row * 2]; ri.mu1 = e_mu[row * 2 + 1];
+      ri.sg0 = e_sigma[row * 2]; ri.sg1 = e_sigma[row * 2 + 1];
+    }
   }
   {   // obs rows, normalised on the way into LDS
     constexpr int NU = (RB * XS + GTB - 1) / GTB;
@@ -1024,75 +1028,89 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   USV_PHASE(ppo, 2);
   const PartOut part_st{__builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4,
                                                           0x00020000)};
-  // ---- per-row losses and output gradients (wave 0, lanes < RB) ----
-  if (tid < 64) {
-    float la = 0.f, lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f, gs0 = 0.f, gs1 = 0.f;
-    if (tid < RB) {
-      const int r = tid;
-      const size_t row = (size_t)rb0 + r;
-      const float mu0 = s.out[r * 4], mu1 = s.out[r * 4 + 1], v = s.out[r * 4 + 2];
-      const float ls0 = mu0 * 0.f + lsig0, ls1 = mu1 * 0.f + lsig1;
-      const float sg0 = expf(ls0), sg1 = expf(ls1);
-      const float z0 = (ri.act0 - mu0) / sg0, z1 = (ri.act1 - mu1) / sg1;
-      const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
-      const float A = ri.adv;
-      // actor_loss (common_losses.py:36-46)
-      const float ratio = expf(ri.nlp - nlp);
-      const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
-      const float rc = clampt(ratio, lo, hi);
-      const float s1 = -(A * ratio), s2 = -(A * rc);
-      const float a_loss = fmaxf(s1, s2);
-      const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-      const float g1 = -A, g2 = -A * inr;                // d(-A r)/dr, d(-A clip(r))/dr
-      const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
-      const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
-      // critic_loss (common_losses.py:10-19)
-      const float vo = ri.val, R = ri.ret;
-      float dv, c_loss;
-      if (c.clip_value) {
-        const float dvr = v - vo;
-        const float dvc = clampt(dvr, -c.e_clip, c.e_clip);
-        const float vc = vo + dvc;
-        const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
-        c_loss = fmaxf(l1, l2);
-        const float d1 = 2.f * (v - R);
-        const float d2 = 2.f * (vc - R) * ((dvr >= -c.e_clip && dvr <= c.e_clip) ? 1.f : 0.f);
-        dv = (l1 > l2) ? d1 : ((l1 < l2) ? d2 : 0.5f * (d1 + d2));
-      } else {
-        c_loss = (R - v) * (R - v);
-        dv = 2.f * (v - R);
+  // ---- per-row losses and output gradients (lane = row < RB): wave 0 the actor side (ratio, clipped
+  // surrogate, dnlp, dmu, dlogstd), wave 1 in parallel the critic, bound, entropy and KL terms and the
+  // mu / sigma write-back (the same per-row arithmetic and lane sums as one wave doing both) ----
+  if (tid < 128) {
+    const int r = lane;
+    const bool rowok = r < RB;
+    const int rr = rowok ? r : 0;
+    const size_t row = (size_t)rb0 + rr;
+    const float mu0 = s.out[rr * 4], mu1 = s.out[rr * 4 + 1], v = s.out[rr * 4 + 2];
+    const float ls0 = mu0 * 0.f + lsig0, ls1 = mu1 * 0.f + lsig1;
+    const float sg0 = expf(ls0), sg1 = expf(ls1);
+    const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
+    const float bh1 = fmaxf(mu1 - 1.1f, 0.f), bl1 = fminf(mu1 + 1.1f, 0.f);
+    if (w == 0) {
+      float la = 0.f, gs0 = 0.f, gs1 = 0.f;
+      if (rowok) {
+        const float z0 = (ri.act0 - mu0) / sg0, z1 = (ri.act1 - mu1) / sg1;
+        const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
+        const float A = ri.adv;
+        // actor_loss (common_losses.py:36-46)
+        const float ratio = expf(ri.nlp - nlp);
+        const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
+        const float rc = clampt(ratio, lo, hi);
+        const float s1 = -(A * ratio), s2 = -(A * rc);
+        const float a_loss = fmaxf(s1, s2);
+        const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float g1 = -A, g2 = -A * inr;                // d(-A r)/dr, d(-A clip(r))/dr
+        const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
+        const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
+        // + bound_loss (a2c_continuous.py:209-217)
+        const float bc = c.bounds_loss_coef * invB;
+        const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
+        const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
+        // d nlp / d logstd = 1 - z^2; - entropy_coef * mean(entropy): d entropy / d logstd = 1 per row
+        const float dent = -c.entropy_coef * invB;
+        gs0 = dnlp * (1.f - z0 * z0) + dent;
+        gs1 = dnlp * (1.f - z1 * z1) + dent;
+        la = a_loss;
+        s.g[r * 4 + 0] = dmu0;
+        s.g[r * 4 + 1] = dmu1;
+        s.g[r * 4 + 3] = dnlp;
       }
-      dv *= 0.5f * c.critic_coef * invB;
-      // bound_loss (a2c_continuous.py:209-217)
-      const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
-      const float bh1 = fmaxf(mu1 - 1.1f, 0.f), bl1 = fminf(mu1 + 1.1f, 0.f);
-      const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
-      const float bc = c.bounds_loss_coef * invB;
-      const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
-      const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
-      // d nlp / d logstd = 1 - z^2; - entropy_coef * mean(entropy): d entropy / d logstd = 1 per row
-      const float dent = -c.entropy_coef * invB;
-      gs0 = dnlp * (1.f - z0 * z0) + dent;
-      gs1 = dnlp * (1.f - z1 * z1) + dent;
-      const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
-      // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
-      const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
-      const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
-      const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
-      e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
-      e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
-      la = a_loss; lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
-      s.g[r * 4 + 0] = dmu0;
-      s.g[r * 4 + 1] = dmu1;
-      s.g[r * 4 + 2] = dv;
-      s.g[r * 4 + 3] = dnlp;
-    }
-    la = wave_sum(la); lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
-    gs0 = wave_sum(gs0); gs1 = wave_sum(gs1);
-    if (tid == 0) {
-      part_st(P_LOSS + 0, la); part_st(P_LOSS + 1, lc); part_st(P_LOSS + 2, le); part_st(P_LOSS + 3, lb);
-      part_st(P_LOSS + 4, lkl);
-      part_st(S_SIG, gs0); part_st(S_SIG + 1, gs1);
+      la = wave_sum(la); gs0 = wave_sum(gs0); gs1 = wave_sum(gs1);
+      if (lane == 0) {
+        part_st(P_LOSS + 0, la);
+        part_st(S_SIG, gs0); part_st(S_SIG + 1, gs1);
+      }
+    } else {
+      float lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f;
+      if (rowok) {
+        // critic_loss (common_losses.py:10-19)
+        const float vo = ri.val, R = ri.ret;
+        float dv, c_loss;
+        if (c.clip_value) {
+          const float dvr = v - vo;
+          const float dvc = clampt(dvr, -c.e_clip, c.e_clip);
+          const float vc = vo + dvc;
+          const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+          c_loss = fmaxf(l1, l2);
+          const float d1 = 2.f * (v - R);
+          const float d2 = 2.f * (vc - R) * ((dvr >= -c.e_clip && dvr <= c.e_clip) ? 1.f : 0.f);
+          dv = (l1 > l2) ? d1 : ((l1 < l2) ? d2 : 0.5f * (d1 + d2));
+        } else {
+          c_loss = (R - v) * (R - v);
+          dv = 2.f * (v - R);
+        }
+        dv *= 0.5f * c.critic_coef * invB;
+        const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
+        const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
+        // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
+        const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
+        const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
+        const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
+        e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
+        e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
+        lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
+        s.g[r * 4 + 2] = dv;
+      }
+      lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
+      if (lane == 0) {
+        part_st(P_LOSS + 1, lc); part_st(P_LOSS + 2, le); part_st(P_LOSS + 3, lb);
+        part_st(P_LOSS + 4, lkl);
+      }
     }
   }
   __syncthreads();
