@@ -698,25 +698,46 @@ __device__ __forceinline__ float clip_coef(const ppo_cfg_t &c, float total_norm)
   }
   return coef;
 }
+// The next step's bias-corrected constants travel in opt[4..7] = (step_size, bc2s, for step,
+// for lr), written by opt_store: a step whose (lr, step) match the tags takes them instead of
+// evaluating the two double pow() again (identical inputs, identical values); anything else --
+// zero-initialised scalars, a learning rate or step count set by the host -- recomputes.
+__device__ __forceinline__ AdamK adam_consts_tagged(const ppo_cfg_t &c, float lr, float step, float t_ss,
+                                                    float t_bc, float t_step, float t_lr) {
+  if (t_step == step && t_lr == lr) return {t_ss, t_bc};
+  return adam_consts(c, lr, step);
+}
 // AdaptiveScheduler.update on a minibatch's KL (schedulers.py:26-32) and the optimiser
-// scalars after its step: opt_in -> opt_out = (lr, step, kl, norm, ...)
+// scalars after its step: opt_in -> opt_out = (lr, step, kl, norm, next step's constants).
+// opt_next needs only opt_in and the KL, so a launch can evaluate it (two double pow) in the
+// shadow of its loads; opt_store then writes it with the clip norm.
+struct OptNext {
+  float nl, kl_keep, step;
+  AdamK nk;
+};
 template <class OptIn>
-__device__ __forceinline__ void opt_advance(const ppo_cfg_t &c, const OptIn &opt_in, float *opt_out, float kl,
-                                            float total_norm, float *kl_out) {
+__device__ __forceinline__ OptNext opt_next(const ppo_cfg_t &c, const OptIn &opt_in, float kl) {
   const float lr = opt_in[0];
   float nl = lr, kl_keep = opt_in[2];
   if (c.lr_adaptive) {
     if (kl > 2.0f * c.kl_threshold) nl = fmaxf(lr / 1.5f, c.lr_min);
     if (kl < 0.5f * c.kl_threshold) nl = fminf(lr * 1.5f, c.lr_max);
     kl_keep = kl;
-    if (kl_out) *kl_out = kl;
   }
-  opt_out[0] = nl;
-  opt_out[1] = opt_in[1] + 1.0f;
-  opt_out[2] = kl_keep;
+  const float step = opt_in[1] + 1.0f;
+  return {nl, kl_keep, step, adam_consts(c, nl, step + 1.0f)};
+}
+__device__ __forceinline__ void opt_store(const ppo_cfg_t &c, const OptNext &x, float *opt_out, float total_norm,
+                                          float kl, float *kl_out) {
+  if (c.lr_adaptive && kl_out) *kl_out = kl;
+  opt_out[0] = x.nl;
+  opt_out[1] = x.step;
+  opt_out[2] = x.kl_keep;
   opt_out[3] = total_norm;
-#pragma unroll
-  for (int i = 4; i < 8; ++i) opt_out[i] = opt_in[i];
+  opt_out[4] = x.nk.step_size;
+  opt_out[5] = x.nk.bc2s;
+  opt_out[6] = x.step + 1.0f;
+  opt_out[7] = x.nl;
 }
 
 // The chained single-GPU update (ppo_minibatch_fused): minibatch k's gradient kernel stages
@@ -803,7 +824,7 @@ struct PartOut {
 // (no workgroup of this launch reads bank cur after its first barrier)
 __device__ __forceinline__ void redo_step(const ppo_cfg_t &c, const ChainIn &ch, const float (&op)[8], float coef,
                                           GradSmem &s, float &ls0, float &ls1) {
-  const AdamK ak = adam_consts(c, op[0], op[1] + 1.0f);
+  const AdamK ak = adam_consts_tagged(c, op[0], op[1] + 1.0f, op[4], op[5], op[6], op[7]);
   for (int q = threadIdx.x; q < PPO_NPARAM; q += GTB) {
     float pn, mn, vn;
     adam_one(c, ak, ch.grad[q] * 1.0f * coef, ch.P_prev[q], ch.m_prev[q], ch.v_prev[q], pn, mn, vn);
@@ -931,8 +952,9 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   if constexpr (kChain) {
     const float total_norm = sqrtf(((s.nrm[0] + s.nrm[1]) + s.nrm[2]) + s.nrm[3]);
     const float coef = clip_coef(c, total_norm);
-    if (blockIdx.x == 0 && tid == 0)
-      opt_advance(c, op, ch.opt_cur, kl_prev, total_norm, ch.kl_out);
+    // (wave 4 of workgroup 0: the kh = 1 waves only commit W2 while layer 1 runs)
+    if (blockIdx.x == 0 && tid == 256)
+      opt_store(c, opt_next(c, op, kl_prev), ch.opt_cur, total_norm, kl_prev, ch.kl_out);
     if (coef < 1.0f) {   // uniform over the launch
       slow = true;
       redo_step(c, ch, op, coef, s, lsig0, lsig1);
@@ -1291,13 +1313,16 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
   const int myslot = blockIdx.x * RD_P + tid;
   const bool mine = kSpec && tid < RD_P && myslot < S_END;
   const int pq = mine ? param_of_slot(myslot) : 0;
-  float p_old = 0.f, m_old = 0.f, v_old = 0.f, lr = 0.f, step = 0.f;
+  float p_old = 0.f, m_old = 0.f, v_old = 0.f;
   if (mine) {
     p_old = a.P0[pq]; m_old = a.m0[pq]; v_old = a.v0[pq];
-    lr = opt_in[0]; step = opt_in[1] + 1.0f;
   }
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-  AdamK ak = {0.f, 1.f};
+  float oin[8] = {};   // the step's scalars: loads issued here, consumed after the row sums
+  if (kSpec) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) oin[q] = opt_in[q];
+  }
   const int p4c = min(p4, NPART_PAD / 4 - 1);
   for (int b0 = grp; b0 < nblk; b0 += RD_G * RD_KB) {
     // branch-free: clamped rows / columns loaded, masked in the sum (every load in flight at once)
@@ -1305,10 +1330,6 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
 #pragma unroll
     for (int k = 0; k < RD_KB; ++k) x[k] = P4[(size_t)min(b0 + RD_G * k, nblk - 1) * (NPART_PAD / 4) + p4c];
     // the bias corrections in the shadow of the row loads (they wait on opt_in only)
-    if (kSpec && mine) {
-      ak = adam_consts(c, lr, step);
-      __asm__ volatile("" : : "v"(ak.step_size), "v"(ak.bc2s));
-    }
 #pragma unroll
     for (int k = 0; k < RD_KB; ++k) {
       if (ok && b0 + RD_G * k < nblk) {
@@ -1316,7 +1337,9 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
       }
     }
   }
-  if (kSpec && mine && grp >= nblk) ak = adam_consts(c, lr, step);   // (row group without rows)
+  AdamK ak = {0.f, 1.f};
+  if (kSpec)   // uniform: precomputed by the previous step's opt_store (no pow on this path)
+    ak = adam_consts_tagged(c, oin[0], oin[1] + 1.0f, oin[4], oin[5], oin[6], oin[7]);
   red[grp][col] = acc;
   __syncthreads();
   float sq = 0.f;
@@ -1379,10 +1402,13 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, AdamBanks a, const
   const float step = opt_in[1] + 1.0f;
   const float kl = grad_in[PPO_NPARAM] * grad_scale;
   __builtin_amdgcn_sched_barrier(0);   // the loads above issue first
-  const AdamK ak = adam_consts(c, lr, step);
-  // pin the bias corrections here, in the shadow of the loads above (the scheduler
-  // would otherwise sink them past the norm's barrier onto the critical path)
-  __asm__ volatile("" : : "v"(ak.step_size), "v"(ak.bc2s));
+  const AdamK ak = adam_consts_tagged(c, lr, step, opt_in[4], opt_in[5], opt_in[6], opt_in[7]);
+  // the next scalars (workgroup 0's first lane) in the same shadow
+  OptNext nx = {};
+  if (blockIdx.x == 0 && tid == 0) nx = opt_next(c, opt_in, kl);
+  // pin these here, in the shadow of the loads above (the scheduler would otherwise sink
+  // them past the norm's barrier onto the critical path)
+  __asm__ volatile("" : : "v"(ak.step_size), "v"(ak.bc2s), "v"(nx.nl), "v"(nx.nk.step_size), "v"(nx.nk.bc2s));
   float ss = 0.f;
   if (kNormFromPartials) {
     ss = tid < RED_BLOCKS ? s0 : 0.f;
@@ -1417,7 +1443,7 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, AdamBanks a, const
     a.m1[q] = mn;
     a.v1[q] = vn;
   }
-  if (blockIdx.x == 0 && tid == 0) opt_advance(c, opt_in, opt_out, kl, total_norm, kl_out);
+  if (blockIdx.x == 0 && tid == 0) opt_store(c, nx, opt_out, total_norm, kl, kl_out);
 }
 
 }  // namespace
