@@ -874,56 +874,62 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   static_assert(NH * XS % GTB == 0 && PPO_OFF_W2 % 2 == 0 && NW2X <= GTB, "staging trip counts");
   float4 w2q[NW2U], w2x = make_float4(0.f, 0.f, 0.f, 0.f);
   float w1r[NW1G], tlr[NTLG];
+  // chained update: minibatch k-1's optimiser scalars (lanes 0-7) and KL (lane 8) as VECTOR loads,
+  // the first in flight -- scalar loads here would share lgkmcnt with the LDS staging writes and
+  // put their latency in front of the first barrier
+  float ov = 0.f;
+  if constexpr (kChain) ov = lane < 8 ? ch.opt_prev[lane] : ch.grad[PPO_NPARAM];
+  // Branch-free: indices clamped, out-of-range values masked after every load is in flight (a
+  // conditional load puts a branch -- and, where another path zero-fills the same registers, a
+  // full vmcnt wait -- between the loads)
   {
     const float4 *P4 = reinterpret_cast<const float4 *>(P);
 #pragma unroll
     for (int u = 0; u < NW1G; ++u) {
       const int q = tid + u * GTB, j = q / XS, k = q % XS;
-      w1r[u] = k < NIN ? P[PPO_OFF_W1 + j * NIN + k] : 0.f;
+      w1r[u] = P[PPO_OFF_W1 + j * NIN + min(k, NIN - 1)];
     }
 #pragma unroll
-    for (int u = 0; u < NTLG; ++u) tlr[u] = (tid + u * GTB < TAIL) ? P[PPO_OFF_B2 + tid + u * GTB] : 0.f;
+    for (int u = 0; u < NTLG; ++u) tlr[u] = P[PPO_OFF_B2 + min(tid + u * GTB, TAIL - 1)];
 #pragma unroll
     for (int u = 0; u < NW2U; ++u) w2q[u] = P4[W2Q0 + tid + u * GTB];
-    if (NW2X > 0 && tid < NW2X) w2x = P4[W2Q0 + NW2U * GTB + tid];
+    if (NW2X > 0) w2x = P4[W2Q0 + NW2U * GTB + min(tid, NW2X - 1)];
   }
-  const float b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
-  float lsig0 = P[PPO_OFF_SIGMA], lsig1 = P[PPO_OFF_SIGMA + 1];
+  const float b1r = P[PPO_OFF_B1 + (tid & (NH - 1))];
+  // log-sigma as a vector load too (read out by readlane where the losses use it)
+  const float lsv = P[PPO_OFF_SIGMA + (lane & 1)];
+  float lsig0 = 0.f, lsig1 = 0.f;
   // chained update: minibatch k-1's chunk squares (its clip norm)
-  const float csq = (kChain && tid < RED_BLOCKS) ? ch.grad[PPO_NPARAM + 8 + tid] : 0.f;
-  // ... and its optimiser scalars and KL (uniform: scalar loads, in flight with the rest)
-  float op[8] = {}, kl_prev = 0.f;
-  if constexpr (kChain) {
+  float csq = 0.f;
+  if constexpr (kChain) csq = ch.grad[PPO_NPARAM + 8 + min(tid, RED_BLOCKS - 1)];
+  // per-row loss inputs, lane = row (waves 0 and 1 use them: the actor / the critic side)
+  RowIn ri;
+  {
+    const size_t row = (size_t)rb0 + (lane & (RB - 1));
+    ri.act0 = e_act[row * 2]; ri.act1 = e_act[row * 2 + 1];
+    ri.nlp = e_nlp[row]; ri.adv = e_adv[row];
+    ri.val = e_val[row]; ri.ret = e_ret[row];
+    ri.mu0 = e_mu[row * 2]; ri.mu1 = e_mu[row * 2 + 1];
+    ri.sg0 = e_sigma[row * 2]; ri.sg1 = e_sigma[row * 2 + 1];
+  }
+  // obs rows and the running statistics (always loaded; obs_rms is non-null, checked on the host)
+  constexpr int NU = (RB * XS + GTB - 1) / GTB;
+  float xo[NU];
+  double mu[NU], var[NU];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) op[q] = ch.opt_prev[q];
-    kl_prev = ch.grad[PPO_NPARAM];
+  for (int u = 0; u < NU; ++u) {
+    const int q = min(tid + u * GTB, RB * XS - 1), r = q / XS, kc = min(q % XS, NIN - 1);
+    xo[u] = e_obs[(size_t)(rb0 + r) * NIN + kc];
+    mu[u] = obs_rms[kc];
+    var[u] = obs_rms[NIN + kc];
   }
-  RowIn ri = {};   // wave 0: the actor side's row inputs, wave 1: the critic / KL side's (lane = row)
-  if (lane < RB && w < 2) {
-    const size_t row = (size_t)rb0 + lane;
-    if (w == 0) {
-      ri.act0 = e_act[row * 2]; ri.act1 = e_act[row * 2 + 1];
-      ri.nlp = e_nlp[row]; ri.adv = e_adv[row];
-    } else {
-      ri.val = e_val[row]; ri.ret = e_ret[row];
-      ri.mu0 = e_mu[row * 2]; ri.mu1 = e_mu[row * 2 + 1];
-      ri.sg0 = e_sigma[row * 2]; ri.sg1 = e_sigma[row * 2 + 1];
-    }
-  }
+  __builtin_amdgcn_sched_barrier(0);   // every load above is issued before anything waits
+#pragma unroll
+  for (int u = 0; u < NW1G; ++u)
+    if ((tid + u * GTB) % XS >= NIN) w1r[u] = 0.f;
+  if (kChain && tid >= RED_BLOCKS) csq = 0.f;
   {   // obs rows, normalised on the way into LDS
-    constexpr int NU = (RB * XS + GTB - 1) / GTB;
-    float v[NU];
-    double mu[NU], var[NU];
     const bool norm = c.normalize_input != 0;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int q = tid + u * GTB, r = q / XS, k = q % XS;
-      const bool ok = q < RB * XS && k < NIN;
-      const int rc = ok ? r : 0, kc = ok ? k : 0;
-      v[u] = e_obs[(size_t)(rb0 + rc) * NIN + kc];
-      mu[u] = norm ? obs_rms[kc] : 0.0;
-      var[u] = norm ? obs_rms[NIN + kc] : 1.0;
-    }
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int q = tid + u * GTB;
@@ -931,7 +937,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
       const int k = q % XS;
       float xv = 0.f;
       if (k < NIN) {
-        xv = v[u];
+        xv = xo[u];
         if (norm) xv = rms_norm(xv, mu[u], var[u], c.rms_eps);
       }
       s.x[q] = xv;
@@ -950,13 +956,25 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   __syncthreads();
   bool slow = false;
   if constexpr (kChain) {
+    // (the scalars are read out of ov's lanes only where they are used: readlane ignores exec)
+    const auto lane_of = [&](int q) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ov), q));
+    };
     const float total_norm = sqrtf(((s.nrm[0] + s.nrm[1]) + s.nrm[2]) + s.nrm[3]);
     const float coef = clip_coef(c, total_norm);
     // (wave 4 of workgroup 0: the kh = 1 waves only commit W2 while layer 1 runs)
-    if (blockIdx.x == 0 && tid == 256)
+    if (blockIdx.x == 0 && tid == 256) {
+      float op[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) op[q] = lane_of(q);
+      const float kl_prev = lane_of(8);
       opt_store(c, opt_next(c, op, kl_prev), ch.opt_cur, total_norm, kl_prev, ch.kl_out);
+    }
     if (coef < 1.0f) {   // uniform over the launch
       slow = true;
+      float op[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) op[q] = lane_of(q);
       redo_step(c, ch, op, coef, s, lsig0, lsig1);
       __syncthreads();
     }
@@ -1059,6 +1077,10 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     const int rr = rowok ? r : 0;
     const size_t row = (size_t)rb0 + rr;
     const float mu0 = s.out[rr * 4], mu1 = s.out[rr * 4 + 1], v = s.out[rr * 4 + 2];
+    if (!slow) {
+      lsig0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lsv), 0));
+      lsig1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lsv), 1));
+    }
     const float ls0 = mu0 * 0.f + lsig0, ls1 = mu1 * 0.f + lsig1;
     const float sg0 = expf(ls0), sg1 = expf(ls1);
     const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
@@ -1518,7 +1540,7 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
                        void *stream) {
   (void)val_rms;
-  if (!cfg || !params || !grad || !partials || !work) return 1;
+  if (!cfg || !params || !obs_rms || !grad || !partials || !work) return 1;
   if (cfg->minibatch % RB != 0) return 2;
   if (reinterpret_cast<uintptr_t>(params) & 15u) return 4;   // 16-byte weight staging loads
   hipStream_t s = (hipStream_t)stream;
@@ -1557,7 +1579,7 @@ int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int
                         const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
                         float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
                         float *kl_prev_out, void *stream) {
-  if (!cfg || !grad || !partials || !work || seq < 0) return 1;
+  if (!cfg || !obs_rms || !grad || !partials || !work || seq < 0) return 1;
   if (!banks_ok(banks)) return 4;
   if (cfg->minibatch % RB != 0) return 2;
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
