@@ -423,7 +423,8 @@ typedef struct ppo_cfg {
  * buffer. Replaces A2CBase.get_action_values (a2c_common.py:385-405) +
  * ModelA2CContinuousLogStd.forward (models.py:366-401) +
  * ExperienceBuffer.update_data (experience.py:392-398).
- * params: [PPO_NPARAM]; obs_rms: double [2][33] (mean, var); val_rms double [2];
+ * params: [PPO_NPARAM]; obs_rms: double [2][33] (mean, var), non-NULL (read also when
+ * normalize_input = 0; the same for ppo_value / ppo_minibatch_grad / _fused); val_rms double [2];
  * buffers of the experience store are env-major [n][H][...].
  * eps_inject: NULL => Philox normal draws, else device [n][2] N(0,1) draws.
  * step_dev (nullable): device counter holding the rollout's first step; slot t draws

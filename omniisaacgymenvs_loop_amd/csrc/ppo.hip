@@ -101,16 +101,21 @@ struct StagedW {
 __device__ __forceinline__ void stage_load(const float *__restrict__ P, StagedW &r) {
   const int tid = threadIdx.x;
   const float2 *W2 = reinterpret_cast<const float2 *>(P + PPO_OFF_W2);   // PPO_OFF_W2 is even
+  // branch-free: clamped indices, masked after every load is issued
 #pragma unroll
   for (int u = 0; u < NW1; ++u) {
     const int i = tid + u * TB, j = i / XS, k = i % XS;
-    r.w1r[u] = k < NIN ? P[PPO_OFF_W1 + j * NIN + k] : 0.f;
+    r.w1r[u] = P[PPO_OFF_W1 + j * NIN + min(k, NIN - 1)];
   }
 #pragma unroll
-  for (int u = 0; u < NTL; ++u) r.tlr[u] = (tid + u * TB < TAIL) ? P[PPO_OFF_B2 + tid + u * TB] : 0.f;
-  r.b1r = tid < NH ? P[PPO_OFF_B1 + tid] : 0.f;
+  for (int u = 0; u < NTL; ++u) r.tlr[u] = P[PPO_OFF_B2 + min(tid + u * TB, TAIL - 1)];
+  r.b1r = P[PPO_OFF_B1 + (tid & (NH - 1))];
 #pragma unroll
   for (int u = 0; u < NW2; ++u) r.w2r[u] = W2[tid + u * TB];
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int u = 0; u < NW1; ++u)
+    if ((tid + u * TB) % XS >= NIN) r.w1r[u] = 0.f;
 }
 
 __device__ __forceinline__ void stage_store_small(const StagedW &r, MlpSmem &s) {
@@ -144,41 +149,53 @@ __device__ __forceinline__ float fast_tanh(float x) {
   return copysignf(ax < 0.0078125f ? small : big, x);
 }
 
-__device__ __forceinline__ void stage_obs(const float *__restrict__ obs, int row0, int nrows, const double *obs_rms,
-                                          bool normalize, float eps, MlpSmem &s) {
-  // compile-time trip count: every obs and statistics load of the thread is in flight
-  // before the first one is waited on
-  constexpr int NU = (RB * XS + TB - 1) / TB;
-  float v[NU];
-  double mu[NU], var[NU];
+// The persistent forward kernels' obs path: a thread's slots q = tid + u TB of a tile's RB x XS
+// block sit in the same columns for every tile, so the running statistics are loaded once per
+// launch; the next tile's rows are loaded (clamped, unconditionally) while the current one runs.
+constexpr int NUO = (RB * XS + TB - 1) / TB;
+struct ObsCols {
+  double mu[NUO], var[NUO];
+};
+__device__ __forceinline__ void load_obs_cols(const double *__restrict__ obs_rms, ObsCols &oc) {
 #pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int i = threadIdx.x + u * TB;
-    const int r = i / XS, k = i % XS;
-    const bool ok = i < RB * XS && r < nrows && k < NIN;
-    const int rc = ok ? r : 0, kc = ok ? k : 0;
-    v[u] = obs[(size_t)(row0 + rc) * NIN + kc];
-    mu[u] = normalize ? obs_rms[kc] : 0.0;
-    var[u] = normalize ? obs_rms[NIN + kc] : 1.0;
+  for (int u = 0; u < NUO; ++u) {
+    const int kc = min(((int)threadIdx.x + u * TB) % XS, NIN - 1);
+    oc.mu[u] = obs_rms[kc];
+    oc.var[u] = obs_rms[NIN + kc];
   }
+}
+__device__ __forceinline__ void load_obs_tile(const float *__restrict__ obs, int n, int tile, float (&x)[NUO]) {
+  const int row0 = tile * RB, nrows = min(RB, n - row0);
 #pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int i = threadIdx.x + u * TB;
-    if (i >= RB * XS) continue;
-    const int r = i / XS, k = i % XS;
-    float x = 0.f;
+  for (int u = 0; u < NUO; ++u) {
+    const int q = min((int)threadIdx.x + u * TB, RB * XS - 1);
+    const int r = min(q / XS, nrows - 1), kc = min(q % XS, NIN - 1);
+    x[u] = obs[(size_t)(row0 + r) * NIN + kc];
+  }
+}
+// normalised rows into s.x; with exp_obs, the raw rows also to the experience buffer (row
+// env * H + t, swap_and_flatten01 layout)
+__device__ __forceinline__ void put_obs_tile(const float (&x)[NUO], const ObsCols &oc, int row0, int nrows,
+                                             bool normalize, float eps, MlpSmem &s, float *exp_obs, int H, int t) {
+#pragma unroll
+  for (int u = 0; u < NUO; ++u) {
+    const int q = threadIdx.x + u * TB;
+    if (q >= RB * XS) continue;
+    const int r = q / XS, k = q % XS;
+    float v = 0.f;
     if (r < nrows && k < NIN) {
-      x = v[u];
-      if (normalize) x = rms_norm(x, mu[u], var[u], eps);
+      v = x[u];
+      if (exp_obs) exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = v;
+      if (normalize) v = rms_norm(v, oc.mu[u], oc.var[u], eps);
     }
-    s.x[i] = x;
+    s.x[q] = v;
   }
 }
 
 // Forward of the RB rows staged in s.x (W1, biases, heads staged; W2 still in
-// registers, committed after layer 1); leaves h1, h2, out.
+// registers on a launch's first tile, committed after layer 1); leaves h1, h2, out.
 template <bool kBf>
-__device__ void block_forward(const StagedW &wr, MlpSmem &s) {
+__device__ void block_forward(const StagedW &wr, MlpSmem &s, bool first_tile) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
   // ---- layer 1: h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero) ----
@@ -193,7 +210,7 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
   }
-  stage_store_w2(wr, s);
+  if (first_tile) stage_store_w2(wr, s);   // nothing else writes s.w2: later tiles reuse it
   __syncthreads();
   // ---- layer 2: h2 = tanh(h1 W2^T + b2) ----
   {
@@ -264,19 +281,20 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   StagedW wr;
   stage_load(P, wr);
   const int ntiles = (n + RB - 1) / RB;
+  ObsCols oc;
+  load_obs_cols(obs_rms, oc);
+  float xo[NUO];
+  load_obs_tile(obs, n, min((int)blockIdx.x, ntiles - 1), xo);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int row0 = tile * RB;
   const int nrows = min(RB, n - row0);
-  // raw obs into the experience buffer (row = env*H + t, swap_and_flatten01 layout)
-  for (int i = threadIdx.x; i < nrows * NIN; i += TB) {
-    const int r = i / NIN, k = i % NIN;
-    exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = obs[(size_t)(row0 + r) * NIN + k];
-  }
+  float xn[NUO];   // the next tile's rows (the last tile again when none is left)
+  load_obs_tile(obs, n, min(tile + (int)gridDim.x, ntiles - 1), xn);
   // s.x of the previous tile was last read before block_forward's first barrier
-  stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+  put_obs_tile(xo, oc, row0, nrows, c.normalize_input != 0, c.rms_eps, s, exp_obs, H, t);
   if (tile == (int)blockIdx.x) stage_store_small(wr, s);
   __syncthreads();
-  block_forward<kBf>(wr, s);   // re-commits the same W2 values on later tiles
+  block_forward<kBf>(wr, s, tile == (int)blockIdx.x);
   const int r = threadIdx.x;
   if (r < nrows) {
     const int e = row0 + r;
@@ -314,6 +332,8 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
     actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
   }
   __syncthreads();   // s.out of this tile is read above before the next tile's forward rewrites it
+#pragma unroll
+  for (int u = 0; u < NUO; ++u) xo[u] = xn[u];
   }
 }
 
@@ -325,13 +345,19 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
   StagedW wr;
   stage_load(P, wr);
   const int ntiles = (n + RB - 1) / RB;
+  ObsCols oc;
+  load_obs_cols(obs_rms, oc);
+  float xo[NUO];
+  load_obs_tile(obs, n, min((int)blockIdx.x, ntiles - 1), xo);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {   // persistent, as k_policy_step
     const int row0 = tile * RB;
     const int nrows = min(RB, n - row0);
-    stage_obs(obs, row0, nrows, obs_rms, c.normalize_input != 0, c.rms_eps, s);
+    float xn[NUO];
+    load_obs_tile(obs, n, min(tile + (int)gridDim.x, ntiles - 1), xn);
+    put_obs_tile(xo, oc, row0, nrows, c.normalize_input != 0, c.rms_eps, s, nullptr, 0, 0);
     if (tile == (int)blockIdx.x) stage_store_small(wr, s);
     __syncthreads();
-    block_forward<kBf>(wr, s);
+    block_forward<kBf>(wr, s, tile == (int)blockIdx.x);
     const int r = threadIdx.x;
     if (r < nrows) {
       float vd = s.out[r * 4 + 2];
@@ -342,6 +368,8 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
       values[row0 + r] = vd;
     }
     __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NUO; ++u) xo[u] = xn[u];
   }
 }
 
@@ -1477,7 +1505,7 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
                     float *exp_mu, float *exp_sigma, uint8_t *exp_done, const int64_t *dones_prev,
                     float *actions_out, uint64_t seed, uint64_t step, const uint64_t *step_dev,
                     const float *eps_inject, void *stream) {
-  if (!cfg || !params || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
+  if (!cfg || !params || !obs_rms || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
   const int grid = policy_grid(cfg->n_envs);
   hipLaunchKernelGGL(cfg->bf16_gemm ? k_policy_step<true> : k_policy_step<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
                      obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
@@ -1488,7 +1516,7 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
 
 int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, const double *val_rms,
               const float *obs, float *values, void *stream) {
-  if (!cfg || !params || !obs || !values || cfg->n_envs <= 0) return 1;
+  if (!cfg || !params || !obs_rms || !obs || !values || cfg->n_envs <= 0) return 1;
   const int grid = policy_grid(cfg->n_envs);
   hipLaunchKernelGGL(cfg->bf16_gemm ? k_value<true> : k_value<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
                      values);
