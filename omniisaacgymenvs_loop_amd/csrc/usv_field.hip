@@ -265,11 +265,12 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
     iy = min(max(iy, 0), G - 1);
     const bool tgt_free = !occ_bit(occ, iy, ix) && ix > 0 && ix < G - 1 && iy > 0 && iy < G - 1;
     // ---- 2. cost-to-go: tiled chamfer sweeps until nothing changes ----
-    // Costs are >= 0, so float order == unsigned order of the bit patterns:
-    // the relaxation runs on u32 min (no NaN canonicalisation).  An occupied
-    // cell holds 0xFFFFFFFF (a NaN): every neighbour's "NaN + w" compares above
-    // +inf and drops out of the min, and the cell keeps its own value by one
-    // max with its own sign bit.  Updates only ever lower a value.
+    // Costs are >= 0, so float order == signed order of the bit patterns: the
+    // relaxation runs on i32 min (no NaN canonicalisation).  An occupied cell
+    // holds 0xFFFFFFFF (a negative NaN, -1 as i32): it is the smallest value in
+    // its own min, so it keeps itself with no extra instruction, and neighbours
+    // read it as |h| + w -- a positive NaN whatever payload the add returns, above
+    // +inf, so it drops out of their min.  Updates only ever lower a value.
     float h[T + 2][T + 2];
     if (tile_ok) {
 #pragma unroll
@@ -336,15 +337,13 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
           for (int i = 1; i <= T; ++i) {
             const int j = L - 2 * (i - 1) + 1;
             if (j < 1 || j > T) continue;
-            const uint32_t hb = __float_as_uint(h[i][j]);
-            uint32_t m = min(hb, __float_as_uint(h[i - 1][j - 1] + 1.414f));
-            m = min(m, __float_as_uint(h[i - 1][j] + 1.0f));
-            m = min(m, __float_as_uint(h[i - 1][j + 1] + 1.414f));
-            m = min(m, __float_as_uint(h[i][j - 1] + 1.0f));
-            // occupied (sign bit set) keeps its marker: max with the sign-extended bit
-            const uint32_t nv = max(m, (uint32_t)((int32_t)hb >> 31));
-            changed |= nv < hb;
-            h[i][j] = __uint_as_float(nv);
+            const int32_t hb = __float_as_int(h[i][j]);
+            int32_t m = min(hb, __float_as_int(fabsf(h[i - 1][j - 1]) + 1.414f));
+            m = min(m, __float_as_int(fabsf(h[i - 1][j]) + 1.0f));
+            m = min(m, __float_as_int(fabsf(h[i - 1][j + 1]) + 1.414f));
+            m = min(m, __float_as_int(fabsf(h[i][j - 1]) + 1.0f));
+            changed |= m < hb;
+            h[i][j] = __int_as_float(m);
           }
 #pragma unroll
         for (int L = 0; L < 3 * T - 2; ++L)
@@ -352,14 +351,13 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
           for (int i = T; i >= 1; --i) {
             const int j = T - (L - 2 * (T - i));
             if (j < 1 || j > T) continue;
-            const uint32_t hb = __float_as_uint(h[i][j]);
-            uint32_t m = min(hb, __float_as_uint(h[i + 1][j + 1] + 1.414f));
-            m = min(m, __float_as_uint(h[i + 1][j] + 1.0f));
-            m = min(m, __float_as_uint(h[i + 1][j - 1] + 1.414f));
-            m = min(m, __float_as_uint(h[i][j + 1] + 1.0f));
-            const uint32_t nv = max(m, (uint32_t)((int32_t)hb >> 31));
-            changed |= nv < hb;
-            h[i][j] = __uint_as_float(nv);
+            const int32_t hb = __float_as_int(h[i][j]);
+            int32_t m = min(hb, __float_as_int(fabsf(h[i + 1][j + 1]) + 1.414f));
+            m = min(m, __float_as_int(fabsf(h[i + 1][j]) + 1.0f));
+            m = min(m, __float_as_int(fabsf(h[i + 1][j - 1]) + 1.414f));
+            m = min(m, __float_as_int(fabsf(h[i][j + 1]) + 1.0f));
+            changed |= m < hb;
+            h[i][j] = __int_as_float(m);
           }
         if (changed) {
 #pragma unroll
