@@ -509,10 +509,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
     constexpr int PER = kChunk / 256;
     float gv[PER], sv[PER];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int q = ch * kChunk + k * 256 + tid;
-      gv[k] = q < q1 ? Fe[q] : 0.f;
-    }
+    for (int k = 0; k < PER; ++k) gv[k] = Fe[min(ch * kChunk + k * 256 + tid, q1 - 1)];   // clamped: no branch
     // the SDF of this chunk (k_field_final reads it back)
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -665,10 +662,22 @@ __global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) 
     float *Fe = b.field + (size_t)e * G2;
     const float *sdf_s = b.sdf + (size_t)slot * G2;
     const int q1 = min(G2, (ch + 1) * kChunk);
-    for (int q = ch * kChunk + threadIdx.x; q < q1; q += 256) {
-      const float g = Fe[q];
+    // compile-time trip count, clamped loads: the chunk's 2 x 8 loads per thread in flight at once
+    constexpr int PER = kChunk / 256;
+    float gv[PER], sv[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int qc = min(ch * kChunk + u * 256 + (int)threadIdx.x, q1 - 1);
+      gv[u] = Fe[qc];
+      sv[u] = sdf_s[qc];
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int q = ch * kChunk + u * 256 + threadIdx.x;
+      if (q >= q1) continue;
+      const float g = gv[u];
       const float cv = isinf(g) ? k.inf_val : g;
-      const float dte = sdf_s[q] - c.obstacle_radius;
+      const float dte = sv[u] - c.obstacle_radius;
       const float jr = j_raw(c, dte, inv_r);
       const float j = (dte < c.influence_radius) ? jr * goal_mask(c, cv, cell) : 0.f;
       const float jv = (any_inside && dte <= 0.f) ? high : j;
