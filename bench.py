@@ -109,18 +109,23 @@ class KernelTimer:
         self._pair(fn, self.pairs)
         self._pair(None, self.empty)    # the same pair around nothing: the event overhead
 
-    def raw_ms(self):
-        if not self.pairs:
+    @staticmethod
+    def _median(pairs):
+        if not pairs:
             return float("nan")
-        return sum(a.elapsed_time(b) for a, b in self.pairs) / len(self.pairs)
+        v = sorted(a.elapsed_time(b) for a, b in pairs)
+        m = len(v) // 2
+        return v[m] if len(v) % 2 else 0.5 * (v[m - 1] + v[m])
+
+    def raw_ms(self):
+        """Median over the launches (a launch that meets a cold cache or a late dispatch does not move it)."""
+        return self._median(self.pairs)
 
     def overhead_ms(self):
-        if not self.empty:
-            return 0.0
-        return sum(a.elapsed_time(b) for a, b in self.empty) / len(self.empty)
+        return self._median(self.empty) if self.empty else 0.0
 
     def mean_ms(self):
-        """Mean launch time, the empty pair's time (event overhead) subtracted."""
+        """Launch time: median event-pair time minus the median empty pair (event overhead)."""
         return self.raw_ms() - self.overhead_ms()
 
 
@@ -264,7 +269,7 @@ def main():
     def timed_call(name, *a):
         if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
             env_timer(lambda: orig_call(name, *a))
-        elif timing[0] and name == "ppo_minibatch_grad":
+        elif timing[0] and name in ("ppo_minibatch_grad", "ppo_minibatch_fused"):
             ppo_timer(lambda: orig_call(name, *a))
         else:
             orig_call(name, *a)
@@ -386,15 +391,19 @@ def main():
                          "envs_per_launch": args.envs,
                          "launch_ms_method": f"HIP event pair around each of the {len(env_timer.pairs)} env-step "
                                              "launches of one eager training epoch, on the launch stream, behind a "
-                                             "spin kernel (host launch latency excluded), minus the same pair around "
-                                             "no launch (event overhead)"},
+                                             "spin kernel (host launch latency excluded); median over the launches "
+                                             "minus the median of the same pair around no launch (event overhead)"},
             "roofline_ppo": {"bound": "mfma",
                              "kernel": "k_mb_grad + k_reduce_partials (f32 MFMA fwd+bwd, 8 waves per 32-row "
                                        "workgroup, fixed-order reduction)",
                              "achieved": ppo_tfs,
                              "peak": BF16_PEAK_TFS if args.mixed_precision else FP32_PEAK_TFS, "unit": "TFLOP/s",
                              "frac": ppo_tfs / (BF16_PEAK_TFS if args.mixed_precision else FP32_PEAK_TFS),
-                             "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size},
+                             "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size,
+                             "launches_timed": len(ppo_timer.pairs),
+                             "launch_ms_method": "median HIP event pair around each minibatch's gradient + reduction "
+                                                 "launches (ppo_minibatch_fused: k_mb_grad + k_reduce_partials with the "
+                                                 "Adam step) of one eager epoch, minus the empty pair"},
             "wall_clock_to_reward": dict(to_reward, unit="s", since="first env reset of this run (random-init policy)",
                                          last100_mean_at_end=float(agent.game_rewards.get_mean())),
             "extra": dict(phase),
