@@ -29,8 +29,10 @@ namespace {
 constexpr int NIN = PPO_NIN, NH = PPO_NH, NA = PPO_NA;
 constexpr int RB = 32;          // rows per block
 constexpr int TB = 256;         // threads per block (4 waves; wave w owns output columns 32w..32w+31)
-constexpr int XS = 36;          // row stride of x / W1 in LDS (k 33..35 zero)
-constexpr int HS = 130;         // row stride of h1 / h2 / W2 in LDS
+constexpr int XS = 35;          // row stride of x / W1 in LDS (k 33, 34 zero; odd: the layer-1 operand
+                                // reads x[i][k] / W1[i][k] of 32 lanes i hit 32 different banks)
+constexpr int HS = 129;         // row stride of h1 / h2 / W2 in LDS (odd: the matrix-core operand reads of
+                                // a column, 32 lanes = 32 rows, hit 32 different banks)
 constexpr int NPART = PPO_NPARAM + 8;   // partial row: params + loss sums
 constexpr int NPART_PAD = (NPART + 3) & ~3;   // partial row stride (16-B aligned rows)
 constexpr int P_LOSS = PPO_NPARAM;      // a, c, entropy, b, kl sums
@@ -76,7 +78,7 @@ constexpr int T_B2 = 0, T_WV = NH, T_BV = 2 * NH, T_WMU = 2 * NH + 1, T_BMU = 4 
 
 struct MlpSmem {
   float w2[NH * HS];      // W2[j][k]
-  float w1[NH * XS];      // W1[j][k], k 33..35 = 0
+  float w1[NH * XS];      // W1[j][k], k 33, 34 = 0
   float x[RB * XS];       // normalised obs (later unchanged: dW1 operand)
   float h1[RB * HS];      // tanh layer 1 (later dz1)
   float h2[RB * HS];      // tanh layer 2 (later dz2)
@@ -91,8 +93,8 @@ struct MlpSmem {
 // registers (compile-time trip counts); W1 / biases / heads go to LDS before
 // layer 1, W2 is committed after layer 1's matrix-core loop so its loads
 // overlap the first layer.
-constexpr int NW2 = NH * NH / 2 / TB, NW1 = NH * XS / TB, NTL = (TAIL + TB - 1) / TB;
-static_assert(NH * NH / 2 % TB == 0 && NH * XS % TB == 0, "staging trip counts");
+constexpr int NW2 = NH * NH / 2 / TB, NW1 = (NH * XS + TB - 1) / TB, NTL = (TAIL + TB - 1) / TB;
+static_assert(NH * NH / 2 % TB == 0, "staging trip counts");
 struct StagedW {
   float2 w2r[NW2];
   float w1r[NW1], tlr[NTL], b1r;
@@ -104,7 +106,7 @@ __device__ __forceinline__ void stage_load(const float *__restrict__ P, StagedW 
   // branch-free: clamped indices, masked after every load is issued
 #pragma unroll
   for (int u = 0; u < NW1; ++u) {
-    const int i = tid + u * TB, j = i / XS, k = i % XS;
+    const int i = min(tid + u * TB, NH * XS - 1), j = i / XS, k = i % XS;
     r.w1r[u] = P[PPO_OFF_W1 + j * NIN + min(k, NIN - 1)];
   }
 #pragma unroll
@@ -121,7 +123,8 @@ __device__ __forceinline__ void stage_load(const float *__restrict__ P, StagedW 
 __device__ __forceinline__ void stage_store_small(const StagedW &r, MlpSmem &s) {
   const int tid = threadIdx.x;
 #pragma unroll
-  for (int u = 0; u < NW1; ++u) s.w1[tid + u * TB] = r.w1r[u];
+  for (int u = 0; u < NW1; ++u)
+    if (tid + u * TB < NH * XS) s.w1[tid + u * TB] = r.w1r[u];
 #pragma unroll
   for (int u = 0; u < NTL; ++u)
     if (tid + u * TB < TAIL) s.tail[tid + u * TB] = r.tlr[u];
@@ -133,7 +136,8 @@ __device__ __forceinline__ void stage_store_w2(const StagedW &r, MlpSmem &s) {
 #pragma unroll
   for (int u = 0; u < NW2; ++u) {
     const int i = tid + u * TB, j = i / (NH / 2), k2 = i % (NH / 2);
-    *reinterpret_cast<float2 *>(&s.w2[j * HS + 2 * k2]) = r.w2r[u];
+    s.w2[j * HS + 2 * k2] = r.w2r[u].x;   // (odd row stride: two 4-byte stores, not one 8-byte)
+    s.w2[j * HS + 2 * k2 + 1] = r.w2r[u].y;
   }
 }
 
@@ -233,12 +237,14 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s, bool first_tile) {
     for (int r = 0; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
   }
   __syncthreads();
-  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (8 threads per row, 16 k each) ----
+  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (8 threads per row, k = part + 8 kk: the 8
+  // threads of a row read 8 consecutive words, not 8 words 16 apart -- no 4-way bank conflicts) ----
   {
     const int r = tid / 8, part = tid % 8;
     float a0 = 0.f, a1 = 0.f, av = 0.f;
 #pragma unroll
-    for (int k = part * 16; k < part * 16 + 16; ++k) {
+    for (int kk = 0; kk < 16; ++kk) {
+      const int k = part + 8 * kk;
       const float hv = s.h2[r * HS + k];
       a0 = fmaf(s.tail[T_WMU + k], hv, a0);
       a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
@@ -783,7 +789,7 @@ struct ChainIn {
 
 struct GradSmem {
   float w2[NH * HS];              // W2[j][k]
-  float w1[NH * XS];              // W1[j][k], k 33..35 = 0
+  float w1[NH * XS];              // W1[j][k], k 33, 34 = 0
   float x[RB * XS];               // normalised obs (dW1 operand)
   float h1[RB * HS];              // tanh layer 1, later dz1
   float h2[RB * HS];              // tanh layer 2, later dz2
@@ -896,10 +902,10 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // ---- every global load issued up front (compile-time trip counts) ----
   // W2 as 16-byte loads from the 16-byte aligned parameter base (checked on the host): the
   // float4s q = W2Q0 .. W2Q0 + NW2Q - 1 cover W2; each is two (even k, k + 1) pairs of one row
-  constexpr int NW1G = NH * XS / GTB, NTLG = (TAIL + GTB - 1) / GTB;
+  constexpr int NW1G = (NH * XS + GTB - 1) / GTB, NTLG = (TAIL + GTB - 1) / GTB;
   constexpr int W2Q0 = PPO_OFF_W2 / 4, W2E0 = 4 * W2Q0 - PPO_OFF_W2;
   constexpr int NW2Q = (PPO_OFF_W2 + NH * NH - 1) / 4 - W2Q0 + 1, NW2U = NW2Q / GTB, NW2X = NW2Q % GTB;
-  static_assert(NH * XS % GTB == 0 && PPO_OFF_W2 % 2 == 0 && NW2X <= GTB, "staging trip counts");
+  static_assert(PPO_OFF_W2 % 2 == 0 && NW2X <= GTB, "staging trip counts");
   float4 w2q[NW2U], w2x = make_float4(0.f, 0.f, 0.f, 0.f);
   float w1r[NW1G], tlr[NTLG];
   // chained update: minibatch k-1's optimiser scalars (lanes 0-7) and KL (lane 8) as VECTOR loads,
@@ -914,7 +920,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     const float4 *P4 = reinterpret_cast<const float4 *>(P);
 #pragma unroll
     for (int u = 0; u < NW1G; ++u) {
-      const int q = tid + u * GTB, j = q / XS, k = q % XS;
+      const int q = min(tid + u * GTB, NH * XS - 1), j = q / XS, k = q % XS;
       w1r[u] = P[PPO_OFF_W1 + j * NIN + min(k, NIN - 1)];
     }
 #pragma unroll
@@ -972,7 +978,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     }
   }
 #pragma unroll
-  for (int u = 0; u < NW1G; ++u) s.w1[tid + u * GTB] = w1r[u];
+  for (int u = 0; u < NW1G; ++u)
+    if (tid + u * GTB < NH * XS) s.w1[tid + u * GTB] = w1r[u];
 #pragma unroll
   for (int u = 0; u < NTLG; ++u)
     if (tid + u * GTB < TAIL) s.tail[tid + u * GTB] = tlr[u];
@@ -1025,8 +1032,14 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   {
     auto put_w2 = [&](int qrel, float4 v) {
       const int e0 = 4 * qrel + W2E0, e1 = e0 + 2;     // both even: a pair never crosses a row
-      if (e0 >= 0) *reinterpret_cast<float2 *>(&s.w2[(e0 >> 7) * HS + (e0 & (NH - 1))]) = make_float2(v.x, v.y);
-      if (e1 < NH * NH) *reinterpret_cast<float2 *>(&s.w2[(e1 >> 7) * HS + (e1 & (NH - 1))]) = make_float2(v.z, v.w);
+      if (e0 >= 0) {   // (odd row stride: 4-byte stores)
+        float *d = &s.w2[(e0 >> 7) * HS + (e0 & (NH - 1))];
+        d[0] = v.x; d[1] = v.y;
+      }
+      if (e1 < NH * NH) {
+        float *d = &s.w2[(e1 >> 7) * HS + (e1 & (NH - 1))];
+        d[0] = v.z; d[1] = v.w;
+      }
     };
     if (!slow) {
 #pragma unroll
@@ -1069,12 +1082,14 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
   __syncthreads();
   USV_PHASE(ppo, 12);
-  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (16 threads per row, 8 k each) ----
+  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (16 threads per row, k = part + 16 kk: the 16
+  // threads of a row read 16 consecutive words -- no 4-way LDS bank conflicts) ----
   {
     const int r = tid / 16, part = tid % 16;
     float a0 = 0.f, a1 = 0.f, av = 0.f;
 #pragma unroll
-    for (int k = part * 8; k < part * 8 + 8; ++k) {
+    for (int kk = 0; kk < 8; ++kk) {
+      const int k = part + 16 * kk;
       const float hv = s.h2[r * HS + k];
       a0 = fmaf(s.tail[T_WMU + k], hv, a0);
       a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
