@@ -93,16 +93,15 @@ struct MlpSmem {
 // registers (compile-time trip counts); W1 / biases / heads go to LDS before
 // layer 1, W2 is committed after layer 1's matrix-core loop so its loads
 // overlap the first layer.
-constexpr int NW2 = NH * NH / 2 / TB, NW1 = (NH * XS + TB - 1) / TB, NTL = (TAIL + TB - 1) / TB;
-static_assert(NH * NH / 2 % TB == 0, "staging trip counts");
+constexpr int NW2 = NH * NH / TB, NW1 = (NH * XS + TB - 1) / TB, NTL = (TAIL + TB - 1) / TB;
+static_assert(NH * NH % TB == 0, "staging trip counts");
 struct StagedW {
-  float2 w2r[NW2];
+  float w2r[NW2];   // W2 element tid + u TB: a wave's LDS writes are 64 consecutive words of one row
   float w1r[NW1], tlr[NTL], b1r;
 };
 
 __device__ __forceinline__ void stage_load(const float *__restrict__ P, StagedW &r) {
   const int tid = threadIdx.x;
-  const float2 *W2 = reinterpret_cast<const float2 *>(P + PPO_OFF_W2);   // PPO_OFF_W2 is even
   // branch-free: clamped indices, masked after every load is issued
 #pragma unroll
   for (int u = 0; u < NW1; ++u) {
@@ -113,7 +112,7 @@ __device__ __forceinline__ void stage_load(const float *__restrict__ P, StagedW 
   for (int u = 0; u < NTL; ++u) r.tlr[u] = P[PPO_OFF_B2 + min(tid + u * TB, TAIL - 1)];
   r.b1r = P[PPO_OFF_B1 + (tid & (NH - 1))];
 #pragma unroll
-  for (int u = 0; u < NW2; ++u) r.w2r[u] = W2[tid + u * TB];
+  for (int u = 0; u < NW2; ++u) r.w2r[u] = P[PPO_OFF_W2 + tid + u * TB];
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int u = 0; u < NW1; ++u)
@@ -135,9 +134,8 @@ __device__ __forceinline__ void stage_store_w2(const StagedW &r, MlpSmem &s) {
   const int tid = threadIdx.x;
 #pragma unroll
   for (int u = 0; u < NW2; ++u) {
-    const int i = tid + u * TB, j = i / (NH / 2), k2 = i % (NH / 2);
-    s.w2[j * HS + 2 * k2] = r.w2r[u].x;   // (odd row stride: two 4-byte stores, not one 8-byte)
-    s.w2[j * HS + 2 * k2 + 1] = r.w2r[u].y;
+    const int e = tid + u * TB;
+    s.w2[(e / NH) * HS + e % NH] = r.w2r[u];
   }
 }
 
@@ -900,13 +898,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   const float invB = 1.0f / (float)c.minibatch;
   USV_PHASE(ppo, 0);
   // ---- every global load issued up front (compile-time trip counts) ----
-  // W2 as 16-byte loads from the 16-byte aligned parameter base (checked on the host): the
-  // float4s q = W2Q0 .. W2Q0 + NW2Q - 1 cover W2; each is two (even k, k + 1) pairs of one row
-  constexpr int NW1G = (NH * XS + GTB - 1) / GTB, NTLG = (TAIL + GTB - 1) / GTB;
-  constexpr int W2Q0 = PPO_OFF_W2 / 4, W2E0 = 4 * W2Q0 - PPO_OFF_W2;
-  constexpr int NW2Q = (PPO_OFF_W2 + NH * NH - 1) / 4 - W2Q0 + 1, NW2U = NW2Q / GTB, NW2X = NW2Q % GTB;
-  static_assert(PPO_OFF_W2 % 2 == 0 && NW2X <= GTB, "staging trip counts");
-  float4 w2q[NW2U], w2x = make_float4(0.f, 0.f, 0.f, 0.f);
+  // W2 element tid + u GTB per thread (4-byte loads): each wave's LDS commit is 64 consecutive words
+  // of one row, conflict-free at the odd row stride (16-byte loads would leave 4-word strided writes)
+  constexpr int NW1G = (NH * XS + GTB - 1) / GTB, NTLG = (TAIL + GTB - 1) / GTB, NW2F = NH * NH / GTB;
+  static_assert(NH * NH % GTB == 0, "staging trip counts");
+  float w2f[NW2F];
   float w1r[NW1G], tlr[NTLG];
   // chained update: minibatch k-1's optimiser scalars (lanes 0-7) and KL (lane 8) as VECTOR loads,
   // the first in flight -- scalar loads here would share lgkmcnt with the LDS staging writes and
@@ -917,7 +913,6 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // conditional load puts a branch -- and, where another path zero-fills the same registers, a
   // full vmcnt wait -- between the loads)
   {
-    const float4 *P4 = reinterpret_cast<const float4 *>(P);
 #pragma unroll
     for (int u = 0; u < NW1G; ++u) {
       const int q = min(tid + u * GTB, NH * XS - 1), j = q / XS, k = q % XS;
@@ -926,8 +921,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
 #pragma unroll
     for (int u = 0; u < NTLG; ++u) tlr[u] = P[PPO_OFF_B2 + min(tid + u * GTB, TAIL - 1)];
 #pragma unroll
-    for (int u = 0; u < NW2U; ++u) w2q[u] = P4[W2Q0 + tid + u * GTB];
-    if (NW2X > 0) w2x = P4[W2Q0 + NW2U * GTB + min(tid, NW2X - 1)];
+    for (int u = 0; u < NW2F; ++u) w2f[u] = P[PPO_OFF_W2 + tid + u * GTB];
   }
   const float b1r = P[PPO_OFF_B1 + (tid & (NH - 1))];
   // log-sigma as a vector load too (read out by readlane where the losses use it)
@@ -1029,22 +1023,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
   USV_PHASE(ppo, 9);
   // W2 into LDS (waves 4-7 do it while 0-3 run layer 1; each thread commits its own loads)
-  {
-    auto put_w2 = [&](int qrel, float4 v) {
-      const int e0 = 4 * qrel + W2E0, e1 = e0 + 2;     // both even: a pair never crosses a row
-      if (e0 >= 0) {   // (odd row stride: 4-byte stores)
-        float *d = &s.w2[(e0 >> 7) * HS + (e0 & (NH - 1))];
-        d[0] = v.x; d[1] = v.y;
-      }
-      if (e1 < NH * NH) {
-        float *d = &s.w2[(e1 >> 7) * HS + (e1 & (NH - 1))];
-        d[0] = v.z; d[1] = v.w;
-      }
-    };
-    if (!slow) {
+  if (!slow) {
 #pragma unroll
-      for (int u = 0; u < NW2U; ++u) put_w2(tid + u * GTB, w2q[u]);
-      if (NW2X > 0 && tid < NW2X) put_w2(NW2U * GTB + tid, w2x);
+    for (int u = 0; u < NW2F; ++u) {
+      const int e = tid + u * GTB;
+      s.w2[(e >> 7) * HS + (e & (NH - 1))] = w2f[u];
     }
   }
   __syncthreads();
