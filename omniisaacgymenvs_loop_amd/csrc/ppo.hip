@@ -23,6 +23,7 @@
 #include "usv_device.h"
 
 USV_PROBE_DEFINE(ppo)
+USV_PROBE_DEFINE(pol)
 
 namespace {
 
@@ -87,6 +88,8 @@ struct MlpSmem {
   float hg[2][4][NH];     // head-gradient / bias half sums
   float b1[NH];
   float tail[TAIL + 1];   // params from b2 on (T_* offsets)
+  float om[NIN], od[NIN]; // policy step: (float)mean, sqrtf((float)var + eps) of the obs statistics
+  float zz[2][RB * 2];    // policy step: the N(0,1) draws of a tile's rows, one tile ahead
 };
 
 // Weight staging in two halves: every global load is issued up front into
@@ -194,6 +197,38 @@ __device__ __forceinline__ void put_obs_tile(const float (&x)[NUO], const ObsCol
   }
 }
 
+// The policy step's obs path runs on waves 1-3 (OT threads, tt = tid - 64) while wave 0 samples
+// the previous tile's actions and draws the next tile's normals; the statistics' per-column float
+// mean and denominator come from LDS (rms_norm's operations, so the same bits).
+constexpr int OT = TB - 64;
+constexpr int NUO3 = (RB * XS + OT - 1) / OT;
+__device__ __forceinline__ void load_obs_tile3(const float *__restrict__ obs, int n, int tile, int tt,
+                                               float (&x)[NUO3]) {
+  const int row0 = tile * RB, nrows = min(RB, n - row0);
+#pragma unroll
+  for (int u = 0; u < NUO3; ++u) {
+    const int q = min(tt + u * OT, RB * XS - 1);
+    const int r = min(q / XS, nrows - 1), kc = min(q % XS, NIN - 1);
+    x[u] = obs[(size_t)(row0 + r) * NIN + kc];
+  }
+}
+__device__ __forceinline__ void put_obs_tile3(const float (&x)[NUO3], int tt, int row0, int nrows, bool normalize,
+                                              float eps, MlpSmem &s, float *exp_obs, int H, int t) {
+#pragma unroll
+  for (int u = 0; u < NUO3; ++u) {
+    const int q = tt + u * OT;
+    if (q >= RB * XS) continue;
+    const int r = q / XS, k = q % XS;
+    float v = 0.f;
+    if (r < nrows && k < NIN) {
+      v = x[u];
+      exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = v;
+      if (normalize) v = clampt((v - s.om[k]) / s.od[k], -5.0f, 5.0f);   // = rms_norm
+    }
+    s.x[q] = v;
+  }
+}
+
 // Forward of the RB rows staged in s.x (W1, biases, heads staged; W2 still in
 // registers on a launch's first tile, committed after layer 1); leaves h1, h2, out.
 template <bool kBf>
@@ -279,65 +314,98 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
                                                     uint64_t seed, uint64_t step, const uint64_t *step_dev,
                                                     const float *eps_inject) {
   __shared__ MlpSmem s;
+  USV_PHASE(pol, 0);
   const int n = c.n_envs, H = c.horizon;
   if (step_dev) step = *step_dev + (uint64_t)t;   // the rollout's first step + slot
-  // persistent over 32-row tiles: the weights are staged once per workgroup, not once per tile
+  // persistent over 32-row tiles: the weights are staged once per workgroup, not once per tile.
+  // Per tile: the forward on all four waves; then wave 0 samples the tile's actions, stores its
+  // experience rows and draws the next tile's normals while waves 1-3 stage the next tile's obs
+  // (loaded during the forward) -- one barrier per tile outside the forward
   StagedW wr;
   stage_load(P, wr);
   const int ntiles = (n + RB - 1) / RB;
-  ObsCols oc;
-  load_obs_cols(obs_rms, oc);
-  float xo[NUO];
-  load_obs_tile(obs, n, min((int)blockIdx.x, ntiles - 1), xo);
+  const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int tt = (int)threadIdx.x - 64;
+  const bool normalize = c.normalize_input != 0;
+  if ((int)blockIdx.x >= ntiles) return;   // (the grid is at most ntiles; uniform)
+  // N(0,1) draws of tile `tl`'s rows (wave 0, lane = row) into s.zz[buf]
+  auto draw = [&](int tl, int buf) {
+    if (w == 0 && lane < RB) {
+      const int e = min(tl * RB + lane, n - 1);
+      float z0, z1;
+      if (eps_inject) {
+        z0 = eps_inject[2 * e];
+        z1 = eps_inject[2 * e + 1];
+      } else {  // Normal.sample via Box-Muller on Philox(site 0x200)
+        float u[4];
+        philox_u4(seed, (uint32_t)e, step, 0x200u, u);
+        const float rr0 = sqrtf(-2.0f * logf(1.0f - u[0])), rr1 = sqrtf(-2.0f * logf(1.0f - u[2]));
+        z0 = rr0 * cosf(USV_2PI_F * u[1]);
+        z1 = rr1 * cosf(USV_2PI_F * u[3]);
+      }
+      s.zz[buf][2 * lane] = z0;
+      s.zz[buf][2 * lane + 1] = z1;
+    }
+  };
+  if (threadIdx.x < NIN) {
+    s.om[threadIdx.x] = (float)obs_rms[threadIdx.x];
+    s.od[threadIdx.x] = sqrtf((float)obs_rms[NIN + threadIdx.x] + c.rms_eps);
+  }
+  float xo[NUO3];
+  if (w > 0) load_obs_tile3(obs, n, blockIdx.x, tt, xo);
+  __syncthreads();
+  if (w > 0) {
+    const int row0 = blockIdx.x * RB;
+    put_obs_tile3(xo, tt, row0, min(RB, n - row0), normalize, c.rms_eps, s, exp_obs, H, t);
+  }
+  draw(blockIdx.x, 0);
+  stage_store_small(wr, s);
+  __syncthreads();
+  int buf = 0;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int row0 = tile * RB;
   const int nrows = min(RB, n - row0);
-  float xn[NUO];   // the next tile's rows (the last tile again when none is left)
-  load_obs_tile(obs, n, min(tile + (int)gridDim.x, ntiles - 1), xn);
-  // s.x of the previous tile was last read before block_forward's first barrier
-  put_obs_tile(xo, oc, row0, nrows, c.normalize_input != 0, c.rms_eps, s, exp_obs, H, t);
-  if (tile == (int)blockIdx.x) stage_store_small(wr, s);
-  __syncthreads();
+  const int nt = tile + (int)gridDim.x;
+  float xn[NUO3];   // the next tile's rows, in flight during the forward
+  if (w > 0 && nt < ntiles) load_obs_tile3(obs, n, nt, tt, xn);
+  USV_PHASE(pol, 1);   // (probe slots 1-4: the launch's last tile)
+  USV_PHASE(pol, 2);
   block_forward<kBf>(wr, s, tile == (int)blockIdx.x);
-  const int r = threadIdx.x;
-  if (r < nrows) {
-    const int e = row0 + r;
-    const size_t slot = (size_t)e * H + t;
-    const float mu0 = s.out[r * 4], mu1 = s.out[r * 4 + 1], v = s.out[r * 4 + 2];
-    const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
-    const float sg0 = expf(ls0), sg1 = expf(ls1);
-    float z0, z1;
-    if (eps_inject) {
-      z0 = eps_inject[2 * e];
-      z1 = eps_inject[2 * e + 1];
-    } else {  // Normal.sample via Box-Muller on Philox(site 0x200)
-      float u[4];
-      philox_u4(seed, (uint32_t)e, step, 0x200u, u);
-      const float rr0 = sqrtf(-2.0f * logf(1.0f - u[0])), rr1 = sqrtf(-2.0f * logf(1.0f - u[2]));
-      z0 = rr0 * cosf(USV_2PI_F * u[1]);
-      z1 = rr1 * cosf(USV_2PI_F * u[3]);
+  USV_PHASE(pol, 3);
+  if (w == 0) {
+    const int r = lane;
+    if (r < nrows) {
+      const int e = row0 + r;
+      const size_t slot = (size_t)e * H + t;
+      const float mu0 = s.out[r * 4], mu1 = s.out[r * 4 + 1], v = s.out[r * 4 + 2];
+      const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
+      const float sg0 = expf(ls0), sg1 = expf(ls1);
+      const float z0 = s.zz[buf][2 * r], z1 = s.zz[buf][2 * r + 1];
+      const float a0 = mu0 + sg0 * z0, a1 = mu1 + sg1 * z1;
+      const float q0 = (a0 - mu0) / sg0, q1 = (a1 - mu1) / sg1;
+      const float nlp = 0.5f * (q0 * q0 + q1 * q1) + kLog2Pi + (ls0 + ls1);
+      float vd = v;
+      if (c.normalize_value) {  // denorm_value (running_mean_std.py:113-115)
+        vd = clampt(v, -5.0f, 5.0f);
+        vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
+      }
+      exp_act[slot * 2] = a0; exp_act[slot * 2 + 1] = a1;
+      exp_mu[slot * 2] = mu0; exp_mu[slot * 2 + 1] = mu1;
+      exp_sigma[slot * 2] = sg0; exp_sigma[slot * 2 + 1] = sg1;
+      exp_nlp[slot] = nlp;
+      exp_val[slot] = vd;
+      exp_done[slot] = (uint8_t)(dones_prev[e] != 0);
+      // preprocess_actions: clamp(-1,1) then rescale to [low, high] = identity (a2c_common.py:1134-1144)
+      actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
+      actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
     }
-    const float a0 = mu0 + sg0 * z0, a1 = mu1 + sg1 * z1;
-    const float q0 = (a0 - mu0) / sg0, q1 = (a1 - mu1) / sg1;
-    const float nlp = 0.5f * (q0 * q0 + q1 * q1) + kLog2Pi + (ls0 + ls1);
-    float vd = v;
-    if (c.normalize_value) {  // denorm_value (running_mean_std.py:113-115)
-      vd = clampt(v, -5.0f, 5.0f);
-      vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
-    }
-    exp_act[slot * 2] = a0; exp_act[slot * 2 + 1] = a1;
-    exp_mu[slot * 2] = mu0; exp_mu[slot * 2 + 1] = mu1;
-    exp_sigma[slot * 2] = sg0; exp_sigma[slot * 2 + 1] = sg1;
-    exp_nlp[slot] = nlp;
-    exp_val[slot] = vd;
-    exp_done[slot] = (uint8_t)(dones_prev[e] != 0);
-    // preprocess_actions: clamp(-1,1) then rescale to [low, high] = identity (a2c_common.py:1134-1144)
-    actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
-    actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
+    if (nt < ntiles) draw(nt, buf ^ 1);
+  } else if (nt < ntiles) {   // s.x was last read by the forward's layer 1 (before its first barrier)
+    put_obs_tile3(xn, tt, nt * RB, min(RB, n - nt * RB), normalize, c.rms_eps, s, exp_obs, H, t);
   }
-  __syncthreads();   // s.out of this tile is read above before the next tile's forward rewrites it
-#pragma unroll
-  for (int u = 0; u < NUO; ++u) xo[u] = xn[u];
+  __syncthreads();   // s.out / s.zz[buf] read above before the next tile's forward and draws rewrite them
+  USV_PHASE(pol, 4);
+  buf ^= 1;
   }
 }
 

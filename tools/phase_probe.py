@@ -59,6 +59,16 @@ def main():
     for k, what in ((9, "layer 1 done"), (10, "W2 committed"), (11, "layer-2 MFMA loop done"),
                     (12, "layer 2 done"), (2, "heads done"), (13, "dW2 MFMA loop done"), (5, "dW2 stored")):
         print(f"  slot {k:2d} {what:24s} t = {np.mean(b[:, k] - b[:, 0]) / 100:7.2f} us")
+    pp = read("pol")
+    b = pp[:256]
+    b = b[b[:, 0] > 0]
+    ntiles = (agent.num_actors + 31) // 32
+    per = (ntiles + 255) // 256
+    print(f"k_policy_step (last launch, {per} tiles per workgroup; slots 1-4 are the last tile):")
+    print(f"  last tile starts at t = {np.mean(b[:, 1] - b[:, 0]) / 100:7.2f} us (launch mean per tile "
+          f"{np.mean(b[:, 4] - b[:, 0]) / 100 / per:6.2f} us)")
+    for k, what in ((2, "obs staged"), (3, "forward done"), (4, "sampled + stored")):
+        print(f"  slot {k} {what:18s} +{np.mean(b[:, k] - b[:, k - 1]) / 100:6.2f} us")
     cnt = int(task.ctl[0].item())
     print("reset count of the last step:", cnt)
     report("k_field_wave (last launch)", read("field"), min(cnt, 512), 4, extra_col=15)
