@@ -125,10 +125,11 @@ def _load_dataset(ag, ppo):
     ag.exp_sigma.copy_(T(ppo["batch_sigmas"]))
 
 
-def _run_update(ppo, monkeypatch, fused, minibatch, mini_epochs, grad_norm=None):
+def _run_update(ppo, monkeypatch, fused, minibatch, mini_epochs, grad_norm=None, bf16=False):
     monkeypatch.setenv("USV_PPO_FUSED", "1" if fused else "0")
     H, N = ppo["exp_rewards"].shape[:2]
     ag = _agent(N, minibatch, mini_epochs)
+    ag.cfg.bf16_gemm = int(bf16)
     if grad_norm is not None:
         ag.cfg.truncate_grads, ag.cfg.grad_norm = 1, grad_norm
     _load_dataset(ag, ppo)
@@ -138,20 +139,20 @@ def _run_update(ppo, monkeypatch, fused, minibatch, mini_epochs, grad_norm=None)
             for k in ("model_params", "adam_m", "adam_v", "opt", "kls", "loss_log", "obs_rms")}
 
 
-@pytest.mark.parametrize("mb_div,mini_epochs", [(4, 8), (1, 3)])
-def test_fused_chain_matches_split_path(ppo, monkeypatch, mb_div, mini_epochs):
+@pytest.mark.parametrize("mb_div,mini_epochs,bf16", [(4, 8, False), (1, 3, False), (4, 8, True)])
+def test_fused_chain_matches_split_path(ppo, monkeypatch, mb_div, mini_epochs, bf16):
     """ppo_minibatch_fused / ppo_minibatch_finish (Adam step speculated inside the reduction, checked by
     the next launch) vs ppo_minibatch_grad + ppo_minibatch_apply: bit-identical parameters, moments,
     optimiser scalars, KLs and losses -- without clipping, with clipping at every step (the redo path),
-    with clipping at some steps, and for an odd chain (state copied back from bank 1)."""
+    with clipping at some steps, for an odd chain (state copied back from bank 1) and in the bf16 GEMM mode."""
     H, N = ppo["exp_rewards"].shape[:2]
     mb = N * H // mb_div
-    ref = _run_update(ppo, monkeypatch, False, mb, mini_epochs)
+    ref = _run_update(ppo, monkeypatch, False, mb, mini_epochs, bf16=bf16)
     last_norm = float(ref["opt"][3])   # the last minibatch's gradient norm: some steps above, some below
     assert last_norm > 0
     for gn in (None, 1e-4, last_norm):
-        a = ref if gn is None else _run_update(ppo, monkeypatch, False, mb, mini_epochs, gn)
-        b = _run_update(ppo, monkeypatch, True, mb, mini_epochs, gn)
+        a = ref if gn is None else _run_update(ppo, monkeypatch, False, mb, mini_epochs, gn, bf16)
+        b = _run_update(ppo, monkeypatch, True, mb, mini_epochs, gn, bf16)
         for k in a:
             np.testing.assert_array_equal(a[k], b[k], err_msg=f"{k} grad_norm={gn}")
         if gn == 1e-4:
