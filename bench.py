@@ -402,8 +402,11 @@ def main():
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size,
                              "launches_timed": len(ppo_timer.pairs),
                              "launch_ms_method": "median HIP event pair around each minibatch's gradient + reduction "
-                                                 "launches (ppo_minibatch_fused: k_mb_grad + k_reduce_partials with the "
-                                                 "Adam step) of one eager epoch, minus the empty pair"},
+                                                 + ("launches (ppo_minibatch_fused: k_mb_grad + k_reduce_partials with "
+                                                    "the Adam step)" if agent._fused_update() else
+                                                    "launches (ppo_minibatch_grad: k_mb_grad + k_reduce_partials; the "
+                                                    "all-reduce and k_apply follow outside the pair)")
+                                                 + " of one eager epoch, minus the empty pair"},
             "wall_clock_to_reward": dict(to_reward, unit="s", since="first env reset of this run (random-init policy)",
                                          last100_mean_at_end=float(agent.game_rewards.get_mean())),
             "extra": dict(phase),
