@@ -272,7 +272,7 @@ typedef struct usv_bufs {
 #define USV_SC_GOAL     37    /* goal_pos x, y */
 #define USV_SCENE_STRIDE 40
 
-#define USV_FIELD_SLOT_STATS 192   /* 16 + 12 per 2048-cell chunk (11 chunks), obstacles at 160 (32) */
+#define USV_FIELD_SLOT_STATS 192   /* 16 + 12 per 30-row band (5 bands), obstacles at 160 (32) */
 
 /* control words */
 #define USV_CTL_RESET_COUNT 0

@@ -480,9 +480,20 @@ __device__ __forceinline__ BatchK batch_k(const usv_cfg_t &c, const usv_bufs_t &
 }
 
 // ------------------------------------------------------------- pass C1 ---
-// Per (slot, 2048-cell chunk): statistics split by finite / infinite cost so
+// Per (slot, band of kBandRows grid rows): statistics split by finite / infinite cost so
 // the batch constant inf_val (known only when every env is done) enters
-// through one monotone scalar per batch.  Partials at slot_stats[slot][16 + 12 ch].
+// through one monotone scalar per batch.  Partials at slot_stats[slot][16 + 12 band].
+// The SDF is formed separably with cell_sdf's rounded operations: a thread owns two
+// adjacent columns, keeps (gx - ox)^2 of both for the 16 obstacles in registers and,
+// per row, forms gy - oy once for the two cells -- fmaf(dy, dy, dx * dx), the same
+// min tree, sqrt, minus the radius: the same bits in about half the instructions.
+// Every statistic is a min / max (any grouping gives the same value).
+constexpr int kBandRows = 30, kBands = G / kBandRows;       // row bands of a slot
+constexpr int kColPairs = G / 2, kRowGroups = 3;            // 75 column pairs x 3 row groups = 225 threads
+constexpr int kBandIters = kBandRows / kRowGroups;          // rows per thread and band
+static_assert(G % kBandRows == 0 && kBandRows % kRowGroups == 0 && kColPairs * kRowGroups <= 256 && G % 2 == 0,
+              "k_field_stats geometry");
+static_assert(kSlotObst >= 16 + 12 * kBands, "slot_stats band partials");
 __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
   __shared__ float red[10][4];
   __shared__ int flags[2];
@@ -490,53 +501,82 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   __shared__ float so[2 * USV_NOBST];
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const bool act = tid < kColPairs * kRowGroups;          // threads 225-255 only join the reductions
+  const int cp = act ? tid % kColPairs : 0, rg = act ? tid / kColPairs : 0;
+  const int c0 = 2 * cp;
   const float cell = (float)((double)c.map_size / G);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
-  const int items = count * kChunks;
+  const int items = count * kBands;
   if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
-    const int slot = w / kChunks, ch = w % kChunks;
+    const int slot = w / kBands, band = w % kBands;
     const int e = b.reset_ids[slot];
     const float *Fe = b.field + (size_t)e * G2;
     float *sdf_s = b.sdf + (size_t)slot * G2;
     if (tid < 2 * USV_NOBST) so[tid] = b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid];
     if (tid < 2) flags[tid] = 0;
     __syncthreads();
+    // the band's raw costs (two adjacent cells per row: one 8-byte load), all in flight at once
+    float2 gv[kBandIters];
+#pragma unroll
+    for (int k = 0; k < kBandIters; ++k) {
+      const int r = band * kBandRows + rg + kRowGroups * k;
+      gv[k] = *reinterpret_cast<const float2 *>(Fe + r * G + c0);
+    }
+    float dxa[USV_NOBST], dxb[USV_NOBST], oy[USV_NOBST];
+    {
+      const float gxa = slin[c0], gxb = slin[c0 + 1];
+#pragma unroll
+      for (int o = 0; o < USV_NOBST; ++o) {
+        const float ox = so[2 * o];
+        const float da = gxa - ox, db = gxb - ox;
+        dxa[o] = da * da;
+        dxb[o] = db * db;
+        oy[o] = so[2 * o + 1];
+      }
+    }
     float gmin = INFINITY, gmax = -INFINITY, jmin_f = INFINITY, jmax_f = -INFINITY, jall_f = 0.f;
     float jrmin_i = INFINITY, jrmax_i = -INFINITY, jrall_i = 0.f;
     int any_inf = 0, inside = 0;
-    const int q1 = min(G2, (ch + 1) * kChunk);
-    constexpr int PER = kChunk / 256;
-    float gv[PER], sv[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) gv[k] = Fe[min(ch * kChunk + k * 256 + tid, q1 - 1)];   // clamped: no branch
-    // the SDF of this chunk (k_field_final reads it back)
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int q = ch * kChunk + k * 256 + tid;
-      const int qc = min(q, G2 - 1);
-      sv[k] = cell_sdf(so, slin[qc % G], slin[qc / G], c.obstacle_radius);
-      if (q < q1) sdf_s[q] = sv[k];
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int q = ch * kChunk + k * 256 + tid;
-      if (q >= q1) continue;
-      const float g = gv[k];
-      const float dte = sv[k] - c.obstacle_radius;
+    // branch-free: each statistic takes its cell's value or the neutral element of its min / max
+    const auto stat = [&](float g, float sv) {
+      const float dte = sv - c.obstacle_radius;
       const bool ins = dte <= 0.f;
       inside |= ins;
       const float jr = j_raw(c, dte, inv_r);
-      if (isinf(g)) {
-        any_inf = 1;
-        jrall_i = fmaxf(jrall_i, jr);
-        if (!ins) { jrmin_i = fminf(jrmin_i, jr); jrmax_i = fmaxf(jrmax_i, jr); }
-      } else {
-        gmin = fminf(gmin, g);
-        gmax = fmaxf(gmax, g);
-        const float j = jr * goal_mask(c, g, cell);
-        jall_f = fmaxf(jall_f, j);
-        if (!ins) { jmin_f = fminf(jmin_f, j); jmax_f = fmaxf(jmax_f, j); }
+      const bool gi = isinf(g);
+      any_inf |= gi;
+      const float j = jr * goal_mask(c, g, cell);
+      jrall_i = fmaxf(jrall_i, gi ? jr : 0.f);
+      jrmin_i = fminf(jrmin_i, (gi && !ins) ? jr : INFINITY);
+      jrmax_i = fmaxf(jrmax_i, (gi && !ins) ? jr : -INFINITY);
+      gmin = fminf(gmin, gi ? INFINITY : g);
+      gmax = fmaxf(gmax, gi ? -INFINITY : g);
+      jall_f = fmaxf(jall_f, gi ? 0.f : j);
+      jmin_f = fminf(jmin_f, (!gi && !ins) ? j : INFINITY);
+      jmax_f = fmaxf(jmax_f, (!gi && !ins) ? j : -INFINITY);
+    };
+#pragma unroll
+    for (int k = 0; k < kBandIters; ++k) {
+      const int r = band * kBandRows + rg + kRowGroups * k;
+      const float gy = slin[r];
+      uint32_t a[USV_NOBST], bb[USV_NOBST];
+#pragma unroll
+      for (int o = 0; o < USV_NOBST; ++o) {
+        const float dy = gy - oy[o];
+        a[o] = __float_as_uint(fmaf(dy, dy, dxa[o]));
+        bb[o] = __float_as_uint(fmaf(dy, dy, dxb[o]));
+      }
+#pragma unroll
+      for (int wd = USV_NOBST / 2; wd >= 1; wd >>= 1)
+#pragma unroll
+        for (int o = 0; o < wd; ++o) { a[o] = min(a[o], a[o + wd]); bb[o] = min(bb[o], bb[o + wd]); }
+      const float sva = sqrtf(__uint_as_float(a[0])) - c.obstacle_radius;
+      const float svb = sqrtf(__uint_as_float(bb[0])) - c.obstacle_radius;
+      if (act) {
+        *reinterpret_cast<float2 *>(sdf_s + r * G + c0) = make_float2(sva, svb);   // k_field_final reads it back
+        stat(gv[k].x, sva);
+        stat(gv[k].y, svb);
       }
     }
     float vals[9] = {wave_min(gmin), wave_max(gmax), wave_min(jmin_f), wave_max(jmax_f), wave_max(jall_f),
@@ -555,13 +595,13 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
         a[2] = fminf(a[2], red[2][v]); a[3] = fmaxf(a[3], red[3][v]); a[4] = fmaxf(a[4], red[4][v]);
         a[5] = fminf(a[5], red[5][v]); a[6] = fmaxf(a[6], red[6][v]); a[7] = fmaxf(a[7], red[7][v]);
       }
-      float *pp = b.slot_stats + (size_t)slot * kSlotStride + 16 + 12 * ch;
+      float *pp = b.slot_stats + (size_t)slot * kSlotStride + 16 + 12 * band;
       pp[SS_GMIN_F] = a[0]; pp[SS_GMAX_F] = a[1]; pp[SS_ANY_INF] = flags[0] ? 1.f : 0.f;
       pp[SS_JMIN_F_NI] = a[2]; pp[SS_JMAX_F_NI] = a[3]; pp[SS_JMAX_F_ALL] = a[4];
       pp[SS_JRMIN_I_NI] = a[5]; pp[SS_JRMAX_I_NI] = a[6]; pp[SS_JRMAX_I_ALL] = a[7];
       pp[SS_INSIDE] = flags[1] ? 1.f : 0.f;
-      // the batch max of finite costs (:205-210) is folded from these chunk maxima by
-      // k_field_batch (one atomic per chunk on a single address serialised this kernel)
+      // the batch max of finite costs (:205-210) is folded from these band maxima by
+      // k_field_batch (one atomic per band on a single address serialised this kernel)
     }
     __syncthreads();
   }
@@ -591,12 +631,12 @@ __global__ __launch_bounds__(256) void k_field_batch(usv_cfg_t c, usv_bufs_t b) 
     float *st = b.slot_stats + (size_t)sl * kSlotStride;
     float a = 0.f;
     if (lane < 10) {
-      float x[kChunks];
+      float x[kBands];
 #pragma unroll
-      for (int ch = 0; ch < kChunks; ++ch) x[ch] = st[16 + 12 * ch + lane];
+      for (int ch = 0; ch < kBands; ++ch) x[ch] = st[16 + 12 * ch + lane];
       a = x[0];
 #pragma unroll
-      for (int ch = 1; ch < kChunks; ++ch) a = is_min ? fminf(a, x[ch]) : fmaxf(a, x[ch]);
+      for (int ch = 1; ch < kBands; ++ch) a = is_min ? fminf(a, x[ch]) : fmaxf(a, x[ch]);
       st[lane] = a;
     }
     const float s_gmax = __shfl(a, SS_GMAX_F, 64), s_anyinf = __shfl(a, SS_ANY_INF, 64);
@@ -705,7 +745,8 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_stats, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
+  const int grid_s = b->n * kBands < 4096 ? b->n * kBands : 4096;
+  hipLaunchKernelGGL(k_field_stats, dim3(grid_s), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_batch, dim3(kBatchBlocks), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
