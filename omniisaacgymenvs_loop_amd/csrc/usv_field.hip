@@ -161,6 +161,33 @@ __device__ __forceinline__ void cost_sweeps_exact(const uint32_t *occ, int ix, i
   }
 }
 
+// CaptureXYTask.get_spawns obstacle part (static_obs.py:968-1048) for every reset env whose
+// obstacles usv_reset handed over (ctl[PLACE], keys of its draws): one wave per reset env runs
+// the rejection sampling around the previous-episode target (usv_reset left the spawn in
+// px / py and that target in field_old_tgt) and stores the centres.  A launch of its own, so the
+// sweep kernel's four waves do not wait on one wave's sampling for every slot.
+constexpr int kPlaceTB = 256;
+__global__ __launch_bounds__(kPlaceTB) void k_field_place(usv_cfg_t c, usv_bufs_t b) {
+  if (b.ctl[USV_CTL_PLACE] == 0) return;
+  const int n = b.n;
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);
+  const uint64_t h_seed = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_HI] << 32);
+  const uint64_t h_step = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_HI] << 32);
+  const float *h_inj = reinterpret_cast<const float *>(
+      (uintptr_t)((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_HI] << 32)));
+  const int lane = threadIdx.x & 63;
+  const int waves = (int)gridDim.x * (kPlaceTB / 64);
+  for (int slot = (int)blockIdx.x * (kPlaceTB / 64) + (int)(threadIdx.x >> 6); slot < count; slot += waves) {
+    const int e = b.reset_ids[slot];
+    const float2 oc = place_obstacles(c, e, b.px[e], b.py[e], b.field_old_tgt[e], b.field_old_tgt[n + e], h_seed,
+                                      h_step, h_inj);
+    if (lane < USV_NOBST) {
+      b.obst[(size_t)(2 * lane) * n + e] = oc.x;
+      b.obst[(size_t)(2 * lane + 1) * n + e] = oc.y;
+    }
+  }
+}
+
 // LDS holds the tile edges and a 2.8 KB occupancy bit map (the SDF itself goes to
 // the per-slot HBM scratch only): 51 KB.  Two launch shapes of the same body:
 // k_field_wave_pack is held to 256 registers (its spills sit in the per-slot
@@ -179,12 +206,6 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);   // slots index reset_ids[0, n)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
-  // obstacle placement handed over by usv_reset (keys of its draws)
-  const bool place = b.ctl[USV_CTL_PLACE] != 0;
-  const uint64_t h_seed = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_HI] << 32);
-  const uint64_t h_step = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_HI] << 32);
-  const float *h_inj = reinterpret_cast<const float *>(
-      (uintptr_t)((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_HI] << 32)));
   // tile of this thread; waves own compact quadrants of the tile grid (8x8,
   // 8x7, 7x8, 7x7 tiles) so a wave idles as a whole while its region is ahead
   // of / behind the front
@@ -209,23 +230,8 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
   for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
     USV_PHASE(field, 0);
     const int e = b.reset_ids[slot];
-    if (place) {
-      // CaptureXYTask.get_spawns obstacle part (static_obs.py:968-1048) for this reset env: wave 0
-      // runs the rejection sampling around the previous-episode target (usv_reset left the spawn
-      // in px/py and that target in field_old_tgt) and publishes the centres
-      if (wid == 0) {
-        const float2 oc = place_obstacles(c, e, b.px[e], b.py[e], b.field_old_tgt[e], b.field_old_tgt[n + e],
-                                          h_seed, h_step, h_inj);
-        if (lane < USV_NOBST) {
-          so[2 * lane] = oc.x;
-          so[2 * lane + 1] = oc.y;
-          b.obst[(size_t)(2 * lane) * n + e] = oc.x;
-          b.obst[(size_t)(2 * lane + 1) * n + e] = oc.y;
-        }
-      }
-    } else if (tid < 2 * USV_NOBST) {
-      so[tid] = b.obst[(size_t)tid * n + e];
-    }
+    // the obstacle centres (placed for this reset by k_field_place, or the env's own)
+    if (tid < 2 * USV_NOBST) so[tid] = b.obst[(size_t)tid * n + e];
     if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
     for (int q = tid; q < G * kOccColWords; q += kWaveThreads) occ[q] = 0u;
     __syncthreads();
@@ -740,6 +746,10 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   // resets per step); USV_FIELD_PACK=0/1 forces either layout (A/B runs, tests)
   const char *pack_env = getenv("USV_FIELD_PACK");
   const bool pack = pack_env ? atoi(pack_env) != 0 : b->n >= kFieldPackMinEnvs;
+  // one wave per reset env: the grid covers n envs at most (the count lives on the device)
+  const int grid_p = (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) < 1024 ? (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) : 1024;
+  hipLaunchKernelGGL(k_field_place, dim3(grid_p), dim3(kPlaceTB), 0, s, *cfg, *b);
+  USV_CHECK_LAUNCH();
   if (pack) hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   else hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
