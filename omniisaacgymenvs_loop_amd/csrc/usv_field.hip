@@ -195,6 +195,7 @@ __global__ __launch_bounds__(kPlaceTB) void k_field_place(usv_cfg_t c, usv_bufs_
 // SIMD -- for batches that fill the chip more than once; k_field_wave keeps the
 // compiler's 256 + 76 registers and one env per CU, for small batches, where the
 // kernel is latency-bound and a shared CU would only slow the slowest env.
+template <bool kPlace>
 __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bufs_t &b) {
   __shared__ uint32_t occ[G * kOccColWords];
   __shared__ float edge[4][NTP * NTP][T];
@@ -206,6 +207,16 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);   // slots index reset_ids[0, n)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wid = tid >> 6;
+  // obstacle placement handed over by usv_reset (keys of its draws): done here only with kPlace
+  const bool place = kPlace && b.ctl[USV_CTL_PLACE] != 0;
+  uint64_t h_seed = 0, h_step = 0;
+  const float *h_inj = nullptr;
+  if (kPlace) {
+    h_seed = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_SEED_HI] << 32);
+    h_step = (uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_STEP_HI] << 32);
+    h_inj = reinterpret_cast<const float *>(
+        (uintptr_t)((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_LO] | ((uint64_t)(uint32_t)b.ctl[USV_CTL_H_INJ_HI] << 32)));
+  }
   // tile of this thread; waves own compact quadrants of the tile grid (8x8,
   // 8x7, 7x8, 7x7 tiles) so a wave idles as a whole while its region is ahead
   // of / behind the front
@@ -230,8 +241,24 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
   for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
     USV_PHASE(field, 0);
     const int e = b.reset_ids[slot];
-    // the obstacle centres (placed for this reset by k_field_place, or the env's own)
-    if (tid < 2 * USV_NOBST) so[tid] = b.obst[(size_t)tid * n + e];
+    if (kPlace && place) {
+      // CaptureXYTask.get_spawns obstacle part (static_obs.py:968-1048) for this reset env, as
+      // k_field_place does it: wave 0 samples and publishes the centres (small batches: one
+      // round of workgroups, where a separate launch would add its latency to the step)
+      if (wid == 0) {
+        const float2 oc = place_obstacles(c, e, b.px[e], b.py[e], b.field_old_tgt[e], b.field_old_tgt[n + e],
+                                          h_seed, h_step, h_inj);
+        if (lane < USV_NOBST) {
+          so[2 * lane] = oc.x;
+          so[2 * lane + 1] = oc.y;
+          b.obst[(size_t)(2 * lane) * n + e] = oc.x;
+          b.obst[(size_t)(2 * lane + 1) * n + e] = oc.y;
+        }
+      }
+    } else if (tid < 2 * USV_NOBST) {
+      // the obstacle centres (placed for this reset by k_field_place, or the env's own)
+      so[tid] = b.obst[(size_t)tid * n + e];
+    }
     if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
     for (int q = tid; q < G * kOccColWords; q += kWaveThreads) occ[q] = 0u;
     __syncthreads();
@@ -423,8 +450,10 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
   }
 }
 
-__global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) { field_wave_body(c, b); }
-__global__ __launch_bounds__(kWaveThreads, 2) void k_field_wave_pack(usv_cfg_t c, usv_bufs_t b) { field_wave_body(c, b); }
+__global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) { field_wave_body<true>(c, b); }
+__global__ __launch_bounds__(kWaveThreads, 2) void k_field_wave_pack(usv_cfg_t c, usv_bufs_t b) {
+  field_wave_body<false>(c, b);
+}
 
 // The reference's literal sweeps for the slots k_field_wave could not certify (SS_EXACT):
 // one workgroup per such slot, the occupancy bit map rebuilt from the slot's obstacles
@@ -746,10 +775,13 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   // resets per step); USV_FIELD_PACK=0/1 forces either layout (A/B runs, tests)
   const char *pack_env = getenv("USV_FIELD_PACK");
   const bool pack = pack_env ? atoi(pack_env) != 0 : b->n >= kFieldPackMinEnvs;
-  // one wave per reset env: the grid covers n envs at most (the count lives on the device)
-  const int grid_p = (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) < 1024 ? (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) : 1024;
-  hipLaunchKernelGGL(k_field_place, dim3(grid_p), dim3(kPlaceTB), 0, s, *cfg, *b);
-  USV_CHECK_LAUNCH();
+  if (pack) {
+    // large batches: placement first, one wave per reset env (the grid covers n envs at most;
+    // the count lives on the device); k_field_wave places in-kernel
+    const int grid_p = (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) < 1024 ? (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) : 1024;
+    hipLaunchKernelGGL(k_field_place, dim3(grid_p), dim3(kPlaceTB), 0, s, *cfg, *b);
+    USV_CHECK_LAUNCH();
+  }
   if (pack) hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   else hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
