@@ -906,15 +906,18 @@ struct RowIn {
 // Partial-gradient stores write through to the MALL (sc1): the 85 KB per workgroup leave
 // during the kernel instead of as dirty L2 lines at the kernel boundary (MI355X_MICROARCH.md,
 // publish-large / boundary rows)
+#ifndef USV_PART_AUX
+#define USV_PART_AUX 16   // cache-policy bits of the partial stores (A/B builds override it)
+#endif
 struct PartOut {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ void operator()(int idx, float v) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (uint32_t)idx * 4u, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (uint32_t)idx * 4u, 0, USV_PART_AUX);
   }
   __device__ __forceinline__ void x4(int idx, float a, float b, float c, float d) const {
     const u32x4_t v = {__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c),
                        __builtin_bit_cast(uint32_t, d)};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)idx * 4u, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)idx * 4u, 0, USV_PART_AUX);
   }
 };
 
