@@ -42,9 +42,14 @@ TASKS = {"CaptureXY": ("USV/IROS2024/USV_Virtual_CaptureXY_SysID-TEST", ENV_STEP
          "GoToPose": ("USV/USV_Virtual_GoToPose", 530, "k_env_step_task<GoToPose> (integrator + obs/reward/done)"),
          "TrackXYOVelocity": ("USV/USV_Virtual_TrackXYOVelocity", 574,
                               "k_env_step_task<TrackXYO> + k_track_finish (integrator + obs/reward/done)")}
-# PPO minibatch gradient kernel: forward (2*(33*128+128*128+128*3)) + backward
-# (2x the two hidden GEMMs + heads) = 6 x 21,120 + 2 x 384 flops per row.
-PPO_FLOPS_PER_ROW = 2 * (33 * 128 + 128 * 128 + 3 * 128) + 2 * (2 * 128 * 128 + 2 * 33 * 128 + 128 * 128 + 3 * 128)
+# PPO minibatch gradient kernel, algorithmic flops per row (DESIGN.md §4 derives them; elementwise work not
+# counted): forward = layer 1 2*33*128 + layer 2 2*128*128 + heads 2*128*3 = 41,984; backward = head weight
+# grads 2*3*128 + dh2 = dmu Wmu + dv Wv 2*3*128 + dW2 = dz2^T h1 2*128*128 + dh1 = dz2 W2 2*128*128 +
+# dW1 = dz1^T x 2*128*33 = 75,520; total 117,504
+PPO_FWD_FLOPS_PER_ROW = 2 * (33 * 128 + 128 * 128 + 128 * 3)
+PPO_BWD_FLOPS_PER_ROW = 2 * 3 * 128 + 2 * 3 * 128 + 2 * 128 * 128 + 2 * 128 * 128 + 2 * 128 * 33
+PPO_FLOPS_PER_ROW = PPO_FWD_FLOPS_PER_ROW + PPO_BWD_FLOPS_PER_ROW
+assert PPO_FLOPS_PER_ROW == 117_504
 
 
 def _dist_setup(gpus):

@@ -190,7 +190,18 @@ typedef struct usv_cfg {
   float tk_tol[2];          /* TrackXYO lin_vel_tolerance, ang_vel_tolerance */
   float tk_goal_rand[2];    /* TrackXYO goal_random_linear_velocity, goal_random_angular_velocity */
   float sig_gain;           /* GoToPoseReward.sig_gain */
+  /* ---- device NaN probe (USV_Virtual.py:57-95, vec_env_rlgames.py:41-80, env USV_NAN_PROBE):
+   * the step kernels OR the USV_NAN_* stage bits of any non-finite clamped action, state,
+   * reward or observation into ctl[USV_CTL_NAN_FLAG]; the host raises after the epoch ---- */
+  int   nan_probe;
 } usv_cfg_t;
+
+/* stage bits of ctl[USV_CTL_NAN_FLAG] / ppo_cfg_t.nan_flag (the reference's probe names) */
+#define USV_NAN_ACTIONS  1   /* actions(clamped)           vec_env_rlgames.py:143 */
+#define USV_NAN_STATE    2   /* state.position/orientation/velocities  USV_Virtual.py:810-813 */
+#define USV_NAN_REWARD   4   /* reward.rew_buf             USV_Virtual.py:1642-1648 */
+#define USV_NAN_OBS      8   /* obs(post_physics_step)     vec_env_rlgames.py:187-192 */
+#define USV_NAN_POLICY  16   /* policy mu / value of the rollout (get_action_values) */
 
 #define USV_TASK_CAPTURE_XY   0
 #define USV_TASK_GO_TO_POSE   1
@@ -415,7 +426,11 @@ typedef struct ppo_cfg {
   float reward_scale, reward_shift;
   float rms_eps;            /* 1e-5 */
   int   bf16_gemm;          /* 0: fp32 (the reference); 1: bf16 operands / fp32 accumulation for the
-                               128x128 products (layer 2, dW2, dh1) -- BASELINE configs[2] */
+                               128x128 products (layer 2, dW2, dh1) of the training step
+                               (ppo_minibatch_*; the reference's autocast covers calc_gradients only,
+                               a2c_continuous.py:121): the rollout kernels stay fp32 -- BASELINE configs[2] */
+  int   nan_probe;          /* 1: ppo_policy_step ORs USV_NAN_POLICY into *nan_flag on a non-finite mu / value */
+  int32_t *nan_flag;        /* device int (nullable) */
 } ppo_cfg_t;
 
 /* Rollout: obs RMS normalise (eval) -> MLP -> mu, value (denormalised),

@@ -231,7 +231,8 @@ __device__ __forceinline__ void put_obs_tile3(const float (&x)[NUO3], int tt, in
 
 // Forward of the RB rows staged in s.x (W1, biases, heads staged; W2 still in
 // registers on a launch's first tile, committed after layer 1); leaves h1, h2, out.
-template <bool kBf>
+// fp32 always: the reference's mixed_precision autocast covers calc_gradients only
+// (a2c_continuous.py:121); get_action_values / get_values run in fp32 under no_grad.
 __device__ void block_forward(const StagedW &wr, MlpSmem &s, bool first_tile) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
@@ -252,18 +253,10 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s, bool first_tile) {
   // ---- layer 2: h2 = tanh(h1 W2^T + b2) ----
   {
     f32x16 acc = {};
-    if constexpr (kBf) {
-#pragma unroll
-      for (int st = 0; st < NH / 16; ++st) {
-        const int k0 = 16 * st + 8 * h;
-        acc = mfma_bf16(ld8(&s.h1[i * HS + k0]), ld8(&s.w2[(n0 + i) * HS + k0]), acc);
-      }
-    } else {
 #pragma unroll 16
-      for (int st = 0; st < NH / 2; ++st) {
-        const int k = 2 * st + h;
-        acc = mfma32(s.h1[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
-      }
+    for (int st = 0; st < NH / 2; ++st) {
+      const int k = 2 * st + h;
+      acc = mfma32(s.h1[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
     }
     const float bj = s.tail[T_B2 + n0 + i];
 #pragma unroll
@@ -304,7 +297,6 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s, bool first_tile) {
 __host__ __device__ constexpr int policy_grid(int n) {
   return (n + RB - 1) / RB < 256 ? (n + RB - 1) / RB : 256;
 }
-template <bool kBf>
 __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms,
                                                     const double *__restrict__ val_rms, const float *__restrict__ obs,
@@ -370,7 +362,7 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   if (w > 0 && nt < ntiles) load_obs_tile3(obs, n, nt, tt, xn);
   USV_PHASE(pol, 1);   // (probe slots 1-4: the launch's last tile)
   USV_PHASE(pol, 2);
-  block_forward<kBf>(wr, s, tile == (int)blockIdx.x);
+  block_forward(wr, s, tile == (int)blockIdx.x);
   USV_PHASE(pol, 3);
   if (w == 0) {
     const int r = lane;
@@ -399,6 +391,10 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
       actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
       actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
     }
+    if (c.nan_probe && c.nan_flag) {   // wave 0, uniform
+      const bool bad = r < nrows && (nonfinite(s.out[r * 4]) | nonfinite(s.out[r * 4 + 1]) | nonfinite(s.out[r * 4 + 2]));
+      nan_report(c.nan_flag, bad ? USV_NAN_POLICY : 0u);
+    }
     if (nt < ntiles) draw(nt, buf ^ 1);
   } else if (nt < ntiles) {   // s.x was last read by the forward's layer 1 (before its first barrier)
     put_obs_tile3(xn, tt, nt * RB, min(RB, n - nt * RB), normalize, c.rms_eps, s, exp_obs, H, t);
@@ -409,7 +405,6 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   }
 }
 
-template <bool kBf>
 __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,
                                               const double *val_rms, const float *__restrict__ obs, float *values) {
   __shared__ MlpSmem s;
@@ -429,7 +424,7 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
     put_obs_tile(xo, oc, row0, nrows, c.normalize_input != 0, c.rms_eps, s, nullptr, 0, 0);
     if (tile == (int)blockIdx.x) stage_store_small(wr, s);
     __syncthreads();
-    block_forward<kBf>(wr, s, tile == (int)blockIdx.x);
+    block_forward(wr, s, tile == (int)blockIdx.x);
     const int r = threadIdx.x;
     if (r < nrows) {
       float vd = s.out[r * 4 + 2];
@@ -569,11 +564,46 @@ __device__ __forceinline__ void rms_merge(double *rm, int len, const double *bme
   rm[2 * len] = tot;
 }
 
-__global__ void k_prepare_finalize(ppo_cfg_t c, double *val_rms, double *work, int nblk) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  double s[6] = {0, 0, 0, 0, 0, 0};
-  for (int b = 0; b < nblk; ++b)
-    for (int q = 0; q < 6; ++q) s[q] += work[8 + (size_t)b * 8 + q];
+// One 256-thread workgroup: thread t folds the block partials t, t + 256, ... in order, then a
+// fixed LDS tree (deterministic, independent of timing) -- the serial fold of 512 partials by one
+// thread was 116 us per epoch at 131072 envs
+constexpr int FIN_TB = 256;
+__global__ __launch_bounds__(FIN_TB) void k_prepare_finalize(ppo_cfg_t c, double *val_rms, double *work, int nblk) {
+  __shared__ double red[6][FIN_TB];
+  const int tid = threadIdx.x;
+  {
+    double a[6] = {0, 0, 0, 0, 0, 0};
+    constexpr int U = 4;   // partial rows in flight per thread
+    for (int b0 = tid; b0 < nblk; b0 += U * FIN_TB) {
+      double x[U][6];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int b = min(b0 + u * FIN_TB, nblk - 1);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) x[u][q] = work[8 + (size_t)b * 8 + q];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (b0 + u * FIN_TB < nblk) {
+#pragma unroll
+          for (int q = 0; q < 6; ++q) a[q] += x[u][q];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red[q][tid] = a[q];
+  }
+  __syncthreads();
+  for (int wdt = FIN_TB / 2; wdt > 0; wdt >>= 1) {
+    if (tid < wdt) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) red[q][tid] += red[q][tid + wdt];
+    }
+    __syncthreads();
+  }
+  if (tid != 0) return;
+  double s[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) s[q] = red[q][0];
   const double B = (double)c.n_envs * c.horizon;
   const double mv = s[0] / B, vv = (s[1] - B * mv * mv) / (B - 1.0);
   const double mr = s[2] / B, vr = (s[3] - B * mr * mr) / (B - 1.0);
@@ -716,33 +746,56 @@ __global__ __launch_bounds__(TB) void k_obs_moments(ppo_cfg_t c, const float *__
   }
 }
 
-__global__ void k_obs_rms_seq(ppo_cfg_t c, const double *__restrict__ part, int nmb, double *obs_rms, double *seq) {
-  const int k = threadIdx.x;
-  if (k >= NIN) return;
+// One 256-thread workgroup.  Phase 1 (all threads, parallel over (minibatch, column)): each
+// minibatch's moments (bmean, unbiased bvar), staged in seq[mb] itself.  Phase 2 (thread k < 33):
+// Chan's merge in minibatch order -- the only serial part -- reading 8 minibatches' moments ahead
+// of the dependent fp64 chain, writing the running (mean, var) over them.
+constexpr int RS_TB = 256, RS_U = 8;
+__global__ __launch_bounds__(RS_TB) void k_obs_rms_seq(ppo_cfg_t c, const double *__restrict__ part, int nmb,
+                                                       double *obs_rms, double *seq) {
   const double rows = (double)c.minibatch;
-  double mean = obs_rms[k], var = obs_rms[NIN + k], count = obs_rms[2 * NIN];
-  for (int mb = 0; mb < nmb; ++mb) {
+  for (int q = threadIdx.x; q < nmb * NIN; q += RS_TB) {
+    const int mb = q / NIN, k = q % NIN;
     double sa = 0, sb = 0;
+#pragma unroll
     for (int ch = 0; ch < OM_CH; ++ch) {
       const double *o = part + ((size_t)mb * OM_CH + ch) * 2 * NIN;
       sa += o[k];
       sb += o[NIN + k];
     }
     const double bmean = sa / rows;
-    const double bvar = (sb - rows * bmean * bmean) / (rows - 1.0);
-    const double tot = count + rows;
-    const double delta = bmean - mean;
-    const double M2 = var * count + bvar * rows + delta * delta * count * rows / tot;
-    mean = mean + delta * rows / tot;
-    var = M2 / tot;
-    count = tot;
-    seq[(size_t)mb * 2 * NIN + k] = mean;
-    seq[(size_t)mb * 2 * NIN + NIN + k] = var;
+    seq[(size_t)mb * 2 * NIN + k] = bmean;
+    seq[(size_t)mb * 2 * NIN + NIN + k] = (sb - rows * bmean * bmean) / (rows - 1.0);
   }
-  obs_rms[k] = mean;
-  obs_rms[NIN + k] = var;
-  __syncthreads();
-  if (k == 0) obs_rms[2 * NIN] = count;
+  __syncthreads();   // (workgroup-scope release / acquire of the staged moments)
+  const int k = threadIdx.x;
+  if (k < NIN) {
+    double mean = obs_rms[k], var = obs_rms[NIN + k], count = obs_rms[2 * NIN];
+    for (int mb0 = 0; mb0 < nmb; mb0 += RS_U) {
+      double bm[RS_U], bv[RS_U];
+#pragma unroll
+      for (int u = 0; u < RS_U; ++u) {
+        const int mb = min(mb0 + u, nmb - 1);
+        bm[u] = seq[(size_t)mb * 2 * NIN + k];
+        bv[u] = seq[(size_t)mb * 2 * NIN + NIN + k];
+      }
+#pragma unroll
+      for (int u = 0; u < RS_U; ++u) {
+        if (mb0 + u >= nmb) break;
+        const double tot = count + rows;
+        const double delta = bm[u] - mean;
+        const double M2 = var * count + bv[u] * rows + delta * delta * count * rows / tot;
+        mean = mean + delta * rows / tot;
+        var = M2 / tot;
+        count = tot;
+        seq[(size_t)(mb0 + u) * 2 * NIN + k] = mean;
+        seq[(size_t)(mb0 + u) * 2 * NIN + NIN + k] = var;
+      }
+    }
+    obs_rms[k] = mean;
+    obs_rms[NIN + k] = var;
+    if (k == 0) obs_rms[2 * NIN] = count;   // (every thread's count is the same)
+  }
 }
 
 // ------------------------------------------------------ minibatch grad ----
@@ -1576,7 +1629,7 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
                     const float *eps_inject, void *stream) {
   if (!cfg || !params || !obs_rms || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
   const int grid = policy_grid(cfg->n_envs);
-  hipLaunchKernelGGL(cfg->bf16_gemm ? k_policy_step<true> : k_policy_step<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
+  hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
                      obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
                      actions_out, seed, step, step_dev, eps_inject);
   USV_CHECK_LAUNCH();
@@ -1587,7 +1640,7 @@ int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, 
               const float *obs, float *values, void *stream) {
   if (!cfg || !params || !obs_rms || !obs || !values || cfg->n_envs <= 0) return 1;
   const int grid = policy_grid(cfg->n_envs);
-  hipLaunchKernelGGL(cfg->bf16_gemm ? k_value<true> : k_value<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
+  hipLaunchKernelGGL(k_value, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
                      values);
   USV_CHECK_LAUNCH();
   return 0;
@@ -1622,7 +1675,7 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
   hipLaunchKernelGGL(k_gae, dim3(nblk), dim3(TB), 0, s, *cfg, last_val, last_dones, exp_done, exp_val, exp_rew,
                      exp_ret, exp_adv, work);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_prepare_finalize, dim3(1), dim3(64), 0, s, *cfg, val_rms, work, nblk);
+  hipLaunchKernelGGL(k_prepare_finalize, dim3(1), dim3(FIN_TB), 0, s, *cfg, val_rms, work, nblk);
   USV_CHECK_LAUNCH();
   const size_t B = (size_t)cfg->n_envs * cfg->horizon;
   hipLaunchKernelGGL(k_prepare_apply, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, *cfg, work, exp_val,
@@ -1736,7 +1789,7 @@ int ppo_obs_rms_epoch(const ppo_cfg_t *cfg, const float *exp_obs, int rows, doub
   double *part = rms_seq + (size_t)nmb * 2 * NIN;
   hipLaunchKernelGGL(k_obs_moments, dim3(nmb, OM_CH), dim3(TB), 0, s, *cfg, exp_obs, part);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_obs_rms_seq, dim3(1), dim3(64), 0, s, *cfg, part, nmb, obs_rms, rms_seq);
+  hipLaunchKernelGGL(k_obs_rms_seq, dim3(1), dim3(RS_TB), 0, s, *cfg, part, nmb, obs_rms, rms_seq);
   USV_CHECK_LAUNCH();
   return 0;
 }

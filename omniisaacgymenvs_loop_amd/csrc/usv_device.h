@@ -132,6 +132,19 @@ __device__ __forceinline__ float wave_min(float v) {
   return v;
 }
 
+// Device NaN probe (the reference's USV_NAN_PROBE fail-fast, USV_Virtual.py:57-95,
+// vec_env_rlgames.py:41-80): each lane brings the USV_NAN_* stage bits it saw; the common
+// path is one ballot, a wave that saw any ORs them into *flag with one atomic.  Call from
+// wave-uniform control flow.
+__device__ __forceinline__ void nan_report(int32_t *flag, uint32_t bits) {
+  if (__ballot(bits != 0u) == 0ull) return;
+  uint32_t m = bits;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) m |= (uint32_t)__shfl_xor((int)m, off, 64);
+  if ((threadIdx.x & 63) == 0) atomicOr(flag, (int)m);
+}
+__device__ __forceinline__ uint32_t nonfinite(float x) { return isfinite(x) ? 0u : 1u; }
+
 // float atomic max for non-negative-or-any floats via int ordering
 __device__ __forceinline__ void atomic_max_f32(float *addr, float v) {
   if (v >= 0.f) atomicMax((int *)addr, __float_as_int(v));

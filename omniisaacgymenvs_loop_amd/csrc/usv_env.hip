@@ -937,6 +937,13 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     const u32x2_t rb64 = {(uint32_t)rb, 0u};
     __builtin_amdgcn_raw_buffer_store_b64(rb64, R, mine ? (uint32_t)ec * 8u : kDrop, w.dones, 0);
     __builtin_amdgcn_raw_buffer_store_b8((uint8_t)0, R, mine ? (uint32_t)ec : kDrop, w.just_reset, 0);
+    if (c.nan_probe) {   // clamped actions, the observed state, the reward (obs: at the row store below)
+      uint32_t bits = ((nonfinite(cmd0) | nonfinite(cmd1)) ? USV_NAN_ACTIONS : 0u) |
+                      ((nonfinite(pxn) | nonfinite(pyn) | nonfinite(yawn) | nonfinite(vxn) | nonfinite(vyn) |
+                        nonfinite(wzn)) ? USV_NAN_STATE : 0u) |
+                      (nonfinite(ro.rew) ? USV_NAN_REWARD : 0u);
+      nan_report(&b.ctl[USV_CTL_NAN_FLAG], mine ? bits : 0u);
+    }
     if (kStats) {
       const float add[25] = {ro.total, ro.dist_r, ro.align_r, rp.hi_r, ro.shaping, rp.speed_r, rp.ang_r, ro.turn_haz,
                              rp.goal_r, c.time_reward, coll, ro.danger, (float)(ro.danger > 0.5f), ro.gate_pos, dist,
@@ -953,18 +960,28 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   const int row0 = blockIdx.x * kBlock;
   const int rows = min(kBlock, n - row0);
   const uint32_t obase = (uint32_t)row0 * (uint32_t)(USV_NOBS * 4);
+  // obs entries are clamped to +-clip_obs, so only a NaN is non-finite: x != x
+  uint32_t obad = 0u;
   if (part == 0) {
     const int nv = rows * USV_NOBS / 4;       // whole float4s (row0 * 33 * 4 B is 16-B aligned)
     for (int i = tid; i < nv; i += kBlock) {
       const float4 v = reinterpret_cast<const float4 *>(sobs)[i];
+      obad |= (uint32_t)((v.x != v.x) | (v.y != v.y) | (v.z != v.z) | (v.w != v.w));
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v),
                                              R, obase + (uint32_t)i * 16u, w.obs, 0);
     }
-    for (int i = nv * 4 + tid; i < rows * USV_NOBS; i += kBlock) bst(R, w.obs, obase + (uint32_t)i * 4u, sobs[i]);
+    for (int i = nv * 4 + tid; i < rows * USV_NOBS; i += kBlock) {
+      obad |= (uint32_t)(sobs[i] != sobs[i]);
+      bst(R, w.obs, obase + (uint32_t)i * 4u, sobs[i]);
+    }
   } else {
     for (int i = tid; i < rows * USV_NOBS; i += kBlock)
-      if (keep[i / USV_NOBS]) bst(R, w.obs, obase + (uint32_t)i * 4u, sobs[i]);
+      if (keep[i / USV_NOBS]) {
+        obad |= (uint32_t)(sobs[i] != sobs[i]);
+        bst(R, w.obs, obase + (uint32_t)i * 4u, sobs[i]);
+      }
   }
+  if (c.nan_probe) nan_report(&b.ctl[USV_CTL_NAN_FLAG], obad ? USV_NAN_OBS : 0u);
   // ---- the step has consumed the Nones (:361, :448, USV_task_rewards.py:450): marked here,
   // promoted to the POT/PEN/REW_VALID flags by the next usv_reset, so the flags never change
   // while a step kernel that reads them runs ----
@@ -1275,7 +1292,18 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(usv_cfg_t c, usv_bufs_
   const int row0 = blockIdx.x * kBlock;
   const int rows = min(kBlock, n - row0);
   float *ob = b.obs + (size_t)row0 * USV_NOBS;
-  for (int i = tid; i < rows * USV_NOBS; i += kBlock) ob[i] = sobs[i];
+  uint32_t obad = 0u;
+  for (int i = tid; i < rows * USV_NOBS; i += kBlock) {
+    obad |= (uint32_t)(sobs[i] != sobs[i]);
+    ob[i] = sobs[i];
+  }
+  if (c.nan_probe) {   // clamped actions, the observed state, the reward (TrackXYO: k_track_finish), obs
+    uint32_t bits = ((nonfinite(cmd0) | nonfinite(cmd1)) ? USV_NAN_ACTIONS : 0u) |
+                    ((nonfinite(pxn) | nonfinite(pyn) | nonfinite(yawn) | nonfinite(vxn) | nonfinite(vyn) |
+                      nonfinite(wzn)) ? USV_NAN_STATE : 0u) |
+                    ((kKind == USV_TASK_GO_TO_POSE && nonfinite(overall + pen_sum)) ? USV_NAN_REWARD : 0u);
+    nan_report(&b.ctl[USV_CTL_NAN_FLAG], (mine ? bits : 0u) | (obad ? USV_NAN_OBS : 0u));
+  }
   if (blockIdx.x == 0 && tid == 0) b.ctl[USV_CTL_STEPPED] = 1;
 }
 
@@ -1298,6 +1326,13 @@ __global__ __launch_bounds__(kBlock) void k_track_finish(usv_cfg_t c, usv_bufs_t
   }
   const float ang_d = sqrtf(sred[0]);
   const int e = blockIdx.x * kBlock + tid;
+  if (c.nan_probe) {   // the reward of every env (one wave-uniform probe ahead of the per-env tail)
+    const int ec = min(e, n - 1);
+    const float *ts = b.task_scratch;
+    const float ang_r = task_term(c.tk_mode[1], ang_d, c.tk_coeff[1]) * c.tk_scale[1];
+    const float rew = (ts[USV_TS_LIN_REW * nn + ec] + ang_r) + ts[USV_TS_PEN * nn + ec];
+    nan_report(&b.ctl[USV_CTL_NAN_FLAG], (e < n && nonfinite(rew)) ? USV_NAN_REWARD : 0u);
+  }
   if (e >= n) return;
   const float *ts = b.task_scratch;
   const int ang_ok = ang_d < c.tk_tol[1];

@@ -57,10 +57,12 @@ class VecEnvRLGames:
     def check_errors(self) -> None:
         """Raise the errors the device path flags instead of raising mid-step (a host sync; called
         by the trainer after each epoch, outside graph capture): scene replay past its last scene
-        with cycle off -> IndexError, as USV_Virtual.py:1386-1390."""
-        chk = getattr(self._task, "check_scene_replay", None)
-        if chk is not None:
-            chk()
+        with cycle off -> IndexError, as USV_Virtual.py:1386-1390; a non-finite action, state, reward or
+        observation -> the USV_NAN_PROBE RuntimeError (USV_Virtual.py:57-95, vec_env_rlgames.py:41-80)."""
+        for name in ("check_scene_replay", "check_nan"):
+            chk = getattr(self._task, name, None)
+            if chk is not None:
+                chk()
 
     def advance_host_clock(self, steps: int) -> None:
         """A captured rollout graph was replayed: the device step clock advanced by `steps`."""

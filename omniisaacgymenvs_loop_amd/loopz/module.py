@@ -173,6 +173,12 @@ class Actor:
     """module.py:54-96."""
 
     def __init__(self, architecture: MLPEncode_wrap, distribution: SquashedGaussianDiagonalCovariance, device="cpu"):
+        # the actor kernels (lz_act, lz_minibatch: loopz.hip k_lz_forward / k_lz_grad) always take tanh of the
+        # mean head, i.e. MLPEncode_wrap(..., output_activation_fn=nn.Tanh); an actor without it would be
+        # sampled and trained as if it had one
+        if not architecture.out_tanh:
+            raise NotImplementedError("loopz actor: the kernels implement a Tanh output activation only "
+                                      "(architecture.activation: tanh)")
         self.architecture = architecture
         self.distribution = distribution
         self.device = device
@@ -193,6 +199,8 @@ class Critic:
     """module.py:98-115."""
 
     def __init__(self, architecture: MLPEncode_wrap, device="cpu"):
+        if architecture.out_tanh:   # the critic kernels emit the linear value head
+            raise NotImplementedError("loopz critic: the kernels implement a linear value head (no output activation)")
         self.architecture = architecture
         self.device = device
 

@@ -122,7 +122,15 @@ class PPO:
         for info in infos:
             ep = info.get("episode") if isinstance(info, dict) else None
             if ep is not None:
-                self.ep_infos.append(ep)
+                # the reference's extras["episode"] holds fresh tensors per reset (USV_Virtual.py:1591-1612);
+                # here they are views of one device buffer the next reset overwrites: snapshot them (one
+                # stack kernel, no host sync)
+                keys = list(ep.keys())
+                vals = [ep[k] for k in keys]
+                if keys and all(torch.is_tensor(v) and v.numel() == 1 for v in vals):
+                    self.ep_infos.append((keys, torch.stack([v.reshape(()).float() for v in vals])))
+                else:
+                    self.ep_infos.append((keys, vals))
 
     def step(self, value_obs, rews, dones, infos):
         self.step_device(torch.as_tensor(np.asarray(rews, np.float32)), torch.as_tensor(np.asarray(dones).astype(np.int64)),
@@ -180,9 +188,24 @@ class PPO:
     def adam_step(self) -> int:
         return int(round(float(self.opt[1].item())))
 
-    def log(self, it):
+    def log(self, it, pad=28):
+        """ppo.py:178-235: per-key 'Mean episode' lines over the episode infos of this update (non-finite
+        values skipped, as _to_float / np.isfinite there), then the losses and the action noise."""
         self.tot_timesteps += self.num_transitions_per_env * self.num_envs
-        print(f"{'#' * 80}\n{'Value function loss:':>28} {self.mean_value_loss:.4f}\n"
+        ep_string = ""
+        if self.ep_infos:
+            keys = self.ep_infos[0][0]
+            rows = []
+            for ks, v in self.ep_infos:
+                v = v.cpu().numpy() if torch.is_tensor(v) else np.array(
+                    [float(x.item()) if torch.is_tensor(x) else float(x) for x in v], np.float64)
+                rows.append(dict(zip(ks, v.tolist())))
+            for key in keys:
+                vals = [r[key] for r in rows if key in r and np.isfinite(r[key])]
+                if vals:
+                    ep_string += f"{f'Mean episode {key}:':>{pad}} {float(np.mean(vals)):.4f}\n"
+        self.last_episode_log = ep_string
+        print(f"{'#' * 80}\n{ep_string}{'Value function loss:':>28} {self.mean_value_loss:.4f}\n"
               f"{'Surrogate loss:':>28} {self.mean_surrogate_loss:.4f}\n"
               f"{'Mean action noise std:':>28} {float(self.actor.distribution.std.mean()):.2f}")
 

@@ -31,6 +31,7 @@ from .._abi import DEFINES, PpoAdamBanks, PpoCfg
 from . import checkpoint as ckpt
 from . import dist_util
 from . import vecenv
+from ..tasks.usv_config import nan_probe_enabled, raise_nan_flag
 
 NIN, NH, NA = DEFINES["PPO_NIN"], DEFINES["PPO_NH"], DEFINES["PPO_NA"]
 NPARAM = DEFINES["PPO_NPARAM"]
@@ -204,6 +205,8 @@ class A2CAgent:
         # elsewhere (no loss scaling needed with bf16's exponent range) -- BASELINE configs[2]
         self.mixed_precision = bool(config.get("mixed_precision", False))
         c.bf16_gemm = int(self.mixed_precision)
+        # device NaN probe of the rollout's policy outputs (USV_NAN_PROBE, USV_Virtual.py:57-95)
+        c.nan_probe = nan_probe_enabled()
         self._alloc()
         self.frame = 0
         self.epoch_num = 0
@@ -284,6 +287,8 @@ class A2CAgent:
         self.kls = torch.zeros(self.mini_epochs_num * self.num_minibatches, **f32)
         # per minibatch: a_loss, c_loss, entropy, b_loss, kl (this rank), written by the reduce kernel
         self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 8), **f32)
+        self.nan_flag = torch.zeros(1, device=dev, dtype=torch.int32)
+        self.cfg.nan_flag = self.nan_flag.data_ptr()
 
     # ------------------------------------------------------------- rollout
     def env_reset(self):
@@ -393,14 +398,24 @@ class A2CAgent:
             self.opt[:8].copy_(self.opt[8:])
 
     def _update_capturable(self) -> bool:
-        """The minibatch update goes into a HIP graph on one GPU and, with several ranks, when the
-        gradient all-reduces are RCCL collectives (capturable on the launch stream; gloo's host-staged
-        collectives are not).  USV_GRAPH_COLLECTIVES=0 keeps the multi-rank update eager."""
+        """The minibatch update goes into a HIP graph on one GPU.  With several ranks, RCCL collectives inside
+        a captured graph are opt-in (USV_GRAPH_COLLECTIVES=1, nccl backend only: gloo's host-staged
+        collectives are not capturable); by default the multi-rank update with torch.distributed
+        collectives runs eagerly."""
         if getattr(self, "_graph_update_failed", False):
             return False
         if not self.multi_gpu or self.rank_size == 1:
             return True
-        return dist_util.backend() == "nccl" and os.getenv("USV_GRAPH_COLLECTIVES", "1") != "0"
+        return dist_util.backend() == "nccl" and os.getenv("USV_GRAPH_COLLECTIVES", "0") == "1"
+
+    def _ranks_agree(self, ok: bool) -> bool:
+        """All ranks succeeded (MIN over ranks; outside any capture), so no rank replays a graph while another
+        falls back to eager collectives."""
+        if not self.multi_gpu or self.rank_size == 1:
+            return ok
+        flag = torch.tensor([1.0 if ok else 0.0], device=self.ppo_device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        return bool(flag.item() == 1.0)
 
     def _graph_capture(self, fn):
         g = torch.cuda.CUDAGraph()
@@ -440,14 +455,17 @@ class A2CAgent:
         self.algo_observer.after_steps()
         if graphs and self._update_capturable():
             if self._graph_update is None:
+                err = None
                 try:
                     self._graph_update = self._graph_capture(self.update_epoch_minibatches)
-                except RuntimeError as err:   # a collective the backend cannot capture: eager from now on
+                except RuntimeError as e:   # a collective the backend cannot capture
+                    err = e
+                torch.cuda.synchronize()
+                if not self._ranks_agree(err is None):   # eager from now on, on every rank
                     self._graph_update_failed = True
                     self._graph_update = None
                     if self.rank == 0:
-                        print(f"update graph capture failed ({err}); the update runs eagerly")
-                    torch.cuda.synchronize()
+                        print(f"update graph capture failed ({err or 'on another rank'}); the update runs eagerly")
                     self.update_epoch_minibatches()
                 else:
                     self._graph_update.replay()
@@ -457,9 +475,10 @@ class A2CAgent:
             self.update_epoch_minibatches()
         torch.cuda.current_stream().synchronize()
         update_time_end = time.time()
-        chk = getattr(self.vec_env, "check_errors", None)   # device-flagged env errors (scene replay)
+        chk = getattr(self.vec_env, "check_errors", None)   # device-flagged env errors (scene replay, NaN probe)
         if chk is not None:
             chk()
+        self._check_nan()
         self._eager_epochs += 1
         self._replay_meters()
         self.last_lr = float(self.opt[0].item())
@@ -468,6 +487,14 @@ class A2CAgent:
             step_time = play_time_end - play_time_start
         return (step_time, play_time_end - play_time_start, update_time_end - play_time_end,
                 update_time_end - play_time_start)
+
+    def _check_nan(self):
+        """USV_NAN_PROBE for the policy side: a non-finite mu / value in the rollout's forward."""
+        if self.cfg.nan_probe:
+            bits = int(self.nan_flag.item())
+            if bits:
+                self.nan_flag.zero_()
+                raise_nan_flag(bits, f"rollout of epoch {self.epoch_num}")
 
     def _replay_meters(self):
         m = self.meter.cpu().numpy()
@@ -539,7 +566,10 @@ class A2CAgent:
     # ----------------------------------------------------------- checkpoints
     def get_full_state_weights(self) -> Dict[str, Any]:
         step = float(self.opt[1].item())
-        return {"model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms, self.obs_dim),
+        # get_weights -> get_stats_weights puts the GradScaler state first under mixed_precision (a2c_common.py:628-631)
+        state = {"scaler": ckpt.grad_scaler_state(step)} if self.mixed_precision else {}
+        return {**state,
+                "model": ckpt.model_state_dict(self.model_params, self.obs_rms, self.val_rms, self.obs_dim),
                 "epoch": self.epoch_num,
                 "optimizer": ckpt.optimizer_state_dict(self.adam_m, self.adam_v, step, float(self.opt[0].item()),
                                                        self.cfg.weight_decay, self.obs_dim),

@@ -123,6 +123,16 @@ def load_optimizer_state_dict(osd: Dict[str, Any], adam_m: torch.Tensor, adam_v:
     return step, float(osd["param_groups"][0]["lr"])
 
 
+def grad_scaler_state(steps: float) -> Dict[str, Any]:
+    """torch.cuda.amp.GradScaler().state_dict() as the reference's mixed_precision run leaves it after `steps`
+    optimizer steps with finite gradients (a2c_common.py:243, 326-330, 631): init scale 2**16, doubled every
+    2000 consecutive finite steps.  The bf16 GEMM mode needs no loss scaling (bf16 keeps fp32's exponent range)
+    and its non-finite guard is the NaN probe, so the entry is bookkeeping for checkpoint compatibility."""
+    steps = int(steps)
+    return {"scale": 65536.0 * 2.0 ** (steps // 2000), "growth_factor": 2.0, "backoff_factor": 0.5,
+            "growth_interval": 2000, "_growth_tracker": steps % 2000}
+
+
 def safe_filesystem_op(func, *args, **kwargs):
     """torch_ext.safe_filesystem_op: 5 attempts with exponential back-off (torch_ext.py:54-69)."""
     for attempt in range(5):

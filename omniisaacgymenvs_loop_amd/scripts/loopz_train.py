@@ -132,7 +132,10 @@ def train(cfg, max_updates=None, log=print):
             action = ppo.observe_device(obs)
             rew, dones = env.step_device(action)
             info = env.get_extras()
-            ppo.step_device(rew, dones, infos=[info] if isinstance(info, dict) and info.get("episode") else [])
+            # episode infos reach the PPO log only on a step where some env is done (rlgames_train.py:440-456)
+            done_any = bool(dones.any().item())
+            ppo.step_device(rew, dones, infos=[info] if done_any and isinstance(info, dict) and info.get("episode")
+                            else [])
             rew_sum += rew.double().sum()
             done_sum += dones.double().sum()
         env.curriculum_callback()

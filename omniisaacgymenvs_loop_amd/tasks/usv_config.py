@@ -15,6 +15,7 @@ resolves every flag the reference resolves at construction time:
 from __future__ import annotations
 
 import math
+import os
 import re
 from typing import Any, Dict
 
@@ -320,7 +321,28 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     c.current_on = int(bool(wc.get("use_water_current", False)))
     flow = list(wc.get("flow_velocity", [0.0, 0.0, 0.0]) or [0.0, 0.0, 0.0])
     c.flow_vel[0], c.flow_vel[1] = float(flow[0]), float(flow[1])
+    # the reference's fail-fast probe toggle (USV_Virtual.py:57-59): on unless USV_NAN_PROBE=0
+    c.nan_probe = nan_probe_enabled()
     return c
+
+
+def nan_probe_enabled() -> int:
+    """USV_NAN_PROBE (USV_Virtual.py:57-59, vec_env_rlgames.py:41-43): default on, "0" disables."""
+    return int(os.getenv("USV_NAN_PROBE", "1") != "0")
+
+
+NAN_STAGES = (("actions(clamped)", "USV_NAN_ACTIONS"), ("state", "USV_NAN_STATE"), ("reward.rew_buf", "USV_NAN_REWARD"),
+              ("obs(post_physics_step)", "USV_NAN_OBS"), ("policy mu/value (get_action_values)", "USV_NAN_POLICY"))
+
+
+def raise_nan_flag(bits: int, where: str) -> None:
+    """The reference's RuntimeError of _raise_if_nonfinite (USV_Virtual.py:91-95) for a device flag word."""
+    if not bits:
+        return
+    from .._abi import DEFINES
+    names = [name for name, key in NAN_STAGES if bits & DEFINES[key]]
+    raise RuntimeError(f"[USV_NAN_PROBE] non-finite detected: {', '.join(names)} ({where}; flag bits {bits:#x}; "
+                       f"set USV_NAN_PROBE=0 to disable)")
 
 
 TASK_KINDS = {"CaptureXY": 0, "GoToPose": 1, "TrackXYOVelocity": 2}   # USV_TASK_* (include/usv_hip.h)

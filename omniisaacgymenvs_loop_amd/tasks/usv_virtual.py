@@ -21,8 +21,8 @@ import torch
 from .. import _capi
 from .._abi import DEFINES, UsvBufs, enum_values
 from ..utils.spaces import Box, DictSpace
-from .usv_config import (action_bias_cfg, build_hydro_cfg, build_usv_cfg, env_origins, has_disturbance, stat_names,
-                         thruster_tables)
+from .usv_config import (action_bias_cfg, build_hydro_cfg, build_usv_cfg, env_origins, has_disturbance,
+                         raise_nan_flag, stat_names, thruster_tables)
 
 NOBS = DEFINES["USV_NOBS"]
 NOBST = DEFINES["USV_NOBST"]
@@ -178,6 +178,18 @@ class USVVirtual:
         """Raise the reference's IndexError if a reset ran past the scenes with cycle off (host sync)."""
         if self.scene is not None and int(self.ctl[DEFINES["USV_CTL_SCENE_ERR"]].item()):
             raise IndexError(f"scene_replay index out of range: num_scenes={self.scene_replay_num_scenes}")
+
+    def check_nan(self) -> None:
+        """The reference's USV_NAN_PROBE fail-fast (USV_Virtual.py:57-95, vec_env_rlgames.py:41-80) for the
+        steps since the last check: the step kernels OR the stage of any non-finite clamped action, state,
+        reward or observation into ctl[USV_CTL_NAN_FLAG] (no per-step host sync); one read here."""
+        if not self.cfg.nan_probe:
+            return
+        i = DEFINES["USV_CTL_NAN_FLAG"]
+        bits = int(self.ctl[i].item())
+        if bits:
+            self.ctl[i] = 0
+            raise_nan_flag(bits, "env step")
 
     def _make_bufs(self) -> UsvBufs:
         b = UsvBufs()

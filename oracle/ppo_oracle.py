@@ -216,6 +216,67 @@ def minibatch_grad(P: dict, xn, act, old_nlp, old_val, ret, adv, old_mu, old_sig
     return flatten(G), losses, float(kl), mu, sigma
 
 
+def prepare_dataset(values_hn, rewards_hn, dones_hn, last_values, last_dones, cfg: PPOConfig, vrms: RMS,
+                    normalize_value=True, normalize_advantage=True):
+    """discount_values + returns (a2c_common.py:525-540, :763) and ContinuousA2CBase.prepare_dataset
+    (:1257-1290): value RMS trained on the values then on the returns, both normalised, advantages
+    (returns - values) normalised by their unbiased std.  Inputs [H, N] (values / rewards / dones of the
+    rollout slots), last_values / last_dones [N]; outputs env-major [N*H] (swap_and_flatten01), vrms updated."""
+    H, N = rewards_hn.shape
+    advs = discount_values(cfg.gamma, cfg.tau, np.asarray(last_dones, F), np.asarray(last_values, F)[:, None],
+                           np.asarray(dones_hn, F), np.asarray(values_hn, F)[:, :, None],
+                           np.asarray(rewards_hn, F)[:, :, None])
+    rets = (advs + np.asarray(values_hn, F)[:, :, None]).astype(F)
+    flat = lambda a: np.ascontiguousarray(np.swapaxes(a, 0, 1).reshape(N * H))
+    values, returns = flat(np.asarray(values_hn, F)), flat(rets[:, :, 0])
+    adv = (returns - values).astype(F)
+    if normalize_value:
+        vrms.update(values[:, None])
+        values = vrms.norm(values)
+        vrms.update(returns[:, None])
+        returns = vrms.norm(returns)
+    if normalize_advantage:
+        a64 = adv.astype(np.float64)
+        adv = ((adv - F(a64.mean())) / (F(a64.std(ddof=1)) + F(1e-8))).astype(F)
+    return values, returns, adv
+
+
+PHILOX_M = (0xD2511F53, 0xCD9E8D57)
+PHILOX_W = (0x9E3779B9, 0xBB67AE85)
+
+
+def philox4x32_10(ctr, key):
+    """Philox4x32-10 (Salmon et al. SC'11) over numpy arrays: ctr = 4 uint32 arrays (broadcast), key = 2
+    ints; the generator of every in-kernel draw (csrc/usv_device.h philox4x32_10), restated vectorised
+    and pinned against the C oracle's Random123 known-answer vectors (tests/test_oracle_golden.py)."""
+    mask = np.uint64(0xFFFFFFFF)
+    c = [np.asarray(x, np.uint64) & mask for x in np.broadcast_arrays(*ctr)]
+    k0, k1 = np.uint64(key[0] & 0xFFFFFFFF), np.uint64(key[1] & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(PHILOX_M[0]) * c[0]
+        p1 = np.uint64(PHILOX_M[1]) * c[2]
+        c = [(p1 >> np.uint64(32)) ^ c[1] ^ k0, p1 & mask, (p0 >> np.uint64(32)) ^ c[3] ^ k1, p0 & mask]
+        k0 = (k0 + np.uint64(PHILOX_W[0])) & mask
+        k1 = (k1 + np.uint64(PHILOX_W[1])) & mask
+    return [x.astype(np.uint32) for x in c]
+
+
+def u01(x):
+    return ((np.asarray(x, np.uint32) >> np.uint32(8)).astype(F) * F(1.0 / 16777216.0)).astype(F)
+
+
+def policy_normals(seed: int, step: int, n: int, site: int = 0x200):
+    """The rollout kernel's Normal.sample draws (models.py:372-386 replaced by Box-Muller on
+    Philox(key = seed, ctr = {env, step_lo, step_hi, site}), csrc/ppo.hip k_policy_step): [n, 2] fp32."""
+    e = np.arange(n, dtype=np.uint64)
+    r = philox4x32_10((e, step & 0xFFFFFFFF, (step >> 32) & 0xFFFFFFFF, site), (seed & 0xFFFFFFFF, seed >> 32))
+    u = [u01(x) for x in r]
+    two_pi = F(6.28318530717958647692)
+    z0 = np.sqrt(F(-2.0) * np.log(F(1.0) - u[0])) * np.cos(two_pi * u[1])
+    z1 = np.sqrt(F(-2.0) * np.log(F(1.0) - u[2])) * np.cos(two_pi * u[3])
+    return np.stack([z0, z1], 1).astype(F)
+
+
 def clip_grad(g: np.ndarray, max_norm: float):
     parts = unflatten(g)
     norms = np.array([np.linalg.norm(parts[k].astype(np.float64)) for k, _ in SHAPES], np.float64)

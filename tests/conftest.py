@@ -7,6 +7,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+# the checker's OpenMP build (bit-identical to the serial one: every parallel loop is over independent envs /
+# reset slots) keeps the headline-size oracle runs (thousands of potential fields) to seconds
+os.environ.setdefault("USV_ORACLE_OMP", "1")
 
 
 def pytest_configure(config):

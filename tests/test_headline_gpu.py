@@ -1,0 +1,225 @@
+"""Parity at the headline size (131,072 envs per GPU: BASELINE configs[4]'s 2^20 envs over 8 GPUs) for the
+code paths that only run above the sizes of the other parity tests:
+
+* the rollout kernels' persistent multi-tile loop (16 tiles per workgroup at 131,072 envs: next-tile obs
+  prefetch, next-tile normal draws by wave 0, W2 committed on the first tile only), with injected draws and
+  with the in-kernel Philox + Box-Muller sampler (models.py:372-386 Normal.sample), and ppo_value;
+* GAE + prepare_dataset over 131,072 x 16 rows (k_gae's 512 block partials, the k_prepare_finalize fold);
+* the potential field for ~1,300 resets in both launch shapes (3 rounds of the 512-workgroup sweep grid,
+  grid-stride statistics / final kernels, the 64-workgroup batch-max fold) and with in-step obstacle
+  placement over 8,192 resets (k_field_place's grid stride);
+* the episode-meter fold over several reward workgroups.
+
+Checkers: the numpy PPO oracle (oracle/ppo_oracle.py) and the C env oracle (oracle/usv_oracle.c, OpenMP
+build), both pinned to the reference's fixtures by the CPU tests.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import oracle as O
+from oracle import ppo_oracle as PO
+from omniisaacgymenvs_loop_amd.tasks.usv_config import load_yaml
+from tests import errtab as ET
+from tests.test_env_gpu import _oracle_for, _run_field, _task, _vs_oracle
+from tests.test_oracle_golden import TEST_YAML
+from tests.test_ppo_gpu import _agent
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+HEAD = 131072          # envs per GPU of BASELINE configs[4]
+H = 16
+
+
+def _rand_agent(n, rng, mini_epochs=1):
+    """Agent with random weights incl. biases / log-sigma and non-trivial obs / value statistics."""
+    ag = _agent(n, 8192, mini_epochs)
+    P = PO.unflatten(ag.model_params.cpu().numpy())
+    for k in ("b1", "b2", "bv", "bmu"):
+        P[k] = rng.normal(0, 0.1, P[k].shape).astype(np.float32)
+    P["sigma"] = np.array([-0.3, 0.2], np.float32)
+    ag.model_params.copy_(torch.tensor(PO.flatten(P), device=DEV))
+    om, ov = rng.normal(0, 0.5, 33), rng.uniform(0.5, 3.0, 33)
+    ag.obs_rms[:33] = torch.tensor(om, dtype=torch.float64)
+    ag.obs_rms[33:66] = torch.tensor(ov, dtype=torch.float64)
+    ag.val_rms[:2] = torch.tensor([0.3, 2.5], dtype=torch.float64)
+    return ag, P, PO.RMS(om, ov, 1.0), PO.RMS(np.array([0.3]), np.array([2.5]), 1.0)
+
+
+@pytest.mark.parametrize("inject", [True, False], ids=["eps_inject", "philox"])
+def test_policy_step_headline_multi_tile(inject):
+    """k_policy_step at 131,072 envs (256 workgroups x 16 tiles) vs the oracle forward: actions, mu, sigma,
+    neglogp, denormalised value, raw obs rows and done flags of rollout slot t, the clamped env actions.
+    philox: the in-kernel sampler (site 0x200, step from the device clock as in graph replay) vs its
+    restatement PO.policy_normals."""
+    from omniisaacgymenvs_loop_amd import _capi as c
+    rng = np.random.default_rng(11)
+    N, t, seed = HEAD, 5, 1234
+    ag, P, orms, vrms = _rand_agent(N, rng)
+    obs = rng.normal(0, 2, (N, 33)).astype(np.float32)
+    dprev = (rng.random(N) < 0.1).astype(np.int64)
+    step0 = 2 ** 33 + 11
+    step_dev = torch.tensor([step0], device=DEV, dtype=torch.int64)
+    z = rng.normal(0, 1, (N, 2)).astype(np.float32) if inject else PO.policy_normals(seed, step0 + t, N)
+    eps = torch.tensor(z, device=DEV) if inject else None
+    c.call("ppo_policy_step", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
+           c.ptr(torch.tensor(obs, device=DEV)), t, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp),
+           c.ptr(ag.exp_val), c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.exp_done),
+           c.ptr(torch.tensor(dprev, device=DEV)), c.ptr(ag.actions), seed, 0, c.ptr(step_dev), c.ptr(eps),
+           c.stream_ptr())
+    torch.cuda.synchronize()
+    _, _, mu, v = PO.forward(P, orms.norm(obs))
+    v = vrms.denorm(v)[:, 0]
+    logstd = mu * 0 + P["sigma"]
+    sigma = np.exp(logstd).astype(np.float32)
+    act = (mu + sigma * z).astype(np.float32)
+    nlp = PO.neglogp(act, mu, sigma, logstd)
+    sl = np.arange(N) * H + t
+    g = lambda x: x.cpu().numpy()[sl]
+    tn = f"headline_policy_{'inj' if inject else 'philox'}"
+    np.testing.assert_array_equal(g(ag.exp_obs), obs)
+    np.testing.assert_array_equal(g(ag.exp_done), dprev.astype(np.uint8))
+    ET.check(tn, "mu", g(ag.exp_mu), mu, 1e-5, 1e-5, ["mu0", "mu1"])
+    ET.check(tn, "sigma", g(ag.exp_sigma), sigma, 1e-5, 1e-5, ["s0", "s1"])
+    ET.check(tn, "value", g(ag.exp_val), v, 1e-5, 1e-5)
+    ET.check(tn, "action", g(ag.exp_act), act, 1e-5, 1e-5, ["a0", "a1"])
+    ET.check(tn, "neglogp", g(ag.exp_nlp), nlp, 1e-5, 1e-5)
+    ET.check(tn, "env_action", ag.actions.cpu().numpy(), np.clip(act, -1, 1), 1e-5, 1e-5, ["a0", "a1"])
+    # the other slots of the experience rows are untouched
+    other = np.arange(N) * H + (t + 1)
+    assert float(np.abs(ag.exp_act.cpu().numpy()[other]).max()) == 0.0
+
+
+def test_value_headline_multi_tile():
+    """k_value (ppo_value) at 131,072 envs vs the oracle's denormalised value."""
+    from omniisaacgymenvs_loop_amd import _capi as c
+    rng = np.random.default_rng(12)
+    ag, P, orms, vrms = _rand_agent(HEAD, rng)
+    obs = rng.normal(0, 2, (HEAD, 33)).astype(np.float32)
+    out = torch.zeros(HEAD, device=DEV)
+    c.call("ppo_value", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
+           c.ptr(torch.tensor(obs, device=DEV)), c.ptr(out), c.stream_ptr())
+    torch.cuda.synchronize()
+    _, _, _, v = PO.forward(P, orms.norm(obs))
+    ET.check("headline_value", "value", out.cpu().numpy(), vrms.denorm(v)[:, 0], 1e-5, 1e-5)
+
+
+def test_prepare_headline_multi_block():
+    """ppo_prepare over 131,072 x 16 rows: GAE (a2c_common.py:525-540), returns, the value RMS trained on the
+    values then the returns, normalised values / returns, normalised advantages (:1257-1290) -- the 512-block
+    fp64 partials and their fold -- vs PO.prepare_dataset."""
+    rng = np.random.default_rng(13)
+    N = HEAD
+    ag, P, orms, vrms = _rand_agent(N, rng)
+    values = rng.normal(0.5, 1.0, (H, N)).astype(np.float32)
+    rewards = rng.normal(0.0, 0.2, (H, N)).astype(np.float32)
+    dones = (rng.random((H, N)) < 0.05).astype(np.uint8)
+    last_obs = rng.normal(0, 2, (N, 33)).astype(np.float32)
+    last_dones = (rng.random(N) < 0.05).astype(np.int64)
+    flat = lambda a: torch.tensor(np.ascontiguousarray(np.swapaxes(a, 0, 1).reshape(N * H)), device=DEV)
+    ag.exp_val.copy_(flat(values))
+    ag.exp_rew.copy_(flat(rewards))
+    ag.exp_done.copy_(flat(dones))
+    ag.obs = {"obs": {"state": torch.tensor(last_obs, device=DEV)}}
+    ag.dones = torch.tensor(last_dones, device=DEV)
+    ag.prepare_dataset()
+    torch.cuda.synchronize()
+    assert ag.normalize_input
+    _, _, _, lv = PO.forward(P, orms.norm(last_obs))
+    lv = (vrms.denorm(lv) if ag.normalize_value else lv)[:, 0]
+    vn, rn, an = PO.prepare_dataset(values, rewards, dones, lv, last_dones, PO.PPOConfig(), vrms,
+                                    ag.normalize_value, ag.normalize_advantage)
+    tn = "headline_prepare"
+    ET.check(tn, "values", ag.exp_val.cpu().numpy(), vn, 1e-5, 1e-5)
+    ET.check(tn, "returns", ag.exp_ret.cpu().numpy(), rn, 1e-5, 1e-5)
+    ET.check(tn, "advantages", ag.exp_adv.cpu().numpy(), an, 1e-5, 1e-5)
+    vr = ag.val_rms.cpu().numpy()
+    np.testing.assert_allclose(vr[:2], [vrms.mean[0], vrms.var[0]], rtol=1e-9)
+    assert vr[2] == vrms.count
+
+
+@pytest.mark.parametrize("pack", ["0", "1"])
+def test_potential_field_1300_resets_vs_oracle(pack, monkeypatch):
+    """~1,300 reset envs (the headline size's steady-state reset count) at 4,096 envs, whose launch geometry
+    equals 131,072 envs' (512 sweep workgroups -> 3 rounds, 4,096 statistics / final workgroups -> grid
+    stride, 64-workgroup batch-max fold): bit-exact against the oracle (d_multi_gemini.py:66-271)."""
+    monkeypatch.setenv("USV_FIELD_PACK", pack)
+    task = _task(load_yaml(TEST_YAML), 4096)
+    rng = np.random.default_rng(21)
+    K = 1300
+    obst = (rng.uniform(0, 1, (K, 16, 2)) * 24 - 12).astype(np.float32)
+    obst[0, :3] = [[0.3, 0.1], [1.2, -0.4], [-0.9, 0.8]]     # crowd the target
+    obst[1, :] = 999.0                                         # empty map
+    obst[2, 5:] = 999.0                                        # leftovers in limbo
+    tgt = rng.uniform(-3, 3, (K, 2)).astype(np.float32)
+    tgt[3] = obst[3, 0]                                        # occupied target cell
+    ids = rng.choice(4096, K, replace=False).astype(np.int32)
+    f = _run_field(task, ids, obst, tgt)
+    ref = O.potential_field(task.cfg, obst, tgt)
+    np.testing.assert_array_equal(f, ref)
+
+
+def test_philox_placement_8192_resets_vs_oracle(monkeypatch):
+    """The large-batch reset path at 8,192 envs, all reset on the first step: k_field_place's grid stride
+    (1,024 workgroups x 4 waves < 8,192 reset envs), 16 rounds of the packed sweep grid and the batch fold,
+    with in-kernel Philox draws vs the oracle: obstacles and every field bit-exact, then two more steps
+    (obs / reward / dones as in test_env_gpu's Philox tests)."""
+    monkeypatch.setenv("USV_FIELD_PACK", "1")
+    task_cfg = load_yaml(TEST_YAML)
+    n = 8192
+    task = _task(task_cfg, n)
+    E = _oracle_for(task.cfg, n, task_cfg)
+    rng = np.random.default_rng(22)
+    dp = np.zeros(n)
+    for t in range(3):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        bias = task.current_action_bias()
+        obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
+        ids = E.full_step(a, bias, t, seed=task.seed)
+        torch.cuda.synchronize()
+        if t == 0:
+            assert len(ids) == n
+            np.testing.assert_array_equal(task.obst.cpu().numpy().reshape(16, 2, n), E.obst)
+            np.testing.assert_array_equal(task.field.cpu().numpy(), E.field)
+        dp = _vs_oracle("headline_philox_8192", task, E, obs, rew, dones, t, dp)
+
+
+def test_meter_fold_multi_workgroup():
+    """ppo_store_reward over 4 reward workgroups (1,024 envs): shaped rewards into the experience rows, the
+    per-slot meter sums folded in workgroup order (a2c_common.py:721-759, tr_helpers.py:33-43), and the
+    AverageMeter replay, vs a numpy restatement of the per-env episode bookkeeping."""
+    from omniisaacgymenvs_loop_amd import _capi as c
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import AverageMeter
+    N = 1024
+    ag = _agent(N, 8192)
+    rng = np.random.default_rng(14)
+    rew = rng.uniform(0.2, 2.0, (H, N)).astype(np.float32)   # positive: the sums have no cancellation
+    dn = (rng.random((H, N)) < 0.15).astype(np.int64)
+    ag.meter_buf.zero_()
+    cr, cs, cl = (np.zeros(N, np.float32) for _ in range(3))
+    sums = np.zeros((H, 4))
+    ends = []
+    scale, shift = ag.cfg.reward_scale, ag.cfg.reward_shift
+    for t in range(H):
+        r_t, d_t = torch.tensor(rew[t], device=DEV), torch.tensor(dn[t], device=DEV)
+        c.call("ppo_store_reward", c.byref(ag.cfg), c.ptr(r_t), c.ptr(d_t), t, c.ptr(ag.exp_rew), c.ptr(ag.cur_rew),
+               c.ptr(ag.cur_shaped), c.ptr(ag.cur_len), c.ptr(ag.meter_buf), None, c.stream_ptr())
+        torch.cuda.synchronize()
+        shaped = ((rew[t] + np.float32(shift)) * np.float32(scale)).astype(np.float32)
+        cr, cs, cl = cr + rew[t], cs + shaped, cl + np.float32(1)
+        d = dn[t] != 0
+        sums[t] = [cr[d].sum(dtype=np.float64), cs[d].sum(dtype=np.float64), cl[d].sum(dtype=np.float64), d.sum()]
+        ends.append((cr[d].copy(), cl[d].copy()))
+        cr, cs, cl = cr * ~d, cs * ~d, cl * ~d
+    np.testing.assert_array_equal(ag.exp_rew.cpu().numpy().reshape(N, H), ((rew + np.float32(shift)) *
+                                                                           np.float32(scale)).T)
+    ET.check("headline_meters", "sums", ag.meter.cpu().numpy(), sums, 1e-5, 1e-5, ["rew", "shaped", "len", "cnt"])
+    ag._replay_meters()
+    ref = AverageMeter(ag.games_to_track)
+    for t in range(H):
+        cnt = int(sums[t, 3])
+        if cnt:
+            ref.update_stats(sums[t, 0] / cnt, cnt)
+    assert ag.game_rewards.current_size == ref.current_size
+    ET.check("headline_meters", "game_rewards", ag.game_rewards.get_mean(), ref.get_mean(), 1e-5, 1e-5)

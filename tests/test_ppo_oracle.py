@@ -95,3 +95,34 @@ def test_minibatch_update_epoch(ppo):
     Pr = _params(ppo, "final")
     for k in Pr:
         np.testing.assert_allclose(Pf[k], Pr[k], rtol=0, atol=2e-5, err_msg=k)
+
+
+def test_vectorised_philox_matches_c_oracle():
+    """PO.philox4x32_10 (numpy, the checker of the rollout kernel's in-kernel normals) == the C oracle's
+    Philox (itself pinned by the Random123 known-answer vectors in test_oracle_golden.py)."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(0)
+    ctr = rng.integers(0, 2 ** 32, (64, 4), dtype=np.uint64)
+    key = rng.integers(0, 2 ** 32, (64, 2), dtype=np.uint64)
+    for c, k in zip(ctr, key):
+        want = O.philox(c.astype(np.uint32), k.astype(np.uint32))
+        got = PO.philox4x32_10(tuple(int(x) for x in c), (int(k[0]), int(k[1])))
+        assert [int(x) for x in got] == [int(x) for x in want]
+    z = PO.policy_normals(42, 2 ** 33 + 7, 200_000)
+    assert abs(float(z.mean())) < 0.01 and abs(float(z.std()) - 1) < 0.01
+
+
+def test_prepare_dataset_helper_vs_reference(ppo):
+    """PO.prepare_dataset (the headline-size checker of ppo_prepare) reproduces the reference's prepared dataset."""
+    P = _params(ppo, "init")
+    cfg = PO.PPOConfig(minibatch=int(ppo["hyper"][2]))
+    H, N = ppo["exp_rewards"].shape[:2]
+    _, _, _, last_v = PO.forward(P, PO.RMS.zeros(33).norm(ppo["env_obs"][H]))
+    last_v = PO.RMS.zeros(1).denorm(last_v)[:, 0]
+    vrms = PO.RMS.zeros(1)
+    vn, rn, an = PO.prepare_dataset(ppo["exp_values"][:, :, 0], ppo["exp_rewards"][:, :, 0], ppo["exp_dones"],
+                                    last_v, ppo["env_dones"][H - 1], cfg, vrms)
+    np.testing.assert_allclose(vn, ppo["ds_old_values"][:, 0], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(rn, ppo["ds_returns"][:, 0], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(an, ppo["ds_advantages"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(vrms.var, ppo["final_value_mean_std__running_var"], rtol=1e-6)
