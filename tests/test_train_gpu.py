@@ -101,3 +101,28 @@ def test_priv4_training_keeps_pad_columns_zero(tmp_path):
     ck = C.load_checkpoint(str(tmp_path / "ck.pth"))
     assert tuple(ck["model"][C.W1_KEY].shape) == (C.NH, 29)
     assert tuple(ck["model"]["running_mean_std.running_mean_std.state.running_mean"].shape) == (29,)
+
+
+def test_nan_probe_raises(monkeypatch):
+    """USV_NAN_PROBE (USV_Virtual.py:57-95, vec_env_rlgames.py:41-80): a NaN action reaches the env step
+    kernel -> the device flag -> RuntimeError naming the stage at the epoch's check; a NaN in the policy
+    weights -> the rollout kernel's flag; USV_NAN_PROBE=0 disables both."""
+    env, task, ag = _agent_env(256, 1024, False, seed=2)
+    ag.obs = ag.env_reset()
+    ag.train_epoch()                                   # finite: no raise
+    a = torch.zeros((256, 2), device="cuda:0")
+    a[17, 1] = float("nan")
+    env.step(a)
+    with pytest.raises(RuntimeError, match=r"USV_NAN_PROBE.*actions\(clamped\)"):
+        env.check_errors()
+    env.check_errors()                                 # the flag was cleared by the raise
+    ag.model_params[5] = float("nan")                  # a W1 entry: every mu / value of the rollout is NaN
+    with pytest.raises(RuntimeError, match=r"USV_NAN_PROBE.*(policy mu/value|actions)"):
+        ag.train_epoch()
+    torch.cuda.synchronize()
+    monkeypatch.setenv("USV_NAN_PROBE", "0")
+    env2, task2, ag2 = _agent_env(256, 1024, False, seed=2)
+    ag2.obs = ag2.env_reset()
+    ag2.model_params[5] = float("nan")
+    ag2.train_epoch()                                  # probe off: no raise
+    assert not torch.isfinite(ag2.exp_mu).all()
