@@ -542,6 +542,41 @@ int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int
 int ppo_minibatch_finish(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int count, const float *grad,
                          float *kl_out, void *stream);
 
+/* ------------------------------------------------------------------------
+ * Several ranks (one process per GPU, a2c_common.py:87-101): the same two-launch chain with the
+ * gradient all-reduce (trancate_gradients_and_step's flat SUM / rank_size, a2c_common.py:308-323, and the
+ * legacy schedule's KL SUM / rank_size, :1218-1222) done INSIDE the reduction kernel as a one-shot
+ * exchange over xGMI peer memory: the workgroup that owns a 128-slot chunk stores its rank's chunk into
+ * every rank's receive buffer (IPC-mapped), raises one flag per receiver, waits for every sender's flag of
+ * its chunk, sums the senders in rank order (deterministic, the same result on every rank), divides by
+ * the rank count and takes the speculative Adam step as ppo_minibatch_fused does.  No collective library,
+ * nothing for the host to launch between the kernels: the whole update stays one HIP graph.
+ * Replaces A2CBase.trancate_gradients_and_step's dist.all_reduce (a2c_common.py:308-323).
+ * ------------------------------------------------------------------------ */
+#define PPO_DP_MAX 8
+typedef struct ppo_dp {
+  int rank, world;              /* this rank, number of ranks (<= PPO_DP_MAX) */
+  void *peer[PPO_DP_MAX];       /* receive buffer of rank r mapped into this process (peer[rank] = own);
+                                   each ppo_dp_buffer_bytes(), zeroed, from ppo_dp_alloc */
+  uint32_t *clock;              /* this rank's device minibatch counter (advanced by the gradient kernel) */
+  int32_t *err;                 /* device word: bit 0 set when a peer's chunk did not arrive within timeout_ms */
+  int timeout_ms;
+  int pad;
+} ppo_dp_t;
+/* bytes of one rank's receive buffer: [2 parities][PPO_DP_MAX senders][slots] floats + arrival flags */
+long long ppo_dp_buffer_bytes(void);
+/* hipMalloc + zero one receive buffer; ipc_handle (64 bytes, hipIpcMemHandle_t) for the other ranks */
+int ppo_dp_alloc(void **dptr, void *ipc_handle);
+/* map another rank's receive buffer (hipIpcOpenMemHandle, lazy peer access) / unmap / free our own */
+int ppo_dp_open(const void *ipc_handle, void **dptr);
+int ppo_dp_close(void *dptr);
+int ppo_dp_free(void *dptr);
+int ppo_minibatch_fused_dp(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, const ppo_dp_t *dp, int seq,
+                           double *obs_rms, int update_obs_rms, int mb_index, const float *exp_obs,
+                           const float *exp_act, const float *exp_nlp, const float *exp_val, const float *exp_ret,
+                           const float *exp_adv, float *exp_mu, float *exp_sigma, float *grad, float *losses,
+                           float *partials, double *work, float *kl_prev_out, void *stream);
+
 /* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad (16-byte aligned) */
 int ppo_partials_floats(int minibatch);
 /* size (floats) of the grad buffer of ppo_minibatch_grad / ppo_minibatch_apply */

@@ -100,6 +100,10 @@ class PpoAdamBanks(ctypes.Structure):
     _fields_ = _struct_fields(_TXT, "ppo_adam_banks", DEFINES)
 
 
+class PpoDp(ctypes.Structure):
+    _fields_ = _struct_fields(_TXT, "ppo_dp", DEFINES)
+
+
 def enum_values(enum_name: str) -> dict:
     m = re.search(r"enum\s+%s\s*\{(.*?)\}" % enum_name, _TXT, flags=re.S)
     vals, cur = {}, -1

@@ -70,6 +70,11 @@ def _declare(lib):
         "ppo_minibatch_apply": [P, P, P, P, P, P, I, F, P, I, P],
         "ppo_minibatch_fused": [P, P, I, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_finish": [P, P, I, P, P, P],
+        "ppo_minibatch_fused_dp": [P, P, P, I, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+        "ppo_dp_alloc": [P, P],
+        "ppo_dp_open": [P, P],
+        "ppo_dp_close": [P],
+        "ppo_dp_free": [P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
         "ppo_obs_rms_epoch": [P, P, I, P, P, P],
@@ -84,6 +89,8 @@ def _declare(lib):
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
+    lib.ppo_dp_buffer_bytes.argtypes = []
+    lib.ppo_dp_buffer_bytes.restype = ctypes.c_longlong
     return lib
 
 

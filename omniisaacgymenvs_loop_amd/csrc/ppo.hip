@@ -20,6 +20,8 @@
 // backward need), activations never leave LDS, and each workgroup writes one
 // deterministic partial gradient (param layout) that k_reduce_partials sums
 // in a fixed order.  clip + Adam + the adaptive LR run in k_apply.
+#include <cstring>
+
 #include "usv_device.h"
 
 USV_PROBE_DEFINE(ppo)
@@ -904,6 +906,8 @@ struct ChainIn {
   const float *opt_prev;                   // optimiser scalars read by minibatch k-1's step
   float *opt_cur;                          // ... and the ones after it (read by minibatch k's)
   float *kl_out;                           // minibatch k-1's KL (log)
+  uint32_t *dp_clock;                      // several ranks: the minibatch counter the next reduction keys its
+                                           // exchange on (advanced here, by workgroup 0; nullable)
 };
 
 struct GradSmem {
@@ -1021,6 +1025,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   const int rb0 = row0 + blockIdx.x * RB;               // first row of this workgroup
   const float invB = 1.0f / (float)c.minibatch;
   USV_PHASE(ppo, 0);
+  // several ranks: this minibatch's exchange key (the previous reduction has finished: stream order)
+  if (ch.dp_clock && blockIdx.x == 0 && tid == 0) *ch.dp_clock += 1u;
   // ---- every global load issued up front (compile-time trip counts) ----
   // W2 element tid + u GTB per thread (4-byte loads): each wave's LDS commit is 64 consecutive words
   // of one row, conflict-free at the odd row stride (16-byte loads would leave 4-word strided writes)
@@ -1470,10 +1476,42 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, ChainIn ch, con
 // Adam step of its parameters speculatively, with clip coefficient 1 (a.from -> a.to): the clip
 // norm needs every chunk, and the next kernel (the next minibatch's gradient kernel or
 // k_apply<.., true>) checks it and redoes the step when clipping was due.
-template <bool kSpec>
+//
+// With kDP (several ranks, ppo_minibatch_fused_dp) the chunk is all-reduced before that step: a one-shot
+// exchange over xGMI peer memory (include/usv_hip.h ppo_dp_t).  Slot q of rank s's chunk goes to every
+// rank r's receive buffer x_r[par][s][q] (system-scope sc0 sc1 stores: write-through to the receiver's
+// memory), every storing wave waits for its stores, then lane r of wave 0 raises rank r's flag of
+// (chunk, sender s) to this minibatch's key v = *dp.clock (par = v & 1: a sender can be at most one
+// minibatch ahead of a receiver, so two parities never collide).  Wave 0 polls this rank's flags of
+// the chunk (system-scope loads; a wall-clock bound sets dp.err instead of hanging on a lost peer),
+// a barrier releases the other waves, and the senders are summed in rank order (sc0 sc1 loads), so
+// every rank forms the same bits; / world as the reference's all_grads / rank_size.  The KL rides in
+// its loss slot as each rank's minibatch mean (av_kls SUM / rank_size, a2c_common.py:1218-1222).
+constexpr int DP_SLOTS = RED_BLOCKS * RD_P;                  // slot space of one sender
+constexpr int DP_FLAG_STRIDE = 32;                            // uint32 per flag: one 128-B line each
+constexpr long long DP_X_BYTES = 2LL * PPO_DP_MAX * DP_SLOTS * 4;
+constexpr long long DP_FLAG_OFF = (DP_X_BYTES + 4095) / 4096 * 4096;
+constexpr long long DP_BYTES = DP_FLAG_OFF + (long long)RED_BLOCKS * PPO_DP_MAX * DP_FLAG_STRIDE * 4;
+__device__ __forceinline__ void st_sys(float *p, float v) {
+  __hip_atomic_store(reinterpret_cast<uint32_t *>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ float ld_sys(const float *p) {
+  return __builtin_bit_cast(float, __hip_atomic_load(reinterpret_cast<const uint32_t *>(p), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM));
+}
+__device__ __forceinline__ float *dp_x(void *buf, int par, int sender) {
+  return reinterpret_cast<float *>(buf) + ((size_t)par * PPO_DP_MAX + sender) * DP_SLOTS;
+}
+__device__ __forceinline__ uint32_t *dp_flag(void *buf, int chunk, int sender) {
+  return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(buf) + DP_FLAG_OFF) +
+         ((size_t)chunk * PPO_DP_MAX + sender) * DP_FLAG_STRIDE;
+}
+
+template <bool kSpec, bool kDP>
 __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
                                                            float *losses, float inv_b, ppo_cfg_t c, AdamBanks a,
-                                                           const float *__restrict__ opt_in) {
+                                                           const float *__restrict__ opt_in, ppo_dp_t dp) {
   __shared__ float4 red[RD_G][RD_L];
   __shared__ float sqw[RD_TB / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1489,6 +1527,8 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
   if (mine) {
     p_old = a.P0[pq]; m_old = a.m0[pq]; v_old = a.v0[pq];
   }
+  uint32_t key = 0u;
+  if (kDP) key = *dp.clock;   // written by the preceding gradient kernel
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   float oin[8] = {};   // the step's scalars: loads issued here, consumed after the row sums
   if (kSpec) {
@@ -1514,12 +1554,52 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     ak = adam_consts_tagged(c, oin[0], oin[1] + 1.0f, oin[4], oin[5], oin[6], oin[7]);
   red[grp][col] = acc;
   __syncthreads();
-  float sq = 0.f;
+  float s = 0.f;
+  const int slot = blockIdx.x * RD_P + tid;
   if (tid < RD_P) {
-    const int slot = blockIdx.x * RD_P + tid;
-    float s = 0.f;
 #pragma unroll
     for (int g = 0; g < RD_G; ++g) s += reinterpret_cast<const float *>(red[g])[tid];
+  }
+  float sl = s;   // this rank's value of the slot (the loss means are rank-local)
+  if constexpr (kDP) {
+    const int par = (int)(key & 1u);
+    if (tid < RD_P) {   // the chunk to every rank (gradient sums; the KL slot as this rank's mean)
+      const float pv = slot < S_END ? s : (slot == PPO_NPARAM + 4 ? s * inv_b : 0.f);
+      for (int r = 0; r < dp.world; ++r) st_sys(dp_x(dp.peer[r], par, dp.rank) + slot, pv);
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its stores are acknowledged
+    __syncthreads();
+    if (w == 0) {
+      if (lane < dp.world)   // lane r raises rank r's flag of (this chunk, this sender)
+        __hip_atomic_store(dp_flag(dp.peer[lane], blockIdx.x, dp.rank), key, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      // poll this rank's flags of the chunk: every sender's key >= ours (a sender may be one ahead)
+      const uint64_t t0 = wall_clock64(), lim = (uint64_t)dp.timeout_ms * 100000ull;   // 100 MHz
+      bool got = lane >= dp.world;
+      while (true) {
+        if (!got) {
+          const uint32_t f = __hip_atomic_load(dp_flag(dp.peer[dp.rank], blockIdx.x, lane), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+          got = (int32_t)(f - key) >= 0;
+        }
+        if (__all(got)) break;
+        if (wall_clock64() - t0 > lim) {   // a lost peer: flag it and go on (the host raises after the epoch)
+          if (lane == 0) atomicOr(dp.err, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+    __syncthreads();
+    if (tid < RD_P) {   // senders in rank order: the same sum on every rank
+      const float *xs = dp_x(dp.peer[dp.rank], par, 0);
+      float t = 0.f;
+      for (int r = 0; r < dp.world; ++r) t += ld_sys(xs + (size_t)r * DP_SLOTS + slot);
+      s = t / (float)dp.world;   // all_grads / rank_size, av_kls / rank_size
+    }
+  }
+  float sq = 0.f;
+  if (tid < RD_P) {
     if (slot < S_END) {
       grad[param_of_slot(slot)] = s;
       sq = s * s;
@@ -1530,8 +1610,8 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
       }
     } else if (slot < PPO_NPARAM + 5) {
       const int q = slot - PPO_NPARAM;
-      if (q == 4) grad[PPO_NPARAM] = s * inv_b;      // kl mean rides with the gradient (all-reduce)
-      if (losses) losses[q] = s * inv_b;
+      if (q == 4) grad[PPO_NPARAM] = kDP ? s : s * inv_b;   // kl mean rides with the gradient (all-reduce)
+      if (losses) losses[q] = sl * inv_b;
     }
   }
   if (w < (RD_P + 63) / 64) {
@@ -1709,8 +1789,8 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                      *cfg, ChainIn{}, params, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv,
                      exp_mu, exp_sigma, partials);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_reduce_partials<false>, dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad, losses,
-                     1.0f / (float)cfg->minibatch, *cfg, AdamBanks{}, nullptr);
+  hipLaunchKernelGGL((k_reduce_partials<false, false>), dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad,
+                     losses, 1.0f / (float)cfg->minibatch, *cfg, AdamBanks{}, nullptr, ppo_dp_t{});
   USV_CHECK_LAUNCH();
   return 0;
 }
@@ -1724,8 +1804,8 @@ static bool banks_ok(const ppo_adam_banks_t *b) {
   return true;
 }
 
-int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int seq, double *obs_rms,
-                        int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+static int fused_launch(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, const ppo_dp_t *dp, int seq,
+                        double *obs_rms, int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
                         const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
                         float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
                         float *kl_prev_out, void *stream) {
@@ -1733,6 +1813,12 @@ int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int
   if (!banks_ok(banks)) return 4;
   if (cfg->minibatch % RB != 0) return 2;
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
+  if (dp) {
+    if (dp->world < 1 || dp->world > PPO_DP_MAX || dp->rank < 0 || dp->rank >= dp->world || !dp->clock || !dp->err)
+      return 5;
+    for (int r = 0; r < dp->world; ++r)
+      if (!dp->peer[r]) return 5;
+  }
   hipStream_t s = (hipStream_t)stream;
   const int cur = seq & 1, prv = cur ^ 1, nblk = cfg->minibatch / RB, row0 = mb_index * cfg->minibatch;
   if (update_obs_rms && cfg->normalize_input) {
@@ -1742,13 +1828,16 @@ int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int
   }
   const float *P = banks->params[cur];
   const dim3 gg(nblk), gb(GTB);
+  uint32_t *clk = dp ? dp->clock : nullptr;
   if (seq == 0) {
+    ChainIn ch{};
+    ch.dp_clock = clk;
     hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, false> : k_mb_grad<false, false>), gg, gb, 0, s, *cfg,
-                       ChainIn{}, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu,
+                       ch, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu,
                        exp_sigma, partials);
   } else {
     const ChainIn ch{banks->params[prv], banks->m[prv], banks->v[prv], banks->params[cur], banks->m[cur],
-                     banks->v[cur], grad, banks->opt + 8 * prv, banks->opt + 8 * cur, kl_prev_out};
+                     banks->v[cur], grad, banks->opt + 8 * prv, banks->opt + 8 * cur, kl_prev_out, clk};
     hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, true> : k_mb_grad<false, true>), gg, gb, 0, s, *cfg, ch, P,
                        obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu, exp_sigma,
                        partials);
@@ -1756,11 +1845,57 @@ int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int
   USV_CHECK_LAUNCH();
   const AdamBanks a{banks->params[cur], banks->m[cur], banks->v[cur], banks->params[prv], banks->m[prv],
                     banks->v[prv]};
-  hipLaunchKernelGGL(k_reduce_partials<true>, dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad, losses,
-                     1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur);
+  if (dp)
+    hipLaunchKernelGGL((k_reduce_partials<true, true>), dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad,
+                       losses, 1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur, *dp);
+  else
+    hipLaunchKernelGGL((k_reduce_partials<true, false>), dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad,
+                       losses, 1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur, ppo_dp_t{});
   USV_CHECK_LAUNCH();
   return 0;
 }
+
+int ppo_minibatch_fused(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int seq, double *obs_rms,
+                        int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+                        const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
+                        float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
+                        float *kl_prev_out, void *stream) {
+  return fused_launch(cfg, banks, nullptr, seq, obs_rms, update_obs_rms, mb_index, exp_obs, exp_act, exp_nlp, exp_val,
+                      exp_ret, exp_adv, exp_mu, exp_sigma, grad, losses, partials, work, kl_prev_out, stream);
+}
+
+int ppo_minibatch_fused_dp(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, const ppo_dp_t *dp, int seq,
+                           double *obs_rms, int update_obs_rms, int mb_index, const float *exp_obs,
+                           const float *exp_act, const float *exp_nlp, const float *exp_val, const float *exp_ret,
+                           const float *exp_adv, float *exp_mu, float *exp_sigma, float *grad, float *losses,
+                           float *partials, double *work, float *kl_prev_out, void *stream) {
+  if (!dp) return 5;
+  return fused_launch(cfg, banks, dp, seq, obs_rms, update_obs_rms, mb_index, exp_obs, exp_act, exp_nlp, exp_val,
+                      exp_ret, exp_adv, exp_mu, exp_sigma, grad, losses, partials, work, kl_prev_out, stream);
+}
+
+long long ppo_dp_buffer_bytes(void) { return DP_BYTES; }
+
+int ppo_dp_alloc(void **dptr, void *ipc_handle) {
+  if (!dptr || !ipc_handle) return 1;
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "ipc handle size");
+  if (hipMalloc(dptr, (size_t)DP_BYTES) != hipSuccess) return 2;
+  if (hipMemset(*dptr, 0, (size_t)DP_BYTES) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return 3;
+  hipIpcMemHandle_t h;
+  if (hipIpcGetMemHandle(&h, *dptr) != hipSuccess) return 4;
+  memcpy(ipc_handle, &h, sizeof(h));
+  return 0;
+}
+
+int ppo_dp_open(const void *ipc_handle, void **dptr) {
+  if (!dptr || !ipc_handle) return 1;
+  hipIpcMemHandle_t h;
+  memcpy(&h, ipc_handle, sizeof(h));
+  return hipIpcOpenMemHandle(dptr, h, hipIpcMemLazyEnablePeerAccess) == hipSuccess ? 0 : 2;
+}
+
+int ppo_dp_close(void *dptr) { return hipIpcCloseMemHandle(dptr) == hipSuccess ? 0 : 1; }
+int ppo_dp_free(void *dptr) { return hipFree(dptr) == hipSuccess ? 0 : 1; }
 
 int ppo_minibatch_finish(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int count, const float *grad,
                          float *kl_out, void *stream) {

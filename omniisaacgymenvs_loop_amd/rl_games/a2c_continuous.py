@@ -289,6 +289,28 @@ class A2CAgent:
         self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 8), **f32)
         self.nan_flag = torch.zeros(1, device=dev, dtype=torch.int32)
         self.cfg.nan_flag = self.nan_flag.data_ptr()
+        self._dp = self._peer_exchange() if self.multi_gpu and self.rank_size > 1 else None
+
+    def _peer_exchange(self):
+        """Several ranks: the one-shot peer exchange of ppo_minibatch_fused_dp (dist_util.PeerExchange) unless
+        USV_DP_EXCHANGE=collective; every rank must map every other rank's buffer, otherwise all ranks fall
+        back to torch.distributed all-reduces (eager, the three-launch split)."""
+        if os.getenv("USV_DP_EXCHANGE", "peer") == "collective":
+            return None
+        ex, err = None, None
+        try:
+            ex = dist_util.PeerExchange(self.rank, self.rank_size, self.ppo_device,
+                                        timeout_ms=int(os.getenv("USV_DP_TIMEOUT_MS", "20000")))
+        except RuntimeError as e:
+            err = e
+        if not self._ranks_agree(ex is not None):
+            if ex is not None:
+                ex.close()
+            if self.rank == 0:
+                print(f"peer exchange unavailable ({err or 'on another rank'}); gradients go through "
+                      f"torch.distributed all-reduces")
+            return None
+        return ex
 
     # ------------------------------------------------------------- rollout
     def env_reset(self):
@@ -345,9 +367,11 @@ class A2CAgent:
         return self._banks[1]
 
     def _fused_update(self) -> bool:
-        """One rank: two launches per minibatch (ppo_minibatch_fused); USV_PPO_FUSED=0 keeps the
-        three-launch split (grad, reduce, apply)."""
-        return not (self.multi_gpu and self.rank_size > 1) and os.environ.get("USV_PPO_FUSED", "1") != "0"
+        """Two launches per minibatch (ppo_minibatch_fused; several ranks: ppo_minibatch_fused_dp with the
+        peer exchange inside the reduction); USV_PPO_FUSED=0 keeps the three-launch split (grad, reduce,
+        [torch.distributed all-reduce], apply), as does a multi-rank run without the peer exchange."""
+        dp_ok = not (self.multi_gpu and self.rank_size > 1) or getattr(self, "_dp", None) is not None
+        return dp_ok and os.environ.get("USV_PPO_FUSED", "1") != "0"
 
     def update_epoch_minibatches(self) -> None:
         """The mini-epoch / minibatch loop (a2c_common.py:1190-1245): per minibatch the gradient kernel
@@ -365,10 +389,12 @@ class A2CAgent:
                    c.ptr(self.rms_seq), s)
         if self._fused_update():
             banks = c.byref(self._adam_banks())
+            dpx = (c.byref(self._dp.desc),) if self._dp is not None else ()
+            fn = "ppo_minibatch_fused_dp" if dpx else "ppo_minibatch_fused"
             for mini_ep in range(self.mini_epochs_num):
                 for i in range(self.num_minibatches):
                     rms = self.rms_seq[2 * NIN * i:] if seq and mini_ep == 0 else self.obs_rms
-                    c.call("ppo_minibatch_fused", cfg, banks, k, c.ptr(rms), int(mini_ep == 0 and not seq), i,
+                    c.call(fn, cfg, banks, *dpx, k, c.ptr(rms), int(mini_ep == 0 and not seq), i,
                            c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp), c.ptr(self.exp_val),
                            c.ptr(self.exp_ret), c.ptr(self.exp_adv), c.ptr(self.exp_mu), c.ptr(self.exp_sigma),
                            c.ptr(self.grad), c.ptr(self.loss_log[k]), c.ptr(self.partials), c.ptr(self.work),
@@ -404,8 +430,8 @@ class A2CAgent:
         collectives runs eagerly."""
         if getattr(self, "_graph_update_failed", False):
             return False
-        if not self.multi_gpu or self.rank_size == 1:
-            return True
+        if not self.multi_gpu or self.rank_size == 1 or self._dp is not None:
+            return True   # (the peer exchange is kernels only)
         return dist_util.backend() == "nccl" and os.getenv("USV_GRAPH_COLLECTIVES", "0") == "1"
 
     def _ranks_agree(self, ok: bool) -> bool:
@@ -413,7 +439,7 @@ class A2CAgent:
         falls back to eager collectives."""
         if not self.multi_gpu or self.rank_size == 1:
             return ok
-        flag = torch.tensor([1.0 if ok else 0.0], device=self.ppo_device)
+        flag = torch.tensor([1.0 if ok else 0.0], device="cpu" if dist.get_backend() == "gloo" else self.ppo_device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         return bool(flag.item() == 1.0)
 
@@ -479,6 +505,8 @@ class A2CAgent:
         if chk is not None:
             chk()
         self._check_nan()
+        if self._dp is not None:
+            self._dp.check()
         self._eager_epochs += 1
         self._replay_meters()
         self.last_lr = float(self.opt[0].item())

@@ -55,3 +55,79 @@ def max_over_ranks(x: float, device) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class PeerExchange:
+    """The one-shot gradient all-reduce of ppo_minibatch_fused_dp (include/usv_hip.h ppo_dp_t): every rank
+    allocates one receive buffer (ppo_dp_alloc), the 64-byte IPC handles go around once through the process
+    group (all_gather_object: gloo or RCCL), every rank maps the others' buffers (ppo_dp_open, lazy peer
+    access over xGMI), and from then on the per-minibatch exchange is a pair of stores and flags inside the
+    reduction kernel -- no collective call, nothing the host launches between kernels, so the update is one
+    HIP graph on every rank.  `peers` (tests) replaces the handle exchange by buffers of this process.
+
+    Raises RuntimeError when a buffer cannot be mapped (no peer access); A2CAgent then agrees with the other
+    ranks to fall back to torch.distributed collectives."""
+
+    def __init__(self, rank: int, world_size: int, device, timeout_ms: int = 20000, peers=None):
+        import ctypes
+        from .. import _capi
+        from .._abi import DEFINES, PpoDp
+        if not 1 <= world_size <= DEFINES["PPO_DP_MAX"]:
+            raise RuntimeError(f"PeerExchange: world size {world_size} > PPO_DP_MAX")
+        lib = _capi.lib()
+        self.rank, self.world = rank, world_size
+        self._lib = lib
+        self._own = ctypes.c_void_p()
+        self._opened = []
+        handle = ctypes.create_string_buffer(64)
+        _capi.call("ppo_dp_alloc", ctypes.byref(self._own), handle)
+        ptrs = [None] * world_size
+        ptrs[rank] = self._own.value
+        if peers is not None:       # in-process "ranks" (tests): the other buffers are plain device pointers
+            for r, p in enumerate(peers):
+                if r != rank:
+                    ptrs[r] = int(p)
+        else:
+            handles = [None] * world_size
+            dist.all_gather_object(handles, bytes(handle.raw))
+            for r in range(world_size):
+                if r == rank:
+                    continue
+                p = ctypes.c_void_p()
+                rc = lib.ppo_dp_open(ctypes.create_string_buffer(handles[r], 64), ctypes.byref(p))
+                if rc != 0:
+                    self.close()
+                    raise RuntimeError(f"PeerExchange: cannot map rank {r}'s buffer (ppo_dp_open status {rc})")
+                self._opened.append(p.value)
+                ptrs[r] = p.value
+        self.clock = torch.zeros(1, device=device, dtype=torch.int32)
+        self.err = torch.zeros(1, device=device, dtype=torch.int32)
+        d = PpoDp()
+        d.rank, d.world, d.timeout_ms = rank, world_size, int(timeout_ms)
+        for r, p in enumerate(ptrs):
+            d.peer[r] = p
+        d.clock, d.err = self.clock.data_ptr(), self.err.data_ptr()
+        self.desc = d
+
+    @property
+    def own_ptr(self) -> int:
+        return self._own.value
+
+    def check(self) -> None:
+        """A peer's chunk missed the kernel's wall-clock bound (a lost or diverged rank): raise."""
+        if int(self.err.item()):
+            raise RuntimeError("[ppo_dp] a peer's gradient chunk did not arrive within the timeout "
+                               "(a rank died or the ranks' minibatch sequences diverged)")
+
+    def close(self) -> None:
+        for p in self._opened:
+            self._lib.ppo_dp_close(ctypes_void(p))
+        self._opened = []
+        if self._own is not None and self._own.value:
+            self._lib.ppo_dp_free(self._own)
+            self._own = None
+
+
+def ctypes_void(p):
+    import ctypes
+    return ctypes.c_void_p(p)

@@ -62,9 +62,10 @@ def _load(ag, data, rows):
         getattr(ag, k).copy_(torch.tensor(np.ascontiguousarray(v[rows]), device="cuda:0"))
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, exchange):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
-                      WORLD_SIZE=str(world), USV_RANKS_SHARE_DEVICE="0", USV_DIST_BACKEND="gloo")
+                      WORLD_SIZE=str(world), USV_RANKS_SHARE_DEVICE="0", USV_DIST_BACKEND="gloo",
+                      USV_DP_EXCHANGE=exchange, USV_DP_TIMEOUT_MS="10000")
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist
@@ -72,10 +73,13 @@ def _worker(rank, world, port, out_dir):
         # different init seeds per rank: the broadcast must make rank 0's weights everyone's
         ag = _agent(N, MB // world, True, params_seed=11 + 100 * rank)
         assert ag.multi_gpu and ag.rank_size == world
+        assert (ag._dp is not None) == (exchange == "peer"), exchange
         _load(ag, _dataset(N * H * world), _rank_rows(rank, world))
         p0 = ag.model_params.cpu().numpy().copy()
         ag.update_epoch_minibatches()
         torch.cuda.synchronize()
+        if ag._dp is not None:
+            ag._dp.check()
         # env streams: the same config on every rank, seeds offset by LOCAL_RANK
         from omniisaacgymenvs_loop_amd.envs.vec_env_rlgames import VecEnvRLGames
         from omniisaacgymenvs_loop_amd.scripts.rlgames_train import build_config
@@ -86,17 +90,43 @@ def _worker(rank, world, port, out_dir):
         torch.cuda.synchronize()
         np.savez(os.path.join(out_dir, f"r{rank}.npz"), p0=p0, p=ag.model_params.cpu().numpy(),
                  lr=float(ag.opt[0].item()), kls=ag.kls.cpu().numpy(), env_seed=task.seed, obs=obs.cpu().numpy(),
-                 mass=task.params[0].cpu().numpy())
+                 mass=task.params[0].cpu().numpy(), norm=float(ag.opt[3].item()))
+        if ag._dp is not None:
+            dist.barrier()          # no rank unmaps / frees a buffer another rank may still touch
+            ag._dp.close()
     finally:
         dist.destroy_process_group()
 
 
-@pytest.fixture(scope="module")
-def two_ranks(tmp_path_factory):
-    import torch.multiprocessing as mp
-    out = tmp_path_factory.mktemp("dist_gpu")
-    mp.spawn(_worker, args=(2, _port(), str(out)), nprocs=2, join=True)
-    return [np.load(out / f"r{r}.npz") for r in range(2)]
+_RUNS = {}
+
+
+def _run_ranks(tmp_path_factory, exchange):
+    if exchange not in _RUNS:
+        import torch.multiprocessing as mp
+        out = tmp_path_factory.mktemp(f"dist_gpu_{exchange}")
+        mp.spawn(_worker, args=(2, _port(), str(out), exchange), nprocs=2, join=True)
+        _RUNS[exchange] = [np.load(out / f"r{r}.npz") for r in range(2)]
+    return _RUNS[exchange]
+
+
+@pytest.fixture(scope="module", params=["peer", "collective"])
+def two_ranks(request, tmp_path_factory):
+    """peer: ppo_minibatch_fused_dp's one-shot exchange through IPC-mapped buffers (two processes on one
+    device: the same kernels, handles and flags as over xGMI); collective: the gloo all-reduce split."""
+    return _run_ranks(tmp_path_factory, request.param)
+
+
+def test_peer_exchange_equals_collective_path(tmp_path_factory):
+    """The peer exchange (rank-order sum / world inside the reduction, speculative Adam step) and the gloo
+    all-reduce + k_apply split give bit-identical weights, KLs and LR for two ranks when no step clips
+    (x0 + x1 == x1 + x0; / 2 == * 0.5)."""
+    a = _run_ranks(tmp_path_factory, "peer")
+    b = _run_ranks(tmp_path_factory, "collective")
+    assert float(b[0]["norm"]) < 1.0                                 # grad_norm 1.0: no clipping here
+    for k in ("p", "kls", "lr"):
+        np.testing.assert_array_equal(a[0][k], b[0][k], err_msg=k)
+        np.testing.assert_array_equal(a[1][k], b[1][k], err_msg=k)
 
 
 def test_two_ranks_equal_single_rank_on_the_union(two_ranks):
