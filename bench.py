@@ -217,6 +217,9 @@ def cpu_baseline(shapes=((32, 512, 4.0), (4096, 8192, 20.0))):
 C2_ENVS = 4096                 # BASELINE configs[1]: secondary line of the same run
 HEADLINE_ENVS = 131072         # BASELINE configs[4] per GPU: 2^20 envs over 8 GPUs
 REWARD_TARGET = 30.0           # BASELINE metric, half 2: wall-clock to rewards/step >= 30
+# 30 is about the untrained policy's level (the first full 100-episode meter of a random-init policy reads
+# ~30); learning milestones of the same rewards/step meter, reported beside it
+MILESTONES = (30.0, 60.0, 80.0, 100.0)
 
 
 def time_epochs(agent, steps, world, local):
@@ -256,6 +259,9 @@ def main():
                          "mixed_precision; BASELINE configs[2] at --envs 65536); physics stays fp32")
     ap.add_argument("--c2-steps", type=int, default=10,
                     help="epochs of the secondary BASELINE configs[1] line (4096 envs/GPU; 0 = skip)")
+    ap.add_argument("--milestone-seconds", type=float, default=30.0,
+                    help="one GPU: keep training after the measurements until rewards/step >= the last milestone "
+                         "or this many seconds (wall-clock to learning milestones; 0 = skip)")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -286,12 +292,24 @@ def main():
     # reset (env / agent construction excluded), through warmup and timed epochs alike
     t_train = time.perf_counter()
     to_reward = {"target": REWARD_TARGET, "seconds": None, "epochs": None}
+    miles = {str(m): None for m in MILESTONES}
+    first_full = {}
 
     def note_reward():
-        if to_reward["seconds"] is None and agent.game_rewards.current_size > 0 and \
-                agent.game_rewards.get_mean() >= REWARD_TARGET:
-            to_reward["seconds"] = time.perf_counter() - t_train
+        gr = agent.game_rewards
+        if gr.current_size == 0:
+            return
+        r = float(gr.get_mean())
+        now = time.perf_counter() - t_train
+        if not first_full and gr.current_size >= gr.max_size:
+            first_full.update(value=r, seconds=now, epochs=agent.epoch_num)
+        if to_reward["seconds"] is None and r >= REWARD_TARGET:
+            to_reward["seconds"] = now
             to_reward["epochs"] = agent.epoch_num
+        for m in MILESTONES:
+            if miles[str(m)] is None and r >= m:
+                miles[str(m)] = {"seconds": now, "epochs": agent.epoch_num,
+                                 "env_steps": agent.epoch_num * args.envs * agent.horizon_length * world}
 
     agent.obs = agent.env_reset()
     # warmup: the first epoch runs eagerly, the second captures the rollout and update HIP graphs
@@ -321,12 +339,16 @@ def main():
           file=sys.stderr, flush=True)
 
     # phase split of one epoch with graph replays: rollout (+ GAE/prepare) vs minibatch update
+    # device time only: a spin kernel ahead of the first event keeps the GPU busy while the host submits both
+    # graphs, so neither pair holds host launch latency (the epoch's remaining host-side share is
+    # ms_per_step - rollout_ms - update_ms, reported as host_gap_ms)
     phase = {}
     if agent._graph_play is not None and agent._graph_update is not None:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         tp = tu = 0.0
         nrep = 3
         for _ in range(nrep):
+            torch.cuda._sleep(int(os.getenv("USV_BENCH_SPIN", "200000000")))
             ev[0].record()
             agent._graph_play.replay()
             ev[1].record()
@@ -337,7 +359,9 @@ def main():
             tp += ev[0].elapsed_time(ev[1])
             tu += ev[1].elapsed_time(ev[2])
         phase = {"rollout_ms": tp / nrep, "update_ms": tu / nrep,
-                 "update_us_per_minibatch": tu / nrep * 1e3 / (agent.mini_epochs_num * agent.num_minibatches)}
+                 "update_us_per_minibatch": tu / nrep * 1e3 / (agent.mini_epochs_num * agent.num_minibatches),
+                 "host_gap_ms": elapsed / args.steps * 1e3 - (tp + tu) / nrep,
+                 "phase_method": "device time of graph replays behind a spin kernel (host submission excluded)"}
 
     # per-launch kernel times inside real epochs (eager: graph replays carry no per-kernel events),
     # HIP events on the launch stream around each C-ABI call
@@ -362,9 +386,18 @@ def main():
     t1 = time.perf_counter()
     nenv = 32
     for _ in range(nenv):
-        env.step(acts)
+        o_env, _, d_env, _ = env.step(acts)
     torch.cuda.synchronize()
+    agent.obs, agent.dones = o_env, d_env   # the agent continues from the env's current state
     env_fps = args.envs * nenv / (time.perf_counter() - t1)
+
+    # wall-clock to learning milestones (one GPU): keep training until the last milestone or the budget
+    if world == 1 and args.milestone_seconds > 0:
+        t_m = time.perf_counter()
+        while miles[str(MILESTONES[-1])] is None and time.perf_counter() - t_m < args.milestone_seconds:
+            agent.update_epoch()
+            agent.train_epoch()
+            note_reward()
 
     env_ms = env_timer.mean_ms()
     ppo_ms = ppo_timer.mean_ms()
@@ -405,6 +438,8 @@ def main():
                              "peak": BF16_PEAK_TFS if args.mixed_precision else FP32_PEAK_TFS, "unit": "TFLOP/s",
                              "frac": ppo_tfs / (BF16_PEAK_TFS if args.mixed_precision else FP32_PEAK_TFS),
                              "launch_ms": ppo_ms, "rows_per_launch": agent.minibatch_size,
+                             "flops_per_row": PPO_FLOPS_PER_ROW, "flops_per_row_fwd": PPO_FWD_FLOPS_PER_ROW,
+                             "flops_per_row_bwd": PPO_BWD_FLOPS_PER_ROW,
                              "launches_timed": len(ppo_timer.pairs),
                              "launch_ms_method": "median HIP event pair around each minibatch's gradient + reduction "
                                                  + ("launches (ppo_minibatch_fused: k_mb_grad + k_reduce_partials with "
@@ -413,6 +448,9 @@ def main():
                                                     "all-reduce and k_apply follow outside the pair)")
                                                  + " of one eager epoch, minus the empty pair"},
             "wall_clock_to_reward": dict(to_reward, unit="s", since="first env reset of this run (random-init policy)",
+                                         note="30 is about the untrained policy's level: see first_full_meter "
+                                              "and the learning milestones",
+                                         first_full_meter=first_full or None, milestones=miles,
                                          last100_mean_at_end=float(agent.game_rewards.get_mean())),
             "extra": dict(phase),
         }

@@ -135,7 +135,7 @@ def test_prepare_headline_multi_block():
     ET.check(tn, "returns", ag.exp_ret.cpu().numpy(), rn, 1e-5, 1e-5)
     ET.check(tn, "advantages", ag.exp_adv.cpu().numpy(), an, 1e-5, 1e-5)
     vr = ag.val_rms.cpu().numpy()
-    np.testing.assert_allclose(vr[:2], [vrms.mean[0], vrms.var[0]], rtol=1e-9)
+    np.testing.assert_allclose(vr[:2], [vrms.mean[0], vrms.var[0]], rtol=1e-7)   # fp64 one-pass vs two-pass
     assert vr[2] == vrms.count
 
 
