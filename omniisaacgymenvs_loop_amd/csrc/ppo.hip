@@ -910,10 +910,13 @@ struct ChainIn {
                                            // exchange on (advanced here, by workgroup 0; nullable)
 };
 
+// x rows of the gradient kernel padded to whole staging passes: every thread stores its slots
+// unconditionally (see the obs staging in mb_grad8w)
+constexpr int GX = ((RB * XS + GTB - 1) / GTB) * GTB;
 struct GradSmem {
   float w2[NH * HS];              // W2[j][k]
   float w1[NH * XS];              // W1[j][k], k 33, 34 = 0
-  float x[RB * XS];               // normalised obs (dW1 operand)
+  float x[GX];                    // normalised obs (dW1 operand); [RB * XS, GX) staging overflow slots
   float h1[RB * HS];              // tanh layer 1, later dz1
   float h2[RB * HS];              // tanh layer 2, later dz2
   float xch[4][16][64];           // upper-K partial accumulators of layer 2 / dh1 (per wave, register, lane)
@@ -1050,8 +1053,6 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     }
 #pragma unroll
     for (int u = 0; u < NTLG; ++u) tlr[u] = P[PPO_OFF_B2 + min(tid + u * GTB, TAIL - 1)];
-#pragma unroll
-    for (int u = 0; u < NW2F; ++u) w2f[u] = P[PPO_OFF_W2 + tid + u * GTB];
   }
   const float b1r = P[PPO_OFF_B1 + (tid & (NH - 1))];
   // log-sigma as a vector load too (read out by readlane where the losses use it)
@@ -1081,24 +1082,25 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     mu[u] = obs_rms[kc];
     var[u] = obs_rms[NIN + kc];
   }
+  // W2 (64 KB of the 85 KB) issued LAST: the staging of x / W1 / biases and layer 1 wait only for the
+  // loads ahead of it (counted vmcnt waits), W2 lands during layer 1 and is committed after it
+#pragma unroll
+  for (int u = 0; u < NW2F; ++u) w2f[u] = P[PPO_OFF_W2 + tid + u * GTB];
   __builtin_amdgcn_sched_barrier(0);   // every load above is issued before anything waits
 #pragma unroll
   for (int u = 0; u < NW1G; ++u)
     if ((tid + u * GTB) % XS >= NIN) w1r[u] = 0.f;
   if (kChain && tid >= RED_BLOCKS) csq = 0.f;
-  {   // obs rows, normalised on the way into LDS
+  {   // obs rows, normalised on the way into LDS: every value formed unconditionally and selected, so no
+      // load is sunk into a branch (a load issued there would come after W2's and wait for all of them)
     const bool norm = c.normalize_input != 0;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int q = tid + u * GTB;
-      if (q >= RB * XS) continue;
       const int k = q % XS;
-      float xv = 0.f;
-      if (k < NIN) {
-        xv = xo[u];
-        if (norm) xv = rms_norm(xv, mu[u], var[u], c.rms_eps);
-      }
-      s.x[q] = xv;
+      const float xn = rms_norm(xo[u], mu[u], var[u], c.rms_eps);
+      const float xv = (k < NIN && q < RB * XS) ? (norm ? xn : xo[u]) : 0.f;
+      s.x[q] = xv;   // q < GX: the slots past RB * XS are never read
     }
   }
 #pragma unroll
