@@ -35,6 +35,15 @@ extern "C" {
 #define USV_NCLOSE       5   /* closest obstacles in obs          (USV_core.py:33) */
 #define USV_GRID       150   /* potential-field grid              (USV_capture_xy_static_obs.py:30) */
 #define USV_GRID2    (USV_GRID * USV_GRID)
+/* the potential field in HBM (usv_bufs_t.field, .sdf): per env USV_FIELD_STRIDE floats of 4 x 8-texel tiles,
+ * one 128-B cache line each, tiles row-major over the grid padded to 152 x 152: texel (row r, column c) at
+ * ((r / 4) * USV_FIELD_TCOLS + c / 8) * 32 + (r % 4) * 8 + c % 8.  The env step's bilinear potential sample
+ * (a 2 x 2 texel block) then touches ~1.4 lines instead of the >= 2 of row-major rows. */
+#define USV_FIELD_TH     4
+#define USV_FIELD_TW     8
+#define USV_FIELD_TROWS  ((USV_GRID + USV_FIELD_TH - 1) / USV_FIELD_TH)
+#define USV_FIELD_TCOLS  ((USV_GRID + USV_FIELD_TW - 1) / USV_FIELD_TW)
+#define USV_FIELD_STRIDE (USV_FIELD_TROWS * USV_FIELD_TCOLS * USV_FIELD_TH * USV_FIELD_TW)
 #define USV_LUT_N     1000   /* thruster LUT points               (TEST yaml dynamics.thrusters) */
 #define USV_NSTAT       28   /* episode_sums keys                 (USV_Virtual.py:586-601) */
 #define USV_SPAWN_ITERS 20   /* obstacle rejection iterations     (static_obs.py:980) */
@@ -234,7 +243,7 @@ typedef struct usv_bufs {
   /* task */
   float *tgt_x, *tgt_y;
   float *obst;                     /* [16][2][n]  obstacle centres, local frame */
-  float *field;                    /* [n][150*150] potential field */
+  float *field;                    /* [n][USV_FIELD_STRIDE] potential field (tiled, see USV_FIELD_STRIDE) */
   /* history */
   float *prev_cmd;                 /* [2][n] raw policy command (obs 23:25) */
   float *prev_dist, *prev_head, *prev_pot, *prev_wz;
@@ -254,7 +263,7 @@ typedef struct usv_bufs {
   float   *extras_acc;             /* [ceil(n/256)][USV_NSTAT] reset-kernel per-workgroup sums (scratch) */
   float   *field_old_tgt;          /* [2][n] target used by the field of each reset env */
   float   *slot_stats;             /* [n][USV_FIELD_SLOT_STATS] per-reset-slot field statistics (scratch) */
-  float   *sdf;                    /* [n][150*150] per-reset-slot signed distance (scratch) */
+  float   *sdf;                    /* [n][USV_FIELD_STRIDE] per-reset-slot signed distance (scratch, tiled) */
   const float *grid_lin;           /* [150] cell centres of the field grid */
   float   *dist;                   /* [USV_NDIST][n] disturbance parameters; NULL when no disturbance is on */
   const float *env_org;            /* [2][n] world x, y of each env's origin (RLTask._env_pos); NULL = 0 */

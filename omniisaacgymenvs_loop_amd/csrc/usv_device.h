@@ -36,6 +36,12 @@ __device__ __forceinline__ void philox_u4(uint64_t seed, uint32_t env, uint64_t 
   out[0] = u01(r.x); out[1] = u01(r.y); out[2] = u01(r.z); out[3] = u01(r.w);
 }
 
+// index of texel (r, c) of an env's potential field in the tiled layout (include/usv_hip.h USV_FIELD_STRIDE)
+__host__ __device__ __forceinline__ int field_idx(int r, int c) {
+  static_assert(USV_FIELD_TH == 4 && USV_FIELD_TW == 8, "tile shifts");
+  return ((r >> 2) * USV_FIELD_TCOLS + (c >> 3)) * (USV_FIELD_TH * USV_FIELD_TW) + ((r & 3) << 3) + (c & 7);
+}
+
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 // torch's clamp/max/min propagate NaN differently from fminf/fmaxf; inputs here are finite.
 __device__ __forceinline__ float maxf(float a, float b) { return a > b ? a : b; }

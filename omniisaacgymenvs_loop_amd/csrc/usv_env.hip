@@ -423,10 +423,10 @@ __device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, flo
   // border clamp: i1/j1 == G only when the weight of that tap is 0 (ix, iy <= G-1);
   // the tap then reads the last column/row (any finite value) and is replaced by 0
   const int i1c = min(i1, G - 1), j1c = min(j1, G - 1);
-  t.v_nw = F[j0 * G + i0];
-  t.v_ne = F[j0 * G + i1c];
-  t.v_sw = F[j1c * G + i0];
-  t.v_se = F[j1c * G + i1c];
+  t.v_nw = F[field_idx(j0, i0)];
+  t.v_ne = F[field_idx(j0, i1c)];
+  t.v_sw = F[field_idx(j1c, i0)];
+  t.v_se = F[field_idx(j1c, i1c)];
   if (i1 >= G) { t.v_ne = 0.f; t.v_se = 0.f; }
   if (j1 >= G) { t.v_sw = 0.f; t.v_se = 0.f; }
   return t;
@@ -796,7 +796,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       pyn = pyn + (u[SU_PX + 1] * K.pos_rng + c.pos_noise_min);
     }
     // the potential sample only needs the position: issue its 4 texel loads now
-    const FieldTaps taps = field_taps(b.field + (size_t)ec * USV_GRID2, c.map_size, pxn, pyn);
+    const FieldTaps taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, c.map_size, pxn, pyn);
     float vxn = vx, vyn = vy, wzn = wz;
     if (c.vel_noise_on) {
       vxn = vxn + (u[SU_VX] * K.vel_rng + c.vel_noise_min);

@@ -36,16 +36,16 @@ namespace {
 
 constexpr int G = USV_GRID;
 constexpr int G2 = USV_GRID2;
+constexpr int FS = USV_FIELD_STRIDE;   // floats per env of the tiled field / SDF buffers
 constexpr int T = 10;            // tile edge
 constexpr int NT = G / T;        // 15 tiles per edge
 constexpr int kWaveThreads = 256;
 constexpr int kMaxIters = 4096;  // safety cap (never reached)
 constexpr int kChunk = 2048;     // cells per k_field_final work item
-constexpr int kChunks = (G2 + kChunk - 1) / kChunk;
+constexpr int kChunks = (FS + kChunk - 1) / kChunk;   // k_field_final: chunks of the tiled index space
 constexpr int kSlotStride = USV_FIELD_SLOT_STATS;   // floats per reset slot: 16 final + 12 per chunk + obstacles
 constexpr int kSlotObst = 160;                      // the slot's 16 obstacle centres (x, y interleaved)
-static_assert(kSlotObst >= 16 + 12 * ((USV_GRID2 + 2047) / 2048) && kSlotObst + 2 * USV_NOBST <= kSlotStride,
-              "slot_stats layout");
+static_assert(kSlotObst + 2 * USV_NOBST <= kSlotStride, "slot_stats layout");
 constexpr int kFieldPackMinEnvs = 32768;           // k_field_wave_pack (two envs per CU) from this many envs
 
 // slot_stats layout (per reset slot)
@@ -427,14 +427,14 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
     }
     const bool exact = __syncthreads_or((hmax > kPinnedCost) || (it >= kMaxIters)) != 0;
     // ---- 3. raw cost out (occupied marker -> +inf); statistics in k_field_stats ----
-    float *Fe = b.field + (size_t)e * G2;
+    float *Fe = b.field + (size_t)e * FS;
     if (tile_ok) {
 #pragma unroll
       for (int i = 0; i < T; ++i)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
           const float g = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
-          Fe[(r0 + i) * G + c0 + j] = g;
+          Fe[field_idx(r0 + i, c0 + j)] = g;
         }
       lastc[tp] = -1000;   // ready for the next slot
     }
@@ -494,10 +494,10 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_b
     ix = min(max(ix, 0), G - 1);
     iy = min(max(iy, 0), G - 1);
     __syncthreads();
-    float *Fe = b.field + (size_t)e * G2;
-    float *scratch = b.sdf + (size_t)slot * G2;   // k_field_stats writes the SDF there afterwards
-    cost_sweeps_exact(occ, ix, iy, Fe, scratch);  // 225 (odd) sweeps: the result is in scratch
-    for (int q = tid; q < G2; q += kWaveThreads) Fe[q] = scratch[q];
+    float *Fe = b.field + (size_t)e * FS;
+    float *scratch = b.sdf + (size_t)slot * FS;   // k_field_stats writes the SDF there afterwards
+    cost_sweeps_exact(occ, ix, iy, Fe, scratch);  // row-major ping-pong, 225 (odd) sweeps: result in scratch
+    for (int q = tid; q < G2; q += kWaveThreads) Fe[field_idx(q / G, q % G)] = scratch[q];   // into the tiles
     if (tid == 0) atomicAdd(&b.ctl[USV_CTL_FIELD_EXACT], 1);
     __syncthreads();
   }
@@ -546,8 +546,8 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
     const int slot = w / kBands, band = w % kBands;
     const int e = b.reset_ids[slot];
-    const float *Fe = b.field + (size_t)e * G2;
-    float *sdf_s = b.sdf + (size_t)slot * G2;
+    const float *Fe = b.field + (size_t)e * FS;
+    float *sdf_s = b.sdf + (size_t)slot * FS;
     if (tid < 2 * USV_NOBST) so[tid] = b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid];
     if (tid < 2) flags[tid] = 0;
     __syncthreads();
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
       const int r = band * kBandRows + rg + kRowGroups * k;
-      gv[k] = *reinterpret_cast<const float2 *>(Fe + r * G + c0);
+      gv[k] = *reinterpret_cast<const float2 *>(Fe + field_idx(r, c0));   // (c0 even: one tile row)
     }
     float dxa[USV_NOBST], dxb[USV_NOBST], oy[USV_NOBST];
     {
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       const float sva = sqrtf(__uint_as_float(a[0])) - c.obstacle_radius;
       const float svb = sqrtf(__uint_as_float(bb[0])) - c.obstacle_radius;
       if (act) {
-        *reinterpret_cast<float2 *>(sdf_s + r * G + c0) = make_float2(sva, svb);   // k_field_final reads it back
+        *reinterpret_cast<float2 *>(sdf_s + field_idx(r, c0)) = make_float2(sva, svb);   // read back by k_field_final
         stat(gv[k].x, sva);
         stat(gv[k].y, svb);
       }
@@ -734,9 +734,9 @@ __global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) 
     if (any_inside && has_inside) { jmn = fminf(jmn, high); jmx = fmaxf(jmx, high); }
     const float gden = (gmax - gmin) + 1e-6f;
     const float jden = (jmx - jmn) + 1e-6f;
-    float *Fe = b.field + (size_t)e * G2;
-    const float *sdf_s = b.sdf + (size_t)slot * G2;
-    const int q1 = min(G2, (ch + 1) * kChunk);
+    float *Fe = b.field + (size_t)e * FS;
+    const float *sdf_s = b.sdf + (size_t)slot * FS;
+    const int q1 = min(FS, (ch + 1) * kChunk);
     // compile-time trip count, clamped loads: the chunk's 2 x 8 loads per thread in flight at once
     constexpr int PER = kChunk / 256;
     float gv[PER], sv[PER];
@@ -749,7 +749,10 @@ __global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) 
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int q = ch * kChunk + u * 256 + threadIdx.x;
-      if (q >= q1) continue;
+      // tiled index -> grid cell: the 152 x 152 padding cells are skipped (never sampled)
+      const int tl = q >> 5, wq = q & 31;
+      const int r = (tl / USV_FIELD_TCOLS) * USV_FIELD_TH + (wq >> 3), cc = (tl % USV_FIELD_TCOLS) * USV_FIELD_TW + (wq & 7);
+      if (q >= q1 || r >= G || cc >= G) continue;
       const float g = gv[u];
       const float cv = isinf(g) ? k.inf_val : g;
       const float dte = sv[u] - c.obstacle_radius;

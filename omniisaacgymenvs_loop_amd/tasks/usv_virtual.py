@@ -27,6 +27,15 @@ from .usv_config import (action_bias_cfg, build_hydro_cfg, build_usv_cfg, env_or
 NOBS = DEFINES["USV_NOBS"]
 NOBST = DEFINES["USV_NOBST"]
 GRID2 = DEFINES["USV_GRID"] ** 2
+FIELD_STRIDE = DEFINES["USV_FIELD_STRIDE"]
+
+
+def field_tile_index() -> np.ndarray:
+    """Row-major cell q = r * 150 + c -> its index in an env's tiled field row (include/usv_hip.h
+    USV_FIELD_STRIDE: 4 x 8-texel tiles, one cache line each)."""
+    G, th, tw, tc = DEFINES["USV_GRID"], DEFINES["USV_FIELD_TH"], DEFINES["USV_FIELD_TW"], DEFINES["USV_FIELD_TCOLS"]
+    r, c = np.divmod(np.arange(G * G), G)
+    return ((r // th) * tc + c // tw) * (th * tw) + (r % th) * tw + c % tw
 NSTAT = DEFINES["USV_NSTAT"]
 NU_RESET = DEFINES["USV_NU_RESET"]
 NU_STEP = DEFINES["USV_NU_STEP"]
@@ -124,7 +133,7 @@ class USVVirtual:
         self.task_scratch = (Z(TS_ROWS * n + (n + 255) // 256, **f32) if self.cfg.task_kind == TASK_TRACK_XYO
                              else None)
         self._has_field = self.cfg.task_kind == TASK_CAPTURE_XY
-        self.field = Z((n if self._has_field else 1, GRID2), **f32)
+        self.field = Z((n if self._has_field else 1, FIELD_STRIDE), **f32)   # tiled rows (USV_FIELD_STRIDE)
         self.ibuf[2] = 1                               # RLTask.cleanup: reset_buf = ones
         self.just_reset.fill_(1)
         self.ctl = Z(CTL_N, **i32)
@@ -136,7 +145,7 @@ class USVVirtual:
         # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
         self.clock = Z(4, device=dev, dtype=torch.int64)
         self.states_buf = Z((n, 0), **f32)
-        self.sdf = torch.empty((n if self._has_field else 1, GRID2), **f32)   # per-reset-slot SDF scratch
+        self.sdf = torch.empty((n if self._has_field else 1, FIELD_STRIDE), **f32)   # per-reset-slot SDF scratch
         self.lut = Z((2, 1000), **f32)
         self.hydro = build_hydro_cfg(self._task_cfg)
         tl, tr = thruster_tables(self._task_cfg)
@@ -225,6 +234,14 @@ class USVVirtual:
             b.scene, b.scene_next, b.scene_last = p(self.scene), p(self.scene_next), p(self.scene_last)
             b.n_scenes, b.scene_cycle = self.scene_replay_num_scenes, int(self.scene_replay_cycle)
         return b
+
+    def field_rowmajor(self, ids=None) -> torch.Tensor:
+        """The potential fields of envs `ids` (all by default) as row-major [k, 150 * 150] grids (the device rows
+        are tiled, include/usv_hip.h USV_FIELD_STRIDE): what BatchedMapGPU returns per env."""
+        if not hasattr(self, "_field_idx"):
+            self._field_idx = torch.tensor(field_tile_index(), device=self._device, dtype=torch.long)
+        f = self.field if ids is None else self.field[ids]
+        return f.index_select(1, self._field_idx)
 
     def set_env_origins(self, org: torch.Tensor) -> None:
         """World x, y of each env's origin ([2][n]; RLTask._env_pos from the stage)."""

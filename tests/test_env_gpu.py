@@ -326,7 +326,7 @@ def _run_field(task, ids, obst, tgt, lin=None):
         task.set_grid_lin(torch.tensor(lin))
     _capi.call("usv_potential_field", _capi.byref(task.cfg), _capi.byref(task._bufs), _capi.stream_ptr())
     torch.cuda.synchronize()
-    return task.field[ids_t.long()].cpu().numpy()
+    return task.field_rowmajor(ids_t.long()).cpu().numpy()
 
 
 @pytest.mark.parametrize("pack", ["0", "1"])

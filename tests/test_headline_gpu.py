@@ -181,7 +181,7 @@ def test_philox_placement_8192_resets_vs_oracle(monkeypatch):
         if t == 0:
             assert len(ids) == n
             np.testing.assert_array_equal(task.obst.cpu().numpy().reshape(16, 2, n), E.obst)
-            np.testing.assert_array_equal(task.field.cpu().numpy(), E.field)
+            np.testing.assert_array_equal(task.field_rowmajor().cpu().numpy(), E.field)
         dp = _vs_oracle("headline_philox_8192", task, E, obs, rew, dones, t, dp)
 
 
