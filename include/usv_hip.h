@@ -358,6 +358,31 @@ int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions
                  const float *lut_dev, float action_bias, uint64_t seed,
                  uint64_t step, const float *u_inject, void *stream);
 
+/* The canonical env slab (tasks/usv_virtual.py allocates it): every per-env array of usv_bufs_t the step kernel
+ * touches at base + USV_SLAB_<X> * row_bytes, row_bytes = the next power of two >= 4 n (>= 256).  When the
+ * pointers follow this layout (and 4 n <= 2^22) usv_env_step runs a variant whose array offsets are compile-time
+ * constants (no per-array scalar registers live across the kernel); any other layout takes the general path. */
+#define USV_SLAB_STATE     0    /* px, py, yaw, vx, vy, wz, fl, fr (8 rows) */
+#define USV_SLAB_PARAMS    8    /* mass, com_x, com_y, com_z, k_drag, thr_l, thr_r, k_iz, mass_r (9) */
+#define USV_SLAB_LIN_DAMP 17    /* 3 rows, then quad_damp 3 rows */
+#define USV_SLAB_QUAD_DAMP 20
+#define USV_SLAB_TGT      23    /* tgt_x, tgt_y */
+#define USV_SLAB_OBST     25    /* 32 rows */
+#define USV_SLAB_PREV_CMD 57    /* 2 */
+#define USV_SLAB_HIST     59    /* prev_dist, prev_head, prev_pot, prev_wz */
+#define USV_SLAB_IBUF     63    /* goal_cnt, progress, reset_buf, done_succ, done_coll (i32) */
+#define USV_SLAB_JUST_RESET 68  /* u8 [n] */
+#define USV_SLAB_STATS    69    /* USV_NSTAT rows */
+#define USV_SLAB_OBS      97    /* [n][USV_NOBS] */
+#define USV_SLAB_REW     130
+#define USV_SLAB_DONES   131    /* i64 [n]: 2 rows */
+#define USV_SLAB_FIELD_OLD_TGT 133
+#define USV_SLAB_RESET_IDS 135
+#define USV_SLAB_DIST    136    /* USV_NDIST rows */
+#define USV_SLAB_ENV_ORG 147    /* 2 */
+#define USV_SLAB_TGT_H   149
+#define USV_SLAB_ROWS    150
+
 /* usv_env_step split in two so the non-reset envs can run while the reset envs'
  * potential fields are built: part 1 = envs not reset this step (needs only
  * usv_reset to have run), part 2 = the envs reset this step (after

@@ -493,6 +493,35 @@ struct StepWin {
   uint32_t n4;      // bytes of one [n] f32 row
   uint32_t bytes;   // window size
 };
+// The same offsets as compile-time constants for the canonical slab (include/usv_hip.h USV_SLAB_*) with
+// 2^kShift-byte rows: the general StepWin keeps ~45 offsets live in scalar registers across the kernel and the
+// compiler spills them into VGPR lanes (~560 v_readlane / v_writelane per wave); constants are rematerialised
+template <int kShift>
+struct FixedWin {
+  static constexpr uint32_t R(int row) { return (uint32_t)row << kShift; }
+  static constexpr uint32_t px = R(USV_SLAB_STATE), py = R(USV_SLAB_STATE + 1), yaw = R(USV_SLAB_STATE + 2),
+                            vx = R(USV_SLAB_STATE + 3), vy = R(USV_SLAB_STATE + 4), wz = R(USV_SLAB_STATE + 5),
+                            fl = R(USV_SLAB_STATE + 6), fr = R(USV_SLAB_STATE + 7);
+  static constexpr uint32_t mass = R(USV_SLAB_PARAMS), com_x = R(USV_SLAB_PARAMS + 1), com_y = R(USV_SLAB_PARAMS + 2),
+                            com_z = R(USV_SLAB_PARAMS + 3), k_drag = R(USV_SLAB_PARAMS + 4),
+                            thr_l = R(USV_SLAB_PARAMS + 5), thr_r = R(USV_SLAB_PARAMS + 6), k_iz = R(USV_SLAB_PARAMS + 7);
+  static constexpr uint32_t lin_damp = R(USV_SLAB_LIN_DAMP), quad_damp = R(USV_SLAB_QUAD_DAMP);
+  static constexpr uint32_t tgt_x = R(USV_SLAB_TGT), tgt_y = R(USV_SLAB_TGT + 1), obst = R(USV_SLAB_OBST);
+  static constexpr uint32_t prev_cmd = R(USV_SLAB_PREV_CMD);
+  static constexpr uint32_t prev_dist = R(USV_SLAB_HIST), prev_head = R(USV_SLAB_HIST + 1),
+                            prev_pot = R(USV_SLAB_HIST + 2), prev_wz = R(USV_SLAB_HIST + 3);
+  static constexpr uint32_t goal_cnt = R(USV_SLAB_IBUF), progress = R(USV_SLAB_IBUF + 1),
+                            reset_buf = R(USV_SLAB_IBUF + 2), done_succ = R(USV_SLAB_IBUF + 3),
+                            done_coll = R(USV_SLAB_IBUF + 4);
+  static constexpr uint32_t just_reset = R(USV_SLAB_JUST_RESET), stats = R(USV_SLAB_STATS), obs = R(USV_SLAB_OBS),
+                            rew = R(USV_SLAB_REW), dones = R(USV_SLAB_DONES), dist = R(USV_SLAB_DIST),
+                            env_org = R(USV_SLAB_ENV_ORG);
+  static constexpr uint32_t n4 = 1u << kShift;
+  static constexpr uint32_t bytes = (uint32_t)USV_SLAB_ROWS << kShift;
+  static_assert((unsigned long long)USV_SLAB_ROWS << kShift < 0x80000000ull, "window < 2 GiB");
+};
+constexpr int kFixedShiftMin = 13, kFixedShiftMax = 22;   // n in (1024, 1048576]
+
 // uniform constants derived on the host from usv_cfg_t (float/double arithmetic of the
 // reference done once; divisors with their correctly rounded reciprocals for div_rn)
 struct StepK {
@@ -582,8 +611,8 @@ __device__ __forceinline__ void top5_of_16(uint64_t k[16]) {
   cx64(k[1], k[2]); cx64(k[3], k[4]);
 }
 
-template <bool kStats, bool kInj, bool kDist>
-__global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, StepWin w, StepK K,
+template <bool kStats, bool kInj, bool kDist, class Win>
+__global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, Win w, StepK K,
                                                      const char *__restrict__ wbase, const float *__restrict__ actions,
                                                      const float *__restrict__ lut, float bias, uint64_t seed,
                                                      uint64_t step, const float *__restrict__ inj, int part) {
@@ -1464,6 +1493,45 @@ int step_window(const usv_cfg_t &c, const usv_bufs_t &b, const char **base, Step
   return 0;
 }
 
+// kShift when every array the step kernel touches sits at its canonical slab row (include/usv_hip.h USV_SLAB_*)
+// with 2^kShift-byte rows, 2^kShift the next power of two >= 4 n; -1 otherwise (the general window path)
+int fixed_slab_shift(const usv_cfg_t &c, const usv_bufs_t &b) {
+  int sh = 8;
+  while ((1ull << sh) < 4ull * (unsigned long long)b.n) ++sh;
+  if (sh < kFixedShiftMin || sh > kFixedShiftMax || !b.px) return -1;
+  const char *base = reinterpret_cast<const char *>(b.px);
+  const size_t rb = (size_t)1 << sh;
+  struct Row {
+    const void *p;
+    int row;
+    bool required;
+  };
+  const Row rows[] = {
+      {b.px, USV_SLAB_STATE, true}, {b.py, USV_SLAB_STATE + 1, true}, {b.yaw, USV_SLAB_STATE + 2, true},
+      {b.vx, USV_SLAB_STATE + 3, true}, {b.vy, USV_SLAB_STATE + 4, true}, {b.wz, USV_SLAB_STATE + 5, true},
+      {b.fl, USV_SLAB_STATE + 6, true}, {b.fr, USV_SLAB_STATE + 7, true}, {b.mass, USV_SLAB_PARAMS, true},
+      {b.com_x, USV_SLAB_PARAMS + 1, true}, {b.com_y, USV_SLAB_PARAMS + 2, true}, {b.com_z, USV_SLAB_PARAMS + 3, true},
+      {b.k_drag, USV_SLAB_PARAMS + 4, true}, {b.thr_l, USV_SLAB_PARAMS + 5, true}, {b.thr_r, USV_SLAB_PARAMS + 6, true},
+      {b.k_iz, USV_SLAB_PARAMS + 7, true}, {b.lin_damp, USV_SLAB_LIN_DAMP, false},
+      {b.quad_damp, USV_SLAB_QUAD_DAMP, false}, {b.tgt_x, USV_SLAB_TGT, true}, {b.tgt_y, USV_SLAB_TGT + 1, true},
+      {b.obst, USV_SLAB_OBST, true}, {b.prev_cmd, USV_SLAB_PREV_CMD, true}, {b.prev_dist, USV_SLAB_HIST, true},
+      {b.prev_head, USV_SLAB_HIST + 1, true}, {b.prev_pot, USV_SLAB_HIST + 2, true},
+      {b.prev_wz, USV_SLAB_HIST + 3, true}, {b.goal_cnt, USV_SLAB_IBUF, true}, {b.progress, USV_SLAB_IBUF + 1, true},
+      {b.reset_buf, USV_SLAB_IBUF + 2, true}, {b.done_succ, USV_SLAB_IBUF + 3, true},
+      {b.done_coll, USV_SLAB_IBUF + 4, true}, {b.just_reset, USV_SLAB_JUST_RESET, true},
+      {c.stats_on ? b.stats : nullptr, USV_SLAB_STATS, c.stats_on != 0}, {b.obs, USV_SLAB_OBS, true},
+      {b.rew, USV_SLAB_REW, true}, {b.dones, USV_SLAB_DONES, true}, {b.dist, USV_SLAB_DIST, false},
+      {b.dist ? b.env_org : nullptr, USV_SLAB_ENV_ORG, false}};
+  for (const Row &r : rows) {
+    if (!r.p) {
+      if (r.required) return -1;
+      continue;
+    }
+    if (reinterpret_cast<const char *>(r.p) != base + (size_t)r.row * rb) return -1;
+  }
+  return sh;
+}
+
 // any per-substep disturbance term on (then usv_bufs_t.dist must be set)
 bool step_has_dist(const usv_cfg_t &c) { return c.fdist_on || c.tdist_on || c.current_on; }
 
@@ -1606,10 +1674,28 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
   hipStream_t s = (hipStream_t)stream;
   const bool dist = b->dist != nullptr;
   if (step_has_dist(*cfg) && !dist) return 4;   // a disturbance / water current is on: dist is required
-  auto kern = dist ? (cfg->stats_on ? (u_inject ? k_env_step<true, true, true> : k_env_step<true, false, true>)
-                                    : (u_inject ? k_env_step<false, true, true> : k_env_step<false, false, true>))
-                   : (cfg->stats_on ? (u_inject ? k_env_step<true, true, false> : k_env_step<true, false, false>)
-                                    : (u_inject ? k_env_step<false, true, false> : k_env_step<false, false, false>));
+  // the production shape (statistics on, in-kernel draws, no disturbance) on the canonical slab: constant offsets
+  const int sh = fixed_slab_shift(*cfg, *b);
+  if (sh >= 0 && cfg->stats_on && !u_inject && !dist) {
+    const char *base = reinterpret_cast<const char *>(b->px);
+#define USV_FIXED_CASE(S)                                                                                            \
+  case S:                                                                                                            \
+    hipLaunchKernelGGL((k_env_step<true, false, false, FixedWin<S>>), dim3(grid), dim3(kBlock), 0, s, *cfg, *b,      \
+                       FixedWin<S>{}, k, base, actions, lut_dev, action_bias, seed, step, u_inject, part);           \
+    break;
+    switch (sh) {
+      USV_FIXED_CASE(13) USV_FIXED_CASE(14) USV_FIXED_CASE(15) USV_FIXED_CASE(16) USV_FIXED_CASE(17)
+      USV_FIXED_CASE(18) USV_FIXED_CASE(19) USV_FIXED_CASE(20) USV_FIXED_CASE(21) USV_FIXED_CASE(22)
+      default: return 6;
+    }
+#undef USV_FIXED_CASE
+    USV_CHECK_LAUNCH();
+    return 0;
+  }
+  auto kern = dist ? (cfg->stats_on ? (u_inject ? k_env_step<true, true, true, StepWin> : k_env_step<true, false, true, StepWin>)
+                                    : (u_inject ? k_env_step<false, true, true, StepWin> : k_env_step<false, false, true, StepWin>))
+                   : (cfg->stats_on ? (u_inject ? k_env_step<true, true, false, StepWin> : k_env_step<true, false, false, StepWin>)
+                                    : (u_inject ? k_env_step<false, true, false, StepWin> : k_env_step<false, false, false, StepWin>));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, w, k, wbase, actions, lut_dev, action_bias, seed,
                      step, u_inject, part);
   USV_CHECK_LAUNCH();

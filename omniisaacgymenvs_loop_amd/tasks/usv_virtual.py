@@ -100,22 +100,31 @@ class USVVirtual:
         f32 = dict(device=dev, dtype=torch.float32)
         i32 = dict(device=dev, dtype=torch.int32)
         Z = lambda *s, **k: torch.zeros(*s, **k)
-        # Every per-env array the step kernel touches comes from ONE slab, so they share a
-        # < 2 GiB window and the kernel addresses them with buffer instructions (one 32-bit
-        # lane offset + a scalar per-array offset; include/usv_hip.h, usv_env_step).
-        slab_spec = [("state", (8, n), torch.float32), ("params", (9, n), torch.float32),
-                     ("damp", (2, 3, n), torch.float32), ("tgt", (2, n), torch.float32),
-                     ("obst", (NOBST * 2, n), torch.float32), ("prev_cmd", (2, n), torch.float32),
-                     ("hist", (4, n), torch.float32), ("ibuf", (5, n), torch.int32),
-                     ("just_reset", (n,), torch.uint8), ("stats", (NSTAT, n), torch.float32),
-                     ("obs_buf_t", (n, NOBS), torch.float32), ("rew_buf", (n,), torch.float32),
-                     ("dones", (n,), torch.int64), ("field_old_tgt", (2, n), torch.float32),
-                     ("reset_ids", (n,), torch.int32), ("dist", (NDIST, n), torch.float32),
-                     ("env_org", (2, n), torch.float32), ("tgt_h", (n,), torch.float32)]
-        sizes = [int(np.prod(shape)) * torch.empty((), dtype=dt).element_size() for _, shape, dt in slab_spec]
-        offs = np.concatenate([[0], np.cumsum([(sz + 255) // 256 * 256 for sz in sizes])])
-        self._slab = torch.zeros(int(offs[-1]), device=dev, dtype=torch.uint8)
-        for (name, shape, dt), o, sz in zip(slab_spec, offs, sizes):
+        # Every per-env array the step kernel touches comes from ONE slab, so they share a < 2 GiB window that the
+        # kernel addresses with buffer instructions (one 32-bit lane offset + a per-array offset; include/usv_hip.h,
+        # usv_env_step).  With n a multiple of 64 the slab is the canonical layout of include/usv_hip.h (USV_SLAB_*:
+        # array X at row USV_SLAB_X of 4 n-byte rows), and for power-of-two 4 n the step kernel takes its
+        # constant-offset variant; otherwise the arrays are packed at 256-byte boundaries.
+        slab_spec = [("state", (8, n), torch.float32, "STATE"), ("params", (9, n), torch.float32, "PARAMS"),
+                     ("damp", (2, 3, n), torch.float32, "LIN_DAMP"), ("tgt", (2, n), torch.float32, "TGT"),
+                     ("obst", (NOBST * 2, n), torch.float32, "OBST"), ("prev_cmd", (2, n), torch.float32, "PREV_CMD"),
+                     ("hist", (4, n), torch.float32, "HIST"), ("ibuf", (5, n), torch.int32, "IBUF"),
+                     ("just_reset", (n,), torch.uint8, "JUST_RESET"), ("stats", (NSTAT, n), torch.float32, "STATS"),
+                     ("obs_buf_t", (n, NOBS), torch.float32, "OBS"), ("rew_buf", (n,), torch.float32, "REW"),
+                     ("dones", (n,), torch.int64, "DONES"), ("field_old_tgt", (2, n), torch.float32, "FIELD_OLD_TGT"),
+                     ("reset_ids", (n,), torch.int32, "RESET_IDS"), ("dist", (NDIST, n), torch.float32, "DIST"),
+                     ("env_org", (2, n), torch.float32, "ENV_ORG"), ("tgt_h", (n,), torch.float32, "TGT_H")]
+        sizes = [int(np.prod(shape)) * torch.empty((), dtype=dt).element_size() for _, shape, dt, _ in slab_spec]
+        if n % 64 == 0:
+            rb = 4 * n
+            offs = [DEFINES[f"USV_SLAB_{key}"] * rb for _, _, _, key in slab_spec]
+            total = DEFINES["USV_SLAB_ROWS"] * rb
+            assert all(o + sz <= total for o, sz in zip(offs, sizes))
+        else:
+            offs = list(np.concatenate([[0], np.cumsum([(sz + 255) // 256 * 256 for sz in sizes])]))
+            total = int(offs[-1])
+        self._slab = torch.zeros(total, device=dev, dtype=torch.uint8)
+        for (name, shape, dt, _), o, sz in zip(slab_spec, offs, sizes):
             setattr(self, name, self._slab[int(o):int(o) + sz].view(dt).view(shape))
         self.params[0] = self.cfg.base_mass
         self.params[4:8] = 1.0
