@@ -677,6 +677,14 @@ int lz_returns(const lz_cfg_t *cfg, const float *last_values, const float *st_re
 int lz_minibatch(const lz_cfg_t *cfg, float *params, float *adam_m, float *adam_v, float *opt, int opt_slot, int mb,
                  const float *st_obs, const float *st_act, const float *st_logp, const float *st_val,
                  const float *st_ret, const float *st_adv, float *partials, float *grad, void *stream);
+/* lz_minibatch with the rows of the minibatch given: rows (device [M], M = N T / mini_batches) are indices
+ * into the flattened [T * N] storage -- the 'shuffle' sampler's minibatch (storage.py:123-134,
+ * BatchSampler(SubsetRandomSampler(range(N T)), M, drop_last=True), the reference PPO's default sampling,
+ * ppo.py:52-53); rows = NULL is lz_minibatch's in-order minibatch mb. */
+int lz_minibatch_rows(const lz_cfg_t *cfg, float *params, float *adam_m, float *adam_v, float *opt, int opt_slot,
+                      int mb, const float *st_obs, const float *st_act, const float *st_logp, const float *st_val,
+                      const float *st_ret, const float *st_adv, const int32_t *rows, float *partials, float *grad,
+                      void *stream);
 /* enforce_minimum_std (module.py:649-659): std = max(finite(std) ? std : min_std, min_std) */
 int lz_enforce_min_std(const lz_cfg_t *cfg, float *params, void *stream);
 int lz_partials_floats(const lz_cfg_t *cfg);

@@ -61,6 +61,7 @@ def _declare(lib):
         "lz_store": [P, P, P, I, P, P, P],
         "lz_returns": [P, P, P, P, P, P, P, P, P],
         "lz_minibatch": [P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P],
+        "lz_minibatch_rows": [P, P, P, P, P, I, I, P, P, P, P, P, P, P, P, P, P],
         "lz_enforce_min_std": [P, P, P],
         "ppo_policy_step": [P, P, P, P, P, I, P, P, P, P, P, P, P, P, P, U64, U64, P, P, P],
         "ppo_value": [P, P, P, P, P, P, P],

@@ -98,16 +98,19 @@ __device__ void stage_net(const float *__restrict__ P, const NetOff &o, int obs_
 }
 
 // Rows [row0, row0 + nrows) of obs (row stride obs_dim) into s.m / s.x (nan_to_num, as
-// storage.add_transitions and PPO.observe sanitise); rows past nrows repeat the last row.
-__device__ void stage_rows(const float *__restrict__ obs, size_t row0, int nrows, int obs_dim, NetSmem &s) {
+// storage.add_transitions and PPO.observe sanitise); rows past nrows repeat the last row.  With ridx
+// (the shuffle sampler's minibatch indices) tile row r is storage row ridx[r] instead of row0 + r.
+__device__ void stage_rows(const float *__restrict__ obs, size_t row0, int nrows, int obs_dim, NetSmem &s,
+                           const int32_t *__restrict__ ridx = nullptr) {
   const int tid = threadIdx.x;
   const int nsp = obs_dim - MS;
   for (int q = tid; q < RB * XS; q += TB) {
     const int r = q / XS, k = q % XS;
     const int rc = r < nrows ? r : nrows - 1;
+    const size_t row = ridx ? (size_t)ridx[rc] : row0 + rc;
     float v = 0.f;
     if (k < obs_dim) {
-      v = obs[(row0 + rc) * (size_t)obs_dim + k];
+      v = obs[row * (size_t)obs_dim + k];
       if (!isfinite(v)) v = 0.f;
     }
     if (k < nsp) s.x[q] = v;
@@ -361,7 +364,7 @@ __device__ void grad_net(const lz_cfg_t &c, const float *__restrict__ P, int wg,
                          const float *__restrict__ st_obs, const float *__restrict__ st_act,
                          const float *__restrict__ st_logp, const float *__restrict__ st_val,
                          const float *__restrict__ st_ret, const float *__restrict__ st_adv, float *part,
-                         NetSmem &s) {
+                         NetSmem &s, const int32_t *__restrict__ ridx) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
   const int D = c.obs_dim, nsp = D - MS, nx = D - 32;   // nx: W1 columns past the first 32 (1..4)
@@ -382,14 +385,15 @@ __device__ void grad_net(const lz_cfg_t &c, const float *__restrict__ P, int wg,
   for (int tile = wg; tile < ntiles; tile += G) {
     const int rt0 = tile * RB, nrows = min(RB, M - rt0);
     const size_t row0 = mb_row0 + rt0;
-    stage_rows(st_obs, row0, nrows, D, s);
+    const int32_t *tidx = ridx ? ridx + rt0 : nullptr;   // shuffle sampler: this tile's storage rows
+    stage_rows(st_obs, row0, nrows, D, s, tidx);
     tile_forward(D, nout, s);
     // ---- losses and head gradients (one thread per row) ----
     if (tid < RB) {
       const int r = tid;
       float d0 = 0.f, d1 = 0.f;
       if (r < nrows) {
-        const size_t q = row0 + r;
+        const size_t q = tidx ? (size_t)tidx[r] : row0 + r;
         if (kActor) {
           const float mu0 = tanhf(s.out[r * NA]), mu1 = tanhf(s.out[r * NA + 1]);
           // SquashedGaussian.evaluate (module.py:586-637): u = atanh(clamp(a / (scale + eps)))
@@ -623,15 +627,15 @@ __global__ __launch_bounds__(TB) void k_lz_grad(lz_cfg_t c, const float *__restr
                                                 const float *__restrict__ st_obs, const float *__restrict__ st_act,
                                                 const float *__restrict__ st_logp, const float *__restrict__ st_val,
                                                 const float *__restrict__ st_ret, const float *__restrict__ st_adv,
-                                                float *part_a, float *part_c) {
+                                                float *part_a, float *part_c, const int32_t *__restrict__ ridx) {
   __shared__ NetSmem s;
   const int stride = part_stride(c.obs_dim);
   if ((int)blockIdx.x < G)
     grad_net<true>(c, P, blockIdx.x, G, mb_row0, M, st_obs, st_act, st_logp, st_val, st_ret, st_adv,
-                   part_a + (size_t)blockIdx.x * stride, s);
+                   part_a + (size_t)blockIdx.x * stride, s, ridx);
   else
     grad_net<false>(c, P, blockIdx.x - G, G, mb_row0, M, st_obs, st_act, st_logp, st_val, st_ret, st_adv,
-                    part_c + (size_t)(blockIdx.x - G) * stride, s);
+                    part_c + (size_t)(blockIdx.x - G) * stride, s, ridx);
 }
 
 // Fixed-order sum of the G partial rows of each network into grad[] (parameter order), the loss
@@ -808,6 +812,14 @@ int lz_returns(const lz_cfg_t *cfg, const float *last_values, const float *st_re
 int lz_minibatch(const lz_cfg_t *cfg, float *params, float *adam_m, float *adam_v, float *opt, int opt_slot, int mb,
                  const float *st_obs, const float *st_act, const float *st_logp, const float *st_val,
                  const float *st_ret, const float *st_adv, float *partials, float *grad, void *stream) {
+  return lz_minibatch_rows(cfg, params, adam_m, adam_v, opt, opt_slot, mb, st_obs, st_act, st_logp, st_val, st_ret,
+                           st_adv, nullptr, partials, grad, stream);
+}
+
+int lz_minibatch_rows(const lz_cfg_t *cfg, float *params, float *adam_m, float *adam_v, float *opt, int opt_slot,
+                      int mb, const float *st_obs, const float *st_act, const float *st_logp, const float *st_val,
+                      const float *st_ret, const float *st_adv, const int32_t *rows, float *partials, float *grad,
+                      void *stream) {
   if (!cfg_ok(cfg) || !params || !adam_m || !adam_v || !opt || !partials || !grad) return 1;
   if (opt_slot != 0 && opt_slot != 1) return 2;
   const int B = cfg->n_envs * cfg->horizon, M = B / cfg->mini_batches;
@@ -817,7 +829,7 @@ int lz_minibatch(const lz_cfg_t *cfg, float *params, float *adam_m, float *adam_
   const int stride = part_stride(cfg->obs_dim);
   float *part_a = partials, *part_c = partials + (size_t)G * stride;
   hipLaunchKernelGGL(k_lz_grad, dim3(2 * G), dim3(TB), 0, s, *cfg, params, G, (size_t)mb * M, M, st_obs, st_act,
-                     st_logp, st_val, st_ret, st_adv, part_a, part_c);
+                     st_logp, st_val, st_ret, st_adv, part_a, part_c, rows);
   USV_CHECK_LAUNCH();
   const int np = nparam(cfg->obs_dim), nch = (np + RD_TB - 1) / RD_TB;
   hipLaunchKernelGGL(k_lz_reduce, dim3(nch), dim3(RD_TB), 0, s, *cfg, part_a, part_c, G, grad);

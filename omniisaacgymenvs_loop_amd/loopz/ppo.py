@@ -5,7 +5,9 @@ update_rl_coeff).  The parameters, the Adam moments, the rollout storage and eve
 observe / step / update live on the GPU; observe() and step() keep the reference's numpy
 interface (they copy to / from the host) and observe_device() / step_device() are the
 device-resident variants the loopz training loop uses.  mini_batch_sampling 'in_order' is the
-trainer's choice (scripts/rlgames_train.py:325); 'shuffle' is not implemented by the kernels."""
+trainer's choice (scripts/rlgames_train.py:325); 'shuffle' (the class default) draws a fresh
+permutation of the T N storage rows per learning epoch on the device and hands each minibatch's
+M rows to the gradient kernel (lz_minibatch_rows)."""
 from __future__ import annotations
 
 import math
@@ -28,8 +30,6 @@ class PPO:
                  mini_batch_sampling='shuffle', log_intervals=10, flat_expert=None, seed=0):
         if mini_batch_sampling not in ("shuffle", "in_order"):
             raise NameError(mini_batch_sampling + ' is not a valid sampling method. Use one of the followings: shuffle, order')
-        if mini_batch_sampling == "shuffle":
-            raise NotImplementedError("loopz kernels implement in_order minibatches (the trainer's setting)")
         if flat_expert is not None:
             raise NotImplementedError("imitation (flat_expert) is off in the loopz trainer (rlgames_train.py:92)")
         self.actor, self.critic = actor, critic
@@ -49,6 +49,11 @@ class PPO:
         self.ep_infos = []
         self.tot_timesteps = 0
         self.seed = int(seed)
+        self.mini_batch_sampling = mini_batch_sampling
+        # shuffle: device permutation stream (the reference draws SubsetRandomSampler's randperm from torch's
+        # global CPU generator, storage.py:123-134); inject_batches() replays recorded minibatches instead
+        self._perm_gen = None
+        self._injected_batches = None
         self._step_counter = 0
         c = LzCfg()
         c.n_envs, c.horizon, c.obs_dim = self.num_envs, self.num_transitions_per_env, obs_dim
@@ -152,19 +157,47 @@ class PPO:
             self.log(update)
         self.ep_infos.clear()
 
+    def inject_batches(self, batches):
+        """Replay recorded 'shuffle' minibatches ([epochs * mini_batches][M] row indices into the flattened
+        T N storage, e.g. the BatchSampler draws of a reference run) on the next update (tests)."""
+        b = torch.as_tensor(np.asarray(batches), dtype=torch.int32)
+        m = self.num_transitions_per_env * self.num_envs // self.num_mini_batches
+        if b.shape != (self.num_learning_epochs * self.num_mini_batches, m):
+            raise ValueError(f"batches shape {tuple(b.shape)} != {(self.num_learning_epochs * self.num_mini_batches, m)}")
+        if int(b.min()) < 0 or int(b.max()) >= self.num_transitions_per_env * self.num_envs:
+            raise ValueError("batch row index out of range")
+        self._injected_batches = b.to(self.params.device).contiguous()
+
+    def _shuffle_rows(self):
+        """[epochs * mini_batches][M] int32 rows: per epoch one permutation of range(T N) cut into
+        mini_batches chunks of M, the tail dropped (BatchSampler(..., drop_last=True), storage.py:123-134)."""
+        if self._injected_batches is not None:
+            rows, self._injected_batches = self._injected_batches, None
+            return rows
+        nt = self.num_transitions_per_env * self.num_envs
+        m = nt // self.num_mini_batches
+        if self._perm_gen is None:
+            self._perm_gen = torch.Generator(device=self.params.device)
+            self._perm_gen.manual_seed(self.seed ^ 0x5EED5A11)
+        perms = [torch.randperm(nt, device=self.params.device, generator=self._perm_gen)[:m * self.num_mini_batches]
+                 for _ in range(self.num_learning_epochs)]
+        return torch.stack(perms).view(-1, m).to(torch.int32).contiguous()
+
     def _train_step(self):
-        """ppo.py:237-321 on the device: epochs x in-order minibatches, each one gradient launch,
-        one fixed-order reduction and one clip + Adam launch (skipped on a non-finite loss)."""
+        """ppo.py:237-321 on the device: epochs x minibatches (in order, or shuffled rows), each one
+        gradient launch, one fixed-order reduction and one clip + Adam launch (skipped on a non-finite loss)."""
         st = self.storage
         s = _capi.stream_ptr()
         k = 0
         logs = torch.zeros((self.num_learning_epochs * self.num_mini_batches, 8), device=self.params.device)
+        rows = self._shuffle_rows() if self.mini_batch_sampling == "shuffle" else None
         for _ in range(self.num_learning_epochs):
             for mb in range(self.num_mini_batches):
-                _capi.call("lz_minibatch", _capi.byref(self.cfg), _capi.ptr(self.params), _capi.ptr(self.adam_m),
+                _capi.call("lz_minibatch_rows", _capi.byref(self.cfg), _capi.ptr(self.params), _capi.ptr(self.adam_m),
                            _capi.ptr(self.adam_v), _capi.ptr(self.opt), k % 2, mb, _capi.ptr(st.actor_obs),
                            _capi.ptr(st.actions), _capi.ptr(st.actions_log_prob), _capi.ptr(st.values),
-                           _capi.ptr(st.returns), _capi.ptr(st.advantages), _capi.ptr(self.partials),
+                           _capi.ptr(st.returns), _capi.ptr(st.advantages),
+                           _capi.ptr(rows[k]) if rows is not None else None, _capi.ptr(self.partials),
                            _capi.ptr(self.grad), s)
                 logs[k].copy_(self.opt[8 * ((k + 1) % 2):8 * ((k + 1) % 2) + 8])
                 k += 1

@@ -244,16 +244,20 @@ def clip_grad(G: dict, obs_dim, max_norm, n_act=2):
     return (g * F(coef)).astype(F), total
 
 
-def train_step(pv, adam: Adam, data: dict, scale, cfg: Config):
-    """PPO._train_step (ppo.py:237-321): epochs x in-order minibatches of the time-major batch."""
+def train_step(pv, adam: Adam, data: dict, scale, cfg: Config, batches=None):
+    """PPO._train_step (ppo.py:237-321): epochs x minibatches of the time-major batch -- in order
+    (storage.mini_batch_generator_inorder), or the rows `batches[k]` of the k-th minibatch
+    (mini_batch_generator_shuffle, storage.py:123-134: BatchSampler(SubsetRandomSampler) indices)."""
     obs_dim = data["obs"].shape[-1]
     flat = {k: np.asarray(v).reshape((-1,) + np.asarray(v).shape[2:]) for k, v in data.items()}
     B = flat["obs"].shape[0]
     M = B // cfg.mini_batches
     vls, sls = [], []
+    k = 0
     for _ in range(cfg.epochs):
         for i in range(cfg.mini_batches):
-            sl = slice(i * M, (i + 1) * M)
+            sl = slice(i * M, (i + 1) * M) if batches is None else np.asarray(batches[k])
+            k += 1
             G, vl, sloss, loss = minibatch_grad(unflatten(pv, obs_dim), flat["obs"][sl], flat["actions"][sl],
                                                 flat["logp"][sl], flat["values"][sl], flat["returns"][sl],
                                                 flat["advantages"][sl], scale, cfg)

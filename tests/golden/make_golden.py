@@ -622,7 +622,7 @@ def gen_hydrostatics(torch):
                         gravity=np.float32(grav))
 
 
-def gen_loopz(torch, n=16, T=24, seed=7):
+def gen_loopz(torch, n=16, T=24, seed=7, sampling="in_order"):
     """The loopz trainer's PPO (omniisaacgymenvs/algo/ppo/{ppo,storage,module}.py) as
     scripts/rlgames_train.py:273-328 builds it (MLPEncode_wrap actor / critic, LeakyReLU, tanh actor
     output, squashed Gaussian init std 0.3, gamma 0.997, lambda 0.95, 4 x 4 in-order minibatches,
@@ -654,6 +654,17 @@ def gen_loopz(torch, n=16, T=24, seed=7):
             return self.loc + self.scale * eps
 
     M.Normal = RecNormal
+    batches = []
+    if sampling == "shuffle":   # record the minibatch indices of storage.mini_batch_generator_shuffle
+        import omniisaacgymenvs.algo.ppo.storage as S
+
+        class RecBatchSampler(S.BatchSampler):
+            def __iter__(self):
+                for b in super().__iter__():
+                    batches.append(np.asarray(list(b), np.int32))
+                    yield b
+
+        S.BatchSampler = RecBatchSampler
     torch.manual_seed(seed)
     ob_dim, act_dim = 33, 2
     kw = dict(speed_dim=3, mass_dim=8, mass_latent_dim=8, mass_encoder_shape=(64, 16))
@@ -662,7 +673,7 @@ def gen_loopz(torch, n=16, T=24, seed=7):
     critic = M.Critic(M.MLPEncode_wrap([128, 128], nn.LeakyReLU, ob_dim, 1, **kw), "cpu")
     ppo = P.PPO(actor=actor, critic=critic, num_envs=n, num_transitions_per_env=T, num_learning_epochs=4,
                 gamma=0.997, lam=0.95, num_mini_batches=4, device="cpu", log_dir="/tmp/loopz_golden",
-                mini_batch_sampling="in_order", learning_rate=5e-4)
+                mini_batch_sampling=sampling, learning_rate=5e-4)
     sd = lambda m: {k: v.detach().clone().numpy() for k, v in m.state_dict().items()}
     init = {"actor": sd(actor.architecture), "dist": sd(actor.distribution), "critic": sd(critic.architecture)}
     rng = np.random.default_rng(seed)
@@ -701,7 +712,10 @@ def gen_loopz(torch, n=16, T=24, seed=7):
     for i, s_ in opt["state"].items():
         out[f"adam_m_{i}"] = s_["exp_avg"].numpy()
         out[f"adam_v_{i}"] = s_["exp_avg_sq"].numpy()
-    np.savez_compressed(os.path.join(OUT, "loopz_update.npz"), **out)
+    if sampling == "shuffle":
+        out["batches"] = np.stack(batches)   # [epochs * mini_batches][M] rows of the flattened [T * N] storage
+    np.savez_compressed(os.path.join(OUT, "loopz_update.npz" if sampling == "in_order" else
+                                     f"loopz_update_{sampling}.npz"), **out)
 
 
 def gen_field(torch):
@@ -1084,6 +1098,7 @@ def main():
         "episodeT": lambda: gen_episode(torch, "T", 12, 64, 32),
         "ppo": lambda: gen_ppo(torch),
         "loopz": lambda: gen_loopz(torch),
+        "loopz_shuffle": lambda: gen_loopz(torch, sampling="shuffle"),
         "ckpt811": lambda: gen_ckpt811(torch),
     }
     for name, fn in jobs.items():

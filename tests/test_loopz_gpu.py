@@ -17,7 +17,7 @@ OBS = 33
 _Leaky, _Tanh = torch.nn.LeakyReLU, torch.nn.Tanh   # the activation constructors the reference passes
 
 
-def _build(n, T, d=None, seed=0):
+def _build(n, T, d=None, seed=0, sampling="in_order"):
     kw = dict(speed_dim=3, mass_dim=8, mass_latent_dim=8, mass_encoder_shape=(64, 16))
     actor = Actor(MLPEncode_wrap([128, 128], _Leaky, OBS, 2, _Tanh, False, seed=seed, **kw),
                   SquashedGaussianDiagonalCovariance(2, 0.3, action_scale=1.0), DEV)
@@ -27,7 +27,7 @@ def _build(n, T, d=None, seed=0):
         actor.architecture.load_state_dict(sd("actor"))
         actor.distribution.load_state_dict(sd("dist"))
         critic.architecture.load_state_dict(sd("critic"))
-    return PPO(actor, critic, n, T, 4, 4, gamma=0.997, lam=0.95, device=DEV, mini_batch_sampling="in_order",
+    return PPO(actor, critic, n, T, 4, 4, gamma=0.997, lam=0.95, device=DEV, mini_batch_sampling=sampling,
                learning_rate=5e-4, log_dir="/tmp/loopz_test")
 
 
@@ -76,10 +76,38 @@ def test_rollout_and_update_vs_reference(golden):
         np.testing.assert_allclose(osd["state"][i]["exp_avg"].numpy(), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
 
 
-@pytest.mark.parametrize("n,T", [(512, 600), (37, 24)])
-def test_minibatch_vs_oracle(n, T):
-    """One full-size in-order minibatch (76800 rows at the loopz default of 512 envs x 600 steps;
-    and a ragged size) through lz_minibatch against the oracle's gradient + clip + Adam."""
+def test_shuffle_update_vs_reference(golden):
+    """mini_batch_sampling='shuffle' (ppo.py:52-53, storage.py:123-134): the reference's recorded
+    BatchSampler(SubsetRandomSampler) minibatches replayed through lz_minibatch_rows."""
+    d = golden("loopz_update_shuffle.npz")
+    T, n = d["rew"].shape
+    ppo = _build(n, T, d, sampling="shuffle")
+    _rollout(ppo, d)
+    ppo.inject_batches(d["batches"])
+    ppo.update(actor_obs=None, value_obs=torch.tensor(d["obs"][T]), log_this_iteration=False, update=0)
+    assert ppo.adam_step() == 16
+    got, want = ppo.params.cpu().numpy(), _params(d, "after")
+    ET.check("loopz_update_shuffle", "params", got, want, 1e-5, 1e-6)
+    np.testing.assert_allclose(ppo.mean_value_loss, float(d["loss_value"]), rtol=1e-5)
+    np.testing.assert_allclose(ppo.mean_surrogate_loss, float(d["loss_surrogate"]), rtol=1e-4, atol=1e-6)
+
+
+def test_shuffle_rows_are_per_epoch_permutations():
+    n, T = 37, 24
+    ppo = _build(n, T, seed=2, sampling="shuffle")
+    rows = ppo._shuffle_rows().cpu().numpy()
+    M = n * T // 4
+    assert rows.shape == (16, M)
+    for e in range(4):
+        ep = rows[4 * e:4 * e + 4].reshape(-1)
+        assert len(np.unique(ep)) == 4 * M and ep.min() >= 0 and ep.max() < n * T
+    assert not np.array_equal(rows[:4], rows[4:8])
+
+
+@pytest.mark.parametrize("n,T,rows_shuffled", [(512, 600, False), (37, 24, False), (512, 600, True), (37, 24, True)])
+def test_minibatch_vs_oracle(n, T, rows_shuffled):
+    """One full-size minibatch (76800 rows at the loopz default of 512 envs x 600 steps; and a ragged
+    size), in order or of shuffled rows, through lz_minibatch_rows against the oracle's gradient + clip + Adam."""
     rng = np.random.default_rng(3)
     ppo = _build(n, T, seed=5)
     st = ppo.storage
@@ -94,16 +122,18 @@ def test_minibatch_vs_oracle(n, T):
         buf.copy_(torch.tensor(data[k]))
     p0 = ppo.params.cpu().numpy()
     mb = 1
-    from omniisaacgymenvs_loop_amd import _capi
-    _capi.call("lz_minibatch", _capi.byref(ppo.cfg), _capi.ptr(ppo.params), _capi.ptr(ppo.adam_m),
-               _capi.ptr(ppo.adam_v), _capi.ptr(ppo.opt), 0, mb, _capi.ptr(st.actor_obs), _capi.ptr(st.actions),
-               _capi.ptr(st.actions_log_prob), _capi.ptr(st.values), _capi.ptr(st.returns), _capi.ptr(st.advantages),
-               _capi.ptr(ppo.partials), _capi.ptr(ppo.grad), _capi.stream_ptr())
-    torch.cuda.synchronize()
     B = n * T
     M = B // 4
+    # in order at full size; the ragged case takes a shuffled minibatch (random rows of the T N storage)
+    sl = slice(mb * M, (mb + 1) * M) if rows_shuffled is False else rng.permutation(B)[:M]
+    rows = None if rows_shuffled is False else torch.tensor(sl, dtype=torch.int32, device=DEV)
+    from omniisaacgymenvs_loop_amd import _capi
+    _capi.call("lz_minibatch_rows", _capi.byref(ppo.cfg), _capi.ptr(ppo.params), _capi.ptr(ppo.adam_m),
+               _capi.ptr(ppo.adam_v), _capi.ptr(ppo.opt), 0, mb, _capi.ptr(st.actor_obs), _capi.ptr(st.actions),
+               _capi.ptr(st.actions_log_prob), _capi.ptr(st.values), _capi.ptr(st.returns), _capi.ptr(st.advantages),
+               _capi.ptr(rows), _capi.ptr(ppo.partials), _capi.ptr(ppo.grad), _capi.stream_ptr())
+    torch.cuda.synchronize()
     flat = {k: v.reshape((B,) + v.shape[2:]) for k, v in data.items()}
-    sl = slice(mb * M, (mb + 1) * M)
     G, vl, sl_loss, loss = L.minibatch_grad(L.unflatten(p0, OBS), flat["obs"][sl], flat["actions"][sl],
                                             flat["logp"][sl], flat["values"][sl], flat["returns"][sl],
                                             flat["advantages"][sl], np.float32(1.0), L.Config())
@@ -111,16 +141,16 @@ def test_minibatch_vs_oracle(n, T):
     np_ = ppo.nparam
     g = ppo.grad[:np_].cpu().numpy()
     scale = float(np.abs(g_ref).max())
-    ET.check(f"loopz_grad_{n}x{T}", "grad/max", g / scale, g_ref / scale, 1e-5, 1e-5)
+    ET.check(f"loopz_grad_{n}x{T}{'s' if rows_shuffled else ''}", "grad/max", g / scale, g_ref / scale, 1e-5, 1e-5)
     gc, _ = L.clip_grad(G, OBS, 0.5)
     adam = L.Adam.zeros(np_)
     want = adam.apply(p0, gc, L.Config())
     # Adam's first step is ~lr * sign(g): where |g| is within the gradient tolerance of 0 the step
     # itself is ill-conditioned, so the 1e-6 parameter check covers |g| > 1e-3 max|g| (recorded in full)
     got = ppo.params.cpu().numpy()
-    ET.record(f"loopz_grad_{n}x{T}", "params(all)", got, want)
+    ET.record(f"loopz_grad_{n}x{T}{'s' if rows_shuffled else ''}", "params(all)", got, want)
     well = np.abs(g_ref) > 1e-3 * scale
-    ET.check(f"loopz_grad_{n}x{T}", "params", got[well], want[well], 1e-5, 1e-6)
+    ET.check(f"loopz_grad_{n}x{T}{'s' if rows_shuffled else ''}", "params", got[well], want[well], 1e-5, 1e-6)
     assert np.abs(got - want).max() <= 2.0 * L.Config().lr + 1e-6
     np.testing.assert_allclose(float(ppo.opt[8 + 2].item()), vl, rtol=1e-5)
 

@@ -54,3 +54,21 @@ def test_update_matches_reference(golden):
         np.testing.assert_allclose(adam.v[o:o + n], d[f"adam_v_{i}"].reshape(-1), rtol=1e-3, atol=1e-10, err_msg=k)
     std = L.enforce_minimum_std(pv, OBS)[[o for k, _, o in lay if k == "std"][0]:][:2]
     np.testing.assert_allclose(std, d["std_enforced"], rtol=1e-6)
+
+
+def test_shuffle_update_matches_reference(golden):
+    """mini_batch_sampling='shuffle' (the reference PPO's default, ppo.py:52-53; storage.py:123-134): the same
+    rollout updated over the recorded BatchSampler(SubsetRandomSampler) minibatches."""
+    d = golden("loopz_update_shuffle.npz")
+    pv0 = _params(d, "init")
+    data = {k: d[k] for k in ("obs", "actions", "logp", "values", "returns", "advantages")}
+    data["obs"] = data["obs"][:-1]
+    adam = L.Adam.zeros(len(pv0))
+    assert d["batches"].shape == (16, d["rew"].size // 4)
+    pv, vl, sl = L.train_step(pv0, adam, data, np.float32(1.0), L.Config(), batches=d["batches"])
+    want = _params(d, "after")
+    np.testing.assert_allclose(vl, float(d["loss_value"]), rtol=1e-5)
+    np.testing.assert_allclose(sl, float(d["loss_surrogate"]), rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(pv - pv0, want - pv0, rtol=1e-3, atol=2e-7)
+    # the shuffled minibatches really differ from the in-order ones
+    assert not np.array_equal(np.sort(d["batches"][0]), np.arange(d["batches"].shape[1]))
