@@ -22,12 +22,15 @@
 //      r = 0.5 m obstacles is < 120; checked on the golden fixtures).  An
 //      occupied target cell is seeded exactly as the reference's first Jacobi
 //      sweep does (its neighbours get 1 / 1.414);
-//   3. raw cost to the field buffer + per-env statistics, split by finite and
-//      infinite cost so that the batch constant inf_val (unknown until every
-//      env is done) enters only through one monotone scalar per batch.
+//   3. raw cost, row-major, to the reset slot's scratch (b.sdf).
+// k_field_stats (per slot and 30-row band): the SDF into the env's field tiles
+//   and per-env statistics, split by finite and infinite cost so that the batch
+//   constant inf_val (unknown until every env is done) enters only through one
+//   monotone scalar per batch.
 // k_field_batch (one workgroup): batch max of finite costs -> inf_val, the
 //   repulsion mask of infinite cells, batch J max, any-inside flag.
-// k_field_final (grid-stride over (slot, 2048-cell chunk)): normalisation.
+// k_field_final (grid-stride over (slot, 2048-texel chunk of the tiles)): normalisation, the
+//   SDF texel read and the field texel written in place, the raw cost gathered from the scratch.
 #include "usv_device.h"
 
 USV_PROBE_DEFINE(field)
@@ -132,8 +135,8 @@ __device__ __forceinline__ bool occ_bit(const uint32_t *occ, int r, int cc) {
 // synchronous sweeps of min(self, 8 rolled neighbours + move cost) with the rolled-in edge at
 // +inf, occupied cells forced to +inf after every sweep, the target cell seeded with 0.  Run
 // only for an env whose tile-sweep fixed point is not certified equal to it (see below):
-// ping-pong through the env's field row and the slot's SDF scratch (k_field_stats writes the
-// SDF later), one block barrier per sweep; all waves of the block share the CU's L1, so plain
+// ping-pong through the env's field row (k_field_stats writes the SDF there later) and the
+// slot's scratch, where the result ends as k_field_wave leaves its raw cost, one block barrier per sweep; all waves of the block share the CU's L1, so plain
 // global loads see the other waves' stores after the barrier.
 constexpr int kRefSweeps = (G * 3) / 2;
 __device__ __forceinline__ void cost_sweeps_exact(const uint32_t *occ, int ix, int iy, float *A, float *B) {
@@ -426,15 +429,17 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
         }
     }
     const bool exact = __syncthreads_or((hmax > kPinnedCost) || (it >= kMaxIters)) != 0;
-    // ---- 3. raw cost out (occupied marker -> +inf); statistics in k_field_stats ----
-    float *Fe = b.field + (size_t)e * FS;
+    // ---- 3. raw cost out (occupied marker -> +inf) into the slot's scratch, row-major (one base
+    // address + immediate offsets: tiled offsets here would be 100 live addresses); statistics and
+    // the SDF in k_field_stats, the tiled field in k_field_final ----
+    float *Sc = b.sdf + (size_t)slot * FS;
     if (tile_ok) {
 #pragma unroll
       for (int i = 0; i < T; ++i)
 #pragma unroll
         for (int j = 0; j < T; ++j) {
           const float g = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
-          Fe[field_idx(r0 + i, c0 + j)] = g;
+          Sc[(r0 + i) * G + c0 + j] = g;
         }
       lastc[tp] = -1000;   // ready for the next slot
     }
@@ -494,10 +499,9 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_b
     ix = min(max(ix, 0), G - 1);
     iy = min(max(iy, 0), G - 1);
     __syncthreads();
-    float *Fe = b.field + (size_t)e * FS;
-    float *scratch = b.sdf + (size_t)slot * FS;   // k_field_stats writes the SDF there afterwards
+    float *Fe = b.field + (size_t)e * FS;          // free until k_field_stats writes the SDF there
+    float *scratch = b.sdf + (size_t)slot * FS;   // the raw cost, row-major, as k_field_wave leaves it
     cost_sweeps_exact(occ, ix, iy, Fe, scratch);  // row-major ping-pong, 225 (odd) sweeps: result in scratch
-    for (int q = tid; q < G2; q += kWaveThreads) Fe[field_idx(q / G, q % G)] = scratch[q];   // into the tiles
     if (tid == 0) atomicAdd(&b.ctl[USV_CTL_FIELD_EXACT], 1);
     __syncthreads();
   }
@@ -546,8 +550,8 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
     const int slot = w / kBands, band = w % kBands;
     const int e = b.reset_ids[slot];
-    const float *Fe = b.field + (size_t)e * FS;
-    float *sdf_s = b.sdf + (size_t)slot * FS;
+    const float *Sc = b.sdf + (size_t)slot * FS;   // raw cost, row-major (k_field_wave / k_field_exact)
+    float *Fe = b.field + (size_t)e * FS;           // the SDF goes to the env's tiles, for k_field_final
     if (tid < 2 * USV_NOBST) so[tid] = b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid];
     if (tid < 2) flags[tid] = 0;
     __syncthreads();
@@ -556,7 +560,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
       const int r = band * kBandRows + rg + kRowGroups * k;
-      gv[k] = *reinterpret_cast<const float2 *>(Fe + field_idx(r, c0));   // (c0 even: one tile row)
+      gv[k] = *reinterpret_cast<const float2 *>(Sc + r * G + c0);
     }
     float dxa[USV_NOBST], dxb[USV_NOBST], oy[USV_NOBST];
     {
@@ -609,7 +613,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       const float sva = sqrtf(__uint_as_float(a[0])) - c.obstacle_radius;
       const float svb = sqrtf(__uint_as_float(bb[0])) - c.obstacle_radius;
       if (act) {
-        *reinterpret_cast<float2 *>(sdf_s + field_idx(r, c0)) = make_float2(sva, svb);   // read back by k_field_final
+        *reinterpret_cast<float2 *>(Fe + field_idx(r, c0)) = make_float2(sva, svb);   // (c0 even: one tile row)
         stat(gv[k].x, sva);
         stat(gv[k].y, svb);
       }
@@ -734,25 +738,29 @@ __global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) 
     if (any_inside && has_inside) { jmn = fminf(jmn, high); jmx = fmaxf(jmx, high); }
     const float gden = (gmax - gmin) + 1e-6f;
     const float jden = (jmx - jmn) + 1e-6f;
-    float *Fe = b.field + (size_t)e * FS;
-    const float *sdf_s = b.sdf + (size_t)slot * FS;
+    float *Fe = b.field + (size_t)e * FS;              // tiled: the SDF in, the field out (same texel)
+    const float *Sc = b.sdf + (size_t)slot * FS;       // raw cost, row-major
     const int q1 = min(FS, (ch + 1) * kChunk);
-    // compile-time trip count, clamped loads: the chunk's 2 x 8 loads per thread in flight at once
+    // compile-time trip count, clamped loads: the chunk's 2 x 8 loads per thread in flight at once;
+    // tiled index -> grid cell, the padding cells of the 152 x 152 tile grid skipped (never sampled)
     constexpr int PER = kChunk / 256;
     float gv[PER], sv[PER];
+    bool ok[PER];
+    int qs[PER];
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int qc = min(ch * kChunk + u * 256 + (int)threadIdx.x, q1 - 1);
-      gv[u] = Fe[qc];
-      sv[u] = sdf_s[qc];
+      const int q = ch * kChunk + u * 256 + (int)threadIdx.x;
+      const int tl = q >> 5, wq = q & 31;
+      const int r = (tl / USV_FIELD_TCOLS) * USV_FIELD_TH + (wq >> 3), cc = (tl % USV_FIELD_TCOLS) * USV_FIELD_TW + (wq & 7);
+      ok[u] = q < q1 && r < G && cc < G;
+      qs[u] = q;
+      sv[u] = Fe[ok[u] ? q : 0];
+      gv[u] = Sc[ok[u] ? r * G + cc : 0];
     }
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
-      const int q = ch * kChunk + u * 256 + threadIdx.x;
-      // tiled index -> grid cell: the 152 x 152 padding cells are skipped (never sampled)
-      const int tl = q >> 5, wq = q & 31;
-      const int r = (tl / USV_FIELD_TCOLS) * USV_FIELD_TH + (wq >> 3), cc = (tl % USV_FIELD_TCOLS) * USV_FIELD_TW + (wq & 7);
-      if (q >= q1 || r >= G || cc >= G) continue;
+      const int q = qs[u];
+      if (!ok[u]) continue;
       const float g = gv[u];
       const float cv = isinf(g) ? k.inf_val : g;
       const float dte = sv[u] - c.obstacle_radius;
