@@ -574,6 +574,21 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
         oy[o] = so[2 * o + 1];
       }
     }
+    // Obstacles that can matter to this band: the SDF enters the field only through j_raw (0 unless
+    // dist - 2 r_obs < influence_radius) and the inside test (dist <= 2 r_obs), so an obstacle whose
+    // row distance to the whole band exceeds far_d can only be the minimum of a cell whose SDF is
+    // irrelevant (jr = 0, not inside, with the exact SDF and with the smaller set alike).  Every wave
+    // forms the same mask from the LDS centres (no barrier); a band with no obstacle in reach writes
+    // +inf (jr = 0, not inside: the same statistics and the same final field).
+    uint32_t omask;
+    {
+      const float ylo = slin[band * kBandRows], yhi = slin[band * kBandRows + kBandRows - 1];
+      const float far_d = c.influence_radius + 2.0f * c.obstacle_radius + 0.01f * cell + 1e-3f;
+      const float oyl = so[2 * (lane & (USV_NOBST - 1)) + 1];
+      const float dyb = fmaxf(fmaxf(ylo - oyl, oyl - yhi), 0.f);
+      omask = (uint32_t)(__ballot(lane < USV_NOBST && !(dyb > far_d)) & 0xFFFFull);
+      omask = __builtin_amdgcn_readfirstlane(omask);
+    }
     float gmin = INFINITY, gmax = -INFINITY, jmin_f = INFINITY, jmax_f = -INFINITY, jall_f = 0.f;
     float jrmin_i = INFINITY, jrmax_i = -INFINITY, jrall_i = 0.f;
     int any_inf = 0, inside = 0;
@@ -595,23 +610,30 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       jmin_f = fminf(jmin_f, (!gi && !ins) ? j : INFINITY);
       jmax_f = fmaxf(jmax_f, (!gi && !ins) ? j : -INFINITY);
     };
+    // squared distances (non-negative: u32 min of the bit patterns is the float min, exact in any
+    // order), obstacle-outer so a skipped obstacle is one scalar branch for the band's rows
+    float gy[kBandIters];
+    uint32_t a[kBandIters], bb[kBandIters];
+#pragma unroll
+    for (int k = 0; k < kBandIters; ++k) {
+      gy[k] = slin[band * kBandRows + rg + kRowGroups * k];
+      a[k] = bb[k] = 0x7F800000u;
+    }
+#pragma unroll
+    for (int o = 0; o < USV_NOBST; ++o) {
+      if (!((omask >> o) & 1u)) continue;   // uniform
+#pragma unroll
+      for (int k = 0; k < kBandIters; ++k) {
+        const float dy = gy[k] - oy[o];
+        a[k] = min(a[k], __float_as_uint(fmaf(dy, dy, dxa[o])));
+        bb[k] = min(bb[k], __float_as_uint(fmaf(dy, dy, dxb[o])));
+      }
+    }
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
       const int r = band * kBandRows + rg + kRowGroups * k;
-      const float gy = slin[r];
-      uint32_t a[USV_NOBST], bb[USV_NOBST];
-#pragma unroll
-      for (int o = 0; o < USV_NOBST; ++o) {
-        const float dy = gy - oy[o];
-        a[o] = __float_as_uint(fmaf(dy, dy, dxa[o]));
-        bb[o] = __float_as_uint(fmaf(dy, dy, dxb[o]));
-      }
-#pragma unroll
-      for (int wd = USV_NOBST / 2; wd >= 1; wd >>= 1)
-#pragma unroll
-        for (int o = 0; o < wd; ++o) { a[o] = min(a[o], a[o + wd]); bb[o] = min(bb[o], bb[o + wd]); }
-      const float sva = sqrtf(__uint_as_float(a[0])) - c.obstacle_radius;
-      const float svb = sqrtf(__uint_as_float(bb[0])) - c.obstacle_radius;
+      const float sva = sqrtf(__uint_as_float(a[k])) - c.obstacle_radius;
+      const float svb = sqrtf(__uint_as_float(bb[k])) - c.obstacle_radius;
       if (act) {
         *reinterpret_cast<float2 *>(Fe + field_idx(r, c0)) = make_float2(sva, svb);   // (c0 even: one tile row)
         stat(gv[k].x, sva);
