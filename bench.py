@@ -280,7 +280,7 @@ def main():
     def timed_call(name, *a):
         if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
             env_timer(lambda: orig_call(name, *a))
-        elif timing[0] and name in ("ppo_minibatch_grad", "ppo_minibatch_fused"):
+        elif timing[0] and name in ("ppo_minibatch_grad", "ppo_minibatch_fused", "ppo_minibatch_fused_dp"):
             ppo_timer(lambda: orig_call(name, *a))
         else:
             orig_call(name, *a)
@@ -442,7 +442,11 @@ def main():
                              "flops_per_row_bwd": PPO_BWD_FLOPS_PER_ROW,
                              "launches_timed": len(ppo_timer.pairs),
                              "launch_ms_method": "median HIP event pair around each minibatch's gradient + reduction "
-                                                 + ("launches (ppo_minibatch_fused: k_mb_grad + k_reduce_partials with "
+                                                 + (("launches (ppo_minibatch_fused_dp: k_mb_grad + k_reduce_partials "
+                                                     "with the in-kernel peer gradient exchange and the Adam step; the "
+                                                     "pair includes waiting for the other ranks' chunks)")
+                                                    if agent._fused_update() and world > 1 else
+                                                    "launches (ppo_minibatch_fused: k_mb_grad + k_reduce_partials with "
                                                     "the Adam step)" if agent._fused_update() else
                                                     "launches (ppo_minibatch_grad: k_mb_grad + k_reduce_partials; the "
                                                     "all-reduce and k_apply follow outside the pair)")
