@@ -599,8 +599,15 @@ typedef struct ppo_dp {
 } ppo_dp_t;
 /* bytes of one rank's receive buffer: [2 parities][PPO_DP_MAX senders][slots] floats + arrival flags */
 long long ppo_dp_buffer_bytes(void);
-/* hipMalloc + zero one receive buffer; ipc_handle (64 bytes, hipIpcMemHandle_t) for the other ranks */
+/* allocate (uncached device memory, else hipMalloc) + zero one receive buffer; ipc_handle (64 bytes,
+   hipIpcMemHandle_t) for the other ranks */
 int ppo_dp_alloc(void **dptr, void *ipc_handle);
+/* start-up check of the exchange on every rank at once (each rank launches it after the handles went
+   around): `rounds` exchanges with keys key0.. of payloads naming (sender, round, slot), every received
+   value compared; sets bit 0 of *dp->err when a flag did not arrive within timeout_ms, bit 1 when a
+   payload arrived wrong or stale.  Afterwards the ranks agree, reset *dp->err and set *dp->clock to
+   key0 + rounds - 1 (the flags' last key), or fall back to collectives. */
+int ppo_dp_selftest(const ppo_dp_t *dp, unsigned key0, int rounds, int timeout_ms, void *stream);
 /* map another rank's receive buffer (hipIpcOpenMemHandle, lazy peer access) / unmap / free our own */
 int ppo_dp_open(const void *ipc_handle, void **dptr);
 int ppo_dp_close(void *dptr);

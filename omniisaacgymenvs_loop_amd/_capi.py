@@ -76,6 +76,7 @@ def _declare(lib):
         "ppo_dp_open": [P, P],
         "ppo_dp_close": [P],
         "ppo_dp_free": [P],
+        "ppo_dp_selftest": [P, ctypes.c_uint, I, I, P],
         "ppo_partials_floats": [I],
         "ppo_grad_floats": [],
         "ppo_obs_rms_epoch": [P, P, I, P, P, P],

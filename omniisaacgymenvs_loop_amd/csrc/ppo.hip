@@ -20,6 +20,7 @@
 // backward need), activations never leave LDS, and each workgroup writes one
 // deterministic partial gradient (param layout) that k_reduce_partials sums
 // in a fixed order.  clip + Adam + the adaptive LR run in k_apply.
+#include <cstdlib>
 #include <cstring>
 
 #include "usv_device.h"
@@ -1510,6 +1511,75 @@ __device__ __forceinline__ uint32_t *dp_flag(void *buf, int chunk, int sender) {
          ((size_t)chunk * PPO_DP_MAX + sender) * DP_FLAG_STRIDE;
 }
 
+// One chunk of the exchange (every thread of an RD_TB workgroup calls it; tid < RD_P carry slot
+// `slot` of chunk `chunk`): this rank's value pv to every rank's receive buffer, the arrival flags,
+// the wait for every sender's key, and the senders' values summed in rank order (the same bits on
+// every rank).  A wait beyond timeout_ms, or an error another workgroup already flagged, sets / sees
+// bit 0 of dp.err and goes on with whatever arrived (the host raises after the epoch), so a lost peer
+// costs one timeout per launch, not one per chunk.
+__device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int slot, float pv, int timeout_ms) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int par = (int)(key & 1u);
+  if (tid < RD_P)
+    for (int r = 0; r < dp.world; ++r) st_sys(dp_x(dp.peer[r], par, dp.rank) + slot, pv);
+  __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its stores are acknowledged
+  __syncthreads();
+  if (w == 0) {
+    if (lane < dp.world)   // lane r raises rank r's flag of (this chunk, this sender)
+      __hip_atomic_store(dp_flag(dp.peer[lane], chunk, dp.rank), key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // poll this rank's flags of the chunk: every sender's key >= ours (a sender may be one ahead)
+    const uint64_t t0 = wall_clock64(), lim = (uint64_t)timeout_ms * 100000ull;   // 100 MHz
+    bool got = lane >= dp.world;
+    while (true) {
+      if (!got) {
+        const uint32_t f = __hip_atomic_load(dp_flag(dp.peer[dp.rank], chunk, lane), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+        got = (int32_t)(f - key) >= 0;
+      }
+      if (__all(got)) break;
+      const int32_t e = __hip_atomic_load(dp.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (e != 0) break;                           // already failed: do not wait again
+      if (wall_clock64() - t0 > lim) {             // a lost peer: flag it and go on
+        if (lane == 0) atomicOr(dp.err, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+  float t = 0.f;
+  if (tid < RD_P) {   // senders in rank order: the same sum on every rank
+    const float *xs = dp_x(dp.peer[dp.rank], par, 0);
+    for (int r = 0; r < dp.world; ++r) t += ld_sys(xs + (size_t)r * DP_SLOTS + slot);
+  }
+  return t;
+}
+
+// Start-up check of the exchange (ppo_dp_selftest): `rounds` exchanges with keys key0, key0 + 1, ...
+// (both parities, each receive region written twice) of a payload that names (sender, round, slot);
+// every received value is compared with what its sender wrote.  Bit 0 of dp.err: a flag did not
+// arrive; bit 1: a payload arrived wrong or stale (a receive buffer the reader's caches do not see
+// the peers' writes in).
+__device__ __forceinline__ float dp_probe_value(int sender, int round, int slot) {
+  return (float)(sender * 1000003 + round * 65537 + slot);   // exact in fp32 for the sizes here
+}
+__global__ __launch_bounds__(RD_TB) void k_dp_selftest(ppo_dp_t dp, uint32_t key0, int rounds, int timeout_ms) {
+  const int tid = threadIdx.x;
+  const int slot = blockIdx.x * RD_P + tid;
+  for (int rd = 0; rd < rounds; ++rd) {
+    const uint32_t key = key0 + (uint32_t)rd;
+    (void)dp_exchange(dp, key, blockIdx.x, slot, dp_probe_value(dp.rank, rd, slot & 0xffff), timeout_ms);
+    if (tid < RD_P) {
+      const float *xs = dp_x(dp.peer[dp.rank], (int)(key & 1u), 0);
+      bool bad = false;
+      for (int r = 0; r < dp.world; ++r)
+        bad |= ld_sys(xs + (size_t)r * DP_SLOTS + slot) != dp_probe_value(r, rd, slot & 0xffff);
+      if (bad) atomicOr(dp.err, 2);
+    }
+    __syncthreads();
+  }
+}
+
 template <bool kSpec, bool kDP>
 __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
                                                            float *losses, float inv_b, ppo_cfg_t c, AdamBanks a,
@@ -1563,42 +1633,9 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     for (int g = 0; g < RD_G; ++g) s += reinterpret_cast<const float *>(red[g])[tid];
   }
   float sl = s;   // this rank's value of the slot (the loss means are rank-local)
-  if constexpr (kDP) {
-    const int par = (int)(key & 1u);
-    if (tid < RD_P) {   // the chunk to every rank (gradient sums; the KL slot as this rank's mean)
-      const float pv = slot < S_END ? s : (slot == PPO_NPARAM + 4 ? s * inv_b : 0.f);
-      for (int r = 0; r < dp.world; ++r) st_sys(dp_x(dp.peer[r], par, dp.rank) + slot, pv);
-    }
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its stores are acknowledged
-    __syncthreads();
-    if (w == 0) {
-      if (lane < dp.world)   // lane r raises rank r's flag of (this chunk, this sender)
-        __hip_atomic_store(dp_flag(dp.peer[lane], blockIdx.x, dp.rank), key, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
-      // poll this rank's flags of the chunk: every sender's key >= ours (a sender may be one ahead)
-      const uint64_t t0 = wall_clock64(), lim = (uint64_t)dp.timeout_ms * 100000ull;   // 100 MHz
-      bool got = lane >= dp.world;
-      while (true) {
-        if (!got) {
-          const uint32_t f = __hip_atomic_load(dp_flag(dp.peer[dp.rank], blockIdx.x, lane), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-          got = (int32_t)(f - key) >= 0;
-        }
-        if (__all(got)) break;
-        if (wall_clock64() - t0 > lim) {   // a lost peer: flag it and go on (the host raises after the epoch)
-          if (lane == 0) atomicOr(dp.err, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-      }
-    }
-    __syncthreads();
-    if (tid < RD_P) {   // senders in rank order: the same sum on every rank
-      const float *xs = dp_x(dp.peer[dp.rank], par, 0);
-      float t = 0.f;
-      for (int r = 0; r < dp.world; ++r) t += ld_sys(xs + (size_t)r * DP_SLOTS + slot);
-      s = t / (float)dp.world;   // all_grads / rank_size, av_kls / rank_size
-    }
+  if constexpr (kDP) {   // the chunk to every rank (gradient sums; the KL slot as this rank's mean)
+    const float pv = slot < S_END ? s : (slot == PPO_NPARAM + 4 ? s * inv_b : 0.f);
+    s = dp_exchange(dp, key, blockIdx.x, slot, pv, dp.timeout_ms) / (float)dp.world;   // all_grads / rank_size
   }
   float sq = 0.f;
   if (tid < RD_P) {
@@ -1878,10 +1915,30 @@ int ppo_minibatch_fused_dp(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, 
 
 long long ppo_dp_buffer_bytes(void) { return DP_BYTES; }
 
+int ppo_dp_selftest(const ppo_dp_t *dp, unsigned key0, int rounds, int timeout_ms, void *stream) {
+  if (!dp || dp->world < 1 || dp->world > PPO_DP_MAX || dp->rank < 0 || dp->rank >= dp->world || !dp->err ||
+      rounds < 1 || timeout_ms < 1)
+    return 1;
+  for (int r = 0; r < dp->world; ++r)
+    if (!dp->peer[r]) return 2;
+  hipLaunchKernelGGL(k_dp_selftest, dim3(RED_BLOCKS), dim3(RD_TB), 0, (hipStream_t)stream, *dp, (uint32_t)key0,
+                     rounds, timeout_ms);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
 int ppo_dp_alloc(void **dptr, void *ipc_handle) {
   if (!dptr || !ipc_handle) return 1;
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "ipc handle size");
-  if (hipMalloc(dptr, (size_t)DP_BYTES) != hipSuccess) return 2;
+  // uncached device memory (as RCCL's IPC buffers): the peers' xGMI writes land in HBM, and no L2 of the
+  // reading device can hold a stale copy of a flag or payload line it polled before; plain device memory
+  // (hipMalloc) only if that allocation is refused.  USV_DP_MALLOC=plain forces hipMalloc (A/B).
+  const char *mode = getenv("USV_DP_MALLOC");
+  const bool plain = mode && strcmp(mode, "plain") == 0;
+  if (plain || hipExtMallocWithFlags(dptr, (size_t)DP_BYTES, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    if (hipMalloc(dptr, (size_t)DP_BYTES) != hipSuccess) return 2;
+  }
   if (hipMemset(*dptr, 0, (size_t)DP_BYTES) != hipSuccess || hipDeviceSynchronize() != hipSuccess) return 3;
   hipIpcMemHandle_t h;
   if (hipIpcGetMemHandle(&h, *dptr) != hipSuccess) return 4;

@@ -170,9 +170,22 @@ __device__ __forceinline__ void atomic_max_f32(float *addr, float v) {
   do {                                                                                 \
     if (threadIdx.x == 0 && blockIdx.x < 4096) g_probe_##tu[blockIdx.x][k] = wall_clock64(); \
   } while (0)
+// the same stamp from thread t (another wave's timeline); USV_PHASE_DRAIN first waits for the
+// wave's outstanding memory operations (probe build only: it changes the schedule it measures)
+#define USV_PHASE_T(tu, k, t)                                                          \
+  do {                                                                                 \
+    if (threadIdx.x == (t) && blockIdx.x < 4096) g_probe_##tu[blockIdx.x][k] = wall_clock64(); \
+  } while (0)
+#define USV_PHASE_DRAIN(tu, k, t)                                                      \
+  do {                                                                                 \
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");                               \
+    USV_PHASE_T(tu, k, t);                                                             \
+  } while (0)
 #else
 #define USV_PROBE_DEFINE(tu)
 #define USV_PHASE(tu, k) ((void)0)
+#define USV_PHASE_T(tu, k, t) ((void)0)
+#define USV_PHASE_DRAIN(tu, k, t) ((void)0)
 #endif
 
 #define USV_CHECK_LAUNCH()                                   \

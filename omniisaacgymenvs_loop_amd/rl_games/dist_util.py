@@ -68,7 +68,10 @@ class PeerExchange:
     Raises RuntimeError when a buffer cannot be mapped (no peer access); A2CAgent then agrees with the other
     ranks to fall back to torch.distributed collectives."""
 
-    def __init__(self, rank: int, world_size: int, device, timeout_ms: int = 20000, peers=None):
+    SELFTEST_ROUNDS = 4
+
+    def __init__(self, rank: int, world_size: int, device, timeout_ms: int = 20000, peers=None,
+                 selftest_ms: int = 5000):
         import ctypes
         from .. import _capi
         from .._abi import DEFINES, PpoDp
@@ -108,6 +111,27 @@ class PeerExchange:
             d.peer[r] = p
         d.clock, d.err = self.clock.data_ptr(), self.err.data_ptr()
         self.desc = d
+        if peers is None and world_size > 1:
+            self._selftest(selftest_ms)
+
+    def _selftest(self, timeout_ms: int) -> None:
+        """Every rank runs the same exchange kernel on a known payload (ppo_dp_selftest) right after the handles
+        went around: a flag that never arrives (no peer access over xGMI) or a payload that arrives wrong or stale
+        (a receive buffer whose remote writes the reader does not see) raises here, before any training, so the
+        agent's rank agreement falls back to collectives instead of a run that times out per minibatch."""
+        import ctypes
+        from .. import _capi
+        _capi.call("ppo_dp_selftest", ctypes.byref(self.desc), 1, self.SELFTEST_ROUNDS, int(timeout_ms),
+                   _capi.stream_ptr())
+        torch.cuda.synchronize()
+        bits = int(self.err.item())
+        self.clock.fill_(self.SELFTEST_ROUNDS)     # the flags hold the last test key: real keys continue after it
+        self.err.zero_()
+        torch.cuda.synchronize()
+        if bits:
+            self.close()
+            what = "a flag did not arrive" if bits & 1 else "a payload arrived wrong or stale"
+            raise RuntimeError(f"PeerExchange: start-up exchange test failed ({what}, err bits {bits})")
 
     @property
     def own_ptr(self) -> int:

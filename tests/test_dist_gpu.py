@@ -151,3 +151,23 @@ def test_ranks_draw_different_env_streams(two_ranks):
     assert int(r0["env_seed"]) == 42 and int(r1["env_seed"]) == 43
     assert not np.array_equal(r0["mass"], r1["mass"])              # SysID domain randomisation
     assert not np.array_equal(r0["obs"], r1["obs"])                # spawns, obstacles, noise
+
+
+def test_dp_selftest_passes_alone_and_fails_fast_without_the_peer():
+    """ppo_dp_selftest, the start-up check PeerExchange runs before training: one rank exchanging with
+    itself passes and leaves the minibatch clock at the last test key; with a second "rank" that never
+    runs, the first wait times out (bit 0), every later wait sees the error and returns at once, and the
+    constructor's path raises -- so the agents fall back to collectives instead of stalling per chunk."""
+    import time
+    from omniisaacgymenvs_loop_amd.rl_games.dist_util import PeerExchange
+    ok = PeerExchange(0, 1, "cuda:0", peers=[0])
+    ok._selftest(2000)
+    assert int(ok.clock.item()) == PeerExchange.SELFTEST_ROUNDS and int(ok.err.item()) == 0
+    ok.close()
+    lost = PeerExchange(0, 1, "cuda:0", peers=[0])       # a receive buffer nobody writes into
+    ex = PeerExchange(0, 2, "cuda:0", peers=[0, lost.own_ptr])
+    t0 = time.time()
+    with pytest.raises(RuntimeError, match="flag did not arrive"):
+        ex._selftest(300)
+    assert time.time() - t0 < 5.0
+    lost.close()
