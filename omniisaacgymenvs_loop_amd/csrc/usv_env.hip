@@ -611,8 +611,27 @@ __device__ __forceinline__ void top5_of_16(uint64_t k[16]) {
   cx64(k[1], k[2]); cx64(k[3], k[4]);
 }
 
+// The config and the host-derived constants travel as ONE first kernel argument, so the kernel can re-read
+// them from the kernel-argument segment (scalar loads through a laundered pointer) at the start of a section:
+// values loaded at the top stay live in scalar registers across the whole kernel otherwise, and the ~50 of
+// them that do not fit were spilled to VGPR lanes (371 v_readlane + the s_nop hazards they bring)
+struct StepCfg {
+  usv_cfg_t c;
+  StepK K;
+};
+typedef __attribute__((address_space(4))) const StepCfg KStepCfg;
+__device__ __forceinline__ StepCfg step_cfg_reload() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  KStepCfg *p = (KStepCfg *)__builtin_amdgcn_kernarg_segment_ptr();
+  __asm__ volatile("" : "+s"(p));   // a new pointer value: nothing loaded before this point is reused
+  return *p;
+#else
+  return StepCfg{};   // (host pass: never called)
+#endif
+}
+
 template <bool kStats, bool kInj, bool kDist, class Win>
-__global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, Win w, StepK K,
+__global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, Win w,
                                                      const char *__restrict__ wbase, const float *__restrict__ actions,
                                                      const float *__restrict__ lut, float bias, uint64_t seed,
                                                      uint64_t step, const float *__restrict__ inj, int part) {
@@ -620,6 +639,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
   __shared__ float2 sob[USV_NOBST][kBlock];
   __shared__ float slut[2 * USV_LUT_N];
   __shared__ uint8_t keep[kBlock];
+  const usv_cfg_t &c = ck.c;
+  const StepK &K = ck.K;
   const int n = b.n;
   const int tid = threadIdx.x;
   const int e = blockIdx.x * kBlock + tid;
@@ -816,6 +837,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     bst(R, w.px, vs, px); bst(R, w.py, vs, py); bst(R, w.yaw, vs, yaw);
     bst(R, w.vx, vs, vx); bst(R, w.vy, vs, vy); bst(R, w.wz, vs, wz);
     bst(R, w.fl, vs, fl); bst(R, w.fr, vs, fr);
+    // the rest of the step reads its config afresh (see StepCfg)
+    const StepCfg ck2 = step_cfg_reload();
+    const usv_cfg_t &c = ck2.c;
+    const StepK &K = ck2.K;
     // ---- post_physics_step: progress, update_state noise (USV_Virtual.py:771-813) ----
     const int progress = progress0 + 1;
     bsti(R, w.progress, vs, progress);
@@ -893,6 +918,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
     bst(R, w.prev_cmd + w.n4, vs, prev_cmd1);
     // ---- privileged tail (USV_Virtual.py:840-976) ----
     write_priv_tail(c, K, m, comx, comy, comz, k_drag, thr_l, thr_r, k_iz, put);
+    {   // the reward / kill / statistics section reads its config afresh too (see StepCfg)
+    const StepCfg ck3 = step_cfg_reload();
+    const usv_cfg_t &c = ck3.c;
+    const StepK &K = ck3.K;
     // ---- compute_reward (static_obs.py:335-657): the potential-independent terms first ----
     constexpr float kGv = (0.15f - 0.02f) + 1e-6f, kGd = 0.01f + 1e-6f;
     constexpr float kSf = (0.60f - 0.15f) + 1e-6f, kSp = 0.8f + 1e-6f, kAn = 0.2f;
@@ -983,6 +1012,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(usv_cfg_t c, usv_bufs_t b, 
       for (int q = 0; q < 25; ++q)
         if (sum_on[q]) bst(R, w.stats + (uint32_t)kSum[q] * w.n4, vs, sums[q] + add[q]);
     }
+    }
   }
   // ---- coalesced obs store: rows of 33 floats staged through LDS ----
   __syncthreads();
@@ -1038,12 +1068,14 @@ __device__ __forceinline__ float task_term(int mode, float x, float coeff) {
 }
 
 template <int kKind, bool kStats, bool kInj>
-__global__ __launch_bounds__(kBlock) void k_env_step_task(usv_cfg_t c, usv_bufs_t b, StepK K,
+__global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t b,
                                                           const float *__restrict__ actions,
                                                           const float *__restrict__ lut, float bias, uint64_t seed,
                                                           uint64_t step, const float *__restrict__ inj) {
   __shared__ float sobs[kBlock * USV_NOBS];
   __shared__ float sred[kBlock / 64];
+  const usv_cfg_t &c = ck.c;
+  const StepK &K = ck.K;
   const int n = b.n;
   const int tid = threadIdx.x;
   const int e = blockIdx.x * kBlock + tid;
@@ -1171,6 +1203,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(usv_cfg_t c, usv_bufs_
     b.px[e] = px; b.py[e] = py; b.yaw[e] = yaw; b.vx[e] = vx; b.vy[e] = vy; b.wz[e] = wz;
     b.fl[e] = fl; b.fr[e] = fr;
   }
+  {   // the rest of the step reads its config afresh (see StepCfg)
+  const StepCfg ck2 = step_cfg_reload();
+  const usv_cfg_t &c = ck2.c;
+  const StepK &K = ck2.K;
   // ---- post_physics_step: progress, update_state noise (USV_Virtual.py:771-813) ----
   const int progress = progress0 + 1;
   float pxn = px, pyn = py;
@@ -1204,6 +1240,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(usv_cfg_t c, usv_bufs_
   put(pa, prev_cmd0);
   put(pa + 1, prev_cmd1);
   write_priv_tail(c, K, m, comx, comy, comz, k_drag, thr_l, thr_r, k_iz, put);
+  {
+  const StepCfg ck3 = step_cfg_reload();
+  const usv_cfg_t &c = ck3.c;
+  const StepK &K = ck3.K;
   // ---- Penalties.compute_penalty (USV_task_rewards.py:440-523) ----
   const float pact0 = c.pen_use_u ? unit0 : cmd0, pact1 = c.pen_use_u ? unit1 : cmd1;
   float p_lin = 0.f, p_ang = 0.f, p_angv = 0.f, p_en = 0.f;
@@ -1334,6 +1374,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(usv_cfg_t c, usv_bufs_
     nan_report(&b.ctl[USV_CTL_NAN_FLAG], (mine ? bits : 0u) | (obad ? USV_NAN_OBS : 0u));
   }
   if (blockIdx.x == 0 && tid == 0) b.ctl[USV_CTL_STEPPED] = 1;
+  }
+  }
 }
 
 // TrackXYOVelocity, phase 2: angular velocity distance over all envs, then the
@@ -1649,13 +1691,13 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
     if (cfg->task_kind == USV_TASK_GO_TO_POSE) {
       auto kern = st ? (ij ? k_env_step_task<USV_TASK_GO_TO_POSE, true, true> : k_env_step_task<USV_TASK_GO_TO_POSE, true, false>)
                      : (ij ? k_env_step_task<USV_TASK_GO_TO_POSE, false, true> : k_env_step_task<USV_TASK_GO_TO_POSE, false, false>);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, k, actions, lut_dev, action_bias, seed, step,
-                         u_inject);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, StepCfg{*cfg, k}, *b, actions, lut_dev, action_bias, seed,
+                         step, u_inject);
     } else if (cfg->task_kind == USV_TASK_TRACK_XYO) {
       auto kern = st ? (ij ? k_env_step_task<USV_TASK_TRACK_XYO, true, true> : k_env_step_task<USV_TASK_TRACK_XYO, true, false>)
                      : (ij ? k_env_step_task<USV_TASK_TRACK_XYO, false, true> : k_env_step_task<USV_TASK_TRACK_XYO, false, false>);
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, k, actions, lut_dev, action_bias, seed, step,
-                         u_inject);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, StepCfg{*cfg, k}, *b, actions, lut_dev, action_bias, seed,
+                         step, u_inject);
       USV_CHECK_LAUNCH();
       hipLaunchKernelGGL(st ? k_track_finish<true> : k_track_finish<false>, dim3(grid), dim3(kBlock), 0, s, *cfg, *b,
                          grid);
@@ -1680,8 +1722,9 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
     const char *base = reinterpret_cast<const char *>(b->px);
 #define USV_FIXED_CASE(S)                                                                                            \
   case S:                                                                                                            \
-    hipLaunchKernelGGL((k_env_step<true, false, false, FixedWin<S>>), dim3(grid), dim3(kBlock), 0, s, *cfg, *b,      \
-                       FixedWin<S>{}, k, base, actions, lut_dev, action_bias, seed, step, u_inject, part);           \
+    hipLaunchKernelGGL((k_env_step<true, false, false, FixedWin<S>>), dim3(grid), dim3(kBlock), 0, s,                \
+                       StepCfg{*cfg, k}, *b, FixedWin<S>{}, base, actions, lut_dev, action_bias, seed, step, u_inject,  \
+                       part);                                                                                        \
     break;
     switch (sh) {
       USV_FIXED_CASE(13) USV_FIXED_CASE(14) USV_FIXED_CASE(15) USV_FIXED_CASE(16) USV_FIXED_CASE(17)
@@ -1696,8 +1739,8 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
                                     : (u_inject ? k_env_step<false, true, true, StepWin> : k_env_step<false, false, true, StepWin>))
                    : (cfg->stats_on ? (u_inject ? k_env_step<true, true, false, StepWin> : k_env_step<true, false, false, StepWin>)
                                     : (u_inject ? k_env_step<false, true, false, StepWin> : k_env_step<false, false, false, StepWin>));
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, w, k, wbase, actions, lut_dev, action_bias, seed,
-                     step, u_inject, part);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, StepCfg{*cfg, k}, *b, w, wbase, actions, lut_dev, action_bias,
+                     seed, step, u_inject, part);
   USV_CHECK_LAUNCH();
   return 0;
 }
