@@ -365,12 +365,20 @@ def main():
 
     # per-launch kernel times inside real epochs (eager: graph replays carry no per-kernel events),
     # HIP events on the launch stream around each C-ABI call
+    # (the plain sequential step: an overlapped step kernel shares the GPU with the field kernels, so its
+    # event pair would time the sharing, not the kernel)
     use_graph = agent.use_graph
     agent.use_graph = False
+    overlap_env = os.environ.get("USV_STEP_OVERLAP")
+    os.environ["USV_STEP_OVERLAP"] = "0"
     timing[0] = True
     agent.train_epoch()
     torch.cuda.synchronize()
     timing[0] = False
+    if overlap_env is None:
+        os.environ.pop("USV_STEP_OVERLAP")
+    else:
+        os.environ["USV_STEP_OVERLAP"] = overlap_env
     agent.use_graph = use_graph
 
     # env + inference only (play_steps) and env only (VecEnv.step with fixed actions), same size

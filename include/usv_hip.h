@@ -280,7 +280,11 @@ typedef struct usv_bufs {
    * it and the step / bias arguments of usv_reset / usv_env_step are ignored, so
    * a captured HIP graph replays consecutive steps. */
   uint64_t *clock;
+  /* usv_env_step_part(.., 3) -> usv_env_step_late: the potential-independent reward terms and the sample
+     position of the envs reset this step ([USV_RSTASH_ROWS][n]); NULL unless the overlapped step is used */
+  float *rstash;
 } usv_bufs_t;
+#define USV_RSTASH_ROWS 14
 
 /* one replay scene (scripts/build_usv_scenes.py:566-577 keys; obstacles padded to
  * 16 with limbo (999, 999) past obstacles_count as CaptureXYTask.apply_scene does,
@@ -391,6 +395,18 @@ int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions
 int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions,
                       const float *lut_dev, float action_bias, uint64_t seed, uint64_t step,
                       const float *u_inject, int part, void *stream);
+
+/* The overlapped step (the reset envs' fields build on a second stream while every env steps): part 3 of
+ * usv_env_step_part runs the whole step for every env except the potential-dependent reward of the envs
+ * reset this step (their fields do not exist yet), which it stashes in b->rstash; after the fields,
+ * usv_env_step_late finishes it (field sample, reward_tail, reward, prev_pot, the reward episode sums).
+ * The observations, dones and state of part 3 are final, so the next policy step can run beside the field
+ * kernels.  Stream order: usv_reset -> usv_field_stage(1) -> {part 3 || usv_field_stage(2)} -> late.
+ * Together they produce exactly part 0's results (usv_potential_field + usv_env_step). */
+int usv_env_step_late(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream);
+/* usv_potential_field in two stages: 1 = the reset envs' obstacle placement (k_field_place: the step
+ * kernels read the new obstacles), 2 = the cost-to-go sweeps, SDF statistics, batch fold and the fields */
+int usv_field_stage(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, void *stream);
 
 /* Planar force/moment model only (no integration), for parity with
  * HydrodynamicsObject.ComputeHydrodynamicsEffects (Hydrodynamics.py:207-245)

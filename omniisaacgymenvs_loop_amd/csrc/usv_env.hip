@@ -611,6 +611,13 @@ __device__ __forceinline__ void top5_of_16(uint64_t k[16]) {
   cx64(k[1], k[2]); cx64(k[3], k[4]);
 }
 
+// the episode sums whose step value comes out of reward_tail (the potential-dependent part of the reward)
+__device__ __forceinline__ constexpr bool stat_of_reward(int key) {
+  return key == ST_TOTAL_REWARD || key == ST_DISTANCE_REWARD || key == ST_ALIGNMENT_REWARD ||
+         key == ST_POTENTIAL_SHAPING_REWARD || key == ST_TURN_HAZARD_PENALTY || key == ST_DANGER_MEAN ||
+         key == ST_DANGER_HI_RATE || key == ST_G_GATE_MEAN;
+}
+
 // The config and the host-derived constants travel as ONE first kernel argument, so the kernel can re-read
 // them from the kernel-argument segment (scalar loads through a laundered pointer) at the start of a section:
 // values loaded at the top stay live in scalar registers across the whole kernel otherwise, and the ~50 of
@@ -772,6 +779,9 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     i1 = min(max(i1, 0), USV_LUT_N - 1);
     bool mine = e < n;
     if (part == 1 || part == 2) mine = mine && ((part == 1) ? !was_reset : was_reset);
+    // part 3: every env, but the envs reset this step leave their potential-dependent reward to
+    // usv_env_step_late (their fields are still being built): stash + no rew / prev_pot / reward sums
+    const bool defer = part == 3 && was_reset;
     keep[tid] = mine ? 1 : 0;
     const uint32_t vs = mine ? v4 : kDrop;
     reinterpret_cast<float4 *>(slut)[tid] = lut_a;
@@ -978,8 +988,15 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     rp.pen_sum = ((p_lin + p_ang) + p_angv) + p_en;
     // ---- the potential-dependent tail ----
     const RewardOut ro = reward_tail(c, rp, field_blend(taps), pot_none || was_reset, prev_pot_mem);
-    bst(R, w.prev_pot, vs, ro.pot);
-    bst(R, w.rew, vs, ro.rew);
+    const uint32_t vr = defer ? kDrop : vs;   // the potential-dependent outputs
+    bst(R, w.prev_pot, vr, ro.pot);
+    bst(R, w.rew, vr, ro.rew);
+    if (defer && mine) {
+      const float st[USV_RSTASH_ROWS] = {rp.dist_r0, rp.align0, rp.g, rp.ggate, rp.turning, rp.sf, rp.goal_r, rp.coll,
+                                         rp.speed_r, rp.ang_r, rp.hi_r, rp.pen_sum, pxn, pyn};
+#pragma unroll
+      for (int q = 0; q < USV_RSTASH_ROWS; ++q) b.rstash[(size_t)q * n + e] = st[q];
+    }
     // ---- update_kills / is_done (static_obs.py:661-706, USV_Virtual.py:1223-1237) ----
     const bool dkill = dist > c.kill_dist;
     const bool ckill = min_od < c.collision_threshold;
@@ -999,7 +1016,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
       uint32_t bits = ((nonfinite(cmd0) | nonfinite(cmd1)) ? USV_NAN_ACTIONS : 0u) |
                       ((nonfinite(pxn) | nonfinite(pyn) | nonfinite(yawn) | nonfinite(vxn) | nonfinite(vyn) |
                         nonfinite(wzn)) ? USV_NAN_STATE : 0u) |
-                      (nonfinite(ro.rew) ? USV_NAN_REWARD : 0u);
+                      ((!defer && nonfinite(ro.rew)) ? USV_NAN_REWARD : 0u);
       nan_report(&b.ctl[USV_CTL_NAN_FLAG], mine ? bits : 0u);
     }
     if (kStats) {
@@ -1010,7 +1027,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
                              ((float)(unit0 < 0.05f) + (float)(unit1 < 0.05f)) / 2.0f, unit0 + unit1};
 #pragma unroll
       for (int q = 0; q < 25; ++q)
-        if (sum_on[q]) bst(R, w.stats + (uint32_t)kSum[q] * w.n4, vs, sums[q] + add[q]);
+        if (sum_on[q]) bst(R, w.stats + (uint32_t)kSum[q] * w.n4, stat_of_reward(kSum[q]) ? vr : vs, sums[q] + add[q]);
     }
     }
   }
@@ -1021,7 +1038,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
   const uint32_t obase = (uint32_t)row0 * (uint32_t)(USV_NOBS * 4);
   // obs entries are clamped to +-clip_obs, so only a NaN is non-finite: x != x
   uint32_t obad = 0u;
-  if (part == 0) {
+  if (part == 0 || part == 3) {
     const int nv = rows * USV_NOBS / 4;       // whole float4s (row0 * 33 * 4 B is 16-B aligned)
     for (int i = tid; i < nv; i += kBlock) {
       const float4 v = reinterpret_cast<const float4 *>(sobs)[i];
@@ -1045,6 +1062,39 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
   // promoted to the POT/PEN/REW_VALID flags by the next usv_reset, so the flags never change
   // while a step kernel that reads them runs ----
   if (blockIdx.x == 0 && tid == 0) b.ctl[USV_CTL_STEPPED] = 1;
+}
+
+
+// usv_env_step_late: the potential-dependent reward of the envs reset this step, once their fields
+// exist (after usv_env_step_part(.., 3) and the field kernels): the stashed potential-independent terms,
+// the field sample at the stashed position, reward_tail with prev_potential None (a reset env), the
+// reward, prev_pot and the reward sums -- the operations part 0 runs for these envs, in the same order.
+__global__ __launch_bounds__(256) void k_env_reward_late(usv_cfg_t c, usv_bufs_t b) {
+  const int n = b.n;
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);
+  for (int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x); slot < count; slot += (int)(gridDim.x * blockDim.x)) {
+    const int e = b.reset_ids[slot];
+    float st[USV_RSTASH_ROWS];
+#pragma unroll
+    for (int q = 0; q < USV_RSTASH_ROWS; ++q) st[q] = b.rstash[(size_t)q * n + e];
+    const RewardPre rp{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11]};
+    const FieldTaps taps = field_taps(b.field + (size_t)e * USV_FIELD_STRIDE, c.map_size, st[12], st[13]);
+    const RewardOut ro = reward_tail(c, rp, field_blend(taps), true, 0.f);
+    b.prev_pot[e] = ro.pot;
+    b.rew[e] = ro.rew;
+    if (c.stats_on) {
+      const float add[8] = {ro.total, ro.dist_r, ro.align_r, ro.shaping, ro.turn_haz, ro.danger,
+                            (float)(ro.danger > 0.5f), ro.gate_pos};
+      constexpr int key[8] = {ST_TOTAL_REWARD, ST_DISTANCE_REWARD, ST_ALIGNMENT_REWARD, ST_POTENTIAL_SHAPING_REWARD,
+                              ST_TURN_HAZARD_PENALTY, ST_DANGER_MEAN, ST_DANGER_HI_RATE, ST_G_GATE_MEAN};
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float *p = b.stats + (size_t)key[q] * n + e;
+        *p = *p + add[q];
+      }
+    }
+    if (c.nan_probe && nonfinite(ro.rew)) atomicOr(&b.ctl[USV_CTL_NAN_FLAG], (int)USV_NAN_REWARD);
+  }
 }
 
 // ------------------------------------------------------------------------
@@ -1677,7 +1727,8 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t
 int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions, const float *lut_dev,
                       float action_bias, uint64_t seed, uint64_t step, const float *u_inject, int part,
                       void *stream) {
-  if (!cfg || !b || !actions || !lut_dev || b->n <= 0 || part < 0 || part > 2) return 1;
+  if (!cfg || !b || !actions || !lut_dev || b->n <= 0 || part < 0 || part > 3) return 1;
+  if (part == 3 && (cfg->task_kind != USV_TASK_CAPTURE_XY || !b->rstash)) return 1;
   if (cfg->priv_dim != 4 && cfg->priv_dim != 8) return 3;
   if (cfg->task_kind != USV_TASK_CAPTURE_XY) {
     // GoToPose / TrackXYOVelocity: no potential field, so no split step
@@ -1741,6 +1792,14 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
                                     : (u_inject ? k_env_step<false, true, false, StepWin> : k_env_step<false, false, false, StepWin>));
   hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, s, StepCfg{*cfg, k}, *b, w, wbase, actions, lut_dev, action_bias,
                      seed, step, u_inject, part);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int usv_env_step_late(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream) {
+  if (!cfg || !b || b->n <= 0 || !b->rstash || !b->field || cfg->task_kind != USV_TASK_CAPTURE_XY) return 1;
+  const int grid = (b->n + 255) / 256 < 512 ? (b->n + 255) / 256 : 512;
+  hipLaunchKernelGGL(k_env_reward_late, dim3(grid), dim3(256), 0, (hipStream_t)stream, *cfg, *b);
   USV_CHECK_LAUNCH();
   return 0;
 }

@@ -47,6 +47,20 @@ class VecEnvRLGames:
         obs_dict = {"obs": {"state": obs}, "states": t.states_buf}
         return obs_dict, rew, dones, t.extras
 
+    def step_async(self, actions: torch.Tensor):
+        """step() whose rewards are final only after join(): the reset envs' potential fields build on a side
+        stream while the caller issues its next policy step (obs and dones are final on return)."""
+        t = self._task
+        a = actions if actions.device == torch.device(t.device) else actions.to(t.device)
+        obs, rew, dones = t.env_step(a, overlap=True)
+        self.sim_frame_count += t.control_frequency_inv
+        return {"obs": {"state": obs}, "states": t.states_buf}, rew, dones, t.extras
+
+    def join(self) -> None:
+        join = getattr(self._task, "join_step", None)
+        if join is not None:
+            join()
+
     def reset(self):
         """Resets the task and applies zero actions to recompute observations (:219-230)."""
         self._task.reset()

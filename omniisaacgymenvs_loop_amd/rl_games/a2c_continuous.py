@@ -319,6 +319,8 @@ class A2CAgent:
 
     def play_steps(self) -> Dict[str, Any]:
         """A2CBase.play_steps (a2c_common.py:670-774): H x (policy kernel, env kernels, reward kernel)."""
+        if os.getenv("USV_STEP_OVERLAP", "1") != "0" and hasattr(self.vec_env, "step_async"):
+            return self._play_steps_overlapped()
         c = _capi
         cfg = c.byref(self.cfg)
         s = c.stream_ptr()
@@ -339,6 +341,42 @@ class A2CAgent:
                    c.ptr(self.step_dev), s)
             self.algo_observer.process_infos(infos, None)
             self._step_counter += 1
+        return {"played_frames": self.batch_size, "step_time": step_time}
+
+    def _play_steps_overlapped(self) -> Dict[str, Any]:
+        """play_steps with each step's reset-env fields built beside the next policy step: policy(n+1) needs
+        only step n's observations and dones, which the overlapped env step (VecEnvRLGames.step_async) makes
+        final on this stream while the reset envs' potential fields and deferred rewards finish on a side
+        stream; store_reward(n) waits for them (vec_env.join()).  Every kernel sees the inputs it sees in
+        the sequential loop, so the experience buffers, meters and env state are the same bits."""
+        c = _capi
+        cfg = c.byref(self.cfg)
+        s = c.stream_ptr()
+        self.meter.zero_()
+        step_time = 0.0
+        base = self._step_counter
+
+        def policy(n):
+            obs = self._obs_in(self.obs["obs"]["state"] if isinstance(self.obs["obs"], dict) else self.obs["obs"])
+            c.call("ppo_policy_step", cfg, c.ptr(self.model_params), c.ptr(self.obs_rms), c.ptr(self.val_rms),
+                   c.ptr(obs), n, c.ptr(self.exp_obs), c.ptr(self.exp_act), c.ptr(self.exp_nlp),
+                   c.ptr(self.exp_val), c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.exp_done),
+                   c.ptr(self.dones), c.ptr(self.actions), self.seed + 7919 * self.rank, base + n,
+                   c.ptr(self.step_dev), None, s)
+
+        policy(0)
+        for n in range(self.horizon_length):
+            t0 = time.time()
+            self.obs, rewards, self.dones, infos = self.vec_env.step_async(self.actions)
+            step_time += time.time() - t0
+            if n + 1 < self.horizon_length:
+                policy(n + 1)
+            self.vec_env.join()
+            c.call("ppo_store_reward", cfg, c.ptr(rewards), c.ptr(self.dones), n, c.ptr(self.exp_rew),
+                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter_buf),
+                   c.ptr(self.step_dev), s)
+            self.algo_observer.process_infos(infos, None)
+        self._step_counter = base + self.horizon_length
         return {"played_frames": self.batch_size, "step_time": step_time}
 
     def prepare_dataset(self) -> None:

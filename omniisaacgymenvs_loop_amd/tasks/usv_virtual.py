@@ -155,6 +155,11 @@ class USVVirtual:
         self.clock = Z(4, device=dev, dtype=torch.int64)
         self.states_buf = Z((n, 0), **f32)
         self.sdf = torch.empty((n if self._has_field else 1, FIELD_STRIDE), **f32)   # per-reset-slot SDF scratch
+        # the overlapped step (env_step(.., overlap=True)): the reset envs' deferred reward terms, a side
+        # stream for the field kernels and the fork / join events
+        self.rstash = Z((DEFINES["USV_RSTASH_ROWS"], n), **f32) if self._has_field else None
+        self._side = None
+        self._step_pending = False
         self.lut = Z((2, 1000), **f32)
         self.hydro = build_hydro_cfg(self._task_cfg)
         tl, tr = thruster_tables(self._task_cfg)
@@ -234,6 +239,7 @@ class USVVirtual:
         b.slot_stats = p(self.slot_stats)
         b.sdf = p(self.sdf)
         b.clock = p(self.clock)
+        b.rstash = p(self.rstash) if self.rstash is not None else None
         b.grid_lin = p(self.grid_lin) if self.grid_lin is not None else None
         b.dist = p(self.dist) if self.dist is not None else None
         b.env_org = p(self.env_org)
@@ -321,7 +327,8 @@ class USVVirtual:
         return 0.0
 
     def env_step(self, actions: torch.Tensor, u_step: Optional[torch.Tensor] = None,
-                 u_reset: Optional[torch.Tensor] = None, post_state: Optional[torch.Tensor] = None):
+                 u_reset: Optional[torch.Tensor] = None, post_state: Optional[torch.Tensor] = None,
+                 overlap: bool = False):
         """pre_physics_step + 10 substeps + post_physics_step (USV_Virtual.py:1042-1652).
 
         Returns the device tensors (obs [n,33], rew [n], dones int64 [n]).  u_step / u_reset replay
@@ -332,8 +339,11 @@ class USVVirtual:
         actions = self._f32(actions)
         s = _capi.stream_ptr()
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
+        self.join_step()
         bias, k = self._advance()
         _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
+        if overlap and self._has_field and post_state is None:
+            return self._step_overlapped(actions, bias, k, u_step)
         if self._has_field:   # CaptureXY only (GoToPose / TrackXYOVelocity have no obstacles)
             _capi.call("usv_potential_field", cfg, b, s)
         substeps = self.cfg.substeps
@@ -346,6 +356,37 @@ class USVVirtual:
         finally:
             self.cfg.substeps = substeps
         return self.obs_view, self.rew_buf, self.dones
+
+    def _step_overlapped(self, actions, bias, k, u_step):
+        """The rest of env_step with the reset envs' fields built on a side stream (usv_hip.h, the overlapped
+        step): obstacle placement, then the step of every env (part 3) on this stream beside the sweeps /
+        statistics / field kernels on the side stream, then the deferred reward of the reset envs there.
+        The returned obs and dones are final on this stream; the rewards are final after join_step(), which
+        the next env_step (or the caller, before reading rewards) issues.  Same results as the plain step."""
+        cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
+        main = torch.cuda.current_stream(self._device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self._device)
+            self._ev_fork, self._ev_early, self._ev_join = (torch.cuda.Event() for _ in range(3))
+        side = self._side
+        _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
+        self._ev_fork.record(main)
+        side.wait_event(self._ev_fork)
+        _capi.call("usv_field_stage", cfg, b, 2, side.cuda_stream)
+        _capi.call("usv_env_step_part", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
+                   self.seed, k, _capi.ptr(u_step), 3, main.cuda_stream)
+        self._ev_early.record(main)
+        side.wait_event(self._ev_early)
+        _capi.call("usv_env_step_late", cfg, b, side.cuda_stream)
+        self._ev_join.record(side)
+        self._step_pending = True
+        return self.obs_view, self.rew_buf, self.dones
+
+    def join_step(self) -> None:
+        """Make the current stream wait for an overlapped step's side stream (rewards, fields final)."""
+        if self._step_pending:
+            torch.cuda.current_stream(self._device).wait_event(self._ev_join)
+            self._step_pending = False
 
     def _f32(self, actions: torch.Tensor) -> torch.Tensor:
         if actions.dtype != torch.float32 or not actions.is_contiguous():
