@@ -243,7 +243,9 @@ typedef struct usv_bufs {
   /* task */
   float *tgt_x, *tgt_y;
   float *obst;                     /* [16][2][n]  obstacle centres, local frame */
-  float *field;                    /* [n][USV_FIELD_STRIDE] potential field (tiled, see USV_FIELD_STRIDE) */
+  float *field;                    /* [n][USV_FIELD_STRIDE] raw cost-to-go of the potential field's grid (tiled, see
+                                      USV_FIELD_STRIDE; +inf unreachable): a field texel = field_value(SDF from the
+                                      env's obstacles, this cost, .fnorm) -- the field is never materialised */
   /* history */
   float *prev_cmd;                 /* [2][n] raw policy command (obs 23:25) */
   float *prev_dist, *prev_head, *prev_pot, *prev_wz;
@@ -263,7 +265,8 @@ typedef struct usv_bufs {
   float   *extras_acc;             /* [ceil(n/256)][USV_NSTAT] reset-kernel per-workgroup sums (scratch) */
   float   *field_old_tgt;          /* [2][n] target used by the field of each reset env */
   float   *slot_stats;             /* [n][USV_FIELD_SLOT_STATS] per-reset-slot field statistics (scratch) */
-  float   *sdf;                    /* [n][USV_FIELD_STRIDE] per-reset-slot signed distance (scratch, tiled) */
+  float   *sdf;                    /* [n][USV_FIELD_STRIDE] raw cost-to-go of each env's field as the sweeps leave it,
+                                      row-major [150][150] (+inf unreachable): k_field_stats tiles it into .field */
   const float *grid_lin;           /* [150] cell centres of the field grid */
   float   *dist;                   /* [USV_NDIST][n] disturbance parameters; NULL when no disturbance is on */
   const float *env_org;            /* [2][n] world x, y of each env's origin (RLTask._env_pos); NULL = 0 */
@@ -283,7 +286,12 @@ typedef struct usv_bufs {
   /* usv_env_step_part(.., 3) -> usv_env_step_late: the potential-independent reward terms and the sample
      position of the envs reset this step ([USV_RSTASH_ROWS][n]); NULL unless the overlapped step is used */
   float *rstash;
+  /* [n][USV_FNORM] per-env normalisation constants of the potential field (usv_potential_field writes them
+     for the reset envs): cost min, cost range + 1e-6, J min, J range + 1e-6, the batch's inf_val, the
+     batch's inside value `high`, the batch's any-inside flag, 0, then RN(1 / cost range), RN(1 / J range) */
+  float *fnorm;
 } usv_bufs_t;
+#define USV_FNORM 12
 #define USV_RSTASH_ROWS 14
 
 /* one replay scene (scripts/build_usv_scenes.py:566-577 keys; obstacles padded to
@@ -347,6 +355,10 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed,
  * compute_potential_field, tasks/USV/d_multi_gemini.py:66-271 (called from
  * USV_capture_xy_static_obs.py:1054-1057). */
 int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream);
+/* The potential fields of envs env_ids[0..count) materialised row-major into out [count][150][150] (what
+ * BatchedMapGPU returns per env; the step kernels sample the field from its parts, never from this). */
+int usv_field_view(const usv_cfg_t *cfg, const usv_bufs_t *b, const int32_t *env_ids, int count, float *out,
+                   void *stream);
 
 /* One control step for all envs: action mapping, thruster LUT + lag,
  * 10 substeps of 3-DoF hydrodynamics + semi-implicit Euler, state readback

@@ -53,6 +53,7 @@ def _declare(lib):
         "usv_reset": [P, P, U64, U64, P, P],
         "usv_potential_field": [P, P, P],
         "usv_field_stage": [P, P, I, P],
+        "usv_field_view": [P, P, P, I, P, P],
         "usv_env_step_late": [P, P, P],
         "usv_env_step": [P, P, P, P, F, U64, U64, P, P],
         "usv_env_step_part": [P, P, P, P, F, U64, U64, P, I, P],

@@ -47,6 +47,7 @@ __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fm
 __device__ __forceinline__ float maxf(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float minf(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float clampt(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
 // torch.norm(v, dim=-1) of a 2-vector == sqrt(fma(y, y, x*x)) (PyTorch CPU reduction)
 __device__ __forceinline__ float tnorm2(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
 // x / b given y = RN(1/b): Markstein's correction (q = x*y, r = x - b*q exactly by fma,
@@ -57,6 +58,77 @@ __device__ __forceinline__ float div_rn(float x, float b, float y) {
   const float q = x * y;
   const float r = fmaf(-q, b, x);
   return fmaf(r, y, q);
+}
+
+// cell centre i of the potential field's grid (BatchedMapGPU's torch.linspace of the cell centres,
+// d_multi_gemini.py:40-48), or the override table (parity tests)
+__device__ __forceinline__ float grid_coord_k(float start, float end, float step, int i) {
+  return (i < USV_GRID / 2) ? start + step * (float)i : end - step * (float)(USV_GRID - i - 1);
+}
+__device__ __forceinline__ float grid_coord(const float *lin, float map_size, int i) {
+  if (lin) return lin[i];
+  const double cell_d = (double)map_size / USV_GRID;
+  const float start = (float)(-(double)map_size / 2 + cell_d / 2);
+  const float end = (float)((double)map_size / 2 - cell_d / 2);
+  const float step = (end - start) / (float)(USV_GRID - 1);
+  return grid_coord_k(start, end, step, i);
+}
+// compute_occupancy_and_sdf (d_multi_gemini.py:66-104) for one cell, ob(o) -> the centre of obstacle o: min
+// over the 16 obstacles of the squared distance (dx*dx rounded, then fma with dy), sqrt, minus the radius --
+// k_field_stats' separable SDF forms the same operations per cell, so the bits are the same.  Squared
+// distances are >= 0: float order == u32 order (balanced min tree).
+template <class Ob>
+__device__ __forceinline__ float cell_sdf(Ob ob, float gx, float gy, float radius) {
+  uint32_t a[USV_NOBST];
+#pragma unroll
+  for (int o = 0; o < USV_NOBST; ++o) {
+    const float2 p = ob(o);
+    const float dx = gx - p.x, dy = gy - p.y;
+    a[o] = __float_as_uint(fmaf(dy, dy, dx * dx));
+  }
+#pragma unroll
+  for (int w = USV_NOBST / 2; w >= 1; w >>= 1)
+#pragma unroll
+    for (int o = 0; o < w; ++o) a[o] = min(a[o], a[o + w]);
+  return sqrtf(__uint_as_float(a[0])) - radius;   // sqrt(min) == min(sqrt), bit-exact
+}
+
+// ---- the potential field's texel value (BatchedMapGPU.compute_potential_field, d_multi_gemini.py:195-271) ----
+// The field is kept as its parts: the raw cost-to-go (usv_bufs_t.field, tiled) and the env's normalisation
+// constants (usv_bufs_t.fnorm); the SDF of a texel is recomputed from the env's 16 obstacle centres
+// (cell_sdf).  Every reader (the step kernels' bilinear sample, usv_field_view) forms a texel with
+// field_value: the operations of the reference's per-env normalisation in its order, so the same bits as
+// the materialised field.
+// eta (1/d - 1/r0)^2 before the goal mask, 0 outside the influence radius
+__device__ __forceinline__ float j_raw(const usv_cfg_t &c, float dte, float inv_r) {
+  if (!(dte < c.influence_radius)) return 0.f;
+  const float d = maxf(dte, 1e-3f);
+  const float t = 1.0f / d - inv_r;
+  return c.eta * (t * t);
+}
+__device__ __forceinline__ float goal_mask(const usv_cfg_t &c, float cv, float cell) {
+  return clampt((cv * cell) / c.safe_radius, 0.f, 1.f);
+}
+struct FieldNorm {
+  float gmin, gden, jmn, jden, inf_val, high, any_inside, inv_gden, inv_jden;
+};
+__device__ __forceinline__ FieldNorm field_norm_of(float4 a, float4 b, float4 r) {
+  return FieldNorm{a.x, a.y, a.z, a.w, b.x, b.y, b.z, r.x, r.y};
+}
+// one texel: sv = SDF, g = raw cost (+inf unreachable); cell = map / G, inv_r = 1 / influence radius,
+// inv_safe = RN(1 / safe_radius).  The divisions by a per-env or config constant are div_rn with the
+// divisor's correctly rounded reciprocal (the IEEE quotient for quotients in [2^-90, 2^120]; 0 stays 0)
+__device__ __forceinline__ float field_value(const usv_cfg_t &c, const FieldNorm &k, float sv, float g, float cell,
+                                             float inv_r, float inv_safe) {
+  const float cv = isinf(g) ? k.inf_val : g;
+  const float dte = sv - c.obstacle_radius;
+  const float jr = j_raw(c, dte, inv_r);
+  const float gm = clampt(div_rn(cv * cell, c.safe_radius, inv_safe), 0.f, 1.f);   // goal_mask
+  const float j = (dte < c.influence_radius) ? jr * gm : 0.f;
+  const float jv = (k.any_inside != 0.f && dte <= 0.f) ? k.high : j;
+  const float gn = div_rn(cv - k.gmin, k.gden, k.inv_gden);
+  const float jn = div_rn(jv - k.jmn, k.jden, k.inv_jden);
+  return gn + c.field_alpha * jn;
 }
 
 // ---------------------------------------------------------------------------

@@ -404,9 +404,15 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
 // field_blend combines them where the reward needs the potential.
 // ------------------------------------------------------------------------
 struct FieldTaps {
-  float v_nw, v_ne, v_sw, v_se, nw, ne, sw, se;
+  float g_nw, g_ne, g_sw, g_se;    // raw costs of the 4 texels (the env's tiles)
+  float4 fn0, fn1, fn2;            // the env's normalisation constants (usv_bufs_t.fnorm)
+  float nw, ne, sw, se;
+  int i0, i1c, j0, j1c;
+  bool i_out, j_out;
 };
-__device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, float map_size, float x, float y) {
+// F: the env's cost tiles, FN: its USV_FNORM constants
+__device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, const float *__restrict__ FN,
+                                                float map_size, float x, float y) {
   constexpr int G = USV_GRID;
   const float gx = 2.0f * x / map_size, gy = 2.0f * y / map_size;
   const float half = (float)G / 2.0f;
@@ -423,16 +429,39 @@ __device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, flo
   // border clamp: i1/j1 == G only when the weight of that tap is 0 (ix, iy <= G-1);
   // the tap then reads the last column/row (any finite value) and is replaced by 0
   const int i1c = min(i1, G - 1), j1c = min(j1, G - 1);
-  t.v_nw = F[field_idx(j0, i0)];
-  t.v_ne = F[field_idx(j0, i1c)];
-  t.v_sw = F[field_idx(j1c, i0)];
-  t.v_se = F[field_idx(j1c, i1c)];
-  if (i1 >= G) { t.v_ne = 0.f; t.v_se = 0.f; }
-  if (j1 >= G) { t.v_sw = 0.f; t.v_se = 0.f; }
+  t.g_nw = F[field_idx(j0, i0)];
+  t.g_ne = F[field_idx(j0, i1c)];
+  t.g_sw = F[field_idx(j1c, i0)];
+  t.g_se = F[field_idx(j1c, i1c)];
+  t.fn0 = reinterpret_cast<const float4 *>(FN)[0];
+  t.fn1 = reinterpret_cast<const float4 *>(FN)[1];
+  t.fn2 = reinterpret_cast<const float4 *>(FN)[2];
+  t.i0 = i0; t.i1c = i1c; t.j0 = j0; t.j1c = j1c;
+  t.i_out = i1 >= G;
+  t.j_out = j1 >= G;
   return t;
 }
-__device__ __forceinline__ float field_blend(const FieldTaps &t) {
-  return fmaf(t.v_se, t.se, fmaf(t.v_sw, t.sw, fmaf(t.v_ne, t.ne, t.v_nw * t.nw)));
+// the field's grid coordinates from the host-derived (start, end, step) or the override table
+struct GridK {
+  float start, end, step;
+  const float *lin;
+  __device__ __forceinline__ float operator()(int i) const { return lin ? lin[i] : grid_coord_k(start, end, step, i); }
+};
+// the texels from their parts (the SDF from the env's obstacles ob(o), field_value: the reference's
+// normalisation), then the bilinear blend
+template <class Ob>
+__device__ __forceinline__ float field_blend(const usv_cfg_t &c, const FieldTaps &t, Ob ob, const GridK &gk, float cell,
+                                             float inv_r, float inv_safe) {
+  const FieldNorm k = field_norm_of(t.fn0, t.fn1, t.fn2);
+  const float x0 = gk(t.i0), x1 = gk(t.i1c), y0 = gk(t.j0), y1 = gk(t.j1c);
+  const float r = c.obstacle_radius;
+  const float v_nw = field_value(c, k, cell_sdf(ob, x0, y0, r), t.g_nw, cell, inv_r, inv_safe);
+  float v_ne = field_value(c, k, cell_sdf(ob, x1, y0, r), t.g_ne, cell, inv_r, inv_safe);
+  float v_sw = field_value(c, k, cell_sdf(ob, x0, y1, r), t.g_sw, cell, inv_r, inv_safe);
+  float v_se = field_value(c, k, cell_sdf(ob, x1, y1, r), t.g_se, cell, inv_r, inv_safe);
+  if (t.i_out) { v_ne = 0.f; v_se = 0.f; }
+  if (t.j_out) { v_sw = 0.f; v_se = 0.f; }
+  return fmaf(v_se, t.se, fmaf(v_sw, t.sw, fmaf(v_ne, t.ne, v_nw * t.nw)));
 }
 
 __device__ __forceinline__ float pen_scalar(int kind, float k, float x0, float cc, float x) {
@@ -532,6 +561,8 @@ struct StepK {
   float enc_lo[3], enc_r[3], inv_enc_r[3];   // kdrag, thr, kiz: minmax range / centered scale
   int enc_ok[3];
   float inv_exp_coeff;
+  float cell, inv_r, inv_safe;    // the potential field's cell size, 1 / influence radius, RN(1 / safe_radius)
+  float gstart, gend, gstep;      // its grid coordinates (grid_coord's float values)
 };
 
 // privileged observation tail (USV_Virtual.py:840-976): raw / centered / minmax encoders
@@ -860,7 +891,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
       pyn = pyn + (u[SU_PX + 1] * K.pos_rng + c.pos_noise_min);
     }
     // the potential sample only needs the position: issue its 4 texel loads now
-    const FieldTaps taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, c.map_size, pxn, pyn);
+    const FieldTaps taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, b.fnorm + (size_t)ec * USV_FNORM,
+                                      c.map_size, pxn, pyn);
     float vxn = vx, vyn = vy, wzn = wz;
     if (c.vel_noise_on) {
       vxn = vxn + (u[SU_VX] * K.vel_rng + c.vel_noise_min);
@@ -987,7 +1019,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     bst(R, w.prev_wz, vs, wzn);
     rp.pen_sum = ((p_lin + p_ang) + p_angv) + p_en;
     // ---- the potential-dependent tail ----
-    const RewardOut ro = reward_tail(c, rp, field_blend(taps), pot_none || was_reset, prev_pot_mem);
+    const RewardOut ro = reward_tail(c, rp, field_blend(c, taps, [&](int o) { return sob[o][tid]; }, GridK{K.gstart, K.gend, K.gstep, b.grid_lin},
+                                                 K.cell, K.inv_r, K.inv_safe), pot_none || was_reset, prev_pot_mem);
     const uint32_t vr = defer ? kDrop : vs;   // the potential-dependent outputs
     bst(R, w.prev_pot, vr, ro.pot);
     bst(R, w.rew, vr, ro.rew);
@@ -1071,6 +1104,12 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
 // reward, prev_pot and the reward sums -- the operations part 0 runs for these envs, in the same order.
 __global__ __launch_bounds__(256) void k_env_reward_late(usv_cfg_t c, usv_bufs_t b) {
   const int n = b.n;
+  const float cell = (float)((double)c.map_size / USV_GRID);
+  const float inv_r = (float)(1.0 / (double)c.influence_radius);
+  const float inv_safe = 1.0f / c.safe_radius;
+  const double cell_d = (double)c.map_size / USV_GRID;
+  const float g_start = (float)(-(double)c.map_size / 2 + cell_d / 2), g_end = (float)((double)c.map_size / 2 - cell_d / 2);
+  const GridK gk{g_start, g_end, (g_end - g_start) / (float)(USV_GRID - 1), b.grid_lin};
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);
   for (int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x); slot < count; slot += (int)(gridDim.x * blockDim.x)) {
     const int e = b.reset_ids[slot];
@@ -1078,8 +1117,14 @@ __global__ __launch_bounds__(256) void k_env_reward_late(usv_cfg_t c, usv_bufs_t
 #pragma unroll
     for (int q = 0; q < USV_RSTASH_ROWS; ++q) st[q] = b.rstash[(size_t)q * n + e];
     const RewardPre rp{st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9], st[10], st[11]};
-    const FieldTaps taps = field_taps(b.field + (size_t)e * USV_FIELD_STRIDE, c.map_size, st[12], st[13]);
-    const RewardOut ro = reward_tail(c, rp, field_blend(taps), true, 0.f);
+    const FieldTaps taps = field_taps(b.field + (size_t)e * USV_FIELD_STRIDE, b.fnorm + (size_t)e * USV_FNORM,
+                                      c.map_size, st[12], st[13]);
+    float2 obs_c[USV_NOBST];
+#pragma unroll
+    for (int o = 0; o < USV_NOBST; ++o)
+      obs_c[o] = make_float2(b.obst[(size_t)(2 * o) * n + e], b.obst[(size_t)(2 * o + 1) * n + e]);
+    const RewardOut ro = reward_tail(c, rp, field_blend(c, taps, [&](int o) { return obs_c[o]; }, gk, cell, inv_r, inv_safe),
+                                     true, 0.f);
     b.prev_pot[e] = ro.pot;
     b.rew[e] = ro.rew;
     if (c.stats_on) {
@@ -1648,6 +1693,15 @@ float enc_minmax_h(float x, float xmin, float xmax) {
 
 StepK step_constants(const usv_cfg_t &c) {
   StepK k{};
+  k.cell = (float)((double)c.map_size / USV_GRID);
+  k.inv_r = (float)(1.0 / (double)c.influence_radius);
+  k.inv_safe = 1.0f / c.safe_radius;
+  {
+    const double cell_d = (double)c.map_size / USV_GRID;
+    k.gstart = (float)(-(double)c.map_size / 2 + cell_d / 2);
+    k.gend = (float)((double)c.map_size / 2 - cell_d / 2);
+    k.gstep = (k.gend - k.gstart) / (float)(USV_GRID - 1);
+  }
   k.act_rng = (float)((double)c.act_noise_max - (double)c.act_noise_min);
   k.pos_rng = (float)((double)c.pos_noise_max - (double)c.pos_noise_min);
   k.vel_rng = (float)((double)c.vel_noise_max - (double)c.vel_noise_min);
@@ -1729,6 +1783,8 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
                       void *stream) {
   if (!cfg || !b || !actions || !lut_dev || b->n <= 0 || part < 0 || part > 3) return 1;
   if (part == 3 && (cfg->task_kind != USV_TASK_CAPTURE_XY || !b->rstash)) return 1;
+  // CaptureXY samples the potential field from its parts (SDF tiles, cost rows, constants)
+  if (cfg->task_kind == USV_TASK_CAPTURE_XY && (!b->field || !b->sdf || !b->fnorm)) return 7;
   if (cfg->priv_dim != 4 && cfg->priv_dim != 8) return 3;
   if (cfg->task_kind != USV_TASK_CAPTURE_XY) {
     // GoToPose / TrackXYOVelocity: no potential field, so no split step
@@ -1797,7 +1853,9 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
 }
 
 int usv_env_step_late(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream) {
-  if (!cfg || !b || b->n <= 0 || !b->rstash || !b->field || cfg->task_kind != USV_TASK_CAPTURE_XY) return 1;
+  if (!cfg || !b || b->n <= 0 || !b->rstash || !b->field || !b->sdf || !b->fnorm ||
+      cfg->task_kind != USV_TASK_CAPTURE_XY)
+    return 1;
   const int grid = (b->n + 255) / 256 < 512 ? (b->n + 255) / 256 : 512;
   hipLaunchKernelGGL(k_env_reward_late, dim3(grid), dim3(256), 0, (hipStream_t)stream, *cfg, *b);
   USV_CHECK_LAUNCH();

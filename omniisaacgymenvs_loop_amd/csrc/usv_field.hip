@@ -22,15 +22,15 @@
 //      r = 0.5 m obstacles is < 120; checked on the golden fixtures).  An
 //      occupied target cell is seeded exactly as the reference's first Jacobi
 //      sweep does (its neighbours get 1 / 1.414);
-//   3. raw cost, row-major, to the reset slot's scratch (b.sdf).
+//   3. raw cost, row-major, to the env's cost row (b.sdf).
 // k_field_stats (per slot and 30-row band): the SDF into the env's field tiles
 //   and per-env statistics, split by finite and infinite cost so that the batch
 //   constant inf_val (unknown until every env is done) enters only through one
 //   monotone scalar per batch.
 // k_field_batch (one workgroup): batch max of finite costs -> inf_val, the
 //   repulsion mask of infinite cells, batch J max, any-inside flag.
-// k_field_final (grid-stride over (slot, 2048-texel chunk of the tiles)): normalisation, the
-//   SDF texel read and the field texel written in place, the raw cost gathered from the scratch.
+// k_field_norm (one thread per slot): the env's normalisation constants (b.fnorm); the field itself is
+//   never materialised -- readers form texels from the SDF, the cost and the constants (field_value).
 #include "usv_device.h"
 
 USV_PROBE_DEFINE(field)
@@ -44,8 +44,6 @@ constexpr int T = 10;            // tile edge
 constexpr int NT = G / T;        // 15 tiles per edge
 constexpr int kWaveThreads = 256;
 constexpr int kMaxIters = 4096;  // safety cap (never reached)
-constexpr int kChunk = 2048;     // cells per k_field_final work item
-constexpr int kChunks = (FS + kChunk - 1) / kChunk;   // k_field_final: chunks of the tiled index space
 constexpr int kSlotStride = USV_FIELD_SLOT_STATS;   // floats per reset slot: 16 final + 12 per chunk + obstacles
 constexpr int kSlotObst = 160;                      // the slot's 16 obstacle centres (x, y interleaved)
 static_assert(kSlotObst + 2 * USV_NOBST <= kSlotStride, "slot_stats layout");
@@ -59,60 +57,12 @@ enum {
   SS_INSIDE, SS_ITERS, SS_EXACT
 };
 
-__device__ __forceinline__ float grid_coord(const float *lin, float map_size, int i) {
-  if (lin) return lin[i];
-  const double cell_d = (double)map_size / G;
-  const float start = (float)(-(double)map_size / 2 + cell_d / 2);
-  const float end = (float)((double)map_size / 2 - cell_d / 2);
-  const float step = (end - start) / (float)(G - 1);
-  return (i < G / 2) ? start + step * (float)i : end - step * (float)(G - i - 1);
-}
-
-__device__ __forceinline__ float min_dist(const float *so, float gx, float gy) {
-  float m2 = INFINITY;
-#pragma unroll
-  for (int o = 0; o < USV_NOBST; ++o) {
-    const float dx = gx - so[2 * o], dy = gy - so[2 * o + 1];
-    m2 = fminf(m2, fmaf(dy, dy, dx * dx));
-  }
-  return sqrtf(m2);   // sqrt is monotone: sqrt(min) == min(sqrt), bit-exact
-}
-
-// compute_occupancy_and_sdf (d_multi_gemini.py:66-104) for one cell: min over the 16
-// obstacles of the squared distance (dx*dx rounded, then fma with dy), sqrt, minus the
-// radius -- the separable SDF's operations per cell, so the bits are the same.
-// Squared distances are >= 0: float order == u32 order (balanced min tree).
-__device__ __forceinline__ float cell_sdf(const float *so, float gx, float gy, float radius) {
-  uint32_t a[USV_NOBST];
-#pragma unroll
-  for (int o = 0; o < USV_NOBST; ++o) {
-    const float dx = gx - so[2 * o], dy = gy - so[2 * o + 1];
-    a[o] = __float_as_uint(fmaf(dy, dy, dx * dx));
-  }
-#pragma unroll
-  for (int w = USV_NOBST / 2; w >= 1; w >>= 1)
-#pragma unroll
-    for (int o = 0; o < w; ++o) a[o] = min(a[o], a[o + w]);
-  return sqrtf(__uint_as_float(a[0])) - radius;   // sqrt(min) == min(sqrt), bit-exact
-}
-
 // +inf for an occupied cell, 0 for a free one (costs are >= 0: max(m, wall) keeps
 // free cells and pins occupied ones), from the tile's free bit mask without a
 // per-cell lane mask
 __device__ __forceinline__ float wall(const uint32_t *freem, int bit) {
   const uint32_t f = (freem[bit >> 5] >> (bit & 31)) & 1u;
   return __uint_as_float((f - 1u) & 0x7f800000u);
-}
-
-// eta (1/d - 1/r0)^2 before the goal mask, 0 outside the influence radius
-__device__ __forceinline__ float j_raw(const usv_cfg_t &c, float dte, float inv_r) {
-  if (!(dte < c.influence_radius)) return 0.f;
-  const float d = maxf(dte, 1e-3f);
-  const float t = 1.0f / d - inv_r;
-  return c.eta * (t * t);
-}
-__device__ __forceinline__ float goal_mask(const usv_cfg_t &c, float cv, float cell) {
-  return clampt((cv * cell) / c.safe_radius, 0.f, 1.f);
 }
 
 // ---------------------------------------------------------------- pass B ---
@@ -429,10 +379,10 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
         }
     }
     const bool exact = __syncthreads_or((hmax > kPinnedCost) || (it >= kMaxIters)) != 0;
-    // ---- 3. raw cost out (occupied marker -> +inf) into the slot's scratch, row-major (one base
+    // ---- 3. raw cost out (occupied marker -> +inf) into the env's cost row, row-major (one base
     // address + immediate offsets: tiled offsets here would be 100 live addresses); statistics and
-    // the SDF in k_field_stats, the tiled field in k_field_final ----
-    float *Sc = b.sdf + (size_t)slot * FS;
+    // the SDF in k_field_stats, the normalisation constants in k_field_norm ----
+    float *Sc = b.sdf + (size_t)e * FS;
     if (tile_ok) {
 #pragma unroll
       for (int i = 0; i < T; ++i)
@@ -499,8 +449,8 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_b
     ix = min(max(ix, 0), G - 1);
     iy = min(max(iy, 0), G - 1);
     __syncthreads();
-    float *Fe = b.field + (size_t)e * FS;          // free until k_field_stats writes the SDF there
-    float *scratch = b.sdf + (size_t)slot * FS;   // the raw cost, row-major, as k_field_wave leaves it
+    float *Fe = b.field + (size_t)e * FS;          // free until k_field_stats writes the cost tiles there
+    float *scratch = b.sdf + (size_t)e * FS;      // the raw cost, row-major, as k_field_wave leaves it
     cost_sweeps_exact(occ, ix, iy, Fe, scratch);  // row-major ping-pong, 225 (odd) sweeps: result in scratch
     if (tid == 0) atomicAdd(&b.ctl[USV_CTL_FIELD_EXACT], 1);
     __syncthreads();
@@ -550,8 +500,8 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
     const int slot = w / kBands, band = w % kBands;
     const int e = b.reset_ids[slot];
-    const float *Sc = b.sdf + (size_t)slot * FS;   // raw cost, row-major (k_field_wave / k_field_exact)
-    float *Fe = b.field + (size_t)e * FS;           // the SDF goes to the env's tiles, for k_field_final
+    const float *Sc = b.sdf + (size_t)e * FS;      // raw cost, row-major (k_field_wave / k_field_exact)
+    float *Fe = b.field + (size_t)e * FS;           // the cost into the env's tiles
     if (tid < 2 * USV_NOBST) so[tid] = b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid];
     if (tid < 2) flags[tid] = 0;
     __syncthreads();
@@ -635,7 +585,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       const float sva = sqrtf(__uint_as_float(a[k])) - c.obstacle_radius;
       const float svb = sqrtf(__uint_as_float(bb[k])) - c.obstacle_radius;
       if (act) {
-        *reinterpret_cast<float2 *>(Fe + field_idx(r, c0)) = make_float2(sva, svb);   // (c0 even: one tile row)
+        *reinterpret_cast<float2 *>(Fe + field_idx(r, c0)) = gv[k];   // (c0 even: one tile row)
         stat(gv[k].x, sva);
         stat(gv[k].y, svb);
       }
@@ -735,17 +685,18 @@ __global__ __launch_bounds__(256) void k_field_batch(usv_cfg_t c, usv_bufs_t b) 
 }
 
 // ---------------------------------------------------------------- pass D ---
-__global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) {
+// The per-env normalisation (d_multi_gemini.py:211-223, 262-271) as constants: the env's cost range
+// with inf_val for unreachable cells, its J range with the batch's `high` for inside cells, and the batch
+// values a texel needs (inf_val, high, any-inside) -> usv_bufs_t.fnorm.  The field is never materialised:
+// its readers form texels with field_value (usv_device.h) from the SDF, the cost and these constants
+// (the reference materialises 150 x 150 floats per reset env that the env step samples at 4 texels).
+__global__ __launch_bounds__(256) void k_field_norm(usv_cfg_t c, usv_bufs_t b) {
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
   const BatchK k = batch_k(c, b);
-  const float cell = (float)((double)c.map_size / G);
-  const float inv_r = (float)(1.0 / (double)c.influence_radius);
   const bool any_inside = b.ctl[USV_CTL_ANY_INSIDE] != 0;
   const float cur_max = b.fscratch[1];
   const float high = (cur_max > 1e-6f) ? cur_max * 10.0f : 100.0f;
-  const int items = count * kChunks;
-  for (int w = blockIdx.x; w < items; w += gridDim.x) {
-    const int slot = w / kChunks, ch = w % kChunks;
+  for (int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x); slot < count; slot += (int)(gridDim.x * blockDim.x)) {
     const int e = b.reset_ids[slot];
     const float *st = b.slot_stats + (size_t)slot * kSlotStride;
     const bool has_inf = st[SS_ANY_INF] != 0.f;
@@ -758,41 +709,31 @@ __global__ __launch_bounds__(256) void k_field_final(usv_cfg_t c, usv_bufs_t b) 
       jmx = fmaxf(jmx, st[SS_JRMAX_I_NI] * k.mask_inf);
     }
     if (any_inside && has_inside) { jmn = fminf(jmn, high); jmx = fmaxf(jmx, high); }
-    const float gden = (gmax - gmin) + 1e-6f;
-    const float jden = (jmx - jmn) + 1e-6f;
-    float *Fe = b.field + (size_t)e * FS;              // tiled: the SDF in, the field out (same texel)
-    const float *Sc = b.sdf + (size_t)slot * FS;       // raw cost, row-major
-    const int q1 = min(FS, (ch + 1) * kChunk);
-    // compile-time trip count, clamped loads: the chunk's 2 x 8 loads per thread in flight at once;
-    // tiled index -> grid cell, the padding cells of the 152 x 152 tile grid skipped (never sampled)
-    constexpr int PER = kChunk / 256;
-    float gv[PER], sv[PER];
-    bool ok[PER];
-    int qs[PER];
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int q = ch * kChunk + u * 256 + (int)threadIdx.x;
-      const int tl = q >> 5, wq = q & 31;
-      const int r = (tl / USV_FIELD_TCOLS) * USV_FIELD_TH + (wq >> 3), cc = (tl % USV_FIELD_TCOLS) * USV_FIELD_TW + (wq & 7);
-      ok[u] = q < q1 && r < G && cc < G;
-      qs[u] = q;
-      sv[u] = Fe[ok[u] ? q : 0];
-      gv[u] = Sc[ok[u] ? r * G + cc : 0];
-    }
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int q = qs[u];
-      if (!ok[u]) continue;
-      const float g = gv[u];
-      const float cv = isinf(g) ? k.inf_val : g;
-      const float dte = sv[u] - c.obstacle_radius;
-      const float jr = j_raw(c, dte, inv_r);
-      const float j = (dte < c.influence_radius) ? jr * goal_mask(c, cv, cell) : 0.f;
-      const float jv = (any_inside && dte <= 0.f) ? high : j;
-      const float gn = (cv - gmin) / gden;
-      const float jn = (jv - jmn) / jden;
-      Fe[q] = gn + c.field_alpha * jn;
-    }
+    float4 *fn = reinterpret_cast<float4 *>(b.fnorm + (size_t)e * USV_FNORM);
+    const float gden = (gmax - gmin) + 1e-6f, jden = (jmx - jmn) + 1e-6f;
+    fn[0] = make_float4(gmin, gden, jmn, jden);
+    fn[1] = make_float4(k.inf_val, high, any_inside ? 1.f : 0.f, 0.f);
+    fn[2] = make_float4(1.0f / gden, 1.0f / jden, 0.f, 0.f);   // field_value's div_rn reciprocals
+  }
+}
+
+// usv_field_view: the materialised fields of `count` envs, row-major [count][G][G] (tests, host views)
+__global__ __launch_bounds__(256) void k_field_view(usv_cfg_t c, usv_bufs_t b, const int32_t *ids, int count,
+                                                    float *out) {
+  const float cell = (float)((double)c.map_size / G);
+  const float inv_r = (float)(1.0 / (double)c.influence_radius);
+  const float inv_safe = 1.0f / c.safe_radius;
+  const long long total = (long long)count * G2;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long long)gridDim.x * blockDim.x) {
+    const int i = (int)(q / G2), cell_i = (int)(q % G2), r = cell_i / G, cc = cell_i % G;
+    const int e = ids[i];
+    const float4 *fn = reinterpret_cast<const float4 *>(b.fnorm + (size_t)e * USV_FNORM);
+    const FieldNorm k = field_norm_of(fn[0], fn[1], fn[2]);
+    const float *ob = b.obst + e;   // [16][2][n]
+    const float sv = cell_sdf([&](int o) { return make_float2(ob[(size_t)(2 * o) * b.n], ob[(size_t)(2 * o + 1) * b.n]); },
+                              grid_coord(b.grid_lin, c.map_size, cc), grid_coord(b.grid_lin, c.map_size, r),
+                              c.obstacle_radius);
+    out[q] = field_value(c, k, sv, b.field[(size_t)e * FS + field_idx(r, cc)], cell, inv_r, inv_safe);
   }
 }
 
@@ -803,7 +744,7 @@ namespace {
 // fallback, statistics, batch fold, final field); 0: usv_potential_field
 int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream_t s) {
   const int grid_b = b->n < 512 ? b->n : 512;
-  const int grid_d = b->n * kChunks < 4096 ? b->n * kChunks : 4096;
+  const int grid_n = (b->n + 255) / 256 < 64 ? (b->n + 255) / 256 : 64;
   const int grid_p = (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) < 1024 ? (b->n + kPlaceTB / 64 - 1) / (kPlaceTB / 64) : 1024;
   if (stage == 1) {
     hipLaunchKernelGGL(k_field_place, dim3(grid_p), dim3(kPlaceTB), 0, s, *cfg, *b);
@@ -819,23 +760,34 @@ int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_batch, dim3(kBatchBlocks), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_final, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
+  hipLaunchKernelGGL(k_field_norm, dim3(grid_n), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   return 0;
 }
 }  // namespace
 
 extern "C" int usv_field_stage(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, void *stream) {
-  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field || !b->sdf || stage < 1 || stage > 2) return 1;
+  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field || !b->sdf || !b->fnorm || stage < 1 || stage > 2) return 1;
   return field_stages(cfg, b, stage, (hipStream_t)stream);
 }
 
+extern "C" int usv_field_view(const usv_cfg_t *cfg, const usv_bufs_t *b, const int32_t *env_ids, int count,
+                              float *out, void *stream) {
+  if (!cfg || !b || b->n <= 0 || !b->field || !b->sdf || !b->fnorm || !env_ids || !out || count < 0) return 1;
+  if (count == 0) return 0;
+  const long long total = (long long)count * G2;
+  const int grid = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
+  hipLaunchKernelGGL(k_field_view, dim3(grid), dim3(256), 0, (hipStream_t)stream, *cfg, *b, env_ids, count, out);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream) {
-  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field || !b->sdf) return 1;
+  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field || !b->sdf || !b->fnorm) return 1;
   hipStream_t s = (hipStream_t)stream;
   // the reset count lives on the device: launch persistent grids, blocks loop over slots
   const int grid_b = b->n < 512 ? b->n : 512;
-  const int grid_d = b->n * kChunks < 4096 ? b->n * kChunks : 4096;
+  const int grid_n = (b->n + 255) / 256 < 64 ? (b->n + 255) / 256 : 64;
   // two reset envs per CU only when the batch fills the chip more than once (a few hundred
   // resets per step); USV_FIELD_PACK=0/1 forces either layout (A/B runs, tests)
   const char *pack_env = getenv("USV_FIELD_PACK");
@@ -857,7 +809,7 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_batch, dim3(kBatchBlocks), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_final, dim3(grid_d), dim3(256), 0, s, *cfg, *b);
+  hipLaunchKernelGGL(k_field_norm, dim3(grid_n), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   return 0;
 }

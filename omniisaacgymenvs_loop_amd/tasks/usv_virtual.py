@@ -30,12 +30,6 @@ GRID2 = DEFINES["USV_GRID"] ** 2
 FIELD_STRIDE = DEFINES["USV_FIELD_STRIDE"]
 
 
-def field_tile_index() -> np.ndarray:
-    """Row-major cell q = r * 150 + c -> its index in an env's tiled field row (include/usv_hip.h
-    USV_FIELD_STRIDE: 4 x 8-texel tiles, one cache line each)."""
-    G, th, tw, tc = DEFINES["USV_GRID"], DEFINES["USV_FIELD_TH"], DEFINES["USV_FIELD_TW"], DEFINES["USV_FIELD_TCOLS"]
-    r, c = np.divmod(np.arange(G * G), G)
-    return ((r // th) * tc + c // tw) * (th * tw) + (r % th) * tw + c % tw
 NSTAT = DEFINES["USV_NSTAT"]
 NU_RESET = DEFINES["USV_NU_RESET"]
 NU_STEP = DEFINES["USV_NU_STEP"]
@@ -142,7 +136,7 @@ class USVVirtual:
         self.task_scratch = (Z(TS_ROWS * n + (n + 255) // 256, **f32) if self.cfg.task_kind == TASK_TRACK_XYO
                              else None)
         self._has_field = self.cfg.task_kind == TASK_CAPTURE_XY
-        self.field = Z((n if self._has_field else 1, FIELD_STRIDE), **f32)   # tiled rows (USV_FIELD_STRIDE)
+        self.field = Z((n if self._has_field else 1, FIELD_STRIDE), **f32)   # tiled raw cost of the field
         self.ibuf[2] = 1                               # RLTask.cleanup: reset_buf = ones
         self.just_reset.fill_(1)
         self.ctl = Z(CTL_N, **i32)
@@ -154,7 +148,10 @@ class USVVirtual:
         # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
         self.clock = Z(4, device=dev, dtype=torch.int64)
         self.states_buf = Z((n, 0), **f32)
-        self.sdf = torch.empty((n if self._has_field else 1, FIELD_STRIDE), **f32)   # per-reset-slot SDF scratch
+        # the potential field in parts (include/usv_hip.h): .field = cost tiles, .fnorm = per-env constants (the SDF
+        # comes from the obstacles), .sdf = the sweeps' raw cost rows
+        self.sdf = Z((n if self._has_field else 1, FIELD_STRIDE), **f32)
+        self.fnorm = Z((n if self._has_field else 1, DEFINES["USV_FNORM"]), **f32)
         # the overlapped step (env_step(.., overlap=True)): the reset envs' deferred reward terms, a side
         # stream for the field kernels and the fork / join events
         self.rstash = Z((DEFINES["USV_RSTASH_ROWS"], n), **f32) if self._has_field else None
@@ -238,6 +235,7 @@ class USVVirtual:
         b.field_old_tgt = p(self.field_old_tgt)
         b.slot_stats = p(self.slot_stats)
         b.sdf = p(self.sdf)
+        b.fnorm = p(self.fnorm)
         b.clock = p(self.clock)
         b.rstash = p(self.rstash) if self.rstash is not None else None
         b.grid_lin = p(self.grid_lin) if self.grid_lin is not None else None
@@ -251,12 +249,16 @@ class USVVirtual:
         return b
 
     def field_rowmajor(self, ids=None) -> torch.Tensor:
-        """The potential fields of envs `ids` (all by default) as row-major [k, 150 * 150] grids (the device rows
-        are tiled, include/usv_hip.h USV_FIELD_STRIDE): what BatchedMapGPU returns per env."""
-        if not hasattr(self, "_field_idx"):
-            self._field_idx = torch.tensor(field_tile_index(), device=self._device, dtype=torch.long)
-        f = self.field if ids is None else self.field[ids]
-        return f.index_select(1, self._field_idx)
+        """The potential fields of envs `ids` (all by default) as row-major [k, 150 * 150] grids: what
+        BatchedMapGPU returns per env, materialised from the parts the device keeps (usv_field_view)."""
+        self.join_step()
+        ids_t = (torch.arange(self._num_envs, device=self._device) if ids is None
+                 else torch.as_tensor(ids, device=self._device).reshape(-1))
+        ids_t = ids_t.to(torch.int32).contiguous()
+        out = torch.empty((int(ids_t.numel()), GRID2), device=self._device, dtype=torch.float32)
+        _capi.call("usv_field_view", _capi.byref(self.cfg), _capi.byref(self._bufs), _capi.ptr(ids_t),
+                   int(ids_t.numel()), _capi.ptr(out), _capi.stream_ptr())
+        return out
 
     def set_env_origins(self, org: torch.Tensor) -> None:
         """World x, y of each env's origin ([2][n]; RLTask._env_pos from the stage)."""

@@ -441,7 +441,7 @@ def test_full_size_properties(n):
         assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
         assert obs.abs().max().item() <= 12.0
         assert acc_done > 0
-        f = task.field
+        f = task.field_rowmajor(torch.arange(0, n, 61, device=DEV))
         assert float(f.min()) >= 0.0 and float(f.max()) <= 1.5 + 1e-5
         outs.append((obs.clone(), rew.clone(), task.state.clone()))
     for a, b in zip(outs[0], outs[1]):

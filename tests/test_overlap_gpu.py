@@ -16,7 +16,7 @@ def _snap(task):
     return {"state": task.state.cpu().numpy(), "obs": task.obs_buf_t.cpu().numpy(), "rew": task.rew_buf.cpu().numpy(),
             "dones": task.dones.cpu().numpy(), "hist": task.hist.cpu().numpy(), "stats": task.stats.cpu().numpy(),
             "ibuf": task.ibuf.cpu().numpy(), "obst": task.obst.cpu().numpy(), "extras": task.extras_buf.cpu().numpy(),
-            "field": task.field.cpu().numpy()}
+            "sdf": task.field.cpu().numpy(), "cost": task.sdf.cpu().numpy(), "fnorm": task.fnorm.cpu().numpy()}
 
 
 @pytest.mark.parametrize("n", [1024, 8192])

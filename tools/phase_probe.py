@@ -53,6 +53,9 @@ def main():
         agent.train_epoch()
     torch.cuda.synchronize()
     pb = read("ppo")
+    out = os.environ.get("USV_PROBE_DUMP")
+    if out:   # raw per-workgroup stamps of the last k_mb_grad launch (wall_clock64 ticks) for offline analysis
+        np.save(out, pb[:agent.minibatch_size // 32])
     report("k_mb_grad (last launch)", pb, agent.minibatch_size // 32, 9)
     b = pb[:agent.minibatch_size // 32]
     b = b[b[:, 0] > 0]
