@@ -32,8 +32,10 @@ BF16_PEAK_TFS = 2500.0         # MI355X dense bf16 MFMA peak (same table, no spa
 # SURVEY §8(d) fused figure (476 B: state, lag, DR params, target, obstacles,
 # reward history, 4 field texels, obs row, reward, done) + the episode_sums
 # read-modify-write the reference performs every step (25 x 8 B) - counted
-# exactly from k_env_step's loads/stores: 357 B read + 313 B written.
-ENV_STEP_BYTES = 670
+# exactly from k_env_step's loads/stores: 389 B read + 313 B written.  The 4 field texels
+# are the tiled raw costs (16 B) + the env's 8 normalisation constants (32 B; the field is
+# kept as its parts), 357 + 32 = 389 B.
+ENV_STEP_BYTES = 702
 # --task: packaged task yamls and the algorithmic bytes per env-step of their step kernels
 # (k_env_step_task): GoToPose 221 B read + 309 B written; TrackXYOVelocity
 # 221 + 293 in the first launch and 32 + 28 in k_track_finish

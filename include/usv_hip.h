@@ -288,10 +288,11 @@ typedef struct usv_bufs {
   float *rstash;
   /* [n][USV_FNORM] per-env normalisation constants of the potential field (usv_potential_field writes them
      for the reset envs): cost min, cost range + 1e-6, J min, J range + 1e-6, the batch's inf_val, the
-     batch's inside value `high`, the batch's any-inside flag, 0, then RN(1 / cost range), RN(1 / J range) */
+     batch's inside value `high` (> 0; negated when no cell of the batch is inside an obstacle),
+     RN(1 / cost range), RN(1 / J range) */
   float *fnorm;
 } usv_bufs_t;
-#define USV_FNORM 12
+#define USV_FNORM 8
 #define USV_RSTASH_ROWS 14
 
 /* one replay scene (scripts/build_usv_scenes.py:566-577 keys; obstacles padded to

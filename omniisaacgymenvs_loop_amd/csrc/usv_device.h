@@ -109,11 +109,14 @@ __device__ __forceinline__ float j_raw(const usv_cfg_t &c, float dte, float inv_
 __device__ __forceinline__ float goal_mask(const usv_cfg_t &c, float cv, float cell) {
   return clampt((cv * cell) / c.safe_radius, 0.f, 1.f);
 }
+// usv_bufs_t.fnorm of an env: (gmin, gden, jmn, jden), (inf_val, +-high, 1 / gden, 1 / jden) -- `high` > 0
+// always, so its sign carries the batch's any-inside flag (+: some cell of the batch is inside an obstacle)
 struct FieldNorm {
-  float gmin, gden, jmn, jden, inf_val, high, any_inside, inv_gden, inv_jden;
+  float gmin, gden, jmn, jden, inf_val, high, inv_gden, inv_jden;
+  bool any_inside;
 };
-__device__ __forceinline__ FieldNorm field_norm_of(float4 a, float4 b, float4 r) {
-  return FieldNorm{a.x, a.y, a.z, a.w, b.x, b.y, b.z, r.x, r.y};
+__device__ __forceinline__ FieldNorm field_norm_of(float4 a, float4 b) {
+  return FieldNorm{a.x, a.y, a.z, a.w, b.x, fabsf(b.y), b.z, b.w, b.y > 0.f};
 }
 // one texel: sv = SDF, g = raw cost (+inf unreachable); cell = map / G, inv_r = 1 / influence radius,
 // inv_safe = RN(1 / safe_radius).  The divisions by a per-env or config constant are div_rn with the
@@ -125,7 +128,7 @@ __device__ __forceinline__ float field_value(const usv_cfg_t &c, const FieldNorm
   const float jr = j_raw(c, dte, inv_r);
   const float gm = clampt(div_rn(cv * cell, c.safe_radius, inv_safe), 0.f, 1.f);   // goal_mask
   const float j = (dte < c.influence_radius) ? jr * gm : 0.f;
-  const float jv = (k.any_inside != 0.f && dte <= 0.f) ? k.high : j;
+  const float jv = (k.any_inside && dte <= 0.f) ? k.high : j;
   const float gn = div_rn(cv - k.gmin, k.gden, k.inv_gden);
   const float jn = div_rn(jv - k.jmn, k.jden, k.inv_jden);
   return gn + c.field_alpha * jn;

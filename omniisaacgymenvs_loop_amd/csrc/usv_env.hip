@@ -405,7 +405,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
 // ------------------------------------------------------------------------
 struct FieldTaps {
   float g_nw, g_ne, g_sw, g_se;    // raw costs of the 4 texels (the env's tiles)
-  float4 fn0, fn1, fn2;            // the env's normalisation constants (usv_bufs_t.fnorm)
+  float4 fn0, fn1;                 // the env's normalisation constants (usv_bufs_t.fnorm)
   float nw, ne, sw, se;
   int i0, i1c, j0, j1c;
   bool i_out, j_out;
@@ -435,7 +435,6 @@ __device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, con
   t.g_se = F[field_idx(j1c, i1c)];
   t.fn0 = reinterpret_cast<const float4 *>(FN)[0];
   t.fn1 = reinterpret_cast<const float4 *>(FN)[1];
-  t.fn2 = reinterpret_cast<const float4 *>(FN)[2];
   t.i0 = i0; t.i1c = i1c; t.j0 = j0; t.j1c = j1c;
   t.i_out = i1 >= G;
   t.j_out = j1 >= G;
@@ -452,7 +451,7 @@ struct GridK {
 template <class Ob>
 __device__ __forceinline__ float field_blend(const usv_cfg_t &c, const FieldTaps &t, Ob ob, const GridK &gk, float cell,
                                              float inv_r, float inv_safe) {
-  const FieldNorm k = field_norm_of(t.fn0, t.fn1, t.fn2);
+  const FieldNorm k = field_norm_of(t.fn0, t.fn1);
   const float x0 = gk(t.i0), x1 = gk(t.i1c), y0 = gk(t.j0), y1 = gk(t.j1c);
   const float r = c.obstacle_radius;
   const float v_nw = field_value(c, k, cell_sdf(ob, x0, y0, r), t.g_nw, cell, inv_r, inv_safe);

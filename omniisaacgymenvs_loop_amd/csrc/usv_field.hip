@@ -712,8 +712,7 @@ __global__ __launch_bounds__(256) void k_field_norm(usv_cfg_t c, usv_bufs_t b) {
     float4 *fn = reinterpret_cast<float4 *>(b.fnorm + (size_t)e * USV_FNORM);
     const float gden = (gmax - gmin) + 1e-6f, jden = (jmx - jmn) + 1e-6f;
     fn[0] = make_float4(gmin, gden, jmn, jden);
-    fn[1] = make_float4(k.inf_val, high, any_inside ? 1.f : 0.f, 0.f);
-    fn[2] = make_float4(1.0f / gden, 1.0f / jden, 0.f, 0.f);   // field_value's div_rn reciprocals
+    fn[1] = make_float4(k.inf_val, any_inside ? high : -high, 1.0f / gden, 1.0f / jden);   // (field_norm_of)
   }
 }
 
@@ -728,7 +727,7 @@ __global__ __launch_bounds__(256) void k_field_view(usv_cfg_t c, usv_bufs_t b, c
     const int i = (int)(q / G2), cell_i = (int)(q % G2), r = cell_i / G, cc = cell_i % G;
     const int e = ids[i];
     const float4 *fn = reinterpret_cast<const float4 *>(b.fnorm + (size_t)e * USV_FNORM);
-    const FieldNorm k = field_norm_of(fn[0], fn[1], fn[2]);
+    const FieldNorm k = field_norm_of(fn[0], fn[1]);
     const float *ob = b.obst + e;   // [16][2][n]
     const float sv = cell_sdf([&](int o) { return make_float2(ob[(size_t)(2 * o) * b.n], ob[(size_t)(2 * o + 1) * b.n]); },
                               grid_coord(b.grid_lin, c.map_size, cc), grid_coord(b.grid_lin, c.map_size, r),
