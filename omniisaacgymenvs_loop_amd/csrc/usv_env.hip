@@ -1855,7 +1855,9 @@ int usv_env_step_late(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream) {
   if (!cfg || !b || b->n <= 0 || !b->rstash || !b->field || !b->sdf || !b->fnorm ||
       cfg->task_kind != USV_TASK_CAPTURE_XY)
     return 1;
-  const int grid = (b->n + 255) / 256 < 512 ? (b->n + 255) / 256 : 512;
+  // a few workgroups striding over the device reset count (~1% of the envs per step at the headline size):
+  // it runs beside the next policy step, so a small grid is dispatched at once
+  const int grid = (b->n + 255) / 256 < 32 ? (b->n + 255) / 256 : 32;
   hipLaunchKernelGGL(k_env_reward_late, dim3(grid), dim3(256), 0, (hipStream_t)stream, *cfg, *b);
   USV_CHECK_LAUNCH();
   return 0;

@@ -17,7 +17,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ENV_STEP_BYTES = 670
+ENV_STEP_BYTES = 702   # bench.py ENV_STEP_BYTES
 
 KEEP = ["Dispatch_Id", "Grid_Size", "Kernel_Name", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size",
         "VGPR_Count", "SGPR_Count", "Counter_Name", "Counter_Value"]
