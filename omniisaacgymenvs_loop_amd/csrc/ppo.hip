@@ -1747,7 +1747,14 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
                     float *actions_out, uint64_t seed, uint64_t step, const uint64_t *step_dev,
                     const float *eps_inject, void *stream) {
   if (!cfg || !params || !obs_rms || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
-  const int grid = policy_grid(cfg->n_envs);
+  // USV_POLICY_GRID caps the persistent grid (A/B knob: fewer CUs for the policy kernel leaves the
+  // rest to the side stream's field kernels in the overlapped step; results do not depend on it)
+  static const int grid_cap = [] {
+    const char *v = getenv("USV_POLICY_GRID");
+    return v ? atoi(v) : 0;
+  }();
+  int grid = policy_grid(cfg->n_envs);
+  if (grid_cap > 0 && grid_cap < grid) grid = grid_cap;
   hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
                      obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
                      actions_out, seed, step, step_dev, eps_inject);

@@ -368,7 +368,8 @@ class USVVirtual:
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
         main = torch.cuda.current_stream(self._device)
         if self._side is None:
-            self._side = torch.cuda.Stream(device=self._device)
+            # USV_SIDE_PRIORITY: the side stream's priority (torch's convention: lower = higher priority)
+            self._side = torch.cuda.Stream(device=self._device, priority=int(os.getenv("USV_SIDE_PRIORITY", "0")))
             self._ev_fork, self._ev_early, self._ev_join = (torch.cuda.Event() for _ in range(3))
         side = self._side
         _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
