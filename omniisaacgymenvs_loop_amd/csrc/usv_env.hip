@@ -75,6 +75,12 @@ struct ResetRng {
 // Per-step scratch reset (reset count, field maxima, extras sums): one tiny
 // kernel instead of four memset nodes.
 // ------------------------------------------------------------------------
+// USV_RESET_FOLD_KERNEL: the episode-extras fold of the reset path in a one-workgroup launch of its own
+// (k_extras_fold) instead of by the last k_reset workgroup behind a device-scope counter and fences
+#ifndef USV_RESET_FOLD_KERNEL
+#define USV_RESET_FOLD_KERNEL 1
+#endif
+
 __global__ void k_step_begin(usv_bufs_t b) {
   const int t = threadIdx.x;
   if (t == 0 && b.clock) {   // device step clock: this step's index and bias-call count
@@ -346,8 +352,6 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   // ---- the last workgroup finalises extras["episode"] = means over this step's resets (:1591-1612).
   // Per-workgroup partials (no float atomics: one address per statistic would serialise
   // every wave of the grid on it, and the sum order would vary run to run) ----
-  __shared__ bool last;
-  __shared__ float fold[8][32];
   __syncthreads();
   const int qs = threadIdx.x;
   if (c.stats_on && qs < USV_NSTAT) {
@@ -355,8 +359,22 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
 #pragma unroll
     for (int w = 1; w < kBlock / 64; ++w) a += wsum[w][qs];
     b.extras_acc[(size_t)blockIdx.x * USV_NSTAT + qs] = a;
+#if !USV_RESET_FOLD_KERNEL
     __threadfence();
+#endif
   }
+#if USV_RESET_FOLD_KERNEL
+  // the fold runs as k_extras_fold right behind this launch (stream order publishes the partials)
+}
+
+__global__ __launch_bounds__(kBlock) void k_extras_fold(usv_cfg_t c, usv_bufs_t b, int nblk) {
+  const int qs = threadIdx.x;
+  __shared__ float fold[8][32];
+  const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
+  const int G = nblk;
+#else
+  __shared__ bool last;
+  __shared__ float fold[8][32];
   __syncthreads();
   if (threadIdx.x == 0) {
     __threadfence();
@@ -366,6 +384,8 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
   __syncthreads();
   if (!last) return;
   const int count = b.ctl[USV_CTL_RESET_COUNT];
+  const int G = (int)gridDim.x;
+#endif
   if (c.stats_on && count > 0) {
     // 8 interleaved block subsets per statistic, each summed in block order, then combined in order
     static_assert(USV_NSTAT <= 32 && kBlock == 256, "fold layout");
@@ -373,7 +393,6 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
     float a = 0.f;
     if (q < USV_NSTAT) {
       // blocks k, k+8, k+16, ... in that order; 16 loads in flight per batch
-      const int G = (int)gridDim.x;
       for (int b0 = k; b0 < G; b0 += 128) {
         float x[16];
 #pragma unroll
@@ -1101,7 +1120,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
 // exist (after usv_env_step_part(.., 3) and the field kernels): the stashed potential-independent terms,
 // the field sample at the stashed position, reward_tail with prev_potential None (a reset env), the
 // reward, prev_pot and the reward sums -- the operations part 0 runs for these envs, in the same order.
-__global__ __launch_bounds__(256) void k_env_reward_late(usv_cfg_t c, usv_bufs_t b) {
+#ifndef USV_LATE_GRID
+#define USV_LATE_GRID 256
+#endif
+constexpr int kLateGrid = USV_LATE_GRID;
+__global__ __launch_bounds__(64) void k_env_reward_late(usv_cfg_t c, usv_bufs_t b) {
   const int n = b.n;
   const float cell = (float)((double)c.map_size / USV_GRID);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
@@ -1110,7 +1133,11 @@ __global__ __launch_bounds__(256) void k_env_reward_late(usv_cfg_t c, usv_bufs_t
   const float g_start = (float)(-(double)c.map_size / 2 + cell_d / 2), g_end = (float)((double)c.map_size / 2 - cell_d / 2);
   const GridK gk{g_start, g_end, (g_end - g_start) / (float)(USV_GRID - 1), b.grid_lin};
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);
-  for (int slot = (int)(blockIdx.x * blockDim.x + threadIdx.x); slot < count; slot += (int)(gridDim.x * blockDim.x)) {
+  // slots spread thinly over many one-wave workgroups (lane l of workgroup g takes slot g + G l, ...): every
+  // lane's loads are gathers from scattered envs, so a wave with few active lanes issues them in few cycles
+  // and every CU takes a share (64 consecutive slots per wave put ~74 x 64 scattered lines on one CU)
+  const int G = (int)gridDim.x;
+  for (int slot = (int)blockIdx.x + G * (int)threadIdx.x; slot < count; slot += G * (int)blockDim.x) {
     const int e = b.reset_ids[slot];
     float st[USV_RSTASH_ROWS];
 #pragma unroll
@@ -1774,6 +1801,12 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t
   const int grid = (b->n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_reset, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, seed, step, u_inject);
   USV_CHECK_LAUNCH();
+#if USV_RESET_FOLD_KERNEL
+  if (cfg->stats_on) {
+    hipLaunchKernelGGL(k_extras_fold, dim3(1), dim3(kBlock), 0, s, *cfg, *b, grid);
+    USV_CHECK_LAUNCH();
+  }
+#endif
   return 0;
 }
 
@@ -1855,10 +1888,9 @@ int usv_env_step_late(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream) {
   if (!cfg || !b || b->n <= 0 || !b->rstash || !b->field || !b->sdf || !b->fnorm ||
       cfg->task_kind != USV_TASK_CAPTURE_XY)
     return 1;
-  // a few workgroups striding over the device reset count (~1% of the envs per step at the headline size):
-  // it runs beside the next policy step, so a small grid is dispatched at once
-  const int grid = (b->n + 255) / 256 < 32 ? (b->n + 255) / 256 : 32;
-  hipLaunchKernelGGL(k_env_reward_late, dim3(grid), dim3(256), 0, (hipStream_t)stream, *cfg, *b);
+  // one-wave workgroups striding over the device reset count (~1% of the envs per step at the headline size)
+  const int grid = (b->n + 63) / 64 < kLateGrid ? (b->n + 63) / 64 : kLateGrid;
+  hipLaunchKernelGGL(k_env_reward_late, dim3(grid), dim3(64), 0, (hipStream_t)stream, *cfg, *b);
   USV_CHECK_LAUNCH();
   return 0;
 }
