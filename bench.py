@@ -279,9 +279,12 @@ def main():
     env_timer, ppo_timer = KernelTimer(), KernelTimer()
     orig_call = _capi.call
 
+    resets = []   # the reset count of each timed env step (device control word, read after the launch)
+
     def timed_call(name, *a):
         if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
             env_timer(lambda: orig_call(name, *a))
+            resets.append(task.ctl[0:1].clone())
         elif timing[0] and name in ("ppo_minibatch_grad", "ppo_minibatch_fused", "ppo_minibatch_fused_dp"):
             ppo_timer(lambda: orig_call(name, *a))
         else:
@@ -436,6 +439,7 @@ def main():
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                          "traffic": None, "bytes_per_env_step": step_bytes, "launch_ms": env_ms,
                          "launch_ms_raw": env_timer.raw_ms(), "event_overhead_ms": env_timer.overhead_ms(),
+                         "resets_per_step": (sorted(int(r.item()) for r in resets) or [None])[len(resets) // 2],
                          "envs_per_launch": args.envs,
                          "launch_ms_method": f"HIP event pair around each of the {len(env_timer.pairs)} env-step "
                                              "launches of one eager training epoch, on the launch stream, behind a "
