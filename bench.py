@@ -281,8 +281,14 @@ def main():
 
     resets = []   # the reset count of each timed env step (device control word, read after the launch)
 
+    # USV_BENCH_FLUSH=<MB>: write that many MB ahead of each timed env step (cache-state experiment)
+    flush_mb = int(os.getenv("USV_BENCH_FLUSH", "0"))
+    flush_buf = torch.empty(flush_mb * 262144, device=f"cuda:{local}") if flush_mb else None
+
     def timed_call(name, *a):
         if timing[0] and name in ("usv_env_step", "usv_env_step_part"):
+            if flush_buf is not None:
+                flush_buf.fill_(1.0)
             env_timer(lambda: orig_call(name, *a))
             resets.append(task.ctl[0:1].clone())
         elif timing[0] and name in ("ppo_minibatch_grad", "ppo_minibatch_fused", "ppo_minibatch_fused_dp"):

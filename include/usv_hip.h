@@ -35,15 +35,17 @@ extern "C" {
 #define USV_NCLOSE       5   /* closest obstacles in obs          (USV_core.py:33) */
 #define USV_GRID       150   /* potential-field grid              (USV_capture_xy_static_obs.py:30) */
 #define USV_GRID2    (USV_GRID * USV_GRID)
-/* the potential field in HBM (usv_bufs_t.field, .sdf): per env USV_FIELD_STRIDE floats of 4 x 8-texel tiles,
- * one 128-B cache line each, tiles row-major over the grid padded to 152 x 152: texel (row r, column c) at
- * ((r / 4) * USV_FIELD_TCOLS + c / 8) * 32 + (r % 4) * 8 + c % 8.  The env step's bilinear potential sample
- * (a 2 x 2 texel block) then touches ~1.4 lines instead of the >= 2 of row-major rows. */
-#define USV_FIELD_TH     4
-#define USV_FIELD_TW     8
+/* the potential field in HBM (usv_bufs_t.field, .sdf): per env USV_FIELD_STRIDE floats of 10 x 10-texel tiles
+ * (400 B, row-major inside), tiles row-major over the 150 x 150 grid: texel (row r, column c) at
+ * ((r / 10) * USV_FIELD_TCOLS + c / 10) * 100 + (r % 10) * 10 + c % 10.  The tiles are the potential-field
+ * sweep kernel's per-thread tiles, so that kernel stores its cells as immediate offsets of one base; the env
+ * step's bilinear potential sample (a 2 x 2 texel block, 44 B inside a tile) touches ~1.5 lines instead of the
+ * >= 2 of row-major rows.  The stride is padded to whole 128-B lines. */
+#define USV_FIELD_TH    10
+#define USV_FIELD_TW    10
 #define USV_FIELD_TROWS  ((USV_GRID + USV_FIELD_TH - 1) / USV_FIELD_TH)
 #define USV_FIELD_TCOLS  ((USV_GRID + USV_FIELD_TW - 1) / USV_FIELD_TW)
-#define USV_FIELD_STRIDE (USV_FIELD_TROWS * USV_FIELD_TCOLS * USV_FIELD_TH * USV_FIELD_TW)
+#define USV_FIELD_STRIDE 22528   /* 15 x 15 tiles x 100 texels = 22,500, padded to whole 128-B lines */
 #define USV_LUT_N     1000   /* thruster LUT points               (TEST yaml dynamics.thrusters) */
 #define USV_NSTAT       28   /* episode_sums keys                 (USV_Virtual.py:586-601) */
 #define USV_SPAWN_ITERS 20   /* obstacle rejection iterations     (static_obs.py:980) */
@@ -728,6 +730,11 @@ int lz_grad_floats(int obs_dim);
 
 /* library version */
 int usv_hip_version(void);
+/* the layout constants this library was compiled with (USV_FIELD_STRIDE, USV_FIELD_TH, USV_FIELD_TW, PPO_NPARAM,
+ * USV_FNORM, USV_RSTASH_ROWS, USV_CTL_N, USV_NSTAT) folded into one key, k = k * 1000003 + v in that order (mod
+ * 2^63): a binding that allocates from this header compares it with the same fold of its own constants before
+ * its first call, so a library built from another layout fails loudly instead of addressing past a buffer */
+long long usv_hip_layout_key(void);
 
 #ifdef __cplusplus
 }

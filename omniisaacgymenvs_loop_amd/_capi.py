@@ -89,6 +89,7 @@ def _declare(lib):
         "lz_partials_floats": [P],
         "ppo_meter_floats": [I, I],
         "usv_hip_version": [],
+        "usv_hip_layout_key": [],   # (restype long long, below)
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -96,7 +97,22 @@ def _declare(lib):
         fn.restype = ctypes.c_int
     lib.ppo_dp_buffer_bytes.argtypes = []
     lib.ppo_dp_buffer_bytes.restype = ctypes.c_longlong
+    lib.usv_hip_layout_key.argtypes = []
+    lib.usv_hip_layout_key.restype = ctypes.c_longlong
     return lib
+
+
+LAYOUT_KEYS = ("USV_FIELD_STRIDE", "USV_FIELD_TH", "USV_FIELD_TW", "PPO_NPARAM", "USV_FNORM", "USV_RSTASH_ROWS",
+               "USV_CTL_N", "USV_NSTAT")
+
+
+def layout_key() -> int:
+    """usv_hip_layout_key() of include/usv_hip.h as this binding's constants give it."""
+    from ._abi import DEFINES
+    k = 0
+    for name in LAYOUT_KEYS:
+        k = (k * 1000003 + int(DEFINES[name])) % (1 << 64)
+    return k & ((1 << 63) - 1)
 
 
 def lib():
@@ -110,7 +126,11 @@ def lib():
         if not os.path.exists(path):
             raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; "
                                f"g.build()'` (hipcc --offload-arch=gfx950)")
-        _lib = _declare(ctypes.CDLL(path))
+        loaded = _declare(ctypes.CDLL(path))
+        if loaded.usv_hip_layout_key() != layout_key():
+            raise RuntimeError(f"{path} was built from another buffer layout than include/usv_hip.h "
+                               "(usv_hip_layout_key mismatch): rebuild it")
+        _lib = loaded
     return _lib
 
 

@@ -37,9 +37,12 @@ __device__ __forceinline__ void philox_u4(uint64_t seed, uint32_t env, uint64_t 
 }
 
 // index of texel (r, c) of an env's potential field in the tiled layout (include/usv_hip.h USV_FIELD_STRIDE)
+static_assert(USV_FIELD_STRIDE >= USV_FIELD_TROWS * USV_FIELD_TCOLS * USV_FIELD_TH * USV_FIELD_TW &&
+              USV_FIELD_STRIDE % 32 == 0, "field stride: every tile, whole 128-B lines");
 __host__ __device__ __forceinline__ int field_idx(int r, int c) {
-  static_assert(USV_FIELD_TH == 4 && USV_FIELD_TW == 8, "tile shifts");
-  return ((r >> 2) * USV_FIELD_TCOLS + (c >> 3)) * (USV_FIELD_TH * USV_FIELD_TW) + ((r & 3) << 3) + (c & 7);
+  const unsigned ur = (unsigned)r, uc = (unsigned)c;   // r, c >= 0: constant divisions become multiplies
+  return (int)(((ur / USV_FIELD_TH) * USV_FIELD_TCOLS + uc / USV_FIELD_TW) * (USV_FIELD_TH * USV_FIELD_TW) +
+               (ur % USV_FIELD_TH) * USV_FIELD_TW + uc % USV_FIELD_TW);
 }
 
 __device__ __forceinline__ float clampf(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }

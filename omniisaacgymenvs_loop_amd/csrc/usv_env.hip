@@ -1918,4 +1918,12 @@ int usv_hydrostatics(const usv_hydro_t *h, int n, const float *quat, const float
 
 int usv_hip_version(void) { return 1; }
 
+long long usv_hip_layout_key(void) {
+  const long long v[] = {USV_FIELD_STRIDE, USV_FIELD_TH, USV_FIELD_TW, PPO_NPARAM, USV_FNORM, USV_RSTASH_ROWS, USV_CTL_N,
+                         USV_NSTAT};
+  unsigned long long k = 0;
+  for (long long x : v) k = k * 1000003ull + (unsigned long long)x;
+  return (long long)(k & 0x7fffffffffffffffull);
+}
+
 }  // extern "C"

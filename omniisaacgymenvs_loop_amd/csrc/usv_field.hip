@@ -22,9 +22,9 @@
 //      r = 0.5 m obstacles is < 120; checked on the golden fixtures).  An
 //      occupied target cell is seeded exactly as the reference's first Jacobi
 //      sweep does (its neighbours get 1 / 1.414);
-//   3. raw cost, row-major, to the env's cost row (b.sdf).
-// k_field_stats (per slot and 30-row band): the SDF into the env's field tiles
-//   and per-env statistics, split by finite and infinite cost so that the batch
+//   3. raw cost into the env's field tiles (b.field: the threads' own 10 x 10 tiles).
+// k_field_stats (per slot and 30-row band): the SDF (recomputed from the obstacles)
+//   and the cost tiles -> per-env statistics, split by finite and infinite cost so that the batch
 //   constant inf_val (unknown until every env is done) enters only through one
 //   monotone scalar per batch.
 // k_field_batch (one workgroup): batch max of finite costs -> inf_val, the
@@ -379,20 +379,19 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
         }
     }
     const bool exact = __syncthreads_or((hmax > kPinnedCost) || (it >= kMaxIters)) != 0;
-    // ---- 3. raw cost out (occupied marker -> +inf) into the env's cost row, row-major (one base
-    // address + immediate offsets: tiled offsets here would be 100 live addresses); statistics and
-    // the SDF in k_field_stats, the normalisation constants in k_field_norm ----
-    float *Sc = b.sdf + (size_t)e * FS;
+    // ---- 3. raw cost out (occupied marker -> +inf) into the env's field tile: the field's 10 x 10 tiles are
+    // these threads' tiles, so the 100 stores are immediate offsets of one base (no per-thread offsets, no
+    // scratch copy).  Statistics and the SDF in k_field_stats, the constants in k_field_norm ----
+    static_assert(USV_FIELD_TH == T && USV_FIELD_TW == T && USV_FIELD_TCOLS == NT, "field tiles = sweep tiles");
     if (tile_ok) {
+      float *Ft = b.field + (size_t)e * FS + (tr * NT + tc) * (T * T);
 #pragma unroll
       for (int i = 0; i < T; ++i)
 #pragma unroll
-        for (int j = 0; j < T; ++j) {
-          const float g = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
-          Sc[(r0 + i) * G + c0 + j] = g;
-        }
-      lastc[tp] = -1000;   // ready for the next slot
+        for (int j = 0; j < T; ++j)
+          Ft[i * T + j] = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
     }
+    if (tile_ok) lastc[tp] = -1000;   // ready for the next slot
     if (tid == 0) {
       b.slot_stats[(size_t)slot * kSlotStride + SS_ITERS] = (float)it;   // iterations (diagnostic)
       b.slot_stats[(size_t)slot * kSlotStride + SS_EXACT] = exact ? 1.f : 0.f;   // k_field_exact redoes it
@@ -449,9 +448,10 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_b
     ix = min(max(ix, 0), G - 1);
     iy = min(max(iy, 0), G - 1);
     __syncthreads();
-    float *Fe = b.field + (size_t)e * FS;          // free until k_field_stats writes the cost tiles there
-    float *scratch = b.sdf + (size_t)e * FS;      // the raw cost, row-major, as k_field_wave leaves it
+    float *Fe = b.field + (size_t)e * FS;          // overwritten: the ping-pong buffer, then the cost tiles
+    float *scratch = b.sdf + (size_t)e * FS;      // the other ping-pong buffer
     cost_sweeps_exact(occ, ix, iy, Fe, scratch);  // row-major ping-pong, 225 (odd) sweeps: result in scratch
+    for (int q = tid; q < G2; q += kWaveThreads) Fe[field_idx(q / G, q % G)] = scratch[q];   // into the tiles
     if (tid == 0) atomicAdd(&b.ctl[USV_CTL_FIELD_EXACT], 1);
     __syncthreads();
   }
@@ -500,8 +500,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
     const int slot = w / kBands, band = w % kBands;
     const int e = b.reset_ids[slot];
-    const float *Sc = b.sdf + (size_t)e * FS;      // raw cost, row-major (k_field_wave / k_field_exact)
-    float *Fe = b.field + (size_t)e * FS;           // the cost into the env's tiles
+    const float *Fe = b.field + (size_t)e * FS;     // the raw cost tiles (k_field_wave / k_field_exact)
     if (tid < 2 * USV_NOBST) so[tid] = b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid];
     if (tid < 2) flags[tid] = 0;
     __syncthreads();
@@ -510,7 +509,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
       const int r = band * kBandRows + rg + kRowGroups * k;
-      gv[k] = *reinterpret_cast<const float2 *>(Sc + r * G + c0);
+      gv[k] = *reinterpret_cast<const float2 *>(Fe + field_idx(r, c0));   // (c0 even: one tile row)
     }
     float dxa[USV_NOBST], dxb[USV_NOBST], oy[USV_NOBST];
     {
@@ -585,7 +584,6 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       const float sva = sqrtf(__uint_as_float(a[k])) - c.obstacle_radius;
       const float svb = sqrtf(__uint_as_float(bb[k])) - c.obstacle_radius;
       if (act) {
-        *reinterpret_cast<float2 *>(Fe + field_idx(r, c0)) = gv[k];   // (c0 even: one tile row)
         stat(gv[k].x, sva);
         stat(gv[k].y, svb);
       }

@@ -39,3 +39,14 @@ def test_ctypes_signatures_cover_the_header():
     src = open(os.path.join(ROOT, "omniisaacgymenvs_loop_amd", "_capi.py")).read()
     for n in declared_functions():
         assert f'"{n}"' in src, f"{n} has no ctypes signature in _capi.py"
+
+
+def test_library_layout_key_matches_the_header():
+    """The library's compiled buffer-layout constants equal the ones the binding allocates with (a library
+    built from another layout is refused by _capi.lib() before any call)."""
+    from omniisaacgymenvs_loop_amd import _capi
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("libusv_hip.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_capi.LIB_PATH)
+    lib.usv_hip_layout_key.restype = ctypes.c_longlong
+    assert lib.usv_hip_layout_key() == _capi.layout_key()
