@@ -39,7 +39,7 @@ extern "C" {
  * (400 B, row-major inside), tiles row-major over the 150 x 150 grid: texel (row r, column c) at
  * ((r / 10) * USV_FIELD_TCOLS + c / 10) * 100 + (r % 10) * 10 + c % 10.  The tiles are the potential-field
  * sweep kernel's per-thread tiles, so that kernel stores its cells as immediate offsets of one base; the env
- * step's bilinear potential sample (a 2 x 2 texel block, 44 B inside a tile) touches ~1.5 lines instead of the
+ * step's bilinear potential sample (a 2 x 2 texel block, 48 B inside a tile) touches ~1.6 lines instead of the
  * >= 2 of row-major rows.  The stride is padded to whole 128-B lines. */
 #define USV_FIELD_TH    10
 #define USV_FIELD_TW    10

@@ -408,251 +408,6 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   }
 }
 
-// The policy step with two 32-row tiles in flight per CU: a 512-thread workgroup whose wave groups
-// g = 0 (waves 0-3) and g = 1 (waves 4-7) run the forward of tiles 2 q + g of the same pair q on the one
-// staged copy of the weights, so every SIMD holds two waves of the latency-bound forward chain instead of
-// one.  Per group the same operations as k_policy_step in the same order (the same bits): layer 2 writes
-// h2 over h1 in place behind one extra barrier, which keeps the two groups' activations within the LDS.
-struct PolSlot {
-  float x[RB * XS];       // normalised obs of the group's tile
-  float h[RB * HS];       // tanh layer 1, then tanh layer 2 (in place)
-  float out[RB * 4];      // mu0, mu1, value
-  float zz[2][RB * 2];    // the N(0,1) draws of a tile's rows, one tile ahead
-};
-struct PolSmem {
-  float w2[NH * HS];
-  float w1[NH * XS];
-  float b1[NH];
-  float tail[TAIL + 1];
-  float om[NIN], od[NIN];
-  PolSlot sl[2];
-};
-constexpr int PTB = 2 * TB;
-static_assert(sizeof(PolSmem) <= 160 * 1024, "paired policy LDS");
-
-// the weight staging of k_policy_step spread over all 512 threads (half the registers per thread)
-constexpr int NW2P = NH * NH / PTB, NW1P = (NH * XS + PTB - 1) / PTB, NTLP = (TAIL + PTB - 1) / PTB;
-static_assert(NH * NH % PTB == 0, "paired staging trip counts");
-struct StagedWP {
-  float w2r[NW2P];
-  float w1r[NW1P], tlr[NTLP], b1r;
-};
-__device__ __forceinline__ void pol_stage_load(const float *__restrict__ P, StagedWP &r) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int u = 0; u < NW1P; ++u) {
-    const int i = min(tid + u * PTB, NH * XS - 1), j = i / XS, k = i % XS;
-    r.w1r[u] = P[PPO_OFF_W1 + j * NIN + min(k, NIN - 1)];
-  }
-#pragma unroll
-  for (int u = 0; u < NTLP; ++u) r.tlr[u] = P[PPO_OFF_B2 + min(tid + u * PTB, TAIL - 1)];
-  r.b1r = P[PPO_OFF_B1 + (tid & (NH - 1))];
-#pragma unroll
-  for (int u = 0; u < NW2P; ++u) r.w2r[u] = P[PPO_OFF_W2 + tid + u * PTB];
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int u = 0; u < NW1P; ++u)
-    if ((tid + u * PTB) % XS >= NIN) r.w1r[u] = 0.f;
-}
-__device__ __forceinline__ void pol_store_small(const StagedWP &r, PolSmem &s) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int u = 0; u < NW1P; ++u)
-    if (tid + u * PTB < NH * XS) s.w1[tid + u * PTB] = r.w1r[u];
-#pragma unroll
-  for (int u = 0; u < NTLP; ++u)
-    if (tid + u * PTB < TAIL) s.tail[tid + u * PTB] = r.tlr[u];
-  if (tid < NH) s.b1[tid] = r.b1r;
-}
-__device__ __forceinline__ void pol_store_w2(const StagedWP &r, PolSmem &s) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int u = 0; u < NW2P; ++u) {
-    const int e = tid + u * PTB;
-    s.w2[(e / NH) * HS + e % NH] = r.w2r[u];
-  }
-}
-// the group's obs staging (waves 1-3 of the group, tt = its thread index - 64): put_obs_tile3's operations
-__device__ __forceinline__ void pol_put_obs(const float (&x)[NUO3], int tt, int row0, int nrows, bool normalize,
-                                            const PolSmem &s, float *xs, float *exp_obs, int H, int t) {
-#pragma unroll
-  for (int u = 0; u < NUO3; ++u) {
-    const int q = tt + u * OT;
-    if (q >= RB * XS) continue;
-    const int r = q / XS, k = q % XS;
-    float v = 0.f;
-    if (r < nrows && k < NIN) {
-      v = x[u];
-      exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = v;
-      if (normalize) v = clampt((v - s.om[k]) / s.od[k], -5.0f, 5.0f);   // = rms_norm
-    }
-    xs[q] = v;
-  }
-}
-// block_forward of the group's tile (valid: the group has a tile this round; uniform per group); every
-// barrier is taken by both groups
-__device__ __forceinline__ void pair_forward(const StagedWP &wr, PolSmem &s, int g, bool first_tile, bool valid) {
-  const int tid = threadIdx.x & (TB - 1), lane = tid & 63, w = tid >> 6;
-  const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
-  PolSlot &sl = s.sl[g];
-  if (valid) {   // layer 1: h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero)
-    f32x16 acc = {};
-#pragma unroll
-    for (int st = 0; st < 17; ++st) {
-      const int k = 2 * st + h;
-      acc = mfma32(sl.x[i * XS + k], s.w1[(n0 + i) * XS + k], acc);
-    }
-    const float bj = s.b1[n0 + i];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sl.h[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
-  }
-  if (first_tile) pol_store_w2(wr, s);   // (nothing else writes s.w2: later tiles reuse it)
-  __syncthreads();
-  f32x16 acc = {};
-  if (valid) {   // layer 2: h2 = tanh(h1 W2^T + b2)
-#pragma unroll 16
-    for (int st = 0; st < NH / 2; ++st) {
-      const int k = 2 * st + h;
-      acc = mfma32(sl.h[i * HS + k], s.w2[(n0 + i) * HS + k], acc);
-    }
-  }
-  __syncthreads();   // every wave has read h1: h2 goes over it
-  if (valid) {
-    const float bj = s.tail[T_B2 + n0 + i];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) sl.h[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
-  }
-  __syncthreads();
-  if (valid) {   // heads: 8 threads per row
-    const int r = tid / 8, part = tid % 8;
-    float a0 = 0.f, a1 = 0.f, av = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < 16; ++kk) {
-      const int k = part + 8 * kk;
-      const float hv = sl.h[r * HS + k];
-      a0 = fmaf(s.tail[T_WMU + k], hv, a0);
-      a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
-      av = fmaf(s.tail[T_WV + k], hv, av);
-    }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
-      a0 += __shfl_xor(a0, m, 64);
-      a1 += __shfl_xor(a1, m, 64);
-      av += __shfl_xor(av, m, 64);
-    }
-    if (part == 0) {
-      sl.out[r * 4 + 0] = a0 + s.tail[T_BMU];
-      sl.out[r * 4 + 1] = a1 + s.tail[T_BMU + 1];
-      sl.out[r * 4 + 2] = av + s.tail[T_BV];
-    }
-  }
-  __syncthreads();
-}
-
-__host__ __device__ constexpr int policy_pair_grid(int n) {
-  return ((n + RB - 1) / RB + 1) / 2 < 256 ? ((n + RB - 1) / RB + 1) / 2 : 256;
-}
-__global__ __launch_bounds__(PTB) void k_policy_pair(ppo_cfg_t c, const float *__restrict__ P,
-                                                     const double *__restrict__ obs_rms,
-                                                     const double *__restrict__ val_rms, const float *__restrict__ obs,
-                                                     int t, float *exp_obs, float *exp_act, float *exp_nlp,
-                                                     float *exp_val, float *exp_mu, float *exp_sigma, uint8_t *exp_done,
-                                                     const int64_t *__restrict__ dones_prev, float *actions_out,
-                                                     uint64_t seed, uint64_t step, const uint64_t *step_dev,
-                                                     const float *eps_inject) {
-  __shared__ PolSmem s;
-  const int n = c.n_envs, H = c.horizon;
-  if (step_dev) step = *step_dev + (uint64_t)t;
-  const int g = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 8);   // wave group
-  const int gt = (int)threadIdx.x & (TB - 1);
-  const int w = __builtin_amdgcn_readfirstlane(gt >> 6), lane = threadIdx.x & 63;
-  const int tt = gt - 64;
-  StagedWP wr;
-  pol_stage_load(P, wr);
-  const int ntiles = (n + RB - 1) / RB;
-  const int npairs = (ntiles + 1) / 2;
-  const bool normalize = c.normalize_input != 0;
-  if ((int)blockIdx.x >= npairs) return;   // uniform (the grid is at most npairs)
-  PolSlot &sl = s.sl[g];
-  auto draw = [&](int tl, int buf) {
-    if (w == 0 && lane < RB) {
-      const int e = min(tl * RB + lane, n - 1);
-      float z0, z1;
-      if (eps_inject) {
-        z0 = eps_inject[2 * e];
-        z1 = eps_inject[2 * e + 1];
-      } else {  // Normal.sample via Box-Muller on Philox(site 0x200)
-        float u[4];
-        philox_u4(seed, (uint32_t)e, step, 0x200u, u);
-        const float rr0 = sqrtf(-2.0f * logf(1.0f - u[0])), rr1 = sqrtf(-2.0f * logf(1.0f - u[2]));
-        z0 = rr0 * cosf(USV_2PI_F * u[1]);
-        z1 = rr1 * cosf(USV_2PI_F * u[3]);
-      }
-      sl.zz[buf][2 * lane] = z0;
-      sl.zz[buf][2 * lane + 1] = z1;
-    }
-  };
-  if (threadIdx.x < NIN) {
-    s.om[threadIdx.x] = (float)obs_rms[threadIdx.x];
-    s.od[threadIdx.x] = sqrtf((float)obs_rms[NIN + threadIdx.x] + c.rms_eps);
-  }
-  const int stride = 2 * (int)gridDim.x;   // tiles between a group's consecutive tiles
-  int tile = 2 * (int)blockIdx.x + g;
-  float xo[NUO3];
-  if (w > 0 && tile < ntiles) load_obs_tile3(obs, n, tile, tt, xo);
-  __syncthreads();
-  if (w > 0 && tile < ntiles) pol_put_obs(xo, tt, tile * RB, min(RB, n - tile * RB), normalize, s, sl.x, exp_obs, H, t);
-  if (tile < ntiles) draw(tile, 0);
-  pol_store_small(wr, s);
-  __syncthreads();
-  int buf = 0;
-  for (int q = (int)blockIdx.x; q < npairs; q += (int)gridDim.x, tile += stride) {
-    const bool valid = tile < ntiles;   // uniform per group
-    const int row0 = tile * RB;
-    const int nrows = valid ? min(RB, n - row0) : 0;
-    const int nt = tile + stride;
-    float xn[NUO3];   // the next tile's rows, in flight during the forward
-    if (w > 0 && nt < ntiles) load_obs_tile3(obs, n, nt, tt, xn);
-    pair_forward(wr, s, g, q == (int)blockIdx.x, valid);
-    if (w == 0) {
-      const int r = lane;
-      if (r < nrows) {
-        const int e = row0 + r;
-        const size_t slot = (size_t)e * H + t;
-        const float mu0 = sl.out[r * 4], mu1 = sl.out[r * 4 + 1], v = sl.out[r * 4 + 2];
-        const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
-        const float sg0 = expf(ls0), sg1 = expf(ls1);
-        const float z0 = sl.zz[buf][2 * r], z1 = sl.zz[buf][2 * r + 1];
-        const float a0 = mu0 + sg0 * z0, a1 = mu1 + sg1 * z1;
-        const float q0 = (a0 - mu0) / sg0, q1 = (a1 - mu1) / sg1;
-        const float nlp = 0.5f * (q0 * q0 + q1 * q1) + kLog2Pi + (ls0 + ls1);
-        float vd = v;
-        if (c.normalize_value) {  // denorm_value (running_mean_std.py:113-115)
-          vd = clampt(v, -5.0f, 5.0f);
-          vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
-        }
-        exp_act[slot * 2] = a0; exp_act[slot * 2 + 1] = a1;
-        exp_mu[slot * 2] = mu0; exp_mu[slot * 2 + 1] = mu1;
-        exp_sigma[slot * 2] = sg0; exp_sigma[slot * 2 + 1] = sg1;
-        exp_nlp[slot] = nlp;
-        exp_val[slot] = vd;
-        exp_done[slot] = (uint8_t)(dones_prev[e] != 0);
-        actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
-        actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
-      }
-      if (c.nan_probe && c.nan_flag && valid) {   // wave 0 of the group, uniform
-        const bool bad = r < nrows && (nonfinite(sl.out[r * 4]) | nonfinite(sl.out[r * 4 + 1]) | nonfinite(sl.out[r * 4 + 2]));
-        nan_report(c.nan_flag, bad ? USV_NAN_POLICY : 0u);
-      }
-      if (nt < ntiles) draw(nt, buf ^ 1);
-    } else if (nt < ntiles) {
-      pol_put_obs(xn, tt, nt * RB, min(RB, n - nt * RB), normalize, s, sl.x, exp_obs, H, t);
-    }
-    __syncthreads();
-    buf ^= 1;
-  }
-}
-
 __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,
                                               const double *val_rms, const float *__restrict__ obs, float *values) {
   __shared__ MlpSmem s;
@@ -1996,18 +1751,6 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
   // rest to the side stream's field kernels in the overlapped step; results do not depend on it)
   const char *gcap = getenv("USV_POLICY_GRID");
   const int grid_cap = gcap ? atoi(gcap) : 0;
-  // USV_POLICY_PAIR (default on): two tiles in flight per CU (k_policy_pair) instead of one (k_policy_step)
-  const char *pv = getenv("USV_POLICY_PAIR");   // read per call: the tests compare both kernels in one process
-  const bool pair = pv ? atoi(pv) != 0 : true;
-  if (pair) {
-    int grid = policy_pair_grid(cfg->n_envs);
-    if (grid_cap > 0 && grid_cap < grid) grid = grid_cap;
-    hipLaunchKernelGGL(k_policy_pair, dim3(grid), dim3(PTB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
-                       obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
-                       actions_out, seed, step, step_dev, eps_inject);
-    USV_CHECK_LAUNCH();
-    return 0;
-  }
   int grid = policy_grid(cfg->n_envs);
   if (grid_cap > 0 && grid_cap < grid) grid = grid_cap;
   hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,

@@ -91,38 +91,6 @@ def test_policy_step_headline_multi_tile(inject):
     assert float(np.abs(ag.exp_act.cpu().numpy()[other]).max()) == 0.0
 
 
-@pytest.mark.parametrize("n", [100, 4128, HEAD])
-@pytest.mark.parametrize("inject", [True, False], ids=["eps_inject", "philox"])
-def test_policy_pair_kernel_equals_single(n, inject, monkeypatch):
-    """k_policy_pair (two 32-row tiles in flight per workgroup, the default) against k_policy_step
-    (USV_POLICY_PAIR=0): every output of the rollout slot bit for bit -- a partial last tile (100 rows), an odd
-    tile count with a pair whose second group is idle (4,128 = 129 tiles), and the headline size (2,048 pairs
-    over 256 workgroups)."""
-    from omniisaacgymenvs_loop_amd import _capi as c
-    rng = np.random.default_rng(5)
-    t, seed = 3, 99
-    ag, _, _, _ = _rand_agent(n, rng, minibatch=n * H)
-    obs = torch.tensor(rng.normal(0, 2, (n, 33)).astype(np.float32), device=DEV)
-    dprev = torch.tensor((rng.random(n) < 0.1).astype(np.int64), device=DEV)
-    step_dev = torch.tensor([2 ** 20 + 3], device=DEV, dtype=torch.int64)
-    eps = torch.tensor(rng.normal(0, 1, (n, 2)).astype(np.float32), device=DEV) if inject else None
-    outs = []
-    for pair in ("0", "1"):
-        monkeypatch.setenv("USV_POLICY_PAIR", pair)
-        for b in (ag.exp_obs, ag.exp_act, ag.exp_nlp, ag.exp_val, ag.exp_mu, ag.exp_sigma, ag.exp_done, ag.actions):
-            b.fill_(7)
-        c.call("ppo_policy_step", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
-               c.ptr(obs), t, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp), c.ptr(ag.exp_val),
-               c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.exp_done), c.ptr(dprev), c.ptr(ag.actions), seed, 0,
-               c.ptr(step_dev), c.ptr(eps), c.stream_ptr())
-        torch.cuda.synchronize()
-        outs.append([b.cpu().numpy().copy() for b in (ag.exp_obs, ag.exp_act, ag.exp_nlp, ag.exp_val, ag.exp_mu,
-                                                      ag.exp_sigma, ag.exp_done, ag.actions)])
-    for a, b in zip(*outs):
-        np.testing.assert_array_equal(a, b)
-    assert float(np.abs(outs[1][1][np.arange(n) * H + t] - 7).min()) > 0   # the slot was written
-
-
 def test_value_headline_multi_tile():
     """k_value (ppo_value) at 131,072 envs vs the oracle's denormalised value."""
     from omniisaacgymenvs_loop_amd import _capi as c
