@@ -420,7 +420,9 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
  * Together they produce exactly part 0's results (usv_potential_field + usv_env_step). */
 int usv_env_step_late(const usv_cfg_t *cfg, const usv_bufs_t *b, void *stream);
 /* usv_potential_field in two stages: 1 = the reset envs' obstacle placement (k_field_place: the step
- * kernels read the new obstacles), 2 = the cost-to-go sweeps, SDF statistics, batch fold and the fields */
+ * kernels read the new obstacles), 2 = the cost-to-go sweeps, SDF statistics, batch fold and the fields;
+ * stage 2 is also available as its two halves 3 (sweeps, exactness fallback, statistics) then 4 (batch fold,
+ * normalisation constants), so a caller can order other work after the statistics */
 int usv_field_stage(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, void *stream);
 
 /* Planar force/moment model only (no integration), for parity with

@@ -738,7 +738,8 @@ __global__ __launch_bounds__(256) void k_field_view(usv_cfg_t c, usv_bufs_t b, c
 
 namespace {
 // stage 1: the obstacle placement alone (k_field_place); stage 2: the rest after it (sweeps, exactness
-// fallback, statistics, batch fold, final field); 0: usv_potential_field
+// fallback, statistics, batch fold, constants) = stage 3 (sweeps, fallback, statistics) + stage 4 (batch fold,
+// constants)
 int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream_t s) {
   const int grid_b = b->n < 512 ? b->n : 512;
   const int grid_n = (b->n + 255) / 256 < 64 ? (b->n + 255) / 256 : 64;
@@ -748,23 +749,27 @@ int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream
     USV_CHECK_LAUNCH();
     return 0;
   }
-  hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
-  USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
-  USV_CHECK_LAUNCH();
-  const int grid_s = b->n * kBands < 4096 ? b->n * kBands : 4096;
-  hipLaunchKernelGGL(k_field_stats, dim3(grid_s), dim3(256), 0, s, *cfg, *b);
-  USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_batch, dim3(kBatchBlocks), dim3(256), 0, s, *cfg, *b);
-  USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_norm, dim3(grid_n), dim3(256), 0, s, *cfg, *b);
-  USV_CHECK_LAUNCH();
+  if (stage == 2 || stage == 3) {
+    hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
+    USV_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
+    USV_CHECK_LAUNCH();
+    const int grid_s = b->n * kBands < 4096 ? b->n * kBands : 4096;
+    hipLaunchKernelGGL(k_field_stats, dim3(grid_s), dim3(256), 0, s, *cfg, *b);
+    USV_CHECK_LAUNCH();
+  }
+  if (stage == 2 || stage == 4) {
+    hipLaunchKernelGGL(k_field_batch, dim3(kBatchBlocks), dim3(256), 0, s, *cfg, *b);
+    USV_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_field_norm, dim3(grid_n), dim3(256), 0, s, *cfg, *b);
+    USV_CHECK_LAUNCH();
+  }
   return 0;
 }
 }  // namespace
 
 extern "C" int usv_field_stage(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, void *stream) {
-  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field || !b->sdf || !b->fnorm || stage < 1 || stage > 2) return 1;
+  if (!cfg || !b || b->n <= 0 || !b->slot_stats || !b->field || !b->sdf || !b->fnorm || stage < 1 || stage > 4) return 1;
   return field_stages(cfg, b, stage, (hipStream_t)stream);
 }
 

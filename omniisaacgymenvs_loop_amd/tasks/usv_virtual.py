@@ -156,6 +156,7 @@ class USVVirtual:
         # stream for the field kernels and the fork / join events
         self.rstash = Z((DEFINES["USV_RSTASH_ROWS"], n), **f32) if self._has_field else None
         self._side = None
+        self._ev_stats = None
         self._step_pending = False
         self.lut = Z((2, 1000), **f32)
         self.hydro = build_hydro_cfg(self._task_cfg)
@@ -375,9 +376,21 @@ class USVVirtual:
         _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
         self._ev_fork.record(main)
         side.wait_event(self._ev_fork)
-        _capi.call("usv_field_stage", cfg, b, 2, side.cuda_stream)
+        # USV_STATS_FIRST=1: the main stream (the next policy step) waits for the field statistics, which then
+        # run alone instead of beside the policy kernel (A/B knob)
+        stats_first = os.getenv("USV_STATS_FIRST", "0") == "1"
+        if stats_first:
+            if self._ev_stats is None:
+                self._ev_stats = torch.cuda.Event()
+            _capi.call("usv_field_stage", cfg, b, 3, side.cuda_stream)
+            self._ev_stats.record(side)
+            _capi.call("usv_field_stage", cfg, b, 4, side.cuda_stream)
+        else:
+            _capi.call("usv_field_stage", cfg, b, 2, side.cuda_stream)
         _capi.call("usv_env_step_part", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
                    self.seed, k, _capi.ptr(u_step), 3, main.cuda_stream)
+        if stats_first:
+            main.wait_event(self._ev_stats)
         self._ev_early.record(main)
         side.wait_event(self._ev_early)
         _capi.call("usv_env_step_late", cfg, b, side.cuda_stream)
