@@ -814,6 +814,10 @@ constexpr int GTB = 512;          // threads per workgroup
 #ifndef USV_RD_P
 #define USV_RD_P 128
 #endif
+#ifndef USV_RD_NT
+#define USV_RD_NT 1   // non-temporal loads of the partial rows (A/B builds override it)
+#endif
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int RD_TB = 512, RD_P = USV_RD_P;            // threads, slots per workgroup
 constexpr int RD_L = RD_P / 4;                          // lanes per row segment (float4 each)
 constexpr int RD_G = (RD_TB / RD_L);                    // row groups
@@ -964,11 +968,13 @@ struct RowIn {
   float act0, act1, nlp, val, ret, adv, mu0, mu1, sg0, sg1;
 };
 
-// Partial-gradient stores write through to the MALL (sc1): the 85 KB per workgroup leave
-// during the kernel instead of as dirty L2 lines at the kernel boundary (MI355X_MICROARCH.md,
-// publish-large / boundary rows)
+// Partial-gradient stores are non-temporal (nt) and k_reduce_partials reads them with non-temporal
+// loads: the 21.8 MB per minibatch stream through without the reduction leaving their lines in the
+// caches, where the next minibatch's stores to the same rows met them (same-box A/B at 131072 envs,
+// rocprof means of gradient + reduction: sc1 write-through + plain loads 21.08 + 6.31 us, nt + nt loads
+// 18.01 + 6.96; sc1 + nt loads 19.94 + 6.86; nt stores with plain loads, round 2: 21.08 + 7.27)
 #ifndef USV_PART_AUX
-#define USV_PART_AUX 16   // cache-policy bits of the partial stores (A/B builds override it)
+#define USV_PART_AUX 2   // cache-policy bits of the partial stores: nt (A/B builds override it)
 #endif
 struct PartOut {
   __amdgpu_buffer_rsrc_t r;
@@ -1612,7 +1618,15 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     // branch-free: clamped rows / columns loaded, masked in the sum (every load in flight at once)
     float4 x[RD_KB];
 #pragma unroll
-    for (int k = 0; k < RD_KB; ++k) x[k] = P4[(size_t)min(b0 + RD_G * k, nblk - 1) * (NPART_PAD / 4) + p4c];
+    for (int k = 0; k < RD_KB; ++k) {
+      const float4 *src = P4 + (size_t)min(b0 + RD_G * k, nblk - 1) * (NPART_PAD / 4) + p4c;
+#if USV_RD_NT
+      const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(src));   // read once
+      x[k] = make_float4(v[0], v[1], v[2], v[3]);
+#else
+      x[k] = *src;
+#endif
+    }
     // the bias corrections in the shadow of the row loads (they wait on opt_in only)
 #pragma unroll
     for (int k = 0; k < RD_KB; ++k) {
