@@ -160,6 +160,17 @@ __device__ __forceinline__ float fast_tanh(float x) {
 // The persistent forward kernels' obs path: a thread's slots q = tid + u TB of a tile's RB x XS
 // block sit in the same columns for every tile, so the running statistics are loaded once per
 // launch; the next tile's rows are loaded (clamped, unconditionally) while the current one runs.
+// The rollout's experience-buffer stores are non-temporal: the 16 steps' 350 MB at 131072 envs exceed the
+// Infinity Cache and the update reads them only after the rollout, so cached they would only evict the env
+// state the next env step reads (same-box A/B: env step 26.7 -> 24.8 us, rollout and update unchanged)
+#ifndef USV_EXP_NT
+#define USV_EXP_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void exp_st(T *p, T v) {
+  if constexpr (USV_EXP_NT != 0) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 constexpr int NUO = (RB * XS + TB - 1) / TB;
 struct ObsCols {
   double mu[NUO], var[NUO];
@@ -225,7 +236,7 @@ __device__ __forceinline__ void put_obs_tile3(const float (&x)[NUO3], int tt, in
     float v = 0.f;
     if (r < nrows && k < NIN) {
       v = x[u];
-      exp_obs[((size_t)(row0 + r) * H + t) * NIN + k] = v;
+      exp_st(&exp_obs[((size_t)(row0 + r) * H + t) * NIN + k], v);
       if (normalize) v = clampt((v - s.om[k]) / s.od[k], -5.0f, 5.0f);   // = rms_norm
     }
     s.x[q] = v;
@@ -384,12 +395,12 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
         vd = clampt(v, -5.0f, 5.0f);
         vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
       }
-      exp_act[slot * 2] = a0; exp_act[slot * 2 + 1] = a1;
-      exp_mu[slot * 2] = mu0; exp_mu[slot * 2 + 1] = mu1;
-      exp_sigma[slot * 2] = sg0; exp_sigma[slot * 2 + 1] = sg1;
-      exp_nlp[slot] = nlp;
-      exp_val[slot] = vd;
-      exp_done[slot] = (uint8_t)(dones_prev[e] != 0);
+      exp_st(&exp_act[slot * 2], a0); exp_st(&exp_act[slot * 2 + 1], a1);
+      exp_st(&exp_mu[slot * 2], mu0); exp_st(&exp_mu[slot * 2 + 1], mu1);
+      exp_st(&exp_sigma[slot * 2], sg0); exp_st(&exp_sigma[slot * 2 + 1], sg1);
+      exp_st(&exp_nlp[slot], nlp);
+      exp_st(&exp_val[slot], vd);
+      exp_st(&exp_done[slot], (uint8_t)(dones_prev[e] != 0));
       // preprocess_actions: clamp(-1,1) then rescale to [low, high] = identity (a2c_common.py:1134-1144)
       actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
       actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
