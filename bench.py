@@ -335,6 +335,7 @@ def main():
     for _ in range(args.steps):
         agent.update_epoch()
         agent.train_epoch()          # synchronises the stream at its end (meters, adaptive LR)
+        note_reward()                # host-side meter (updated at that sync): the milestones at epoch resolution
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
