@@ -974,6 +974,14 @@ __device__ __forceinline__ int param_of_slot(int s) {
   return -1;
 }
 
+// USV_ROW_NT: the gradient kernel's row inputs (experience rows, read once per mini-epoch) as non-temporal loads
+#ifndef USV_ROW_NT
+#define USV_ROW_NT 0
+#endif
+__device__ __forceinline__ float row_ld(const float *p) {
+  if constexpr (USV_ROW_NT != 0) return __builtin_nontemporal_load(p);
+  else return *p;
+}
 // per-row inputs of the losses (wave 0: lane = row), loaded with the weights
 struct RowIn {
   float act0, act1, nlp, val, ret, adv, mu0, mu1, sg0, sg1;
@@ -1083,11 +1091,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   RowIn ri;
   {
     const size_t row = (size_t)rb0 + (lane & (RB - 1));
-    ri.act0 = e_act[row * 2]; ri.act1 = e_act[row * 2 + 1];
-    ri.nlp = e_nlp[row]; ri.adv = e_adv[row];
-    ri.val = e_val[row]; ri.ret = e_ret[row];
-    ri.mu0 = e_mu[row * 2]; ri.mu1 = e_mu[row * 2 + 1];
-    ri.sg0 = e_sigma[row * 2]; ri.sg1 = e_sigma[row * 2 + 1];
+    ri.act0 = row_ld(&e_act[row * 2]); ri.act1 = row_ld(&e_act[row * 2 + 1]);
+    ri.nlp = row_ld(&e_nlp[row]); ri.adv = row_ld(&e_adv[row]);
+    ri.val = row_ld(&e_val[row]); ri.ret = row_ld(&e_ret[row]);
+    ri.mu0 = row_ld(&e_mu[row * 2]); ri.mu1 = row_ld(&e_mu[row * 2 + 1]);
+    ri.sg0 = row_ld(&e_sigma[row * 2]); ri.sg1 = row_ld(&e_sigma[row * 2 + 1]);
   }
   // obs rows and the running statistics (always loaded; obs_rms is non-null, checked on the host)
   constexpr int NU = (RB * XS + GTB - 1) / GTB;
@@ -1096,7 +1104,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int q = min(tid + u * GTB, RB * XS - 1), r = q / XS, kc = min(q % XS, NIN - 1);
-    xo[u] = e_obs[(size_t)(rb0 + r) * NIN + kc];
+    xo[u] = row_ld(&e_obs[(size_t)(rb0 + r) * NIN + kc]);
     mu[u] = obs_rms[kc];
     var[u] = obs_rms[NIN + kc];
   }
