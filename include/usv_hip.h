@@ -732,10 +732,12 @@ int lz_grad_floats(int obs_dim);
 
 /* library version */
 int usv_hip_version(void);
-/* the layout constants this library was compiled with (USV_FIELD_STRIDE, USV_FIELD_TH, USV_FIELD_TW, PPO_NPARAM,
- * USV_FNORM, USV_RSTASH_ROWS, USV_CTL_N, USV_NSTAT) folded into one key, k = k * 1000003 + v in that order (mod
- * 2^63): a binding that allocates from this header compares it with the same fold of its own constants before
- * its first call, so a library built from another layout fails loudly instead of addressing past a buffer */
+/* the layout this library was compiled with: every object-like integer #define of this header (except the
+ * include guard), every enumerator, and sizeof / offsetof of every field of every struct above, in header order,
+ * each folded with its name: k = k * 1000003 + fnv1a(name), k = k * 1000003 + value (mod 2^64, top bit cleared).
+ * A binding that allocates from this header compares it with the same fold of its own parse before its first
+ * call (omniisaacgymenvs_loop_amd/_abi.py layout_entries), so a library built from another layout fails loudly
+ * instead of addressing past a buffer */
 long long usv_hip_layout_key(void);
 
 #ifdef __cplusplus

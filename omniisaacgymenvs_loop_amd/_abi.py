@@ -124,6 +124,91 @@ def enum_values(enum_name: str) -> dict:
 STAT_KEYS_ENUM = enum_values("usv_stat_key")
 PEN = enum_values("usv_pen_kind")
 
+# ---- buffer / ABI layout key -------------------------------------------------------------------
+# Every object-like integer #define of the header, every enumerator, and sizeof + offsetof of every
+# field of every ABI struct, in header order.  libusv_hip.so folds the same list (compiled from
+# csrc/usv_layout_gen.h, which gen_layout_header() writes from this function) into
+# usv_hip_layout_key(); _capi.lib() refuses a library whose key differs from layout_key() here, so a
+# library built from another header -- a moved slab row, a resized buffer, a reordered struct --
+# fails loudly before its first call instead of addressing past a buffer.
+LAYOUT_STRUCTS = ("usv_cfg", "usv_bufs", "usv_hydro", "ppo_cfg", "ppo_adam_banks", "ppo_dp", "lz_cfg")
+LAYOUT_ENUMS = ("usv_stat_key", "usv_pen_kind", "usv_dist_row")
+_STRUCT_CLASSES = {"usv_cfg": UsvCfg, "usv_bufs": UsvBufs, "usv_hydro": UsvHydro, "ppo_cfg": PpoCfg,
+                   "ppo_adam_banks": PpoAdamBanks, "ppo_dp": PpoDp, "lz_cfg": LzCfg}
+GUARD_DEFINES = ("USV_HIP_H",)
+
+
+def header_int_defines() -> list:
+    """(name, value) of every object-like #define of the header with an integer value, in order
+    (C integer division for '/'); the include guard excluded."""
+    out, env = [], {}
+    for line in _TXT.splitlines():
+        m = re.match(r"\s*#define\s+(\w+)(?:\s+(.*?))?\s*$", line)
+        if not m or m.group(1) in GUARD_DEFINES:
+            continue
+        name, val = m.group(1), (m.group(2) or "")
+        if "(" in name or not val:
+            raise RuntimeError(f"{HEADER}: #define {name} has no integer value (layout key)")
+        v = int(eval(val.replace("/", "//"), {}, dict(env)))
+        env[name] = v
+        out.append((name, v))
+    return out
+
+
+def layout_entries() -> list:
+    """The layout list as (C expression, name, value) in fold order."""
+    ent = [(n, n, v) for n, v in header_int_defines()]
+    for e in LAYOUT_ENUMS:
+        ent += [(k, k, v) for k, v in enum_values(e).items()]
+    for s in LAYOUT_STRUCTS:
+        cls = _STRUCT_CLASSES[s]
+        ent.append((f"sizeof({s}_t)", f"sizeof {s}", ctypes.sizeof(cls)))
+        for fname, _ in cls._fields_:
+            ent.append((f"offsetof({s}_t, {fname})", f"{s}.{fname}", getattr(cls, fname).offset))
+    return ent
+
+
+def fnv1a(s: str) -> int:
+    h = 1469598103934665603
+    for ch in s.encode():
+        h = ((h ^ ch) * 1099511628211) % (1 << 64)
+    return h
+
+
+def layout_key_of(entries) -> int:
+    """k = k * 1000003 + fnv1a(name), then k = k * 1000003 + value, per entry (mod 2^64), top bit cleared."""
+    k = 0
+    for _, name, v in entries:
+        k = (k * 1000003 + fnv1a(name)) % (1 << 64)
+        k = (k * 1000003 + (v % (1 << 64))) % (1 << 64)
+    return k & ((1 << 63) - 1)
+
+
+def layout_header_text() -> str:
+    lines = ["/* generated from include/usv_hip.h by omniisaacgymenvs_loop_amd/_abi.py (gen_layout_header): do not edit.",
+             " * X(expression, \"name\") for every entry of usv_hip_layout_key() in fold order. */",
+             "#define USV_LAYOUT_ENTRIES(X) \\"]
+    lines += [f"  X({expr}, \"{name}\") \\" for expr, name, _ in layout_entries()]
+    lines.append("")
+    return "\n".join(lines) + "\n"
+
+
+LAYOUT_GEN = os.path.join(_HERE, "csrc", "usv_layout_gen.h")
+
+
+def gen_layout_header(path: str = LAYOUT_GEN) -> bool:
+    """Write csrc/usv_layout_gen.h if its text differs from the header's; True when rewritten."""
+    txt = layout_header_text()
+    try:
+        with open(path, "r", encoding="utf-8") as f:
+            if f.read() == txt:
+                return False
+    except FileNotFoundError:
+        pass
+    with open(path, "w", encoding="utf-8") as f:
+        f.write(txt)
+    return True
+
 # episode_sums key names in reference order (USV_Virtual.py:586-601)
 STAT_NAMES = [
     "total_reward", "distance_reward", "alignment_reward", "heading_improve_reward",

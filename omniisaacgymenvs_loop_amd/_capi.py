@@ -22,7 +22,8 @@ LIB_PATH = os.path.join(LIB_DIR, "libusv_hip.so")
 # instrumented build (per-workgroup phase timestamps, tools/phase_probe.py); selected with USV_HIP_PROBE=1
 PROBE_LIB_PATH = os.path.join(LIB_DIR, "libusv_hip_probe.so")
 SOURCES = [os.path.join(HERE, "csrc", f) for f in ("usv_env.hip", "usv_field.hip", "ppo.hip", "loopz.hip")]
-DEPS = SOURCES + [os.path.join(HERE, "csrc", "usv_device.h"), os.path.join(ROOT, "include", "usv_hip.h")]
+DEPS = SOURCES + [os.path.join(HERE, "csrc", "usv_device.h"), os.path.join(HERE, "csrc", "usv_layout_gen.h"),
+                  os.path.join(ROOT, "include", "usv_hip.h")]
 
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
                # no implicit FMA contraction: the arithmetic follows the reference op by op
@@ -34,6 +35,8 @@ _lib = None
 def build(force: bool = False, verbose: bool = False, probe: bool = False) -> str:
     """Compile the HIP kernels for gfx950 into lib/libusv_hip.so (in-tree)."""
     os.makedirs(LIB_DIR, exist_ok=True)
+    from ._abi import gen_layout_header
+    gen_layout_header()   # csrc/usv_layout_gen.h follows the header (rewritten only when its text changes)
     out = PROBE_LIB_PATH if probe else LIB_PATH
     if not force and os.path.exists(out):
         lib_m = os.path.getmtime(out)
@@ -102,17 +105,11 @@ def _declare(lib):
     return lib
 
 
-LAYOUT_KEYS = ("USV_FIELD_STRIDE", "USV_FIELD_TH", "USV_FIELD_TW", "PPO_NPARAM", "USV_FNORM", "USV_RSTASH_ROWS",
-               "USV_CTL_N", "USV_NSTAT")
-
-
 def layout_key() -> int:
-    """usv_hip_layout_key() of include/usv_hip.h as this binding's constants give it."""
-    from ._abi import DEFINES
-    k = 0
-    for name in LAYOUT_KEYS:
-        k = (k * 1000003 + int(DEFINES[name])) % (1 << 64)
-    return k & ((1 << 63) - 1)
+    """usv_hip_layout_key() as this binding's parse of include/usv_hip.h gives it: every integer #define,
+    every enumerator, sizeof / offsetof of every ABI struct field (_abi.layout_entries)."""
+    from ._abi import layout_entries, layout_key_of
+    return layout_key_of(layout_entries())
 
 
 def lib():

@@ -18,9 +18,11 @@
 //   envs/USV/{Hydrodynamics,ThrusterDynamics}.py  damping + thruster LUT/lag
 // The rigid-body integrator replaces PhysX (no reference implementation).
 #include "usv_device.h"
+#include "usv_layout_gen.h"
 
 #include <algorithm>
 #include <cmath>
+#include <cstddef>
 
 namespace {
 
@@ -1918,11 +1920,20 @@ int usv_hydrostatics(const usv_hydro_t *h, int n, const float *quat, const float
 
 int usv_hip_version(void) { return 1; }
 
+// Every integer #define, enumerator and ABI struct size / field offset of include/usv_hip.h (the generated
+// list csrc/usv_layout_gen.h, in header order), folded with its name: see _abi.layout_key_of.
+static unsigned long long fnv1a(const char *s) {
+  unsigned long long h = 1469598103934665603ull;
+  for (; *s; ++s) h = (h ^ (unsigned char)*s) * 1099511628211ull;
+  return h;
+}
 long long usv_hip_layout_key(void) {
-  const long long v[] = {USV_FIELD_STRIDE, USV_FIELD_TH, USV_FIELD_TW, PPO_NPARAM, USV_FNORM, USV_RSTASH_ROWS, USV_CTL_N,
-                         USV_NSTAT};
   unsigned long long k = 0;
-  for (long long x : v) k = k * 1000003ull + (unsigned long long)x;
+#define USV_LAYOUT_FOLD(expr, name)                                    \
+  k = k * 1000003ull + fnv1a(name);                                    \
+  k = k * 1000003ull + (unsigned long long)(long long)(expr);
+  USV_LAYOUT_ENTRIES(USV_LAYOUT_FOLD)
+#undef USV_LAYOUT_FOLD
   return (long long)(k & 0x7fffffffffffffffull);
 }
 

@@ -50,3 +50,43 @@ def test_library_layout_key_matches_the_header():
     lib = ctypes.CDLL(_capi.LIB_PATH)
     lib.usv_hip_layout_key.restype = ctypes.c_longlong
     assert lib.usv_hip_layout_key() == _capi.layout_key()
+
+
+def test_layout_key_covers_every_define_enum_and_struct_of_the_header():
+    """usv_hip_layout_key folds EVERY object-like #define of include/usv_hip.h (slab rows, field / PPO / ctl
+    constants, ...), every enumerator and sizeof / offsetof of every field of every ABI struct: a library built
+    from another header -- e.g. a moved USV_SLAB_* row, the stale library behind round 3's status-800 fault --
+    is refused before its first call.  The compiled list (csrc/usv_layout_gen.h) is the header's, current."""
+    from omniisaacgymenvs_loop_amd import _abi
+    src = re.sub(r"/\*.*?\*/", " ", open(HEADER).read(), flags=re.S)
+    defines = set(re.findall(r"^\s*#define\s+(\w+)", src, flags=re.M)) - set(_abi.GUARD_DEFINES)
+    names = {name for _, name, _ in _abi.layout_entries()}
+    assert defines <= names, f"defines outside the layout key: {sorted(defines - names)}"
+    assert {n for n in defines if n.startswith("USV_SLAB_")} and all(
+        n in names for n in defines if n.startswith(("USV_SLAB_", "USV_FIELD_", "PPO_", "USV_CTL_", "USV_N")))
+    structs = set(re.findall(r"typedef\s+struct\s+(\w+)\s*\{", src))
+    assert structs == set(_abi.LAYOUT_STRUCTS), structs ^ set(_abi.LAYOUT_STRUCTS)
+    for s in structs:
+        cls = _abi._STRUCT_CLASSES[s]
+        assert f"sizeof {s}" in names and all(f"{s}.{f}" in names for f, _ in cls._fields_)
+    enums = set(re.findall(r"enum\s+(\w+)\s*\{", src))
+    assert enums == set(_abi.LAYOUT_ENUMS)
+    for e in enums:
+        assert set(_abi.enum_values(e)) <= names
+    with open(_abi.LAYOUT_GEN) as f:
+        assert f.read() == _abi.layout_header_text(), "csrc/usv_layout_gen.h is stale: run _capi.build()"
+
+
+def test_layout_key_changes_with_any_entry():
+    """Moving one slab row, resizing one struct or renaming one define changes the key."""
+    from omniisaacgymenvs_loop_amd import _abi
+    ent = _abi.layout_entries()
+    k0 = _abi.layout_key_of(ent)
+    i_slab = next(i for i, e in enumerate(ent) if e[1] == "USV_SLAB_STATS")
+    i_size = next(i for i, e in enumerate(ent) if e[1] == "sizeof usv_cfg")
+    for i, (expr, name, v) in ((i_slab, (ent[i_slab][0], ent[i_slab][1], ent[i_slab][2] + 1)),
+                               (i_size, (ent[i_size][0], ent[i_size][1], ent[i_size][2] + 4)),
+                               (0, (ent[0][0], ent[0][1] + "_X", ent[0][2]))):
+        mod = list(ent)
+        mod[i] = (expr, name, v)
+        assert _abi.layout_key_of(mod) != k0
