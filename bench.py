@@ -36,6 +36,7 @@ BF16_PEAK_TFS = 2500.0         # MI355X dense bf16 MFMA peak (same table, no spa
 # are the tiled raw costs (16 B) + the env's 8 normalisation constants (32 B; the field is
 # kept as its parts), 357 + 32 = 389 B.
 ENV_STEP_BYTES = 702
+SURVEY_STEP_BYTES = 476        # SURVEY §8(d)'s algorithmic bytes of the fused env step (the roofline's frac_476)
 # --task: packaged task yamls and the algorithmic bytes per env-step of their step kernels
 # (k_env_step_task): GoToPose 221 B read + 309 B written; TrackXYOVelocity
 # 221 + 293 in the first launch and 32 + 28 in k_track_finish
@@ -271,7 +272,8 @@ def main():
     task_name = args.task if args.task != "multitask" else ("GoToPose", "TrackXYOVelocity")[rank % 2]
     step_bytes, step_kernel = TASKS[task_name][1], TASKS[task_name][2]
     t_start = time.perf_counter()
-    env, task, agent = build(args.envs, local, world, args.seed + rank, task_name, args.mixed_precision)
+    # (the task adds LOCAL_RANK to the seed itself on several ranks, task_util.initialize_task)
+    env, task, agent = build(args.envs, local, world, args.seed, task_name, args.mixed_precision)
     agent.use_graph = not args.no_graph
     from omniisaacgymenvs_loop_amd import _capi
 
@@ -331,6 +333,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    agent.phase_events = []          # (start, rollout end, update end) events recorded inside each timed epoch
     t0 = time.perf_counter()
     for _ in range(args.steps):
         agent.update_epoch()
@@ -345,16 +348,30 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     note_reward()
+    timed_events, agent.phase_events = agent.phase_events, None
+    epoch_timed_last = agent.epoch_num
     frames = world * args.envs * agent.horizon_length * args.steps
     value = frames / elapsed
     print(f"[bench] rank {rank}: {args.steps} epochs in {elapsed:.3f} s -> {value / 1e6:.2f} M env-steps/s",
           file=sys.stderr, flush=True)
 
-    # phase split of one epoch with graph replays: rollout (+ GAE/prepare) vs minibatch update
-    # device time only: a spin kernel ahead of the first event keeps the GPU busy while the host submits both
-    # graphs, so neither pair holds host launch latency (the epoch's remaining host-side share is
-    # ms_per_step - rollout_ms - update_ms, reported as host_gap_ms)
+    # phase split of the TIMED epochs: rollout (+ GAE/prepare) vs minibatch update from the HIP events each
+    # timed epoch recorded around its two halves on the stream (the intervals hold whatever the GPU did or
+    # waited for between the events, host submission included); host_gap_ms = the rest of the timed epoch
+    # (the epoch-end synchronisation, meters, the next submission), >= 0 by construction
     phase = {}
+    if timed_events:
+        rp = [a.elapsed_time(b) for a, b, _ in timed_events]
+        up = [b.elapsed_time(c) for _, b, c in timed_events]
+        phase = {"rollout_ms": sum(rp) / len(rp), "update_ms": sum(up) / len(up),
+                 "update_us_per_minibatch": sum(up) / len(up) * 1e3 / (agent.mini_epochs_num * agent.num_minibatches),
+                 "host_gap_ms": elapsed / args.steps * 1e3 - (sum(rp) + sum(up)) / len(rp),
+                 "rollout_ms_min_max": [min(rp), max(rp)], "update_ms_min_max": [min(up), max(up)],
+                 "phase_method": f"HIP events recorded on the stream inside each of the {len(rp)} timed epochs "
+                                 f"(epochs {epoch_timed_last - len(rp) + 1}-{epoch_timed_last}) around the rollout "
+                                 "(+ GAE / prepare) and the update; mean over the timed epochs"}
+    # the same two graphs replayed behind a spin kernel after the timed epochs: device time only (no host
+    # submission inside the pairs), at a later training state (more resets per step as the policy learns)
     if agent._graph_play is not None and agent._graph_update is not None:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         tp = tu = 0.0
@@ -370,10 +387,11 @@ def main():
             agent._advance_host_clocks()
             tp += ev[0].elapsed_time(ev[1])
             tu += ev[1].elapsed_time(ev[2])
-        phase = {"rollout_ms": tp / nrep, "update_ms": tu / nrep,
-                 "update_us_per_minibatch": tu / nrep * 1e3 / (agent.mini_epochs_num * agent.num_minibatches),
-                 "host_gap_ms": elapsed / args.steps * 1e3 - (tp + tu) / nrep,
-                 "phase_method": "device time of graph replays behind a spin kernel (host submission excluded)"}
+        phase["device_only"] = {"rollout_ms": tp / nrep, "update_ms": tu / nrep,
+                                "update_us_per_minibatch": tu / nrep * 1e3 / (agent.mini_epochs_num * agent.num_minibatches),
+                                "epochs": [epoch_timed_last + 1, epoch_timed_last + nrep],
+                                "method": "graph replays behind a spin kernel after the timed epochs (host "
+                                          "submission excluded), mean of 3"}
 
     # per-launch kernel times inside real epochs (eager: graph replays carry no per-kernel events),
     # HIP events on the launch stream around each C-ABI call
@@ -384,6 +402,7 @@ def main():
     overlap_env = os.environ.get("USV_STEP_OVERLAP")
     os.environ["USV_STEP_OVERLAP"] = "0"
     timing[0] = True
+    timing_after_epoch = agent.epoch_num
     agent.train_epoch()
     torch.cuda.synchronize()
     timing[0] = False
@@ -444,7 +463,11 @@ def main():
             "fps_step_inference": play_fps, "fps_step_env_only": env_fps,
             "roofline": {"bound": "hbm", "kernel": step_kernel,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "traffic": None, "bytes_per_env_step": step_bytes, "launch_ms": env_ms,
+                         "traffic": None, "bytes_per_env_step": step_bytes,
+                         # SURVEY 8(d)'s fused-step figure (no episode-sum read-modify-writes, no field constants)
+                         "frac_476": SURVEY_STEP_BYTES * args.envs / (env_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "achieved_476": SURVEY_STEP_BYTES * args.envs / (env_ms * 1e-3) / 1e9,
+                         "launch_ms": env_ms, "timed_after_epoch": timing_after_epoch,
                          "launch_ms_raw": env_timer.raw_ms(), "event_overhead_ms": env_timer.overhead_ms(),
                          "resets_per_step": (sorted(int(r.item()) for r in resets) or [None])[len(resets) // 2],
                          "envs_per_launch": args.envs,
@@ -487,12 +510,14 @@ def main():
                 tr = json.load(f)
             if tr.get("envs") == args.envs:
                 out["roofline"]["traffic"] = tr.get("bytes_per_launch")
+                out["roofline"]["traffic_read"] = tr.get("read_bytes_per_launch")
+                out["roofline"]["traffic_write"] = tr.get("write_bytes_per_launch")
                 out["roofline"]["traffic_source"] = tr.get("source")
     # secondary line: BASELINE configs[1] (4096 envs/GPU), same code path, graph-replayed epochs
     if args.c2_steps and args.envs != C2_ENVS and task_name == "CaptureXY":
         del agent, env, task
         torch.cuda.empty_cache()
-        env2, task2, agent2 = build(C2_ENVS, local, world, args.seed + rank, task_name)
+        env2, task2, agent2 = build(C2_ENVS, local, world, args.seed, task_name)
         agent2.use_graph = not args.no_graph
         agent2.obs = agent2.env_reset()
         for _ in range(3):

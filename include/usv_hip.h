@@ -213,6 +213,7 @@ typedef struct usv_cfg {
 #define USV_NAN_REWARD   4   /* reward.rew_buf             USV_Virtual.py:1642-1648 */
 #define USV_NAN_OBS      8   /* obs(post_physics_step)     vec_env_rlgames.py:187-192 */
 #define USV_NAN_POLICY  16   /* policy mu / value of the rollout (get_action_values) */
+#define USV_NAN_EXTRAS  32   /* extras["episode"][key] NaN before masking   USV_Virtual.py:1601-1605 */
 
 #define USV_TASK_CAPTURE_XY   0
 #define USV_TASK_GO_TO_POSE   1

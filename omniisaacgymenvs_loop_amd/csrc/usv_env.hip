@@ -412,6 +412,8 @@ __global__ __launch_bounds__(kBlock) void k_extras_fold(usv_cfg_t c, usv_bufs_t 
       for (int kk = 1; kk < 8; ++kk) tot += fold[kk][qs];
       float m = tot / (float)count;
       if (qs != ST_SUCCESS && qs != ST_COLLISION) m = m / (float)c.max_episode_length;
+      // USV_NAN_PROBE: the reference raises on a NaN extra before zeroing it (USV_Virtual.py:1601-1605)
+      if (c.nan_probe && isnan(m)) atomicOr(&b.ctl[USV_CTL_NAN_FLAG], (int)USV_NAN_EXTRAS);
       b.extras[qs] = isnan(m) ? 0.f : m;
     }
   }

@@ -47,6 +47,7 @@
   X(USV_NAN_REWARD, "USV_NAN_REWARD") \
   X(USV_NAN_OBS, "USV_NAN_OBS") \
   X(USV_NAN_POLICY, "USV_NAN_POLICY") \
+  X(USV_NAN_EXTRAS, "USV_NAN_EXTRAS") \
   X(USV_TASK_CAPTURE_XY, "USV_TASK_CAPTURE_XY") \
   X(USV_TASK_GO_TO_POSE, "USV_TASK_GO_TO_POSE") \
   X(USV_TASK_TRACK_XYO, "USV_TASK_TRACK_XYO") \

@@ -115,8 +115,11 @@ class PPO:
         """ppo.py:102-141 (numpy in, numpy actions out)."""
         return self.observe_device(torch.from_numpy(np.ascontiguousarray(actor_obs, np.float32))).cpu().numpy()
 
-    def step_device(self, rews: torch.Tensor, dones: torch.Tensor, infos=()):
-        """ppo.py:143-153: values were formed in observe_device; stores rewards / dones."""
+    def step_device(self, rews: torch.Tensor, dones: torch.Tensor, infos=(), valid=None):
+        """ppo.py:143-153: values were formed in observe_device; stores rewards / dones.  `valid` (a device
+        bool, nullable): the infos count only if it holds -- the trainer passes dones.any() so that the
+        reference's "infos only on a step where some env is done" (rlgames_train.py:440-456) is decided at
+        log time, once per update, instead of by a host sync every step."""
         st = self.storage
         r = rews.to(self.params.device, torch.float32).contiguous()
         d = dones.to(self.params.device, torch.int64).contiguous()
@@ -133,9 +136,15 @@ class PPO:
                 keys = list(ep.keys())
                 vals = [ep[k] for k in keys]
                 if keys and all(torch.is_tensor(v) and v.numel() == 1 for v in vals):
-                    self.ep_infos.append((keys, torch.stack([v.reshape(()).float() for v in vals])))
+                    self.ep_infos.append((keys, torch.stack([v.reshape(()).float() for v in vals]), valid))
                 else:
-                    self.ep_infos.append((keys, vals))
+                    self.ep_infos.append((keys, vals, valid))
+
+    def _valid_ep_infos(self):
+        """The episode infos whose step had a done env (one host read of all the step flags)."""
+        flags = [v for _, _, v in self.ep_infos if torch.is_tensor(v)]
+        got = iter(torch.stack([f.reshape(()).bool() for f in flags]).cpu().tolist()) if flags else iter(())
+        return [(k, v) for k, v, f in self.ep_infos if (next(got) if torch.is_tensor(f) else f is None or bool(f))]
 
     def step(self, value_obs, rews, dones, infos):
         self.step_device(torch.as_tensor(np.asarray(rews, np.float32)), torch.as_tensor(np.asarray(dones).astype(np.int64)),
@@ -153,8 +162,10 @@ class PPO:
                    _capi.ptr(self.work), s)
         self.mean_value_loss, self.mean_surrogate_loss = self._train_step()
         st.clear()
-        if log_this_iteration and len(self.ep_infos) > 0:
-            self.log(update)
+        if log_this_iteration and self.ep_infos:
+            self.ep_infos = self._valid_ep_infos()
+            if len(self.ep_infos) > 0:
+                self.log(update)
         self.ep_infos.clear()
 
     def inject_batches(self, batches):
@@ -226,10 +237,11 @@ class PPO:
         values skipped, as _to_float / np.isfinite there), then the losses and the action noise."""
         self.tot_timesteps += self.num_transitions_per_env * self.num_envs
         ep_string = ""
-        if self.ep_infos:
-            keys = self.ep_infos[0][0]
+        infos = [e[:2] for e in self.ep_infos]
+        if infos:
+            keys = infos[0][0]
             rows = []
-            for ks, v in self.ep_infos:
+            for ks, v in infos:
                 v = v.cpu().numpy() if torch.is_tensor(v) else np.array(
                     [float(x.item()) if torch.is_tensor(x) else float(x) for x in v], np.float64)
                 rows.append(dict(zip(ks, v.tolist())))

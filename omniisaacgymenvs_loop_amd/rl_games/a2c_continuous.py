@@ -226,6 +226,7 @@ class A2CAgent:
         self._graph_play = None
         self._graph_update = None
         self._eager_epochs = 0
+        self.phase_events = None      # bench: per-epoch (start, rollout end, update end) HIP events
         self.algo_observer.after_init(self)
 
     def _obs_in(self, obs: torch.Tensor) -> torch.Tensor:
@@ -298,7 +299,7 @@ class A2CAgent:
         if os.getenv("USV_DP_EXCHANGE", "peer") == "collective":
             return None
         ex, err = None, None
-        try:
+        try:   # every rank succeeds or every rank raises (PeerExchange agrees over the ranks itself)
             ex = dist_util.PeerExchange(self.rank, self.rank_size, self.ppo_device,
                                         timeout_ms=int(os.getenv("USV_DP_TIMEOUT_MS", "20000")))
         except RuntimeError as e:
@@ -468,8 +469,9 @@ class A2CAgent:
         collectives runs eagerly."""
         if getattr(self, "_graph_update_failed", False):
             return False
-        if not self.multi_gpu or self.rank_size == 1 or self._dp is not None:
+        if not self.multi_gpu or self.rank_size == 1 or (self._dp is not None and self._fused_update()):
             return True   # (the peer exchange is kernels only)
+        # the split path's torch.distributed all-reduces (no peer exchange, or USV_PPO_FUSED=0)
         return dist_util.backend() == "nccl" and os.getenv("USV_GRAPH_COLLECTIVES", "0") == "1"
 
     def _ranks_agree(self, ok: bool) -> bool:
@@ -477,9 +479,7 @@ class A2CAgent:
         falls back to eager collectives."""
         if not self.multi_gpu or self.rank_size == 1:
             return ok
-        flag = torch.tensor([1.0 if ok else 0.0], device="cpu" if dist.get_backend() == "gloo" else self.ppo_device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        return bool(flag.item() == 1.0)
+        return dist_util.agree(ok, self.ppo_device)
 
     def _graph_capture(self, fn):
         g = torch.cuda.CUDAGraph()
@@ -503,6 +503,12 @@ class A2CAgent:
         """ContinuousA2CBase.train_epoch (a2c_common.py:1152-1255)."""
         self.vec_env.set_train_info(self.frame, self)
         play_time_start = time.time()
+        # phase_events (bench): a list that receives (start, rollout end, update end) HIP events of this epoch,
+        # recorded on the stream in the epoch itself (no extra synchronisation)
+        pev = None
+        if self.phase_events is not None:
+            pev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            pev[0].record()
         graphs = self.use_graph and self._eager_epochs >= 1
         if graphs:
             if self._graph_play is None:
@@ -515,6 +521,8 @@ class A2CAgent:
         else:
             batch = self._play_and_prepare()
         play_time_end = time.time()
+        if pev is not None:
+            pev[1].record()
         self.curr_frames = batch["played_frames"]
         self.algo_observer.after_steps()
         if graphs and self._update_capturable():
@@ -537,6 +545,9 @@ class A2CAgent:
                 self._graph_update.replay()
         else:
             self.update_epoch_minibatches()
+        if pev is not None:
+            pev[2].record()
+            self.phase_events.append(tuple(pev))
         torch.cuda.current_stream().synchronize()
         update_time_end = time.time()
         chk = getattr(self.vec_env, "check_errors", None)   # device-flagged env errors (scene replay, NaN probe)

@@ -127,10 +127,18 @@ def grad_scaler_state(steps: float) -> Dict[str, Any]:
     """torch.cuda.amp.GradScaler().state_dict() as the reference's mixed_precision run leaves it after `steps`
     optimizer steps with finite gradients (a2c_common.py:243, 326-330, 631): init scale 2**16, doubled every
     2000 consecutive finite steps.  The bf16 GEMM mode needs no loss scaling (bf16 keeps fp32's exponent range)
-    and its non-finite guard is the NaN probe, so the entry is bookkeeping for checkpoint compatibility."""
-    steps = int(steps)
-    return {"scale": 65536.0 * 2.0 ** (steps // 2000), "growth_factor": 2.0, "backoff_factor": 0.5,
+    and its non-finite guard is the NaN probe, so the entry is bookkeeping for checkpoint compatibility.
+    The growth is capped at GRAD_SCALE_MAX: a real fp16 run backs off long before (scaled fp16 gradients overflow),
+    and an uncapped power would leave the fp32 range after ~224k steps (a reference GradScaler loading it would
+    hold an inf scale and skip every step) and raise OverflowError past ~2M steps."""
+    steps = max(int(steps), 0)
+    doublings = min(steps // 2000, GRAD_SCALE_MAX_DOUBLINGS)
+    return {"scale": 65536.0 * 2.0 ** doublings, "growth_factor": 2.0, "backoff_factor": 0.5,
             "growth_interval": 2000, "_growth_tracker": steps % 2000}
+
+
+GRAD_SCALE_MAX_DOUBLINGS = 8        # 2**16 init -> at most 2**24
+GRAD_SCALE_MAX = 65536.0 * 2.0 ** GRAD_SCALE_MAX_DOUBLINGS
 
 
 def safe_filesystem_op(func, *args, **kwargs):

@@ -65,8 +65,12 @@ class PeerExchange:
     reduction kernel -- no collective call, nothing the host launches between kernels, so the update is one
     HIP graph on every rank.  `peers` (tests) replaces the handle exchange by buffers of this process.
 
-    Raises RuntimeError when a buffer cannot be mapped (no peer access); A2CAgent then agrees with the other
-    ranks to fall back to torch.distributed collectives."""
+    Set-up is a fixed sequence of collectives that every rank runs whatever fails locally: a rank whose
+    allocation failed still takes part in the handle exchange (with an empty handle), the ranks agree (MIN
+    all-reduce) after the mapping and again after the start-up self-test, and on any failure every rank
+    unmaps the peers' buffers, waits at a barrier (no peer can still write into or hold a mapping of its
+    buffer) and only then frees its own -- then every rank raises RuntimeError, and A2CAgent falls back to
+    torch.distributed collectives on all of them."""
 
     SELFTEST_ROUNDS = 4
 
@@ -78,31 +82,43 @@ class PeerExchange:
         if not 1 <= world_size <= DEFINES["PPO_DP_MAX"]:
             raise RuntimeError(f"PeerExchange: world size {world_size} > PPO_DP_MAX")
         lib = _capi.lib()
-        self.rank, self.world = rank, world_size
+        self.rank, self.world, self.device = rank, world_size, device
         self._lib = lib
         self._own = ctypes.c_void_p()
         self._opened = []
         handle = ctypes.create_string_buffer(64)
-        _capi.call("ppo_dp_alloc", ctypes.byref(self._own), handle)
+        rc = lib.ppo_dp_alloc(ctypes.byref(self._own), handle)
+        alloc_ok = rc == 0 and bool(self._own.value)
+        if not alloc_ok:
+            self._own = None
         ptrs = [None] * world_size
-        ptrs[rank] = self._own.value
         if peers is not None:       # in-process "ranks" (tests): the other buffers are plain device pointers
+            if not alloc_ok:
+                raise RuntimeError(f"PeerExchange: ppo_dp_alloc failed (status {rc})")
+            ptrs[rank] = self._own.value
             for r, p in enumerate(peers):
                 if r != rank:
                     ptrs[r] = int(p)
         else:
             handles = [None] * world_size
-            dist.all_gather_object(handles, bytes(handle.raw))
-            for r in range(world_size):
-                if r == rank:
-                    continue
-                p = ctypes.c_void_p()
-                rc = lib.ppo_dp_open(ctypes.create_string_buffer(handles[r], 64), ctypes.byref(p))
-                if rc != 0:
-                    self.close()
-                    raise RuntimeError(f"PeerExchange: cannot map rank {r}'s buffer (ppo_dp_open status {rc})")
-                self._opened.append(p.value)
-                ptrs[r] = p.value
+            dist.all_gather_object(handles, bytes(handle.raw) if alloc_ok else b"")
+            why = None
+            if any(h is None or len(h) != 64 for h in handles):
+                why = "a rank could not allocate its receive buffer (ppo_dp_alloc)"
+            else:
+                ptrs[rank] = self._own.value
+                for r in range(world_size):
+                    if r == rank:
+                        continue
+                    p = ctypes.c_void_p()
+                    rc = lib.ppo_dp_open(ctypes.create_string_buffer(handles[r], 64), ctypes.byref(p))
+                    if rc != 0:
+                        why = f"cannot map rank {r}'s buffer (ppo_dp_open status {rc})"
+                        break
+                    self._opened.append(p.value)
+                    ptrs[r] = p.value
+            if not agree(why is None, device):
+                self._fail(why or "another rank could not allocate or map a peer buffer")
         self.clock = torch.zeros(1, device=device, dtype=torch.int32)
         self.err = torch.zeros(1, device=device, dtype=torch.int32)
         d = PpoDp()
@@ -114,24 +130,39 @@ class PeerExchange:
         if peers is None and world_size > 1:
             self._selftest(selftest_ms)
 
+    def _fail(self, why: str) -> None:
+        """Every rank calls this together (after an agreement): unmap, barrier, free, raise."""
+        for p in self._opened:
+            self._lib.ppo_dp_close(ctypes_void(p))
+        self._opened = []
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()          # every rank has unmapped our buffer and finished its kernels on it
+        self.close()
+        raise RuntimeError(f"PeerExchange: {why}")
+
     def _selftest(self, timeout_ms: int) -> None:
         """Every rank runs the same exchange kernel on a known payload (ppo_dp_selftest) right after the handles
         went around: a flag that never arrives (no peer access over xGMI) or a payload that arrives wrong or stale
-        (a receive buffer whose remote writes the reader does not see) raises here, before any training, so the
-        agent's rank agreement falls back to collectives instead of a run that times out per minibatch."""
+        (a receive buffer whose remote writes the reader does not see) fails the test on some rank, the ranks
+        agree on it before any training, and all of them fall back to collectives instead of a run that times out
+        per minibatch."""
         import ctypes
         from .. import _capi
-        _capi.call("ppo_dp_selftest", ctypes.byref(self.desc), 1, self.SELFTEST_ROUNDS, int(timeout_ms),
-                   _capi.stream_ptr())
-        torch.cuda.synchronize()
-        bits = int(self.err.item())
+        bits = 4
+        try:
+            _capi.call("ppo_dp_selftest", ctypes.byref(self.desc), 1, self.SELFTEST_ROUNDS, int(timeout_ms),
+                       _capi.stream_ptr())
+            torch.cuda.synchronize()
+            bits = int(self.err.item())
+        except RuntimeError:
+            pass
         self.clock.fill_(self.SELFTEST_ROUNDS)     # the flags hold the last test key: real keys continue after it
         self.err.zero_()
         torch.cuda.synchronize()
-        if bits:
-            self.close()
-            what = "a flag did not arrive" if bits & 1 else "a payload arrived wrong or stale"
-            raise RuntimeError(f"PeerExchange: start-up exchange test failed ({what}, err bits {bits})")
+        if not agree(bits == 0, self.device):
+            what = ("a flag did not arrive" if bits & 1 else "a payload arrived wrong or stale" if bits & 2
+                    else "the test kernel failed to launch" if bits & 4 else "it failed on another rank")
+            self._fail(f"start-up exchange test failed ({what}, err bits {bits})")
 
     @property
     def own_ptr(self) -> int:
@@ -150,6 +181,15 @@ class PeerExchange:
         if self._own is not None and self._own.value:
             self._lib.ppo_dp_free(self._own)
             self._own = None
+
+
+def agree(ok: bool, device) -> bool:
+    """True when `ok` holds on every rank (MIN all-reduce; gloo reduces on the host)."""
+    if world() == 1:
+        return bool(ok)
+    flag = torch.tensor([1.0 if ok else 0.0], device="cpu" if dist.get_backend() == "gloo" else device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    return bool(flag.item() == 1.0)
 
 
 def ctypes_void(p):

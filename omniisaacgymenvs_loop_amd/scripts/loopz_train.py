@@ -132,10 +132,10 @@ def train(cfg, max_updates=None, log=print):
             action = ppo.observe_device(obs)
             rew, dones = env.step_device(action)
             info = env.get_extras()
-            # episode infos reach the PPO log only on a step where some env is done (rlgames_train.py:440-456)
-            done_any = bool(dones.any().item())
-            ppo.step_device(rew, dones, infos=[info] if done_any and isinstance(info, dict) and info.get("episode")
-                            else [])
+            # episode infos reach the PPO log only on a step where some env is done (rlgames_train.py:440-456):
+            # the step's done flag stays on the device and the log filters on it once per update (no host sync)
+            ppo.step_device(rew, dones, infos=[info] if isinstance(info, dict) and info.get("episode") else [],
+                            valid=dones.any())
             rew_sum += rew.double().sum()
             done_sum += dones.double().sum()
         env.curriculum_callback()

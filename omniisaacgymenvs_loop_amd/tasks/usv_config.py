@@ -332,7 +332,8 @@ def nan_probe_enabled() -> int:
 
 
 NAN_STAGES = (("actions(clamped)", "USV_NAN_ACTIONS"), ("state", "USV_NAN_STATE"), ("reward.rew_buf", "USV_NAN_REWARD"),
-              ("obs(post_physics_step)", "USV_NAN_OBS"), ("policy mu/value (get_action_values)", "USV_NAN_POLICY"))
+              ("obs(post_physics_step)", "USV_NAN_OBS"), ("policy mu/value (get_action_values)", "USV_NAN_POLICY"),
+              ("episode extra is NaN before masking", "USV_NAN_EXTRAS"))
 
 
 def raise_nan_flag(bits: int, where: str) -> None:

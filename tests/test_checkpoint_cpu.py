@@ -146,3 +146,17 @@ def test_reference_checkpoint_optimizer_round_trip(golden):
     for i in range(len(C.PARAM_LAYOUT)):
         torch.testing.assert_close(back["state"][i]["exp_avg"], osd["state"][i]["exp_avg"], rtol=0, atol=0)
         torch.testing.assert_close(back["state"][i]["exp_avg_sq"], osd["state"][i]["exp_avg_sq"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("steps", [0, 1999, 224_000, 2_100_000, 3_000_000])
+def test_grad_scaler_state_stays_finite_and_loads(steps):
+    """The mixed_precision checkpoint's 'scaler' entry stays a finite fp32 scale however long the run
+    (a2c_continuous.get_full_state_weights at 3000 epochs x 1024 steps), and a reference GradScaler loads it."""
+    import math
+    import torch
+    st = C.grad_scaler_state(steps)
+    assert math.isfinite(st["scale"]) and torch.isfinite(torch.tensor(st["scale"], dtype=torch.float32))
+    assert 65536.0 <= st["scale"] <= C.GRAD_SCALE_MAX and 0 <= st["_growth_tracker"] < 2000
+    sc = torch.amp.GradScaler("cpu")
+    sc.load_state_dict(st)
+    assert sc.get_scale() == st["scale"] and sc.state_dict()["_growth_tracker"] == st["_growth_tracker"]

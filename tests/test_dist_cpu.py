@@ -102,3 +102,91 @@ def test_allreduced_gradient_equals_full_minibatch(two_ranks):
 
 def test_max_over_ranks(two_ranks):
     assert all(float(r["tmax"]) == 1.5 for r in two_ranks)
+
+
+class _FakeDpLib:
+    """Stands in for libusv_hip.so's ppo_dp_* calls so the set-up protocol of PeerExchange runs on CPU ranks
+    with chosen failures (no device memory is touched)."""
+
+    def __init__(self, rank, fail_alloc, fail_open):
+        self.rank, self.fail_alloc, self.fail_open = rank, fail_alloc, fail_open
+        self.log = []
+
+    def ppo_dp_alloc(self, pp, handle):
+        if self.rank in self.fail_alloc:
+            return 7
+        pp._obj.value = 0x1000 * (self.rank + 1)
+        handle.raw = bytes([self.rank + 1]) * 64
+        self.log.append("alloc")
+        return 0
+
+    def ppo_dp_open(self, handle, pp):
+        if self.rank in self.fail_open:
+            return 9
+        pp._obj.value = 0x100000 + handle.raw[0]
+        self.log.append("open")
+        return 0
+
+    def ppo_dp_close(self, p):
+        self.log.append("close")
+        return 0
+
+    def ppo_dp_free(self, p):
+        self.log.append("free")
+        return 0
+
+
+def _pe_worker(rank, world, port, out_dir, fail_alloc, fail_open):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from omniisaacgymenvs_loop_amd import _capi
+        from omniisaacgymenvs_loop_amd.rl_games import dist_util
+        fake = _FakeDpLib(rank, fail_alloc, fail_open)
+        _capi.lib = lambda: fake
+        msg = ""
+        try:
+            dist_util.PeerExchange(rank, world, "cpu")
+        except RuntimeError as e:
+            msg = str(e)
+        dist.barrier()      # both ranks got here: no rank hangs in a mismatched collective
+        np.savez(os.path.join(out_dir, f"pe{rank}.npz"), msg=msg, log=np.array(fake.log))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_alloc,fail_open", [((1,), ()), ((), (1,)), ((0, 1), ())])
+def test_peer_exchange_setup_failure_is_agreed_and_frees_after_the_barrier(tmp_path, fail_alloc, fail_open):
+    """A failed allocation or mapping on ONE rank: every rank still runs the same collectives (handle exchange,
+    agreement), every rank raises, and each frees its own buffer only after unmapping the peers' (ADVICE r3)."""
+    mp.spawn(_pe_worker, args=(2, _port(), str(tmp_path), fail_alloc, fail_open), nprocs=2, join=True)
+    for r in range(2):
+        z = np.load(tmp_path / f"pe{r}.npz")
+        assert "PeerExchange" in str(z["msg"]), (r, z["msg"])
+        log = list(z["log"])
+        if r not in fail_alloc:
+            assert log[0] == "alloc" and log[-1] == "free" and log.count("free") == 1
+            if "open" in log:
+                assert log.index("close") < log.index("free")
+        else:
+            assert "free" not in log
+
+
+def test_update_capturable_gates_on_the_path_that_runs(monkeypatch):
+    """Several ranks: the update graph is captured by default only when the peer exchange's kernels ARE the
+    update (fused chain); the split path's torch.distributed all-reduces stay behind USV_GRAPH_COLLECTIVES."""
+    from types import SimpleNamespace
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
+    ns = SimpleNamespace(multi_gpu=True, rank_size=2, _dp=object())
+    ns._fused_update = lambda: A2CAgent._fused_update(ns)
+    monkeypatch.delenv("USV_GRAPH_COLLECTIVES", raising=False)
+    monkeypatch.setenv("USV_PPO_FUSED", "1")
+    assert A2CAgent._update_capturable(ns)
+    monkeypatch.setenv("USV_PPO_FUSED", "0")
+    assert not A2CAgent._update_capturable(ns)
+    ns._dp = None
+    monkeypatch.setenv("USV_PPO_FUSED", "1")
+    assert not A2CAgent._update_capturable(ns)
+    ns.rank_size = 1
+    assert A2CAgent._update_capturable(ns)

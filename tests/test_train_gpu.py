@@ -126,3 +126,23 @@ def test_nan_probe_raises(monkeypatch):
     ag2.model_params[5] = float("nan")
     ag2.train_epoch()                                  # probe off: no raise
     assert not torch.isfinite(ag2.exp_mu).all()
+
+
+def test_nan_probe_raises_on_a_nan_episode_extra():
+    """USV_Virtual.py:1601-1605: under the probe a NaN episode statistic raises '[USV_NAN_PROBE] episode extra is
+    NaN before masking' instead of being zeroed silently (the extras fold ORs USV_NAN_EXTRAS); it is still masked
+    to 0 in extras["episode"] as the reference does after the check."""
+    from omniisaacgymenvs_loop_amd._abi import STAT_KEYS_ENUM
+    env, task, ag = _agent_env(256, 1024, False, seed=2)
+    ag.obs = ag.env_reset()
+    z = torch.zeros((256, 2), device="cuda:0")
+    env.step(z)
+    env.check_errors()
+    k = STAT_KEYS_ENUM["ST_U_MEAN"]
+    task.stats[k, 5] = float("nan")       # a non-reward statistic of env 5 ...
+    task.ibuf[2, 5] = 1                   # ... which resets at the start of the next step
+    env.step(z)
+    torch.cuda.synchronize()
+    assert float(task.extras_buf[k]) == 0.0
+    with pytest.raises(RuntimeError, match=r"USV_NAN_PROBE.*episode extra is NaN before masking"):
+        env.check_errors()
