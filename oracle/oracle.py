@@ -58,6 +58,7 @@ def lib():
         _lib.oracle_sample_field.argtypes = [P, ctypes.c_float, ctypes.c_float, ctypes.c_float]
         _lib.oracle_sample_field.restype = ctypes.c_float
         _lib.oracle_threads.restype = ctypes.c_int
+        _lib.oracle_set_skip_field.argtypes = [ctypes.c_int]
     return _lib
 
 

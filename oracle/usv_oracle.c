@@ -8,7 +8,7 @@
  * and bench.py's cpu_baseline may load it; the product (libusv_hip.so) never
  * links or calls it.
  *
- * Parity pinning: tests/golden/*.npz were produced by importing the reference
+ * Parity pinning: tests/golden/ fixtures (.npz) were produced by importing the reference
  * Python in the build container (tests/golden/make_golden.py) and recording its
  * outputs together with every torch.rand draw it consumed; tests/test_oracle_*.py
  * replay those draws through this file.
@@ -309,8 +309,10 @@ void oracle_potential_field(const usv_cfg_t *c, int K, const float *obst /*[K][1
     const float tx = (tgt[k * 2 + 0] + half_map) / cell;
     const float ty = (tgt[k * 2 + 1] + half_map) / cell;
     long ix = (long)tx, iy = (long)ty;       /* .long() truncates */
-    if (ix < 0) ix = 0; if (ix > G - 1) ix = G - 1;
-    if (iy < 0) iy = 0; if (iy > G - 1) iy = G - 1;
+    if (ix < 0) ix = 0;
+    if (ix > G - 1) ix = G - 1;
+    if (iy < 0) iy = 0;
+    if (iy > G - 1) iy = G - 1;
     C[iy * G + ix] = 0.f;
     for (int it = 0; it < c->field_iters; ++it) {
       int changed = 0;
@@ -454,6 +456,9 @@ static float enc_minmax(float x, float xmin, float xmax) {
 /* Reset path: USVVirtual.reset_idx (USV_Virtual.py:1502-1618)               */
 /* ids: compacted reset list (reset_buf.nonzero(), :1045); u: [k][NU_RESET]. */
 /* ------------------------------------------------------------------------ */
+static int g_skip_field = 0;
+void oracle_set_skip_field(int on) { g_skip_field = on; }
+
 void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids, const float *U,
                         const float *rows);
 void oracle_reset(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_t *ids, const float *U) {
@@ -714,8 +719,9 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
     E->tgt_x[e] = u[RU_GOAL + 0] * g * 2.0f - g;
     E->tgt_y[e] = u[RU_GOAL + 1] * g * 2.0f - g;
   }
-  /* potential field of the reset batch (static_obs.py:1054-1057) */
-  if (c->task_kind == USV_TASK_CAPTURE_XY) {
+  /* potential field of the reset batch (static_obs.py:1054-1057); skipped when a test supplies the fields
+     itself (oracle_set_skip_field: the full-size check copies the device's fields into E->field) */
+  if (c->task_kind == USV_TASK_CAPTURE_XY && !g_skip_field) {
     oracle_potential_field(c, k, obst_k, tgt_k, fld_k, NULL, E->grid_lin);
     for (int s = 0; s < k; ++s)
       memcpy(E->field + (size_t)ids[s] * USV_GRID2, fld_k + (size_t)s * USV_GRID2, sizeof(float) * USV_GRID2);

@@ -223,3 +223,67 @@ def test_meter_fold_multi_workgroup():
             ref.update_stats(sums[t, 0] / cnt, cnt)
     assert ag.game_rewards.current_size == ref.current_size
     ET.check("headline_meters", "game_rewards", ag.game_rewards.get_mean(), ref.get_mean(), 1e-5, 1e-5)
+
+
+def _detile(t):
+    """[k][USV_FIELD_STRIDE] tiled raw cost (include/usv_hip.h: 10 x 10 tiles, row-major inside and over the
+    15 x 15 tiles) -> [k][150 * 150] row-major."""
+    k = t.shape[0]
+    return t[:, :22500].reshape(k, 15, 15, 10, 10).transpose(0, 1, 3, 2, 4).reshape(k, 22500)
+
+
+def test_full_size_131072_step_vs_oracle():
+    """BASELINE configs[4]'s per-GPU size through the constant-shift step kernel (FixedWin<19>: every slab row
+    at base + (row << 19)) and the reset path of 131,072 envs in one batch, against the C oracle on the same
+    Philox draws: every env reset on the first step -- DR parameters, spawns and obstacles bit-exact for all
+    131,072 envs, the raw cost-to-go of 64 sampled envs bit-exact against the oracle's wavefront, the batch's
+    inf_val equal to 1.5 x the largest finite cost over all 131,072 fields -- then three steps with obs /
+    state at 1e-5, dones exact and the reward within 1e-5 + the potential-sample bound (test_env_gpu.py).
+    The oracle's reset skips its own 131,072 fields (oracle_set_skip_field: hours of CPU) and steps on the
+    device's fields, whose texels are checked above and at 8,192 resets in
+    test_philox_placement_8192_resets_vs_oracle; later resets (few envs) build their fields in the oracle."""
+    task_cfg = load_yaml(TEST_YAML)
+    n = HEAD
+    task = _task(task_cfg, n)
+    E = _oracle_for(task.cfg, n, task_cfg)
+    rng = np.random.default_rng(31)
+    dp = np.zeros(n)
+    for t in range(4):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        bias = task.current_action_bias()
+        obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
+        if t == 0:
+            ids = E.compact()
+            assert len(ids) == n
+            O.lib().oracle_set_skip_field(1)
+            try:
+                E.reset(ids, O.reset_uniforms(task.seed, 0, ids))
+            finally:
+                O.lib().oracle_set_skip_field(0)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(task.obst.cpu().numpy().reshape(16, 2, n), E.obst)
+            for j, k in enumerate(("mass", "com_x", "com_y", "com_z", "k_drag", "thr_l", "thr_r", "k_iz", "mass_r")):
+                np.testing.assert_allclose(task.params[j].cpu().numpy(), getattr(E, k), rtol=1e-6, atol=1e-6, err_msg=k)
+            # fields: raw cost of a sample vs the oracle's wavefront, the batch constant, then the device's
+            # materialised fields become the oracle's
+            smp = np.sort(rng.choice(n, 64, replace=False))
+            obst_s = task.obst[:, smp].cpu().numpy().reshape(16, 2, 64).transpose(2, 0, 1).copy()
+            tgt_s = task.field_old_tgt[:, smp].cpu().numpy().T.copy()
+            _, cost_ref = O.potential_field(task.cfg, obst_s, tgt_s, want_cost=True)
+            np.testing.assert_array_equal(_detile(task.field[smp].cpu().numpy()), cost_ref)
+            raw = task.field[:, :22500]
+            fin_max = torch.where(torch.isfinite(raw), raw, torch.full_like(raw, -1.0)).max()
+            inf_val = (fin_max * 1.5).item()
+            assert torch.all(task.fnorm[:, 4] == inf_val), "batch inf_val != 1.5 x max finite cost"
+            for c0 in range(0, n, 16384):
+                idx = torch.arange(c0, min(c0 + 16384, n), device=DEV)
+                E.field[c0:c0 + len(idx)] = task.field_rowmajor(idx).cpu().numpy()
+            E.step(a, bias, O.step_uniforms(task.seed, 0, n))
+        else:
+            E.full_step(a, bias, t, seed=task.seed)
+        torch.cuda.synchronize()
+        dp = _vs_oracle("full_size_131072", task, E, obs, rew, dones, t, dp)
+        st = task.state.cpu().numpy()
+        for j, k in enumerate(("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr")):
+            ET.check("full_size_131072", f"state_{k}", st[j][:, None], getattr(E, k)[:, None], 1e-5, 1e-5,
+                     [k], f"{k} t={t}")
