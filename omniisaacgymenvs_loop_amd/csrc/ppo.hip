@@ -1542,6 +1542,15 @@ __device__ __forceinline__ uint32_t *dp_flag(void *buf, int chunk, int sender) {
 // every rank).  A wait beyond timeout_ms, or an error another workgroup already flagged, sets / sees
 // bit 0 of dp.err and goes on with whatever arrived (the host raises after the epoch), so a lost peer
 // costs one timeout per launch, not one per chunk.
+// USV_DP_ORDER (A/B builds override it): 1 = a system-scope RELEASE fence before the flag store (every payload
+// store of the workgroup is ordered before the flag in the memory model, not only by the drained write-through
+// stores)
+// and the poll is followed by one system-scope ACQUIRE fence (the payload loads are ordered after the
+// flags seen); 0 = relaxed flag store and poll (the payload stores' own sc0 sc1 write-through + vmcnt(0)
+// drain and the poll's control dependency carry the order)
+#ifndef USV_DP_ORDER
+#define USV_DP_ORDER 1
+#endif
 __device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int slot, float pv, int timeout_ms) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int par = (int)(key & 1u);
@@ -1550,8 +1559,19 @@ __device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int sl
   __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its stores are acknowledged
   __syncthreads();
   if (w == 0) {
-    if (lane < dp.world)   // lane r raises rank r's flag of (this chunk, this sender)
-      __hip_atomic_store(dp_flag(dp.peer[lane], chunk, dp.rank), key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (lane < dp.world) {   // lane r raises rank r's flag of (this chunk, this sender)
+      if constexpr (USV_DP_ORDER != 0) {
+        // release at system scope: the workgroup's payload stores (drained behind the barrier above) happen
+        // before the flag in every rank's view; the explicit wait keeps the flag behind the write-back even
+        // where the compiler's scoreboard analysis would drop it (MI355X_MICROARCH.md, compiler hazard)
+        // (the guide's producer form: drained stores -> barrier -> release fence -> asm wait -> relaxed flag)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(dp_flag(dp.peer[lane], chunk, dp.rank), key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        __hip_atomic_store(dp_flag(dp.peer[lane], chunk, dp.rank), key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
     // poll this rank's flags of the chunk: every sender's key >= ours (a sender may be one ahead)
     const uint64_t t0 = wall_clock64(), lim = (uint64_t)timeout_ms * 100000ull;   // 100 MHz
     bool got = lane >= dp.world;
@@ -1569,6 +1589,12 @@ __device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int sl
         break;
       }
       __builtin_amdgcn_s_sleep(2);
+    }
+    // acquire at system scope, once after the poll (polling with acquire loads costs 2-3x per hop): the
+    // payload loads below are ordered after every flag this wave saw
+    if constexpr (USV_DP_ORDER != 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
   }
   __syncthreads();
