@@ -924,6 +924,7 @@ struct ChainIn {
   float *kl_out;                           // minibatch k-1's KL (log)
   uint32_t *dp_clock;                      // several ranks: the minibatch counter the next reduction keys its
                                            // exchange on (advanced here, by workgroup 0; nullable)
+  int fold_skip;                           // group fold: arrive but fold nothing (tests: the reduction's raw-row path)
 };
 
 // x rows of the gradient kernel padded to whole staging passes: every thread stores its slots
@@ -942,6 +943,7 @@ struct GradSmem {
   float b1[NH];
   float tail[TAIL + 1];
   float nrm[4];                   // chained update: wave sums of the chunk squares
+  int fold[2];                    // group fold: all members arrived, this launch's generation
 };
 
 // Partial-gradient slot layout (a permutation of the parameters, then the loss sums): the
@@ -995,17 +997,48 @@ struct RowIn {
 #ifndef USV_PART_AUX
 #define USV_PART_AUX 2   // cache-policy bits of the partial stores: nt (A/B builds override it)
 #endif
-struct PartOut {
+template <int kAux>
+struct PartOutT {
   __amdgpu_buffer_rsrc_t r;
   __device__ __forceinline__ void operator()(int idx, float v) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (uint32_t)idx * 4u, 0, USV_PART_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (uint32_t)idx * 4u, 0, kAux);
   }
   __device__ __forceinline__ void x4(int idx, float a, float b, float c, float d) const {
     const u32x4_t v = {__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c),
                        __builtin_bit_cast(uint32_t, d)};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)idx * 4u, 0, USV_PART_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)idx * 4u, 0, kAux);
   }
 };
+constexpr int AUX_SC1 = 16;   // sc1: write-through (the in-launch group fold reads the rows from another CU)
+
+// ---- The XCD-group fold of the partial rows (kFold launches of k_mb_grad; k_reduce_partials(fold = 1)) ----
+// The 256 per-workgroup partial rows of an 8192-row minibatch (21.8 MB) were written by the gradient kernel and
+// read back whole by the reduction.  With the fold, workgroups b = g + 8 m (group g = b % 8, member m: the blocks
+// the dispatcher deals to one XCD, speed only -- correctness holds at any placement) meet at a per-group arrival
+// counter after storing their rows write-through (sc1, every wave drained); member m then sums the M = nblk / 8
+// rows of its group over slice m of the row (sc1 loads) and writes the group row's slice, so the reduction reads
+// 8 group rows per slot instead of nblk rows.  Summation order (the same bits in every path):
+//   group(g) = half0 + half1,  half0 = 0 + p[g] + p[g + 8] + ... (m < H0),  half1 = 0 + ... (H0 <= m < M),
+//   H0 = (M + 1) / 2;  gradient = 0 + group(0) + ... + group(7).
+// A member that does not see its whole group arrive within FOLD_WAIT_TICKS (another kernel or process holding
+// CUs: the group's rows cannot all be resident) folds nothing; the reduction then forms that group's sum from
+// the raw rows in the same order, so the result does not depend on whether a group folded.
+// Buffer (ppo_partials_floats): [nblk][NPART_PAD] rows | [8][NPART_PAD] group rows | fold control: per group
+// one 128-B line holding the arrival counter (monotonic: a member's arrival value tells its launch generation)
+// and 32 slice words (the generation whose fold wrote slice m).
+constexpr int FOLD_G = 8;
+constexpr int FOLD_MAX_M = 32;                      // nblk <= 256: the grid is resident at one workgroup per CU
+constexpr int FOLD_CTL_STRIDE = 64;                 // u32 words per group: [0] counter, [32 + m] slice gens
+constexpr uint64_t FOLD_WAIT_TICKS = 10000;         // 100 us at the 100 MHz wall clock
+__device__ __forceinline__ uint32_t *fold_ctl(float *partials, int nblk) {
+  return reinterpret_cast<uint32_t *>(partials + (size_t)(nblk + FOLD_G) * NPART_PAD);
+}
+__device__ __forceinline__ const uint32_t *fold_ctl(const float *partials, int nblk) {
+  return reinterpret_cast<const uint32_t *>(partials + (size_t)(nblk + FOLD_G) * NPART_PAD);
+}
+__device__ __forceinline__ f32x4v ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, AUX_SC1));
+}
 
 // chained update, clipping due: minibatch k-1's step redone from bank prev with the clip
 // coefficient, straight into this workgroup's LDS weights (and sigma into ls0 / ls1);
@@ -1041,7 +1074,7 @@ __device__ __forceinline__ void redo_step(const ppo_cfg_t &c, const ChainIn &ch,
   ls1 = pn;
 }
 
-template <bool kBf, bool kChain>
+template <bool kBf, bool kChain, bool kFold>
 __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch, const float *__restrict__ P,
                                           const double *__restrict__ obs_rms, int row0,
                                           const float *__restrict__ e_obs, const float *__restrict__ e_act,
@@ -1250,8 +1283,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
   __syncthreads();
   USV_PHASE(ppo, 2);
-  const PartOut part_st{__builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4,
-                                                          0x00020000)};
+  const PartOutT<kFold ? AUX_SC1 : USV_PART_AUX> part_st{
+      __builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4, 0x00020000)};
   // ---- per-row losses and output gradients (lane = row < RB): wave 0 the actor side (ratio, clipped
   // surrogate, dnlp, dmu, dlogstd), wave 1 in parallel the critic, bound, entropy and KL terms and the
   // mu / sigma write-back (the same per-row arithmetic and lane sums as one wave doing both) ----
@@ -1478,9 +1511,65 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     }
   }
   USV_PHASE(ppo, 8);
+  if constexpr (kFold) {
+    // ---- the group fold (see FOLD_G): arrive once every wave's write-through stores are drained ----
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int nblk = (int)gridDim.x, M = nblk / FOLD_G, g = blockIdx.x % FOLD_G, m = blockIdx.x / FOLD_G;
+    uint32_t *ctl = fold_ctl(partials, nblk) + g * FOLD_CTL_STRIDE;
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t gen = old / (uint32_t)M + 1u, target = gen * (uint32_t)M;
+      const uint64_t t0 = wall_clock64();
+      int ok = 0;
+      while (true) {
+        const uint32_t v = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 poll
+        if ((int32_t)(v - target) >= 0) { ok = 1; break; }
+        if (wall_clock64() - t0 > FOLD_WAIT_TICKS) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s.fold[0] = ok && !ch.fold_skip;
+      s.fold[1] = (int)gen;
+    }
+    __syncthreads();
+    if (s.fold[0]) {
+      constexpr int NQ = NPART_PAD / 4;
+      const int q4 = (NQ + M - 1) / M, qa = m * q4, qb = min(qa + q4, NQ);
+      const int h0 = (M + 1) / 2;
+      float4 *lds = reinterpret_cast<float4 *>(s.w2);   // the weights are no longer read
+      // the group's rows through one buffer descriptor (sc1 loads: served from L2 / memory, never L1)
+      const __amdgpu_buffer_rsrc_t rows = __builtin_amdgcn_make_buffer_rsrc(
+          partials + (size_t)g * NPART_PAD, 0, (int)((size_t)(nblk - g) * NPART_PAD * 4), 0x00020000);
+      float *grow = partials + (size_t)(nblk + g) * NPART_PAD;
+      for (int c0 = qa; c0 < qb; c0 += GTB / 2) {
+        const int half = tid / (GTB / 2), q = c0 + tid % (GTB / 2);
+        const int mb = half ? h0 : 0, me = half ? M : h0;
+        const int qc = min(q, NQ - 1);
+        f32x4v x[FOLD_MAX_M / 2];
+#pragma unroll
+        for (int k = 0; k < FOLD_MAX_M / 2; ++k)
+          x[k] = ld4_sc1(rows, (uint32_t)((FOLD_G * min(mb + k, M - 1) * NPART_PAD + 4 * qc) * 4));
+        f32x4v acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int k = 0; k < FOLD_MAX_M / 2; ++k)
+          if (mb + k < me) acc += x[k];
+        if (half) lds[tid % (GTB / 2)] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        __syncthreads();
+        if (!half && q < qb) {
+          const float4 o = lds[tid];
+          const f32x4v t = {acc[0] + o.x, acc[1] + o.y, acc[2] + o.z, acc[3] + o.w};
+          __builtin_nontemporal_store(t, reinterpret_cast<f32x4v *>(grow + 4 * q));
+        }
+        __syncthreads();
+      }
+      __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) ctl[32 + m] = (uint32_t)s.fold[1];   // this slice of the group row is this launch's
+    }
+  }
 }
 
-template <bool kBf, bool kChain>
+template <bool kBf, bool kChain, bool kFold>
 __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, ChainIn ch, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms, int row0,
                                                     const float *__restrict__ e_obs, const float *__restrict__ e_act,
@@ -1488,7 +1577,8 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, ChainIn ch, con
                                                     const float *__restrict__ e_ret, const float *__restrict__ e_adv,
                                                     float *e_mu, float *e_sigma, float *partials) {
   __shared__ GradSmem s;
-  mb_grad8w<kBf, kChain>(c, ch, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma, partials, s);
+  mb_grad8w<kBf, kChain, kFold>(c, ch, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma,
+                                partials, s);
 }
 
 // k_reduce_partials: the per-workgroup partial rows (stride NPART_PAD floats, 16-B aligned)
@@ -1634,7 +1724,7 @@ __global__ __launch_bounds__(RD_TB) void k_dp_selftest(ppo_dp_t dp, uint32_t key
 template <bool kSpec, bool kDP>
 __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restrict__ partials, int nblk, float *grad,
                                                            float *losses, float inv_b, ppo_cfg_t c, AdamBanks a,
-                                                           const float *__restrict__ opt_in, ppo_dp_t dp) {
+                                                           const float *__restrict__ opt_in, ppo_dp_t dp, int fold) {
   __shared__ float4 red[RD_G][RD_L];
   __shared__ float sqw[RD_TB / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1659,6 +1749,27 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     for (int q = 0; q < 8; ++q) oin[q] = opt_in[q];
   }
   const int p4c = min(p4, NPART_PAD / 4 - 1);
+  if (fold) {   // the gradient kernel folded the rows of group g = grp (FOLD_G): one group row per group
+    if (grp < FOLD_G) {
+      const int M = nblk / FOLD_G;
+      const uint32_t *ctl = fold_ctl(partials, nblk) + grp * FOLD_CTL_STRIDE;
+      const uint32_t gen = ctl[0] / (uint32_t)M;
+      bool folded = true;
+      for (int mm = 0; mm < M; ++mm) folded &= ctl[32 + mm] == gen;
+      if (folded) {
+        acc = P4[(size_t)(nblk + grp) * (NPART_PAD / 4) + p4c];
+      } else {   // a member timed out: the same sums from the raw rows, in the fold's order
+        const int h0 = (M + 1) / 2;
+        float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+        for (int mm = 0; mm < M; ++mm) {
+          const float4 x = P4[(size_t)(grp + FOLD_G * mm) * (NPART_PAD / 4) + p4c];
+          float4 &t = mm < h0 ? a0 : a1;
+          t.x += x.x; t.y += x.y; t.z += x.z; t.w += x.w;
+        }
+        acc = make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
+      }
+    }
+  } else
   for (int b0 = grp; b0 < nblk; b0 += RD_G * RD_KB) {
     // branch-free: clamped rows / columns loaded, masked in the sum (every load in flight at once)
     float4 x[RD_KB];
@@ -1867,6 +1978,17 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
   return 0;
 }
 
+// the XCD-group fold of the partial rows (FOLD_G): minibatches of 8 x 1..32 workgroups (the whole grid resident at
+// one workgroup per CU); USV_PPO_FOLD=0 turns it off (A/B builds, or ranks sharing one device)
+// (USV_PPO_FOLD=2: every member arrives but none folds -- the reduction's raw-row path, for the tests)
+static int fold_env() {
+  const char *e = getenv("USV_PPO_FOLD");
+  return e ? atoi(e) : 1;
+}
+static bool fold_on(int nblk) {
+  return fold_env() != 0 && nblk % FOLD_G == 0 && nblk / FOLD_G >= 1 && nblk / FOLD_G <= FOLD_MAX_M;
+}
+
 int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rms, const double *val_rms,
                        int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
                        const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
@@ -1888,12 +2010,16 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
   }
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
   const int nblk = cfg->minibatch / RB;
-  hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, false> : k_mb_grad<false, false>), dim3(nblk), dim3(GTB), 0, s,
-                     *cfg, ChainIn{}, params, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv,
-                     exp_mu, exp_sigma, partials);
+  const bool fold = fold_on(nblk);
+  ChainIn ch{};
+  ch.fold_skip = fold_env() == 2;
+  hipLaunchKernelGGL((cfg->bf16_gemm ? (fold ? k_mb_grad<true, false, true> : k_mb_grad<true, false, false>)
+                                     : (fold ? k_mb_grad<false, false, true> : k_mb_grad<false, false, false>)),
+                     dim3(nblk), dim3(GTB), 0, s, *cfg, ch, params, obs_rms, row0, exp_obs, exp_act, exp_nlp,
+                     exp_val, exp_ret, exp_adv, exp_mu, exp_sigma, partials);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL((k_reduce_partials<false, false>), dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad,
-                     losses, 1.0f / (float)cfg->minibatch, *cfg, AdamBanks{}, nullptr, ppo_dp_t{});
+                     losses, 1.0f / (float)cfg->minibatch, *cfg, AdamBanks{}, nullptr, ppo_dp_t{}, (int)fold);
   USV_CHECK_LAUNCH();
   return 0;
 }
@@ -1932,28 +2058,33 @@ static int fused_launch(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, con
   const float *P = banks->params[cur];
   const dim3 gg(nblk), gb(GTB);
   uint32_t *clk = dp ? dp->clock : nullptr;
+  const bool fold = fold_on(nblk);
   if (seq == 0) {
     ChainIn ch{};
     ch.dp_clock = clk;
-    hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, false> : k_mb_grad<false, false>), gg, gb, 0, s, *cfg,
-                       ch, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu,
-                       exp_sigma, partials);
+    ch.fold_skip = fold_env() == 2;
+    hipLaunchKernelGGL((cfg->bf16_gemm ? (fold ? k_mb_grad<true, false, true> : k_mb_grad<true, false, false>)
+                                       : (fold ? k_mb_grad<false, false, true> : k_mb_grad<false, false, false>)),
+                       gg, gb, 0, s, *cfg, ch, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv,
+                       exp_mu, exp_sigma, partials);
   } else {
     const ChainIn ch{banks->params[prv], banks->m[prv], banks->v[prv], banks->params[cur], banks->m[cur],
-                     banks->v[cur], grad, banks->opt + 8 * prv, banks->opt + 8 * cur, kl_prev_out, clk};
-    hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, true> : k_mb_grad<false, true>), gg, gb, 0, s, *cfg, ch, P,
-                       obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv, exp_mu, exp_sigma,
-                       partials);
+                     banks->v[cur], grad, banks->opt + 8 * prv, banks->opt + 8 * cur, kl_prev_out, clk,
+                     fold_env() == 2};
+    hipLaunchKernelGGL((cfg->bf16_gemm ? (fold ? k_mb_grad<true, true, true> : k_mb_grad<true, true, false>)
+                                       : (fold ? k_mb_grad<false, true, true> : k_mb_grad<false, true, false>)),
+                       gg, gb, 0, s, *cfg, ch, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret, exp_adv,
+                       exp_mu, exp_sigma, partials);
   }
   USV_CHECK_LAUNCH();
   const AdamBanks a{banks->params[cur], banks->m[cur], banks->v[cur], banks->params[prv], banks->m[prv],
                     banks->v[prv]};
   if (dp)
     hipLaunchKernelGGL((k_reduce_partials<true, true>), dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad,
-                       losses, 1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur, *dp);
+                       losses, 1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur, *dp, (int)fold);
   else
     hipLaunchKernelGGL((k_reduce_partials<true, false>), dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad,
-                       losses, 1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur, ppo_dp_t{});
+                       losses, 1.0f / (float)cfg->minibatch, *cfg, a, banks->opt + 8 * cur, ppo_dp_t{}, (int)fold);
   USV_CHECK_LAUNCH();
   return 0;
 }
@@ -2065,7 +2196,8 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
   return 0;
 }
 
-int ppo_partials_floats(int minibatch) { return (minibatch / RB) * NPART_PAD; }
+// per-workgroup rows, the fold's group rows and its control lines (zero-initialised by the caller)
+int ppo_partials_floats(int minibatch) { return (minibatch / RB + FOLD_G) * NPART_PAD + FOLD_G * FOLD_CTL_STRIDE; }
 int ppo_grad_floats(void) { return PPO_NPARAM + 8 + RED_BLOCKS; }
 int ppo_meter_floats(int n_envs, int horizon) {
   return horizon * 4 + horizon * ((n_envs + kStoreTB - 1) / kStoreTB) * 4;

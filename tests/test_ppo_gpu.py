@@ -381,3 +381,59 @@ def test_player_runs_the_usv_task(tmp_path):
     torch.testing.assert_close(pl.model_params, ag.model_params, rtol=0, atol=0)
     mean_reward = pl.run()
     assert np.isfinite(mean_reward)
+
+
+@pytest.mark.parametrize("minibatch", [8192, 1024, 256])
+def test_group_fold_matches_raw_row_path_and_oracle(minibatch, monkeypatch):
+    """The XCD-group fold of the partial rows (ppo.hip FOLD_G; 8 groups of nblk / 8 = 32, 4 or 1 workgroups):
+    folded in the gradient kernel (USV_PPO_FOLD=1, the default), or every member arriving without folding so
+    the reduction sums the raw rows in the fold's order (USV_PPO_FOLD=2): bit-identical gradients, losses and
+    KL, twice in a row (the monotonic arrival counters carry the launch generation); without the fold
+    (USV_PPO_FOLD=0, the reduction's 16-group order) the same gradient within 1e-6 of its largest component,
+    and the oracle's within 1e-5."""
+    from omniisaacgymenvs_loop_amd import _capi as c
+    N, H = minibatch // 16, 16
+    ag = _agent(N, minibatch, mini_epochs=1)
+    rng = np.random.default_rng(5)
+    B = N * H
+    obs = rng.normal(0, 2, (B, 33)).astype(np.float32)
+    act = rng.normal(0, 1, (B, 2)).astype(np.float32)
+    P = PO.unflatten(ag.model_params.cpu().numpy())
+    xn = PO.RMS.zeros(33)
+    xn.update(obs)
+    _, _, mu0, _ = PO.forward(P, xn.norm(obs))
+    sig0 = np.ones_like(mu0)
+    nlp0 = PO.neglogp(act, mu0, sig0, np.zeros_like(mu0)) + rng.normal(0, 0.05, B).astype(np.float32)
+    val = rng.normal(0, 1, B).astype(np.float32)
+    ret = (val + rng.normal(0, 0.5, B)).astype(np.float32)
+    adv = rng.normal(0, 1, B).astype(np.float32)
+    T = lambda a: torch.tensor(np.ascontiguousarray(a), device=DEV)
+    for name, arr in (("exp_obs", obs), ("exp_act", act), ("exp_nlp", nlp0), ("exp_val", val), ("exp_ret", ret),
+                      ("exp_adv", adv), ("exp_mu", mu0 + 0.01), ("exp_sigma", sig0)):
+        getattr(ag, name).copy_(T(arr))
+    orms = ag.obs_rms.clone()
+
+    def grad(mode):
+        monkeypatch.setenv("USV_PPO_FOLD", mode)
+        ag.obs_rms.copy_(orms)
+        c.call("ppo_minibatch_grad", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
+               1, 0, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp), c.ptr(ag.exp_val), c.ptr(ag.exp_ret),
+               c.ptr(ag.exp_adv), c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.grad), c.ptr(ag.losses),
+               c.ptr(ag.partials), c.ptr(ag.work), c.stream_ptr())
+        torch.cuda.synchronize()
+        return ag.grad[:PO.NPARAM + 1].cpu().numpy().copy(), ag.losses.cpu().numpy()[:5].copy()
+
+    g1, l1 = grad("1")
+    g2, l2 = grad("2")
+    g1b, _ = grad("1")
+    g0, _ = grad("0")
+    np.testing.assert_array_equal(g1, g2)
+    np.testing.assert_array_equal(l1, l2)
+    np.testing.assert_array_equal(g1, g1b)
+    scale = np.abs(g0[:PO.NPARAM]).max()
+    ET.check(f"group_fold_{minibatch}", "fold vs unfolded", g1[:PO.NPARAM] / scale, g0[:PO.NPARAM] / scale, 0, 1e-6)
+    o = PO.RMS.zeros(33)
+    o.update(obs)
+    g_ref, _, _, _, _ = PO.minibatch_grad(P, o.norm(obs), act, nlp0, val, ret, adv, mu0 + 0.01, sig0,
+                                          PO.PPOConfig(minibatch=minibatch))
+    ET.check(f"group_fold_{minibatch}", "grad/max", g1[:PO.NPARAM] / scale, g_ref / scale, 0, 1e-5)
