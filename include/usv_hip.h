@@ -205,6 +205,17 @@ typedef struct usv_cfg {
    * the step kernels OR the USV_NAN_* stage bits of any non-finite clamped action, state,
    * reward or observation into ctl[USV_CTL_NAN_FLAG]; the host raises after the epoch ---- */
   int   nan_probe;
+  /* ---- GoToPose spawn curriculum (GoToPoseTask.get_spawns / update_kills, USV_go_to_pose.py:183-209,
+   * 256-300; GoToPoseParameters.spawn_curriculum*, USV_task_parameters.py:70-76): the spawn disk and the kill
+   * distance move linearly from the curriculum values to the task's as the reference's USVVirtual.step (a
+   * Python float += 1 / horizon_length per calculate_metrics, USV_Virtual.py:1633) goes from warmup to end;
+   * get_spawns sees the value at the step's reset, update_kills the value after its calculate_metrics
+   * (usv_bufs_t.clock[4..5]).  Doubles: the reference's Python floats. ---- */
+  int   curriculum_on;
+  int   pad_curriculum;
+  double step_inc;          /* 1 / horizon_length (the increment of USVVirtual.step) */
+  double cur_min_dist, cur_max_dist, cur_kill_dist, cur_warmup, cur_end;
+  double min_spawn_d, max_spawn_d, kill_dist_d;   /* the task's min_spawn_dist, max_spawn_dist, kill_dist */
 } usv_cfg_t;
 
 /* stage bits of ctl[USV_CTL_NAN_FLAG] / ppo_cfg_t.nan_flag (the reference's probe names) */
@@ -282,7 +293,9 @@ typedef struct usv_bufs {
   int32_t *scene_last;             /* [n] scene index applied at the env's last reset */
   int32_t n_scenes, scene_cycle;
   /* device step clock (nullable): [0] next step index, [1] next bias-call count,
-   * [2] current step, [3] current bias-call count.  When set, usv_reset advances
+   * [2] current step, [3] current bias-call count, [4] / [5] the bits of the double
+   * USVVirtual.step at the current step's reset / after its calculate_metrics (cfg.step_inc
+   * per step, USV_CLOCK_WORDS words, zero-initialised).  When set, usv_reset advances
    * it and the step / bias arguments of usv_reset / usv_env_step are ignored, so
    * a captured HIP graph replays consecutive steps. */
   uint64_t *clock;
@@ -297,6 +310,7 @@ typedef struct usv_bufs {
 } usv_bufs_t;
 #define USV_FNORM 8
 #define USV_RSTASH_ROWS 14
+#define USV_CLOCK_WORDS 6
 
 /* one replay scene (scripts/build_usv_scenes.py:566-577 keys; obstacles padded to
  * 16 with limbo (999, 999) past obstacles_count as CaptureXYTask.apply_scene does,
@@ -688,6 +702,12 @@ typedef struct lz_cfg {
   float lr, adam_b1, adam_b2, adam_eps;
   float min_std;             /* enforce_minimum_std 0.05 */
   float action_scale[LZ_NA]; /* clipActions */
+  /* imitation term of PPO._train_step (ppo.py:253-286, flat_expert + update_rl_coeff :97-100): loss +=
+   * mean_rows((1 - rl_coeff) * sum_a (expert_a - action_mean_a)^2); expert_act [T][N][2] (storage-row order)
+   * holds flat_expert.evaluate of the stored observations (the expert is frozen: once per update), NULL = no
+   * expert (the trainer's flat_expert = None, rlgames_train.py:92) */
+  float im_coef;             /* 1 - rl_coeff */
+  const float *expert_act;
 } lz_cfg_t;
 
 /* size (floats) of the flat loopz parameter vector (actor | std | critic) for obs_dim */

@@ -61,7 +61,7 @@ __host__ __device__ inline int critic_base(int obs_dim) { return std_base(obs_di
 __host__ __device__ inline int nparam(int obs_dim) { return critic_base(obs_dim) + net_off(obs_dim, 1).size; }
 // per-workgroup partial row of one network: its parameters, then 4 extra slots
 // (actor: dstd0, dstd1, surrogate sum, log-prob sum; critic: value-loss sum, 0, 0, 0)
-__host__ __device__ inline int part_stride(int obs_dim) { return (net_off(obs_dim, NA).size + 4 + 3) & ~3; }
+__host__ __device__ inline int part_stride(int obs_dim) { return (net_off(obs_dim, NA).size + 5 + 3) & ~3; }
 
 constexpr int ENC_N = E1 * MS + E1 + E2 * E1 + E2 + LT * E2 + LT;   // 1752
 struct NetSmem {
@@ -380,7 +380,7 @@ __device__ void grad_net(const lz_cfg_t &c, const float *__restrict__ P, int wg,
   const int j = tid & (NH - 1), hf = tid >> 7;            // (unit, row half) for the VALU reductions
   float gw3[NA] = {}, gb2 = 0.f, gb1 = 0.f, gw1x[4] = {}, gb3[NA] = {};
   float ge4w = 0.f, ge4b = 0.f, ge2w[4] = {}, ge2b = 0.f, ge0w[2] = {}, ge0b = 0.f;
-  float l_a = 0.f, l_b = 0.f, gsd0 = 0.f, gsd1 = 0.f;   // loss sums (thread r < 32)
+  float l_a = 0.f, l_b = 0.f, l_im = 0.f, gsd0 = 0.f, gsd1 = 0.f;   // loss sums (thread r < 32)
   const int ntiles = (M + RB - 1) / RB;
   for (int tile = wg; tile < ntiles; tile += G) {
     const int rt0 = tile * RB, nrows = min(RB, M - rt0);
@@ -412,7 +412,13 @@ __device__ void grad_net(const lz_cfg_t &c, const float *__restrict__ P, int wg,
           // loss = mean(surr + c_v vl - c_e entropy), entropy = -log_prob
           const float dlp = (g_r * ratio + c.entropy_coef) * invB;
           const float var0 = sd0 * sd0, var1 = sd1 * sd1;
-          const float dmu0 = dlp * (u0 - mu0) / var0, dmu1 = dlp * (u1 - mu1) / var1;
+          float dmu0 = dlp * (u0 - mu0) / var0, dmu1 = dlp * (u1 - mu1) / var1;
+          if (c.expert_act) {   // imitation: (1 - rl) * sum_a (expert_a - mu_a)^2, row mean (ppo.py:279-282)
+            const float e0 = c.expert_act[2 * q], e1 = c.expert_act[2 * q + 1];
+            dmu0 = dmu0 + c.im_coef * (2.0f * (mu0 - e0)) * invB;
+            dmu1 = dmu1 + c.im_coef * (2.0f * (mu1 - e1)) * invB;
+            l_im += c.im_coef * ((e0 - mu0) * (e0 - mu0) + (e1 - mu1) * (e1 - mu1));
+          }
           d0 = dmu0 * (1.0f - mu0 * mu0);
           d1 = dmu1 * (1.0f - mu1 * mu1);
           gsd0 += dlp * ((u0 - mu0) * (u0 - mu0) / (var0 * sd0) - 1.0f / sd0);
@@ -615,9 +621,10 @@ __device__ void grad_net(const lz_cfg_t &c, const float *__restrict__ P, int wg,
   // extras: wave 0 sums the per-row loss terms (lanes 32..63 hold zeros)
   if (w == 0) {
     const float sa = wave_sum(l_a), sb = wave_sum(l_b), q0 = wave_sum(gsd0), q1 = wave_sum(gsd1);
+    const float si = wave_sum(l_im);
     if (lane == 0) {
       const int x = o.size;
-      if (kActor) { pr[x] = q0; pr[x + 1] = q1; pr[x + 2] = sa; pr[x + 3] = sb; }
+      if (kActor) { pr[x] = q0; pr[x + 1] = q1; pr[x + 2] = sa; pr[x + 3] = sb; pr[x + 4] = si; }
       else { pr[x] = sa; pr[x + 1] = 0.f; pr[x + 2] = 0.f; pr[x + 3] = 0.f; }
     }
   }
@@ -639,7 +646,7 @@ __global__ __launch_bounds__(TB) void k_lz_grad(lz_cfg_t c, const float *__restr
 }
 
 // Fixed-order sum of the G partial rows of each network into grad[] (parameter order), the loss
-// sums into grad[np .. np + 3] (surrogate, log-prob, value loss) and each chunk's squared norm
+// sums into grad[np .. np + 4) (surrogate, log-prob, value loss, imitation) and each chunk's squared norm
 // into grad[np + 8 + chunk].  One thread per parameter, 16 row loads in flight.
 constexpr int RD_TB = 256;
 __global__ __launch_bounds__(RD_TB) void k_lz_reduce(lz_cfg_t c, const float *__restrict__ part_a,
@@ -669,9 +676,10 @@ __global__ __launch_bounds__(RD_TB) void k_lz_reduce(lz_cfg_t c, const float *__
   if ((threadIdx.x & 63) == 0) sq[threadIdx.x >> 6] = s2;
   __syncthreads();
   if (threadIdx.x == 0) grad[np + 8 + blockIdx.x] = ((sq[0] + sq[1]) + sq[2]) + sq[3];
-  if (blockIdx.x == 0 && threadIdx.x < 3) {   // loss sums
-    const float *s_ = threadIdx.x < 2 ? part_a : part_c;
-    const int cc = threadIdx.x == 0 ? na + 2 : (threadIdx.x == 1 ? na + 3 : net_off(D, 1).size);
+  if (blockIdx.x == 0 && threadIdx.x < 4) {   // loss sums: surrogate, log-prob, value loss, imitation
+    const float *s_ = threadIdx.x == 2 ? part_c : part_a;
+    const int cc = threadIdx.x == 0 ? na + 2 : (threadIdx.x == 1 ? na + 3 : (threadIdx.x == 2 ? net_off(D, 1).size
+                                                                                                : na + 4));
     float a = 0.f;
     for (int b = 0; b < G; ++b) a += s_[(size_t)b * stride + cc];
     grad[np + threadIdx.x] = a;
@@ -694,7 +702,8 @@ __global__ __launch_bounds__(AP_TB) void k_lz_apply(lz_cfg_t c, float *P, const 
   for (int k = tid; k < nchunks; k += AP_TB) ss += grad[np + 8 + k];
   const float invB = 1.0f / (float)M;
   const float surr = grad[np] * invB, lps = grad[np + 1] * invB, vl = grad[np + 2] * invB;
-  const float loss = (surr + c.value_loss_coef * vl) + c.entropy_coef * lps;
+  // rl_loss + im_loss (ppo.py:276-283); only its finiteness is used (the non-finite skip)
+  const float loss = ((surr + c.value_loss_coef * vl) + c.entropy_coef * lps) + (c.expert_act ? grad[np + 3] * invB : 0.f);
   const bool ok = isfinite(loss);
   const float step = opt_in[1] + (ok ? 1.0f : 0.0f);
   const float lr = opt_in[0];

@@ -50,6 +50,20 @@ __global__ void k_build_lut(const float *__restrict__ tl, const float *__restric
 
 // step index / action bias of this step: the device clock when present
 __device__ __forceinline__ uint64_t step_of(const usv_bufs_t &b, uint64_t step) { return b.clock ? b.clock[2] : step; }
+// USVVirtual.step at this step's reset (which = 4) or after its calculate_metrics (which = 5); without the device
+// clock, from the step index (exact for power-of-two horizons)
+__device__ __forceinline__ double ref_step_of(const usv_cfg_t &c, const usv_bufs_t &b, uint64_t step, int which) {
+  if (b.clock) return __longlong_as_double((long long)b.clock[which]);
+  return (double)(step + (which == 5 ? 1 : 0)) * c.step_inc;
+}
+// GoToPoseTask's spawn curriculum (USV_go_to_pose.py:266-290 radii, :188-202 kill distance): linear in the
+// reference step between warmup and end, in the reference's double arithmetic
+__device__ __forceinline__ double curriculum_lerp(const usv_cfg_t &c, double st, double cur, double fin) {
+  if (st < c.cur_warmup) return cur;
+  if (st > c.cur_end) return fin;
+  const double r = (st - c.cur_warmup) / (c.cur_end - c.cur_warmup);
+  return r * (fin - cur) + cur;
+}
 __device__ __forceinline__ float bias_of(const usv_cfg_t &c, const usv_bufs_t &b, float bias) {
   if (!b.clock) return bias;
   return (c.act_bias_steps > 0 && b.clock[3] < (uint64_t)c.act_bias_steps) ? c.act_bias : 0.f;
@@ -83,11 +97,16 @@ struct ResetRng {
 #define USV_RESET_FOLD_KERNEL 1
 #endif
 
-__global__ void k_step_begin(usv_bufs_t b) {
+__global__ void k_step_begin(usv_bufs_t b, double step_inc) {
   const int t = threadIdx.x;
   if (t == 0 && b.clock) {   // device step clock: this step's index and bias-call count
     b.clock[2] = b.clock[0]++;
     b.clock[3] = b.clock[1]++;
+    // USVVirtual.step (a double, += 1 / horizon_length per calculate_metrics, USV_Virtual.py:1633): its value
+    // at this step's reset_idx and after this step's calculate_metrics, accumulated as the reference does
+    const uint64_t after = b.clock[5];
+    b.clock[4] = after;
+    b.clock[5] = (uint64_t)__double_as_longlong(__longlong_as_double((long long)after) + step_inc);
   }
   if (t == 0) b.ctl[USV_CTL_RESET_COUNT] = 0;
   if (t == 3 && b.ctl[USV_CTL_STEPPED]) {   // a step has run: prev_* are no longer None
@@ -275,7 +294,13 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         b.field_old_tgt[e] = tx;
         b.field_old_tgt[n + e] = ty;
       } else if (c.task_kind == USV_TASK_GO_TO_POSE) {   // GoToPoseTask.get_spawns (USV_go_to_pose.py:256-319)
-        const float r = U(RU_SPAWN_R) * (float)((double)c.spawn_rmax - (double)c.spawn_rmin) + c.spawn_rmin;
+        double rmax = c.spawn_rmax, rmin = c.spawn_rmin;
+        if (c.curriculum_on) {   // :266-290, with the step the reference passes (USV_Virtual.py:1546)
+          const double st = ref_step_of(c, b, step, 4);
+          rmax = curriculum_lerp(c, st, c.cur_max_dist, c.max_spawn_d);
+          rmin = curriculum_lerp(c, st, c.cur_min_dist, c.min_spawn_d);
+        }
+        const float r = U(RU_SPAWN_R) * (float)(rmax - rmin) + (float)rmin;
         const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
         sx = r * cosf(th) + tx;
         sy = r * sinf(th) + ty;
@@ -1415,8 +1440,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
     const float head_r = hw * c.tk_scale[1] * task_term(c.tk_mode[1], hdist, c.tk_coeff[1]);
     const float act_pen = -0.05f * (fabsf(cmd0) + fabsf(cmd1));
     overall = (((pos_r + head_r) + prog_r) + 2.0f * (float)gir) + act_pen;
-    // update_kills (:183-209): kill_dist / goal counter
-    die = (pdist > c.kill_dist) || (goal_cnt >= c.kill_after_n);
+    // update_kills (:183-209): kill_dist (the curriculum's at the step after calculate_metrics) / goal counter
+    const float kd = c.curriculum_on ? (float)curriculum_lerp(c, ref_step_of(c, b, step, 5), c.cur_kill_dist,
+                                                              c.kill_dist_d)
+                                     : c.kill_dist;
+    die = (pdist > kd) || (goal_cnt >= c.kill_after_n);
     t_add[0] = pos_r; t_add[1] = head_r; t_add[2] = pdist; t_add[3] = speed;   // update_statistics (:211-219)
   } else {
     // TrackXYOVelocityTask.get_state_observations (:75-101)
@@ -1800,7 +1828,7 @@ int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t
     return 1;
   hipStream_t s = (hipStream_t)stream;
   // per-step scratch: reset count, field maxima, extras sums
-  hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, s, *b);
+  hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, s, *b, cfg->step_inc);
   USV_CHECK_LAUNCH();
   const int grid = (b->n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_reset, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, seed, step, u_inject);

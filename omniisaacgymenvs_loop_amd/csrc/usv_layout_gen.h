@@ -58,6 +58,7 @@
   X(USV_TS_ROWS, "USV_TS_ROWS") \
   X(USV_FNORM, "USV_FNORM") \
   X(USV_RSTASH_ROWS, "USV_RSTASH_ROWS") \
+  X(USV_CLOCK_WORDS, "USV_CLOCK_WORDS") \
   X(USV_SC_OBST, "USV_SC_OBST") \
   X(USV_SC_START, "USV_SC_START") \
   X(USV_SC_YAW, "USV_SC_YAW") \
@@ -323,6 +324,17 @@
   X(offsetof(usv_cfg_t, tk_goal_rand), "usv_cfg.tk_goal_rand") \
   X(offsetof(usv_cfg_t, sig_gain), "usv_cfg.sig_gain") \
   X(offsetof(usv_cfg_t, nan_probe), "usv_cfg.nan_probe") \
+  X(offsetof(usv_cfg_t, curriculum_on), "usv_cfg.curriculum_on") \
+  X(offsetof(usv_cfg_t, pad_curriculum), "usv_cfg.pad_curriculum") \
+  X(offsetof(usv_cfg_t, step_inc), "usv_cfg.step_inc") \
+  X(offsetof(usv_cfg_t, cur_min_dist), "usv_cfg.cur_min_dist") \
+  X(offsetof(usv_cfg_t, cur_max_dist), "usv_cfg.cur_max_dist") \
+  X(offsetof(usv_cfg_t, cur_kill_dist), "usv_cfg.cur_kill_dist") \
+  X(offsetof(usv_cfg_t, cur_warmup), "usv_cfg.cur_warmup") \
+  X(offsetof(usv_cfg_t, cur_end), "usv_cfg.cur_end") \
+  X(offsetof(usv_cfg_t, min_spawn_d), "usv_cfg.min_spawn_d") \
+  X(offsetof(usv_cfg_t, max_spawn_d), "usv_cfg.max_spawn_d") \
+  X(offsetof(usv_cfg_t, kill_dist_d), "usv_cfg.kill_dist_d") \
   X(sizeof(usv_bufs_t), "sizeof usv_bufs") \
   X(offsetof(usv_bufs_t, n), "usv_bufs.n") \
   X(offsetof(usv_bufs_t, pad0), "usv_bufs.pad0") \
@@ -457,4 +469,6 @@
   X(offsetof(lz_cfg_t, adam_eps), "lz_cfg.adam_eps") \
   X(offsetof(lz_cfg_t, min_std), "lz_cfg.min_std") \
   X(offsetof(lz_cfg_t, action_scale), "lz_cfg.action_scale") \
+  X(offsetof(lz_cfg_t, im_coef), "lz_cfg.im_coef") \
+  X(offsetof(lz_cfg_t, expert_act), "lz_cfg.expert_act") \
 

@@ -30,9 +30,12 @@ class PPO:
                  mini_batch_sampling='shuffle', log_intervals=10, flat_expert=None, seed=0):
         if mini_batch_sampling not in ("shuffle", "in_order"):
             raise NameError(mini_batch_sampling + ' is not a valid sampling method. Use one of the followings: shuffle, order')
-        if flat_expert is not None:
-            raise NotImplementedError("imitation (flat_expert) is off in the loopz trainer (rlgames_train.py:92)")
         self.actor, self.critic = actor, critic
+        # imitation (ppo.py:93-94, 253-286): any object with evaluate(obs [rows][D]) -> expert actions [rows][2]
+        # (module.py Expert / Steps_Expert); frozen, so it is evaluated once per update on the stored
+        # observations and the gradient kernel adds (1 - rl_coeff) * sum_a (expert_a - action_mean_a)^2
+        self.flat_expert = flat_expert
+        self._expert_act = None
         self.device = device if str(device).startswith("cuda") else "cuda:0"
         obs_dim = int(actor.obs_shape[0])
         self.storage = RolloutStorage(num_envs, num_transitions_per_env, [obs_dim], [int(critic.obs_shape[0])],
@@ -160,6 +163,7 @@ class PPO:
         _capi.call("lz_returns", _capi.byref(self.cfg), _capi.ptr(self.last_values), _capi.ptr(st.rewards),
                    _capi.ptr(st.dones), _capi.ptr(st.values), _capi.ptr(st.returns), _capi.ptr(st.advantages),
                    _capi.ptr(self.work), s)
+        self._bind_expert()
         self.mean_value_loss, self.mean_surrogate_loss = self._train_step()
         st.clear()
         if log_this_iteration and self.ep_infos:
@@ -193,6 +197,24 @@ class PPO:
         perms = [torch.randperm(nt, device=self.params.device, generator=self._perm_gen)[:m * self.num_mini_batches]
                  for _ in range(self.num_learning_epochs)]
         return torch.stack(perms).view(-1, m).to(torch.int32).contiguous()
+
+    def _bind_expert(self):
+        """flat_expert.evaluate of every stored observation row (storage-row order, T N rows) into the buffer the
+        gradient kernel reads, with the imitation coefficient 1 - rl_coeff (ppo.py:279-282)."""
+        if self.flat_expert is None:
+            self.cfg.expert_act = None
+            self.cfg.im_coef = 0.0
+            return
+        st = self.storage
+        with torch.no_grad():
+            ea = self.flat_expert.evaluate(st.actor_obs.reshape(-1, st.actor_obs.shape[-1]))
+        ea = torch.as_tensor(ea).to(self.params.device, torch.float32).reshape(-1, 2).contiguous()
+        if ea.shape[0] != self.num_transitions_per_env * self.num_envs:
+            raise ValueError(f"flat_expert.evaluate returned {tuple(ea.shape)} for "
+                             f"{self.num_transitions_per_env * self.num_envs} rows")
+        self._expert_act = ea
+        self.cfg.expert_act = ea.data_ptr()
+        self.cfg.im_coef = float(np.float32(1.0 - self.rl_coeff))
 
     def _train_step(self):
         """ppo.py:237-321 on the device: epochs x minibatches (in order, or shuffled rows), each one

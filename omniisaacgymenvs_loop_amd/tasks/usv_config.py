@@ -323,6 +323,7 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     c.flow_vel[0], c.flow_vel[1] = float(flow[0]), float(flow[1])
     # the reference's fail-fast probe toggle (USV_Virtual.py:57-59): on unless USV_NAN_PROBE=0
     c.nan_probe = nan_probe_enabled()
+    c.step_inc = 1 / int(env.get("horizon_length", 16))   # USVVirtual.step += 1 / horizon_length (:1633)
     return c
 
 
@@ -379,7 +380,17 @@ def _pose_task_cfg(c: UsvCfg, name: str, env: Dict[str, Any]) -> Dict[str, Any]:
         rp = dict(_POSE_REWARD)
         rp.update(env.get("reward_parameters", {}) or {})
         if bool(tp.get("spawn_curriculum", False)):
-            raise NotImplementedError("GoToPose spawn_curriculum is not supported (off in every packaged config)")
+            # GoToPoseParameters (USV_task_parameters.py:70-92): linear mode only, as the reference asserts
+            if str(tp.get("spawn_curriculum_mode", "linear")).lower() != "linear":
+                raise AssertionError("Linear is the only currently supported mode.")
+            c.curriculum_on = 1
+            c.cur_min_dist = float(tp.get("spawn_curriculum_min_dist", 0.2))
+            c.cur_max_dist = float(tp.get("spawn_curriculum_max_dist", 3.0))
+            c.cur_kill_dist = float(tp.get("spawn_curriculum_kill_dist", 30.0))
+            c.cur_warmup = float(int(tp.get("spawn_curriculum_warmup", 250)))
+            c.cur_end = float(int(tp.get("spawn_curriculum_end", 1000)))
+            c.min_spawn_d, c.max_spawn_d = float(tp["min_spawn_dist"]), float(tp["max_spawn_dist"])
+            c.kill_dist_d = float(tp["kill_dist"])
         c.tk_mode[0], c.tk_mode[1] = _mode(rp["position_reward_mode"]), _mode(rp["heading_reward_mode"])
         c.tk_coeff[0] = rp["position_exponential_reward_coeff"]
         c.tk_coeff[1] = rp["heading_exponential_reward_coeff"]

@@ -146,7 +146,7 @@ class USVVirtual:
         self.slot_stats = Z((n, DEFINES["USV_FIELD_SLOT_STATS"]), **f32)
         # device step clock (next step, next bias call, current step, current bias call): the kernels take
         # the step index and the action bias from it, so a captured HIP graph replays consecutive steps
-        self.clock = Z(4, device=dev, dtype=torch.int64)
+        self.clock = Z(DEFINES["USV_CLOCK_WORDS"], device=dev, dtype=torch.int64)
         self.states_buf = Z((n, 0), **f32)
         # the potential field in parts (include/usv_hip.h): .field = cost tiles, .fnorm = per-env constants (the SDF
         # comes from the obstacles), .sdf = the sweeps' raw cost rows

@@ -151,6 +151,7 @@ class Config:
     epochs: int = 4
     mini_batches: int = 4
     use_clipped_value_loss: bool = True
+    im_coef: float = 0.0               # 1 - rl_coeff of the imitation term (ppo.py:279-282), with `expert`
 
 
 def _net_backward(p, pre, cache, dout, G):
@@ -174,8 +175,9 @@ def _net_backward(p, pre, cache, dout, G):
     G[pre + "enc0.b"] = de1.sum(0)
 
 
-def minibatch_grad(p: dict, obs, act, old_logp, old_val, ret, adv, scale, cfg: Config):
-    """PPO._train_step's loss (ppo.py:252-288) and its gradient."""
+def minibatch_grad(p: dict, obs, act, old_logp, old_val, ret, adv, scale, cfg: Config, expert=None):
+    """PPO._train_step's loss (ppo.py:252-288) and its gradient; `expert` [B][2]: flat_expert.evaluate of the
+    minibatch observations -> + mean((1 - rl_coeff) * sum_a (expert_a - action_mean_a)^2) (:253-256, 279-282)."""
     B = obs.shape[0]
     mu, ca = net_forward(p, "actor.", obs, True)
     v_out, cc = net_forward(p, "critic.", obs, False)
@@ -206,11 +208,15 @@ def minibatch_grad(p: dict, obs, act, old_logp, old_val, ret, adv, scale, cfg: C
     dv = (dv * F(cfg.value_loss_coef) / F(B)).astype(F)
     var = (std * std).astype(F)
     dmu = (dlp[:, None] * (u - mu) / var).astype(F)
+    im = 0.0
+    if expert is not None:   # MSELoss(expert, action_mean) summed over actions, row mean, x (1 - rl_coeff)
+        dmu = (dmu + F(cfg.im_coef) * (F(2) * (mu - expert)) / F(B)).astype(F)
+        im = float((F(cfg.im_coef) * ((expert - mu) ** 2).sum(1)).mean())
     dstd = (dlp[:, None] * (((u - mu) ** 2) / (var * std) - F(1) / std)).sum(0).astype(F)
     G = {"std": dstd}
     _net_backward(p, "actor.", ca, (dmu * (F(1) - mu * mu)).astype(F), G)
     _net_backward(p, "critic.", cc, dv[:, None], G)
-    loss = float((surr + F(cfg.value_loss_coef) * vl - F(cfg.entropy_coef) * (-lp)).mean())
+    loss = float((surr + F(cfg.value_loss_coef) * vl - F(cfg.entropy_coef) * (-lp)).mean()) + im
     return G, float(vl.mean()), float(surr.mean()), loss
 
 
@@ -244,12 +250,13 @@ def clip_grad(G: dict, obs_dim, max_norm, n_act=2):
     return (g * F(coef)).astype(F), total
 
 
-def train_step(pv, adam: Adam, data: dict, scale, cfg: Config, batches=None):
+def train_step(pv, adam: Adam, data: dict, scale, cfg: Config, batches=None, expert=None):
     """PPO._train_step (ppo.py:237-321): epochs x minibatches of the time-major batch -- in order
     (storage.mini_batch_generator_inorder), or the rows `batches[k]` of the k-th minibatch
     (mini_batch_generator_shuffle, storage.py:123-134: BatchSampler(SubsetRandomSampler) indices)."""
     obs_dim = data["obs"].shape[-1]
     flat = {k: np.asarray(v).reshape((-1,) + np.asarray(v).shape[2:]) for k, v in data.items()}
+    ex = None if expert is None else np.asarray(expert, F).reshape(-1, 2)   # [T N][2] storage-row order
     B = flat["obs"].shape[0]
     M = B // cfg.mini_batches
     vls, sls = [], []
@@ -260,7 +267,8 @@ def train_step(pv, adam: Adam, data: dict, scale, cfg: Config, batches=None):
             k += 1
             G, vl, sloss, loss = minibatch_grad(unflatten(pv, obs_dim), flat["obs"][sl], flat["actions"][sl],
                                                 flat["logp"][sl], flat["values"][sl], flat["returns"][sl],
-                                                flat["advantages"][sl], scale, cfg)
+                                                flat["advantages"][sl], scale, cfg,
+                                                None if ex is None else ex[sl])
             if not math.isfinite(loss):
                 continue
             g, _ = clip_grad(G, obs_dim, cfg.max_grad_norm)

@@ -78,7 +78,7 @@ class _OracleEnvC(ctypes.Structure):
     _fields_ = ([("n", ctypes.c_int)] + [(k, ctypes.c_void_p) for k in _PTR_FIELDS] +
                 [("ctl", ctypes.c_int32 * 20), ("extras", ctypes.c_float * NSTAT), ("dbg", ctypes.c_void_p),
                  ("tmp", ctypes.c_void_p), ("grid_lin", ctypes.c_void_p), ("dist", ctypes.c_void_p),
-                 ("env_org", ctypes.c_void_p), ("tgt_h", ctypes.c_void_p)])
+                 ("env_org", ctypes.c_void_p), ("tgt_h", ctypes.c_void_p), ("step_f", ctypes.c_double)])
 
 
 class OracleEnv:

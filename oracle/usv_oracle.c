@@ -147,7 +147,18 @@ typedef struct oracle_env {
   float *dist;                      /* [USV_NDIST][n] disturbance parameters or NULL */
   const float *env_org;             /* [2][n] env origins (RLTask._env_pos) or NULL */
   float *tgt_h;                     /* [n] GoToPose target heading / TrackXYO target yaw rate */
+  double step_f;                    /* USVVirtual.step (+= 1 / horizon_length per calculate_metrics,
+                                       USV_Virtual.py:1633): the GoToPose curriculum's clock */
 } oracle_env_t;
+
+/* GoToPoseTask spawn curriculum (USV_go_to_pose.py:188-202 kill distance, :266-290 spawn radii): linear in
+ * USVVirtual.step between warmup and end, in the reference's Python-float (double) arithmetic */
+static double curriculum_lerp(const usv_cfg_t *c, double st, double cur, double fin) {
+  if (st < c->cur_warmup) return cur;
+  if (st > c->cur_end) return fin;
+  const double r = (st - c->cur_warmup) / (c->cur_end - c->cur_warmup);
+  return r * (fin - cur) + cur;
+}
 
 /* ------------------------------------------------------------------------ */
 /* Forces: HydrodynamicsObject.ComputeDampingMatrix/ComputeHydrodynamicsEffects
@@ -598,8 +609,14 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
     const float yaw0 = u[RU_YAW] * (float)OPI;
     float sx, sy;
     if (c->task_kind == USV_TASK_GO_TO_POSE) {
-      /* GoToPoseTask.get_spawns (USV_go_to_pose.py:256-319): disk around the previous target */
-      const float r = u[RU_SPAWN_R] * (float)((double)rmax - (double)rmin) + rmin;
+      /* GoToPoseTask.get_spawns (USV_go_to_pose.py:256-319): disk around the previous target, radii from the
+         curriculum at the reset's USVVirtual.step when it is on (:266-290) */
+      double dmax = rmax, dmin = rmin;
+      if (c->curriculum_on) {
+        dmax = curriculum_lerp(c, E->step_f, c->cur_max_dist, c->max_spawn_d);
+        dmin = curriculum_lerp(c, E->step_f, c->cur_min_dist, c->min_spawn_d);
+      }
+      const float r = u[RU_SPAWN_R] * (float)(dmax - dmin) + (float)dmin;
       const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
       sx = r * cosf(th) + E->tgt_x[e];
       sy = r * sinf(th) + E->tgt_y[e];
@@ -862,7 +879,12 @@ static void priv_tail(const usv_cfg_t *c, const oracle_env_t *E, int e, float *o
 
 static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const float *U);
 
+static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const float *U);
 void oracle_step_post(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
+  oracle_step_post_impl(c, E, U);
+  E->step_f += c->step_inc;   /* calculate_metrics: USVVirtual.step += 1 / horizon_length (USV_Virtual.py:1633) */
+}
+static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
   if (c->task_kind != USV_TASK_CAPTURE_XY) { oracle_step_post_task(c, E, U); return; }
   const int n = E->n;
   const int any_reset_none = (E->ctl[USV_CTL_POT_VALID] == 0);
@@ -1165,8 +1187,11 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
       const float act_pen = -0.05f * (fabsf(cmd[0]) + fabsf(cmd[1]));
       const float overall = pos_r + head_r + prog + 2.0f * (float)gir + act_pen;
       E->rew[e] = overall + pens;
-      /* update_kills (:183-209) */
-      const int die = (pdist > c->kill_dist) || (E->goal_cnt[e] >= c->kill_after_n);
+      /* update_kills (:183-209), with the step after this calculate_metrics */
+      const float kd = c->curriculum_on ? (float)curriculum_lerp(c, E->step_f + c->step_inc, c->cur_kill_dist,
+                                                                 c->kill_dist_d)
+                                        : c->kill_dist;
+      const int die = (pdist > kd) || (E->goal_cnt[e] >= c->kill_after_n);
       const int tout = E->progress[e] >= c->max_episode_length - 1;
       E->reset_buf[e] = c->fixed_horizon_eval ? tout : (tout ? 1 : die);
       t_add[0] = pos_r; t_add[1] = head_r; t_add[2] = pdist; t_add[3] = speed;   /* update_statistics (:211-219) */

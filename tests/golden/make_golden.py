@@ -355,20 +355,29 @@ def load_task_cfg(variant: str):
         sr.update(enabled=True, npz_path=os.path.join(OUT, "scenes_S.npz"), start_index=2, cycle=True,
                   strict_hash=True)
         cfg["env"]["maxEpisodeLength"] = 24
-    if variant in ("P", "T"):
+    if variant in ("P", "T", "Q"):
         # SURVEY A20 tasks on the TEST glue: the task's own yaml task/reward parameters
         # (cfg/task/USV/USV_Virtual_GoToPose.yaml, USV_Virtual_TrackXYOVelocity.yaml)
         import yaml
-        name = "USV_Virtual_GoToPose.yaml" if variant == "P" else "USV_Virtual_TrackXYOVelocity.yaml"
+        name = "USV_Virtual_TrackXYOVelocity.yaml" if variant == "T" else "USV_Virtual_GoToPose.yaml"
         with open(os.path.join(REF, "omniisaacgymenvs/cfg/task/USV", name)) as f:
             tcfg = yaml.safe_load(f)
         env = cfg["env"]
         env["task_parameters"] = dict(tcfg["env"]["task_parameters"])
         env["reward_parameters"] = dict(tcfg["env"]["reward_parameters"])
-        if variant == "P":
+        if variant in ("P", "Q"):
             env["task_parameters"]["goal_random_position"] = 2.0
             env["task_parameters"]["position_tolerance"] = 0.3   # reachable within the short episode
         env["maxEpisodeLength"] = 40
+        if variant == "Q":
+            # the GoToPose spawn curriculum (USV_go_to_pose.py:188-202, 266-290) across its three regimes
+            # within 64 steps: USVVirtual.step = steps / 16 < warmup 1, between 1 and 3, > end 3; short
+            # episodes so resets land in every regime, kill distances small enough to kill
+            env["task_parameters"].update(spawn_curriculum=True, spawn_curriculum_min_dist=0.2,
+                                          spawn_curriculum_max_dist=1.5, spawn_curriculum_kill_dist=2.5,
+                                          spawn_curriculum_warmup=1, spawn_curriculum_end=3,
+                                          min_spawn_dist=0.3, max_spawn_dist=3.0, kill_dist=3.5)
+            env["maxEpisodeLength"] = 9
     return cfg
 
 
@@ -407,7 +416,7 @@ def build_usv(torch, n, variant):
     usv._heron = heron
     usv._env_pos = torch.zeros((n, 3))
     usv.task._env = usv
-    if variant in ("P", "T"):
+    if variant in ("P", "T", "Q"):
         # the live glue cannot run these tasks; minimal harness fixes:
         # Core's 20-column task_data block, the marker buffer set_targets reads, and
         # update_kills(step) called with the extra current_state argument
@@ -622,7 +631,21 @@ def gen_hydrostatics(torch):
                         gravity=np.float32(grav))
 
 
-def gen_loopz(torch, n=16, T=24, seed=7, sampling="in_order"):
+class ScriptedExpert:
+    """A frozen flat_expert for the imitation fixture (PPO(flat_expert=...) calls only .evaluate(obs),
+    ppo.py:253-256): a fixed smooth map of the observation to actions in (-1, 1)."""
+
+    def __init__(self, torch):
+        g = torch.Generator().manual_seed(5)
+        self.w = torch.randn((33, 2), generator=g) * 0.2
+        self.torch = torch
+
+    def evaluate(self, obs):
+        with self.torch.no_grad():
+            return self.torch.tanh(obs @ self.w)
+
+
+def gen_loopz(torch, n=16, T=24, seed=7, sampling="in_order", expert=False):
     """The loopz trainer's PPO (omniisaacgymenvs/algo/ppo/{ppo,storage,module}.py) as
     scripts/rlgames_train.py:273-328 builds it (MLPEncode_wrap actor / critic, LeakyReLU, tanh actor
     output, squashed Gaussian init std 0.3, gamma 0.997, lambda 0.95, 4 x 4 in-order minibatches,
@@ -671,9 +694,12 @@ def gen_loopz(torch, n=16, T=24, seed=7, sampling="in_order"):
     actor = M.Actor(M.MLPEncode_wrap([128, 128], nn.LeakyReLU, ob_dim, act_dim, nn.Tanh, False, **kw),
                     M.SquashedGaussianDiagonalCovariance(act_dim, 0.3, action_scale=1.0), "cpu")
     critic = M.Critic(M.MLPEncode_wrap([128, 128], nn.LeakyReLU, ob_dim, 1, **kw), "cpu")
+    fe = ScriptedExpert(torch) if expert else None
     ppo = P.PPO(actor=actor, critic=critic, num_envs=n, num_transitions_per_env=T, num_learning_epochs=4,
                 gamma=0.997, lam=0.95, num_mini_batches=4, device="cpu", log_dir="/tmp/loopz_golden",
-                mini_batch_sampling=sampling, learning_rate=5e-4)
+                mini_batch_sampling=sampling, learning_rate=5e-4, flat_expert=fe)
+    if expert:
+        ppo.update_rl_coeff(0.3)   # the trainer's value (rlgames_train.py:352-354)
     sd = lambda m: {k: v.detach().clone().numpy() for k, v in m.state_dict().items()}
     init = {"actor": sd(actor.architecture), "dist": sd(actor.distribution), "critic": sd(critic.architecture)}
     rng = np.random.default_rng(seed)
@@ -714,8 +740,12 @@ def gen_loopz(torch, n=16, T=24, seed=7, sampling="in_order"):
         out[f"adam_v_{i}"] = s_["exp_avg_sq"].numpy()
     if sampling == "shuffle":
         out["batches"] = np.stack(batches)   # [epochs * mini_batches][M] rows of the flattened [T * N] storage
-    np.savez_compressed(os.path.join(OUT, "loopz_update.npz" if sampling == "in_order" else
-                                     f"loopz_update_{sampling}.npz"), **out)
+    if expert:   # the expert's actions on the stored observations (storage-row order) and its weights
+        out["expert_act"] = fe.evaluate(st.actor_obs.reshape(-1, ob_dim)).numpy()
+        out["expert_w"] = fe.w.numpy()
+        out["rl_coeff"] = np.float64(ppo.rl_coeff)
+    name = "loopz_update" + ("" if sampling == "in_order" else f"_{sampling}") + ("_expert" if expert else "")
+    np.savez_compressed(os.path.join(OUT, name + ".npz"), **out)
 
 
 def gen_field(torch):
@@ -860,7 +890,7 @@ def gen_episode(torch, variant, n, steps, seed):
                 data["thr_l"].append(td.thruster_multiplier[:, 0].numpy().copy())
                 data["thr_r"].append(td.thruster_multiplier[:, 0].numpy().copy())
             data["k_iz"].append(usv.k_Iz[:, 0].numpy().copy())
-            if variant in ("P", "T"):
+            if variant in ("P", "T", "Q"):
                 data["obst"].append(np.zeros((n, 16, 2), np.float32))
                 data.setdefault("tgt_h", []).append(_task_targets(usv.task)[1])
             else:
@@ -869,7 +899,7 @@ def gen_episode(torch, variant, n, steps, seed):
             data["goal_cnt"].append(usv.task._goal_reached.numpy().copy())
             tk = usv.task
             pen = usv._penalties
-            if variant in ("P", "T"):
+            if variant in ("P", "T", "Q"):
                 data["terms"].append(np.zeros((n, 15), np.float32))
             else:
               data["terms"].append(torch.stack([tk.distance_reward, tk.alignment_reward, tk.potential_shaping_reward,
@@ -888,7 +918,7 @@ def gen_episode(torch, variant, n, steps, seed):
                     td_.disturbance_torques_const[:, 2], td_._torque_freq, td_._torque_shift, td_._torque_amp],
                     0).numpy().copy())
             ex = extras.get("episode", {})
-            names = STAT_NAMES if variant not in ("P", "T") else list(usv.episode_sums.keys())
+            names = STAT_NAMES if variant not in ("P", "T", "Q") else list(usv.episode_sums.keys())
             data["extras"].append(np.array([float(ex[k]) if k in ex else np.nan for k in names], np.float32))
     out = {k: np.stack(v) for k, v in data.items()}
     out["reset_U"] = np.concatenate(reset_U, 0) if reset_U else np.zeros((0, NU_RESET), np.float32)
@@ -897,7 +927,7 @@ def gen_episode(torch, variant, n, steps, seed):
                        else np.zeros(150, np.float32))
     out["config_json"] = np.frombuffer(json.dumps(task_cfg).encode(), dtype=np.uint8)
     out["bias_steps"] = np.int64(usv._initial_action_bias_steps)
-    if variant in ("P", "T"):
+    if variant in ("P", "T", "Q"):
         out["extras_names"] = np.array(list(usv.episode_sums.keys()))
     np.savez_compressed(os.path.join(OUT, f"episode_{variant}.npz"), **out)
     print(f"episode_{variant}: resets per step", out["reset_mask"].sum(1).tolist())
@@ -1094,11 +1124,13 @@ def main():
         "episodeD": lambda: gen_episode(torch, "D", 10, 48, 55),
         "episodeE": lambda: gen_episode(torch, "E", 10, 48, 56),
         "episodeP": lambda: gen_episode(torch, "P", 12, 64, 31),
+        "episodeQ": lambda: gen_episode(torch, "Q", 12, 64, 33),
         "episodeS": lambda: (make_scene_file(), gen_episode(torch, "S", 6, 64, 41)),
         "episodeT": lambda: gen_episode(torch, "T", 12, 64, 32),
         "ppo": lambda: gen_ppo(torch),
         "loopz": lambda: gen_loopz(torch),
         "loopz_shuffle": lambda: gen_loopz(torch, sampling="shuffle"),
+        "loopz_expert": lambda: gen_loopz(torch, expert=True),
         "ckpt811": lambda: gen_ckpt811(torch),
     }
     for name, fn in jobs.items():

@@ -56,7 +56,7 @@ def _post_state(d, t):
     return torch.tensor(np.stack([d[k][t] for k in STATE_KEYS]).astype(np.float32), device=DEV)
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "T", "S"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "Q", "T", "S"])
 def test_fixture_replay_on_gpu(golden, variant):
     """The reference's recorded episodes replayed through the HIP path, two ways in lockstep:
     * post: pre_physics + post_physics on the reference's own post-integration state -> obs, reward,

@@ -17,7 +17,7 @@ OBS = 33
 _Leaky, _Tanh = torch.nn.LeakyReLU, torch.nn.Tanh   # the activation constructors the reference passes
 
 
-def _build(n, T, d=None, seed=0, sampling="in_order"):
+def _build(n, T, d=None, seed=0, sampling="in_order", flat_expert=None):
     kw = dict(speed_dim=3, mass_dim=8, mass_latent_dim=8, mass_encoder_shape=(64, 16))
     actor = Actor(MLPEncode_wrap([128, 128], _Leaky, OBS, 2, _Tanh, False, seed=seed, **kw),
                   SquashedGaussianDiagonalCovariance(2, 0.3, action_scale=1.0), DEV)
@@ -28,7 +28,7 @@ def _build(n, T, d=None, seed=0, sampling="in_order"):
         actor.distribution.load_state_dict(sd("dist"))
         critic.architecture.load_state_dict(sd("critic"))
     return PPO(actor, critic, n, T, 4, 4, gamma=0.997, lam=0.95, device=DEV, mini_batch_sampling=sampling,
-               learning_rate=5e-4, log_dir="/tmp/loopz_test")
+               learning_rate=5e-4, log_dir="/tmp/loopz_test", flat_expert=flat_expert)
 
 
 def _params(d, tag):
@@ -194,3 +194,42 @@ def test_loopz_trainer_runs_on_the_usv_task(tmp_path, monkeypatch):
     assert LT.load_full(str(ck), actor, critic, ppo2) == 2
     p_saved = np.concatenate([v.numpy().reshape(-1) for v in sd["actor_architecture_state_dict"].values()])
     np.testing.assert_array_equal(actor.architecture.flat().numpy(), p_saved)
+
+
+class _Expert:
+    """The fixture's frozen expert (tests/golden/make_golden.py ScriptedExpert): tanh(obs @ w)."""
+
+    def __init__(self, w):
+        self.w = torch.tensor(w, device=DEV)
+
+    def evaluate(self, obs):
+        return torch.tanh(obs @ self.w)
+
+
+def test_imitation_update_vs_reference(golden):
+    """PPO(flat_expert=...) + update_rl_coeff(0.3) (ppo.py:93-100, 253-286): the expert's actions on the stored
+    observations feed the gradient kernel's (1 - rl_coeff) * sum_a (expert_a - action_mean_a)^2 term.  Against
+    the reference run (loopz_update_expert.npz) with the oracle test's tolerance (clip_grad_norm_ is active at
+    every step), and against the oracle (same gradient kernel inputs) at 1e-5."""
+    d = golden("loopz_update_expert.npz")
+    T, n = d["rew"].shape
+    ppo = _build(n, T, d, flat_expert=_Expert(d["expert_w"]))
+    ppo.update_rl_coeff(0.3)
+    _rollout(ppo, d)
+    ppo.update(actor_obs=None, value_obs=torch.tensor(d["obs"][T]), log_this_iteration=False, update=0)
+    np.testing.assert_allclose(ppo._expert_act.cpu().numpy(), d["expert_act"], rtol=1e-5, atol=1e-6)
+    assert ppo.adam_step() == 16
+    got, want, p0 = ppo.params.cpu().numpy(), _params(d, "after"), _params(d, "init")
+    a, b = got - p0, want - p0
+    bad = ~np.isclose(a, b, rtol=1e-3, atol=2e-7)
+    ET.record("loopz_update_expert", "param_delta", a, b)
+    assert bad.mean() < 2e-3 and np.abs(a - b).max() < 3e-4, (int(bad.sum()), float(np.abs(a - b).max()))
+    np.testing.assert_allclose(ppo.mean_value_loss, float(d["loss_value"]), rtol=1e-5)
+    np.testing.assert_allclose(ppo.mean_surrogate_loss, float(d["loss_surrogate"]), rtol=5e-4)
+    # the same update on the oracle from the same rollout buffers: the kernels' arithmetic, tight
+    data = {k: d[k] for k in ("obs", "actions", "logp", "values", "returns", "advantages")}
+    data["obs"] = data["obs"][:-1]
+    pv, _, _ = L.train_step(p0, L.Adam.zeros(len(p0)), data, np.float32(1.0),
+                            L.Config(im_coef=float(np.float32(0.7))), expert=d["expert_act"])
+    bad_o = ~np.isclose(got - p0, pv - p0, rtol=1e-3, atol=2e-7)
+    assert bad_o.mean() < 2e-3, int(bad_o.sum())

@@ -72,3 +72,32 @@ def test_shuffle_update_matches_reference(golden):
     np.testing.assert_allclose(pv - pv0, want - pv0, rtol=1e-3, atol=2e-7)
     # the shuffled minibatches really differ from the in-order ones
     assert not np.array_equal(np.sort(d["batches"][0]), np.arange(d["batches"].shape[1]))
+
+
+def test_imitation_update_matches_reference(golden):
+    """PPO(flat_expert=...) with update_rl_coeff(0.3) (ppo.py:93-100, 253-286): the loss gains
+    mean((1 - rl_coeff) * sum_a (expert_a - action_mean_a)^2) over each minibatch; the fixture's expert is a
+    fixed map of the observation, recorded with its actions on the stored observations."""
+    d = golden("loopz_update_expert.npz")
+    assert float(d["rl_coeff"]) == 0.3
+    obs = d["obs"][:-1].reshape(-1, OBS)
+    np.testing.assert_allclose(d["expert_act"], np.tanh(obs @ d["expert_w"]), rtol=1e-5, atol=1e-6)
+    pv0 = _params(d, "init")
+    data = {k: d[k] for k in ("obs", "actions", "logp", "values", "returns", "advantages")}
+    data["obs"] = data["obs"][:-1]
+    adam = L.Adam.zeros(len(pv0))
+    cfg = L.Config(im_coef=float(np.float32(1 - 0.3)))
+    pv, vl, sl = L.train_step(pv0, adam, data, np.float32(1.0), cfg, expert=d["expert_act"])
+    want = _params(d, "after")
+    np.testing.assert_allclose(vl, float(d["loss_value"]), rtol=1e-5)
+    np.testing.assert_allclose(sl, float(d["loss_surrogate"]), rtol=5e-4)
+    # the imitation gradient is large enough to engage clip_grad_norm_ (0.5) at every step, and the summation
+    # order of 96-row sums differs from torch's: 16 Adam steps leave ~0.1% of the weights beyond the tight
+    # tolerance of the other updates (51 of 45,621 here, each within 3e-4 of lr 5e-4 x 16 steps); the imitation
+    # term's own head (mlp4) agrees to 1e-6
+    a, b = pv - pv0, want - pv0
+    bad = ~np.isclose(a, b, rtol=1e-3, atol=2e-7)
+    assert bad.mean() < 2e-3 and np.abs(a - b).max() < 3e-4, (int(bad.sum()), float(np.abs(a - b).max()))
+    # the imitation term moved the actor: without it the update lands elsewhere
+    pv_rl, _, _ = L.train_step(pv0, L.Adam.zeros(len(pv0)), data, np.float32(1.0), L.Config())
+    assert np.abs((pv_rl - pv0) - (want - pv0)).max() > 1e-2

@@ -191,7 +191,7 @@ def test_episode_c_exercises_disturbances(golden):
     assert (d["dist"][-1][7] < 0).any() and (d["dist"][-1][7] > 0).any()   # torque sign flip
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "T", "S"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "Q", "T", "S"])
 def test_episode_post_physics(golden, variant):
     """obs / reward / done / DR / spawns given the reference's post-integration state."""
     d = golden(f"episode_{variant}.npz")
@@ -212,7 +212,7 @@ def test_episode_post_physics(golden, variant):
         np.testing.assert_array_equal(obst.transpose(2, 0, 1), d["obst"][t])
 
 
-@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "T", "S"])
+@pytest.mark.parametrize("variant", ["A", "B", "C", "D", "E", "P", "Q", "T", "S"])
 def test_episode_end_to_end(golden, variant):
     """Full replay incl. this build's integrator; the reference's potential-shaping
     term amplifies ~1e-7 state differences by 100, hence the reward tolerance."""
