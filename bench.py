@@ -225,6 +225,22 @@ REWARD_TARGET = 30.0           # BASELINE metric, half 2: wall-clock to rewards/
 MILESTONES = (30.0, 60.0, 80.0, 100.0)
 
 
+def phase_split(timed_events, ms_per_step, minibatches, last_epoch):
+    """Rollout / update split of the timed epochs from the (start, rollout end, update end) HIP events each
+    recorded on the stream (A2CAgent.phase_events): means over the epochs; host_gap_ms = the rest of the epoch."""
+    if not timed_events:
+        return {}
+    rp = [a.elapsed_time(b) for a, b, _ in timed_events]
+    up = [b.elapsed_time(c) for _, b, c in timed_events]
+    r, u = sum(rp) / len(rp), sum(up) / len(up)
+    return {"rollout_ms": r, "update_ms": u, "update_us_per_minibatch": u * 1e3 / minibatches,
+            "host_gap_ms": ms_per_step - (r + u),
+            "rollout_ms_min_max": [min(rp), max(rp)], "update_ms_min_max": [min(up), max(up)],
+            "phase_method": f"HIP events recorded on the stream inside each of the {len(rp)} timed epochs "
+                            f"(epochs {last_epoch - len(rp) + 1}-{last_epoch}) around the rollout (+ GAE / prepare) "
+                            "and the update; mean over the timed epochs"}
+
+
 def time_epochs(agent, steps, world, local):
     """`steps` train epochs between barrier + synchronize pairs; max over ranks (seconds)."""
     import torch
@@ -359,17 +375,8 @@ def main():
     # timed epoch recorded around its two halves on the stream (the intervals hold whatever the GPU did or
     # waited for between the events, host submission included); host_gap_ms = the rest of the timed epoch
     # (the epoch-end synchronisation, meters, the next submission), >= 0 by construction
-    phase = {}
-    if timed_events:
-        rp = [a.elapsed_time(b) for a, b, _ in timed_events]
-        up = [b.elapsed_time(c) for _, b, c in timed_events]
-        phase = {"rollout_ms": sum(rp) / len(rp), "update_ms": sum(up) / len(up),
-                 "update_us_per_minibatch": sum(up) / len(up) * 1e3 / (agent.mini_epochs_num * agent.num_minibatches),
-                 "host_gap_ms": elapsed / args.steps * 1e3 - (sum(rp) + sum(up)) / len(rp),
-                 "rollout_ms_min_max": [min(rp), max(rp)], "update_ms_min_max": [min(up), max(up)],
-                 "phase_method": f"HIP events recorded on the stream inside each of the {len(rp)} timed epochs "
-                                 f"(epochs {epoch_timed_last - len(rp) + 1}-{epoch_timed_last}) around the rollout "
-                                 "(+ GAE / prepare) and the update; mean over the timed epochs"}
+    phase = phase_split(timed_events, elapsed / args.steps * 1e3, agent.mini_epochs_num * agent.num_minibatches,
+                        epoch_timed_last)
     # the same two graphs replayed behind a spin kernel after the timed epochs: device time only (no host
     # submission inside the pairs), at a later training state (more resets per step as the policy learns)
     if agent._graph_play is not None and agent._graph_update is not None:

@@ -37,3 +37,26 @@ def test_adam_banks_struct_matches_header():
     b = PpoAdamBanks()
     b.params[0], b.params[1] = 16, 32
     assert (b.params[0], b.params[1]) == (16, 32)
+
+
+class _At:
+    """An event at a fixed time: a.elapsed_time(b) = b.t - a.t."""
+
+    def __init__(self, t):
+        self.t = t
+
+    def elapsed_time(self, other):
+        return other.t - self.t
+
+
+def test_phase_split_from_timed_epoch_events():
+    """The rollout / update split of the timed epochs (events recorded inside them): means, the epochs named,
+    and host_gap_ms = ms_per_step - rollout - update (>= 0 whenever the events lie inside the timed epochs)."""
+    bench = pytest.importorskip("bench")
+    ev = [(_At(0.0), _At(10.0), _At(60.0)), (_At(100.0), _At(112.0), _At(164.0))]
+    ph = bench.phase_split(ev, 65.0, 2048, 30)
+    assert ph["rollout_ms"] == pytest.approx(11.0) and ph["update_ms"] == pytest.approx(51.0)
+    assert ph["host_gap_ms"] == pytest.approx(3.0) and ph["host_gap_ms"] >= 0
+    assert ph["update_us_per_minibatch"] == pytest.approx(51.0e3 / 2048)
+    assert ph["rollout_ms_min_max"] == [10.0, 12.0] and "epochs 29-30" in ph["phase_method"]
+    assert bench.phase_split([], 65.0, 2048, 30) == {}
