@@ -141,7 +141,8 @@ typedef struct oracle_env {
   int32_t ctl[USV_CTL_N];
   float extras[USV_NSTAT];
   /* diagnostics of the last step (for parity tests) */
-  float *dbg;                       /* [n][16]: u_l, u_r, target_l, target_r, pot, danger, ... */
+  float *dbg;                       /* [n][16]: u_l, u_r, target_l, target_r, pot, danger, total, pens, shaping, dist_r, align_r,
+                                       praw (before the dead zone), ppos, ggate */
   float *tmp;                       /* [n][8]: cmd[2], thrust[2], unit[2], target force[2] */
   const float *grid_lin;            /* [150] potential-field cell centres, NULL => linspace formula */
   float *dist;                      /* [USV_NDIST][n] disturbance parameters or NULL */
@@ -1002,6 +1003,7 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
     E->prev_head[e] = herr;
     const float prev_pot = (any_reset_none || was_reset) ? pot : E->prev_pot[e];
     float praw = (prev_pot - pot) * 100.0f;
+    const float praw_in = praw;   /* before the dead zone (dbg[11]: the tests' discontinuity margins) */
     if (fabsf(praw) < 0.01f) praw = 0.f;
     const float pa1 = 2.0f * tanhf(praw / (2.0f + 1e-6f));
     const float gdx = ex / (dist + 1e-6f), gdy = ey / (dist + 1e-6f);
@@ -1077,7 +1079,8 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
       ADDS(ST_U_SUM, unit[0] + unit[1]);
 #undef ADDS
     }
-    if (dbg) { dbg[4] = pot; dbg[5] = danger; dbg[6] = total; dbg[7] = pens; dbg[8] = shaping; dbg[9] = dist_r; dbg[10] = align_r; }
+    if (dbg) { dbg[4] = pot; dbg[5] = danger; dbg[6] = total; dbg[7] = pens; dbg[8] = shaping; dbg[9] = dist_r; dbg[10] = align_r;
+               dbg[11] = praw_in; dbg[12] = ppos; dbg[13] = ggate; }
     /* ---- _process_data: clamp obs (vec_env_rlgames.py:85-95) ---- */
     for (int q = 0; q < USV_NOBS; ++q) E->obs[(size_t)e * USV_NOBS + q] = clampf_(obs[q], -c->clip_obs, c->clip_obs);
     E->just_reset[e] = 0;

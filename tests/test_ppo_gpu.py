@@ -412,10 +412,15 @@ def test_group_fold_matches_raw_row_path_and_oracle(minibatch, monkeypatch):
                       ("exp_adv", adv), ("exp_mu", mu0 + 0.01), ("exp_sigma", sig0)):
         getattr(ag, name).copy_(T(arr))
     orms = ag.obs_rms.clone()
+    mu_in, sig_in = ag.exp_mu.clone(), ag.exp_sigma.clone()
 
     def grad(mode):
+        # the gradient kernel writes each row's new mu / sigma back (rl_games' dataset.update_mu_sigma), so every
+        # call starts from the same experience
         monkeypatch.setenv("USV_PPO_FOLD", mode)
         ag.obs_rms.copy_(orms)
+        ag.exp_mu.copy_(mu_in)
+        ag.exp_sigma.copy_(sig_in)
         c.call("ppo_minibatch_grad", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
                1, 0, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp), c.ptr(ag.exp_val), c.ptr(ag.exp_ret),
                c.ptr(ag.exp_adv), c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.grad), c.ptr(ag.losses),
