@@ -1532,6 +1532,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
       s.fold[1] = (int)gen;
     }
     __syncthreads();
+    USV_PHASE(ppo, 14);
     if (s.fold[0]) {
       constexpr int NQ = NPART_PAD / 4;
       const int q4 = (NQ + M - 1) / M, qa = m * q4, qb = min(qa + q4, NQ);
@@ -1566,6 +1567,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
       __syncthreads();
       if (tid == 0) ctl[32 + m] = (uint32_t)s.fold[1];   // this slice of the group row is this launch's
     }
+    USV_PHASE(ppo, 15);
   }
 }
 
@@ -1979,11 +1981,14 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
 }
 
 // the XCD-group fold of the partial rows (FOLD_G): minibatches of 8 x 1..32 workgroups (the whole grid resident at
-// one workgroup per CU); USV_PPO_FOLD=0 turns it off (A/B builds, or ranks sharing one device)
-// (USV_PPO_FOLD=2: every member arrives but none folds -- the reduction's raw-row path, for the tests)
+// one workgroup per CU).  Off by default: same-box A/B at 131072 envs (profiles/r04/r04c_fold_ab.txt), rocprof
+// means fold 22.57 + 5.11 us vs 18.39 + 7.00 us without (write-through partial stores and the group wait
+// +1.5 us, the fold's own load / store round 3.6 us, against 1.9 us saved in the reduction, whose time is its
+// fixed latency rather than the 21.8 MB it reads).  USV_PPO_FOLD=1 turns it on; USV_PPO_FOLD=2: every member
+// arrives but none folds -- the reduction's raw-row path, for the tests.
 static int fold_env() {
   const char *e = getenv("USV_PPO_FOLD");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }
 static bool fold_on(int nblk) {
   return fold_env() != 0 && nblk % FOLD_G == 0 && nblk / FOLD_G >= 1 && nblk / FOLD_G <= FOLD_MAX_M;

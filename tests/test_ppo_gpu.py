@@ -139,12 +139,15 @@ def _run_update(ppo, monkeypatch, fused, minibatch, mini_epochs, grad_norm=None,
             for k in ("model_params", "adam_m", "adam_v", "opt", "kls", "loss_log", "obs_rms")}
 
 
-@pytest.mark.parametrize("mb_div,mini_epochs,bf16", [(4, 8, False), (1, 3, False), (4, 8, True)])
-def test_fused_chain_matches_split_path(ppo, monkeypatch, mb_div, mini_epochs, bf16):
+@pytest.mark.parametrize("mb_div,mini_epochs,bf16,fold", [(4, 8, False, "0"), (1, 3, False, "0"), (4, 8, True, "0"),
+                                                         (4, 8, False, "1")])
+def test_fused_chain_matches_split_path(ppo, monkeypatch, mb_div, mini_epochs, bf16, fold):
     """ppo_minibatch_fused / ppo_minibatch_finish (Adam step speculated inside the reduction, checked by
     the next launch) vs ppo_minibatch_grad + ppo_minibatch_apply: bit-identical parameters, moments,
     optimiser scalars, KLs and losses -- without clipping, with clipping at every step (the redo path),
-    with clipping at some steps, for an odd chain (state copied back from bank 1) and in the bf16 GEMM mode."""
+    with clipping at some steps, for an odd chain (state copied back from bank 1), in the bf16 GEMM mode and
+    with the XCD-group fold of the partial rows (USV_PPO_FOLD=1, off by default)."""
+    monkeypatch.setenv("USV_PPO_FOLD", fold)
     H, N = ppo["exp_rewards"].shape[:2]
     mb = N * H // mb_div
     ref = _run_update(ppo, monkeypatch, False, mb, mini_epochs, bf16=bf16)
@@ -386,7 +389,7 @@ def test_player_runs_the_usv_task(tmp_path):
 @pytest.mark.parametrize("minibatch", [8192, 1024, 256])
 def test_group_fold_matches_raw_row_path_and_oracle(minibatch, monkeypatch):
     """The XCD-group fold of the partial rows (ppo.hip FOLD_G; 8 groups of nblk / 8 = 32, 4 or 1 workgroups):
-    folded in the gradient kernel (USV_PPO_FOLD=1, the default), or every member arriving without folding so
+    folded in the gradient kernel (USV_PPO_FOLD=1; off by default, see ppo.hip fold_env), or every member arriving without folding so
     the reduction sums the raw rows in the fold's order (USV_PPO_FOLD=2): bit-identical gradients, losses and
     KL, twice in a row (the monotonic arrival counters carry the launch generation); without the fold
     (USV_PPO_FOLD=0, the reduction's 16-group order) the same gradient within 1e-6 of its largest component,

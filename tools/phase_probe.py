@@ -62,11 +62,14 @@ def main():
     for k, what in ((9, "layer 1 done"), (10, "W2 committed"), (11, "layer-2 MFMA loop done"),
                     (12, "layer 2 done"), (2, "heads done"), (3, "losses done"), (4, "dz2 done"),
                     (13, "dW2 MFMA loop done"), (5, "dW2 stored"), (6, "dh1 done"), (7, "dz1 done"),
-                    (8, "dW1 done"), (14, "w4 stores drained"), (15, "w0 stores drained")):
+                    (8, "dW1 done"), (14, "fold: group arrived"), (15, "fold: slice written")):
         if np.all(b[:, k] == 0):   # not stamped by this build
             continue
         print(f"  slot {k:2d} {what:24s} t = {np.mean(b[:, k] - b[:, 0]) / 100:7.2f} us "
               f"(max {np.max(b[:, k] - b[:, 0]) / 100:7.2f})")
+    last = 15 if np.any(b[:, 15] != 0) else 8
+    print(f"  launch span (first start -> last slot-{last} stamp): {(b[:, last].max() - b[:, 0].min()) / 100:7.2f} us; "
+          f"start spread {(b[:, 0].max() - b[:, 0].min()) / 100:5.2f} us")
     pp = read("pol")
     b = pp[:256]
     b = b[b[:, 0] > 0]
