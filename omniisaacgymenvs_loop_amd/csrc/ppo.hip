@@ -1634,14 +1634,15 @@ __device__ __forceinline__ uint32_t *dp_flag(void *buf, int chunk, int sender) {
 // every rank).  A wait beyond timeout_ms, or an error another workgroup already flagged, sets / sees
 // bit 0 of dp.err and goes on with whatever arrived (the host raises after the epoch), so a lost peer
 // costs one timeout per launch, not one per chunk.
-// USV_DP_ORDER (A/B builds override it): 1 = a system-scope RELEASE fence before the flag store (every payload
-// store of the workgroup is ordered before the flag in the memory model, not only by the drained write-through
-// stores)
-// and the poll is followed by one system-scope ACQUIRE fence (the payload loads are ordered after the
-// flags seen); 0 = relaxed flag store and poll (the payload stores' own sc0 sc1 write-through + vmcnt(0)
-// drain and the poll's control dependency carry the order)
+// USV_DP_ORDER (bit mask; A/B builds override it): bit 0 = a system-scope RELEASE fence before the flag store
+// (every payload store of the workgroup is ordered before the flag in the memory model, not only by the drained
+// write-through stores); bit 1 = one system-scope ACQUIRE fence after the poll (the payload loads are ordered
+// after the flags seen); 0 = relaxed flag store and poll: the guide's {sc0 sc1 stores and loads both sides}
+// form (MI355X_MICROARCH.md, valid hand-off forms) -- every payload store and load is sc0 sc1, every storing wave
+// drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane per receiver
+// raises the flag, and every payload load follows the polling wave's match through a workgroup barrier
 #ifndef USV_DP_ORDER
-#define USV_DP_ORDER 1
+#define USV_DP_ORDER 3
 #endif
 __device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int slot, float pv, int timeout_ms) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1652,7 +1653,7 @@ __device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int sl
   __syncthreads();
   if (w == 0) {
     if (lane < dp.world) {   // lane r raises rank r's flag of (this chunk, this sender)
-      if constexpr (USV_DP_ORDER != 0) {
+      if constexpr ((USV_DP_ORDER & 1) != 0) {
         // release at system scope: the workgroup's payload stores (drained behind the barrier above) happen
         // before the flag in every rank's view; the explicit wait keeps the flag behind the write-back even
         // where the compiler's scoreboard analysis would drop it (MI355X_MICROARCH.md, compiler hazard)
@@ -1684,7 +1685,7 @@ __device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int sl
     }
     // acquire at system scope, once after the poll (polling with acquire loads costs 2-3x per hop): the
     // payload loads below are ordered after every flag this wave saw
-    if constexpr (USV_DP_ORDER != 0) {
+    if constexpr ((USV_DP_ORDER & 2) != 0) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
