@@ -1640,9 +1640,15 @@ __device__ __forceinline__ uint32_t *dp_flag(void *buf, int chunk, int sender) {
 // after the flags seen); 0 = relaxed flag store and poll: the guide's {sc0 sc1 stores and loads both sides}
 // form (MI355X_MICROARCH.md, valid hand-off forms) -- every payload store and load is sc0 sc1, every storing wave
 // drains its stores (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane per receiver
-// raises the flag, and every payload load follows the polling wave's match through a workgroup barrier
+// raises the flag, and every payload load follows the polling wave's match through a workgroup barrier.
+// Default 2: the guide keeps the consumer's acquire for a hand-off that matches none of its measured rows
+// (these are single-device rows; the exchange crosses xGMI), and the producer then needs sc1 stores drained
+// before the flag (its conditions (2)-(3)), which the payload stores are.  Two-rank rehearsal on one box
+// (profiles/r04/r04e_dp_order_ab.txt, update us per minibatch): 0: 46.7-46.8, 2: 47.4-48.1, 1: 58.0-58.2,
+// 3: 59.2-60.4 -- the system-scope release (buffer_wbl2 sc0 sc1: the XCD L2's dirty lines written back) costs
+// ~11 us per minibatch and orders nothing the drained write-through payload stores have not already.
 #ifndef USV_DP_ORDER
-#define USV_DP_ORDER 3
+#define USV_DP_ORDER 2
 #endif
 __device__ float dp_exchange(const ppo_dp_t &dp, uint32_t key, int chunk, int slot, float pv, int timeout_ms) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
