@@ -148,6 +148,17 @@ __global__ __launch_bounds__(kPlaceTB) void k_field_place(usv_cfg_t c, usv_bufs_
 // SIMD -- for batches that fill the chip more than once; k_field_wave keeps the
 // compiler's 256 + 76 registers and one env per CU, for small batches, where the
 // kernel is latency-bound and a shared CU would only slow the slowest env.
+// USV_SWEEP_CHG 1: a sweep notes a lowered cell by OR-ing the old ^ new bit patterns into a per-lane VGPR
+// (updates only ever lower a value, so the tile changed iff the OR is non-zero); 0: a per-cell compare into a
+// lane mask (one VALU compare + one SALU OR per cell, the SALU op waiting on the compare)
+#ifndef USV_SWEEP_CHG
+#define USV_SWEEP_CHG 1
+#endif
+#if USV_SWEEP_CHG
+#define USV_SWEEP_NOTE(hb, m) (chg |= (uint32_t)((hb) ^ (m)))
+#else
+#define USV_SWEEP_NOTE(hb, m) (changed |= (m) < (hb))
+#endif
 template <bool kPlace>
 __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bufs_t &b) {
   __shared__ uint32_t occ[G * kOccColWords];
@@ -291,6 +302,9 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
     int it = 0;
     for (; it < kMaxIters; ++it) {
       int changed = 0;
+#if USV_SWEEP_CHG
+      uint32_t chg = 0u;   // OR of (old ^ new) over the tile's cells: a VGPR, no per-cell lane-mask SALU op
+#endif
       bool dirty = false;
       if (tile_ok) {
 #pragma unroll
@@ -328,7 +342,7 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
             m = min(m, __float_as_int(fabsf(h[i - 1][j]) + 1.0f));
             m = min(m, __float_as_int(fabsf(h[i - 1][j + 1]) + 1.414f));
             m = min(m, __float_as_int(fabsf(h[i][j - 1]) + 1.0f));
-            changed |= m < hb;
+            USV_SWEEP_NOTE(hb, m);
             h[i][j] = __int_as_float(m);
           }
 #pragma unroll
@@ -342,9 +356,14 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
             m = min(m, __float_as_int(fabsf(h[i + 1][j]) + 1.0f));
             m = min(m, __float_as_int(fabsf(h[i + 1][j - 1]) + 1.414f));
             m = min(m, __float_as_int(fabsf(h[i][j + 1]) + 1.0f));
-            changed |= m < hb;
+            USV_SWEEP_NOTE(hb, m);
             h[i][j] = __int_as_float(m);
           }
+#if USV_SWEEP_CHG
+        // opaque to the optimiser: otherwise it folds (OR of old ^ new) != 0 back into per-cell compares
+        __asm__("" : "+v"(chg));
+        changed = chg != 0u;
+#endif
         if (changed) {
 #pragma unroll
           for (int k = 0; k < T; ++k) {
