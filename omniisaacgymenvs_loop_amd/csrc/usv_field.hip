@@ -514,6 +514,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   const int c0 = 2 * cp;
   const float cell = (float)((double)c.map_size / G);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
+  const float inv_safe = 1.0f / c.safe_radius;   // goal_mask's quotient as div_rn (field_value's form)
   const int items = count * kBands;
   if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
@@ -568,7 +569,9 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       const float jr = j_raw(c, dte, inv_r);
       const bool gi = isinf(g);
       any_inf |= gi;
-      const float j = jr * goal_mask(c, g, cell);
+      // goal_mask(c, g, cell) as div_rn by the correctly rounded reciprocal: the same bits for every finite
+      // g (usv_device.h div_rn); an infinite g gives NaN here, and j is only read where g is finite
+      const float j = jr * clampt(div_rn(g * cell, c.safe_radius, inv_safe), 0.f, 1.f);
       jrall_i = fmaxf(jrall_i, gi ? jr : 0.f);
       jrmin_i = fminf(jrmin_i, (gi && !ins) ? jr : INFINITY);
       jrmax_i = fmaxf(jrmax_i, (gi && !ins) ? jr : -INFINITY);
