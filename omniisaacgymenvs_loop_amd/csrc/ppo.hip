@@ -1084,7 +1084,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5;
   const int kh = w >> 2, cb = w & 3, n0 = 32 * cb;      // K half, column block
+#ifdef USV_DIAG_HOT_ROWS
+  const int rb0 = blockIdx.x * RB;   // DIAGNOSTIC build only (wrong rows): every minibatch reads the first one's rows
+#else
   const int rb0 = row0 + blockIdx.x * RB;               // first row of this workgroup
+#endif
   const float invB = 1.0f / (float)c.minibatch;
   USV_PHASE(ppo, 0);
   // several ranks: this minibatch's exchange key (the previous reduction has finished: stream order)
