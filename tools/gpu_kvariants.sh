@@ -13,4 +13,5 @@ for v in $VARIANTS; do
     python3 $R/bench.py --steps 3 --warmup 2 --no-cpu-baseline --c2-steps 0 > $O/$v.log 2>&1 || exit $?
   echo "== $v"
   python3 $R/tools/kstats.py $(find $O/$v -name "*kernel_stats.csv" | head -1) ${TOP:-4}
+  find $O/$v -name "*kernel_trace.csv" -delete   # the per-dispatch trace: tens of MB, not copied back
 done
