@@ -27,6 +27,7 @@
 
 USV_PROBE_DEFINE(ppo)
 USV_PROBE_DEFINE(pol)
+USV_PROBE_DEFINE(red)
 
 namespace {
 
@@ -1740,6 +1741,7 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
                                                            const float *__restrict__ opt_in, ppo_dp_t dp, int fold) {
   __shared__ float4 red[RD_G][RD_L];
   __shared__ float sqw[RD_TB / 64];
+  USV_PHASE(red, 0);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int col = tid % RD_L, grp = tid / RD_L;
   const int p4 = blockIdx.x * RD_L + col;                 // float4 column of the partial rows
@@ -1804,6 +1806,7 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
       }
     }
   }
+  USV_PHASE(red, 1);   // (thread 0's row sums: its loads have landed)
   AdamK ak = {0.f, 1.f};
   if (kSpec)   // uniform: precomputed by the previous step's opt_store (no pow on this path)
     ak = adam_consts_tagged(c, oin[0], oin[1] + 1.0f, oin[4], oin[5], oin[6], oin[7]);
@@ -1815,6 +1818,7 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
 #pragma unroll
     for (int g = 0; g < RD_G; ++g) s += reinterpret_cast<const float *>(red[g])[tid];
   }
+  USV_PHASE(red, 2);
   float sl = s;   // this rank's value of the slot (the loss means are rank-local)
   if constexpr (kDP) {   // the chunk to every rank (gradient sums; the KL slot as this rank's mean)
     const float pv = slot < S_END ? s : (slot == PPO_NPARAM + 4 ? s * inv_b : 0.f);
@@ -1836,6 +1840,7 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
       if (losses) losses[q] = sl * inv_b;
     }
   }
+  USV_PHASE(red, 3);
   if (w < (RD_P + 63) / 64) {
     sq = wave_sum(sq);
     if (lane == 0) sqw[w] = sq;
@@ -1847,6 +1852,7 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     for (int q = 0; q < (RD_P + 63) / 64; ++q) t += sqw[q];
     grad[PPO_NPARAM + 8 + blockIdx.x] = t;
   }
+  USV_PHASE(red, 4);
 }
 
 // clip_grad_norm_ + Adam + AdaptiveScheduler.  Every workgroup forms the same

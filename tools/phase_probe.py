@@ -70,6 +70,20 @@ def main():
     last = 15 if np.any(b[:, 15] != 0) else 8
     print(f"  launch span (first start -> last slot-{last} stamp): {(b[:, last].max() - b[:, 0].min()) / 100:7.2f} us; "
           f"start spread {(b[:, 0].max() - b[:, 0].min()) / 100:5.2f} us")
+    # k_reduce_partials: stamps 0 start, 1 row sums (thread 0's loads landed), 2 LDS fold, 3 Adam + stores
+    # issued, 4 end; against the gradient kernel's stamps of the same minibatch (the last one of the epoch)
+    rb = read("red")[:167]
+    rb = rb[rb[:, 0] > 0]
+    if len(rb):
+        g0 = pb[:agent.minibatch_size // 32]
+        g0 = g0[g0[:, 0] > 0]
+        gend = g0[:, 8].max()
+        print(f"k_reduce_partials (last launch): {len(rb)} workgroups; first start {(rb[:, 0].min() - gend) / 100:+.2f} us "
+              f"after the gradient kernel's last dW1 stamp, start spread {(rb[:, 0].max() - rb[:, 0].min()) / 100:.2f} us")
+        for k, what in ((1, "row sums"), (2, "LDS fold"), (3, "Adam + stores issued"), (4, "end")):
+            d = (rb[:, k] - rb[:, 0]) / 100.0
+            print(f"  stamp {k} {what:22s} t = {d.mean():6.2f} us (max {d.max():6.2f})")
+        print(f"  launch span (first start -> last end stamp): {(rb[:, 4].max() - rb[:, 0].min()) / 100:.2f} us")
     pp = read("pol")
     b = pp[:256]
     b = b[b[:, 0] > 0]
