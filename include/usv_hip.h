@@ -366,6 +366,13 @@ int usv_build_lut(const float *table_l21, const float *table_r21, int n_table,
  * uniforms per reset slot (parity tests). */
 int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed,
               uint64_t step, const float *u_inject, void *stream);
+/* usv_reset in two parts (the overlapped step, tasks/usv_virtual.py): part 1 = the step clock / scratch reset,
+ * the reset kernel (compaction, DR, spawns, goals, the per-workgroup episode-extras partials); part 2 = the
+ * fold of those partials into b->extras (in workgroup order).  Part 1 then part 2 == usv_reset; part 2 must run
+ * before the next part 1 (which rewrites the partials).  Same Python-side API as usv_reset, no reference analogue
+ * beyond it. */
+int usv_reset_part(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t step,
+                   const float *u_inject, int part, void *stream);
 
 /* Reset path, part 2: per-reset-env potential field (occupancy/SDF,
  * 8-neighbour wavefront cost-to-go, repulsion, batch-global normalisation).

@@ -54,6 +54,7 @@ def _declare(lib):
     sig = {
         "usv_build_lut": [P, P, I, P, P],
         "usv_reset": [P, P, U64, U64, P, P],
+        "usv_reset_part": [P, P, U64, U64, P, I, P],
         "usv_potential_field": [P, P, P],
         "usv_field_stage": [P, P, I, P],
         "usv_field_view": [P, P, P, I, P, P],

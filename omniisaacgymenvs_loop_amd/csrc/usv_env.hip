@@ -1821,25 +1821,32 @@ int usv_build_lut(const float *table_l21, const float *table_r21, int n_table, f
   return 0;
 }
 
-int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t step, const float *u_inject,
-              void *stream) {
-  if (!cfg || !b || b->n <= 0) return 1;
+int usv_reset_part(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t step, const float *u_inject,
+                   int part, void *stream) {
+  if (!cfg || !b || b->n <= 0 || part < 0 || part > 2) return 1;
   if (b->scene && (b->n_scenes <= 0 || !b->scene_next || !b->scene_last || cfg->task_kind != USV_TASK_CAPTURE_XY))
     return 1;
   hipStream_t s = (hipStream_t)stream;
-  // per-step scratch: reset count, field maxima, extras sums
-  hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, s, *b, cfg->step_inc);
-  USV_CHECK_LAUNCH();
   const int grid = (b->n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_reset, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, seed, step, u_inject);
-  USV_CHECK_LAUNCH();
+  if (part != 2) {
+    // per-step scratch: reset count, field maxima, extras sums
+    hipLaunchKernelGGL(k_step_begin, dim3(1), dim3(64), 0, s, *b, cfg->step_inc);
+    USV_CHECK_LAUNCH();
+    hipLaunchKernelGGL(k_reset, dim3(grid), dim3(kBlock), 0, s, *cfg, *b, seed, step, u_inject);
+    USV_CHECK_LAUNCH();
+  }
 #if USV_RESET_FOLD_KERNEL
-  if (cfg->stats_on) {
+  if (part != 1 && cfg->stats_on) {
     hipLaunchKernelGGL(k_extras_fold, dim3(1), dim3(kBlock), 0, s, *cfg, *b, grid);
     USV_CHECK_LAUNCH();
   }
 #endif
   return 0;
+}
+
+int usv_reset(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uint64_t step, const float *u_inject,
+              void *stream) {
+  return usv_reset_part(cfg, b, seed, step, u_inject, 0, stream);
 }
 
 int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions, const float *lut_dev,

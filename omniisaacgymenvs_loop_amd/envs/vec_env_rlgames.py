@@ -47,12 +47,14 @@ class VecEnvRLGames:
         obs_dict = {"obs": {"state": obs}, "states": t.states_buf}
         return obs_dict, rew, dones, t.extras
 
-    def step_async(self, actions: torch.Tensor):
+    def step_async(self, actions: torch.Tensor, chain: bool = False):
         """step() whose rewards are final only after join(): the reset envs' potential fields build on a side
-        stream while the caller issues its next policy step (obs and dones are final on return)."""
+        stream while the caller issues its next policy step (obs and dones are final on return).  chain=True
+        when this call follows another step_async of the same rollout (one captured graph) with nothing but
+        the caller's own kernels in between: the step's reset then runs on the side stream too."""
         t = self._task
         a = actions if actions.device == torch.device(t.device) else actions.to(t.device)
-        obs, rew, dones = t.env_step(a, overlap=True)
+        obs, rew, dones = t.env_step(a, overlap=True, chain=chain)
         self.sim_frame_count += t.control_frequency_inv
         return {"obs": {"state": obs}, "states": t.states_buf}, rew, dones, t.extras
 

@@ -368,7 +368,7 @@ class A2CAgent:
         policy(0)
         for n in range(self.horizon_length):
             t0 = time.time()
-            self.obs, rewards, self.dones, infos = self.vec_env.step_async(self.actions)
+            self.obs, rewards, self.dones, infos = self.vec_env.step_async(self.actions, chain=n > 0)
             step_time += time.time() - t0
             if n + 1 < self.horizon_length:
                 policy(n + 1)

@@ -158,6 +158,8 @@ class USVVirtual:
         self._side = None
         self._ev_stats = None
         self._step_pending = False
+        self._host_dirty = True   # host-side buffer writes since the last join (the allocation's fills)
+        self._side_tail_late = False   # the side stream's last work is an overlapped step's deferred reward
         self.lut = Z((2, 1000), **f32)
         self.hydro = build_hydro_cfg(self._task_cfg)
         tl, tr = thruster_tables(self._task_cfg)
@@ -261,11 +263,20 @@ class USVVirtual:
                    int(ids_t.numel()), _capi.ptr(out), _capi.stream_ptr())
         return out
 
+    def _touch(self) -> None:
+        """A host-side write to the env buffers on the current stream: the next overlapped step runs its reset on
+        that stream again (behind the write) instead of on the side stream (see _step_overlapped)."""
+        self.join_step()
+        self._host_dirty = True
+        self._side_tail_late = False
+
     def set_env_origins(self, org: torch.Tensor) -> None:
+        self._touch()
         """World x, y of each env's origin ([2][n]; RLTask._env_pos from the stage)."""
         self.env_org.copy_(org.to(self._device, torch.float32).reshape(2, self._num_envs))
 
     def set_grid_lin(self, lin: torch.Tensor) -> None:
+        self._touch()
         """Override the field grid's cell centres (parity tests vs CPU fixtures)."""
         self.grid_lin = lin.to(self._device, torch.float32).contiguous()
         self._bufs = self._make_bufs()
@@ -305,6 +316,7 @@ class USVVirtual:
 
     def reset(self) -> None:
         """RLTask.reset: flag every env for reset (rl_task.py:268-270)."""
+        self._touch()
         self.ibuf[2].fill_(1)
 
     def update_state(self) -> None:
@@ -331,21 +343,33 @@ class USVVirtual:
 
     def env_step(self, actions: torch.Tensor, u_step: Optional[torch.Tensor] = None,
                  u_reset: Optional[torch.Tensor] = None, post_state: Optional[torch.Tensor] = None,
-                 overlap: bool = False):
+                 overlap: bool = False, chain: bool = False):
         """pre_physics_step + 10 substeps + post_physics_step (USV_Virtual.py:1042-1652).
 
         Returns the device tensors (obs [n,33], rew [n], dones int64 [n]).  u_step / u_reset replay
         recorded uniforms (parity tests) instead of the in-kernel Philox draws.  post_state ([8][n]:
         px, py, yaw, vx, vy, wz, fl, fr) replaces the integrator by a recorded post-integration state:
         the step then runs pre_physics_step and RLTask.post_physics_step (rl_task.py:283-303) on that
-        state, as the reference does on whatever PhysX returned (parity of the post-physics path alone)."""
+        state, as the reference does on whatever PhysX returned (parity of the post-physics path alone).
+        overlap: the overlapped step (_step_overlapped); chain: this overlapped step directly follows one in the
+        same sequence of calls (a rollout, or one captured graph), so its reset may run on the side stream."""
         actions = self._f32(actions)
         s = _capi.stream_ptr()
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
+        overlapped = overlap and self._has_field and post_state is None
+        if (overlapped and chain and self._side_tail_late and not self._host_dirty and u_step is None
+                and u_reset is None and os.getenv("USV_RESET_ON_SIDE", "1") == "1"):
+            # the previous overlapped step's side stream ends with its deferred reward; this step's reset and
+            # obstacle placement depend on that and on the dones of its part 3 (final on this stream long
+            # before), not on this stream's later work (the next policy step, the reward store), so they run
+            # on the side stream right behind it (no join here: the caller joins before reading rewards)
+            bias, k = self._advance()
+            return self._step_overlapped(actions, bias, k, u_step, reset_on_side=True)
         self.join_step()
+        self._host_dirty = False
         bias, k = self._advance()
         _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
-        if overlap and self._has_field and post_state is None:
+        if overlapped:
             return self._step_overlapped(actions, bias, k, u_step)
         if self._has_field:   # CaptureXY only (GoToPose / TrackXYOVelocity have no obstacles)
             _capi.call("usv_potential_field", cfg, b, s)
@@ -360,7 +384,7 @@ class USVVirtual:
             self.cfg.substeps = substeps
         return self.obs_view, self.rew_buf, self.dones
 
-    def _step_overlapped(self, actions, bias, k, u_step):
+    def _step_overlapped(self, actions, bias, k, u_step, reset_on_side=False):
         """The rest of env_step with the reset envs' fields built on a side stream (usv_hip.h, the overlapped
         step): obstacle placement, then the step of every env (part 3) on this stream beside the sweeps /
         statistics / field kernels on the side stream, then the deferred reward of the reset envs there.
@@ -373,9 +397,19 @@ class USVVirtual:
             self._side = torch.cuda.Stream(device=self._device, priority=int(os.getenv("USV_SIDE_PRIORITY", "0")))
             self._ev_fork, self._ev_early, self._ev_join = (torch.cuda.Event() for _ in range(3))
         side = self._side
-        _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
-        self._ev_fork.record(main)
-        side.wait_event(self._ev_fork)
+        if reset_on_side:
+            # reset + obstacle placement on the side stream behind the previous step's deferred reward; this
+            # stream waits for the placement, then folds the episode extras (so what it reads of them between
+            # steps is what the plain step leaves) and runs part 3 (every kernel sees the plain step's inputs)
+            _capi.call("usv_reset_part", cfg, b, self.seed, k, None, 1, side.cuda_stream)
+            _capi.call("usv_field_stage", cfg, b, 1, side.cuda_stream)
+            self._ev_fork.record(side)
+            main.wait_event(self._ev_fork)
+            _capi.call("usv_reset_part", cfg, b, self.seed, k, None, 2, main.cuda_stream)
+        else:
+            _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
+            self._ev_fork.record(main)
+            side.wait_event(self._ev_fork)
         # USV_STATS_FIRST=1: the main stream (the next policy step) waits for the field statistics, which then
         # run alone instead of beside the policy kernel (A/B knob)
         stats_first = os.getenv("USV_STATS_FIRST", "0") == "1"
@@ -396,6 +430,7 @@ class USVVirtual:
         _capi.call("usv_env_step_late", cfg, b, side.cuda_stream)
         self._ev_join.record(side)
         self._step_pending = True
+        self._side_tail_late = True
         return self.obs_view, self.rew_buf, self.dones
 
     def join_step(self) -> None:
