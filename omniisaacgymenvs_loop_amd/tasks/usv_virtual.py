@@ -358,11 +358,11 @@ class USVVirtual:
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
         overlapped = overlap and self._has_field and post_state is None
         if (overlapped and chain and self._side_tail_late and not self._host_dirty and u_step is None
-                and u_reset is None and os.getenv("USV_RESET_ON_SIDE", "1") == "1"):
-            # the previous overlapped step's side stream ends with its deferred reward; this step's reset and
-            # obstacle placement depend on that and on the dones of its part 3 (final on this stream long
-            # before), not on this stream's later work (the next policy step, the reward store), so they run
-            # on the side stream right behind it (no join here: the caller joins before reading rewards)
+                and u_reset is None and os.getenv("USV_RESET_ON_SIDE", "0") == "1"):
+            # (A/B knob, off: measured slower) the previous overlapped step's side stream ends
+            # with its deferred reward; this step's reset and obstacle placement depend on that and on the dones
+            # of its part 3 (final on this stream long before), not on this stream's later work (the next policy
+            # step, the reward store), so they can run on the side stream right behind it
             bias, k = self._advance()
             return self._step_overlapped(actions, bias, k, u_step, reset_on_side=True)
         self.join_step()
