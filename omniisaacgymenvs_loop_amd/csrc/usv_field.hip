@@ -48,6 +48,12 @@ constexpr int kSlotStride = USV_FIELD_SLOT_STATS;   // floats per reset slot: 16
 constexpr int kSlotObst = 160;                      // the slot's 16 obstacle centres (x, y interleaved)
 static_assert(kSlotObst + 2 * USV_NOBST <= kSlotStride, "slot_stats layout");
 constexpr int kFieldPackMinEnvs = 32768;           // k_field_wave_pack (two envs per CU) from this many envs
+// USV_SWEEP_WAVES: waves per SIMD the packed sweep kernel is compiled for (2: two reset envs per CU at <= 256
+// VGPRs; 3: three envs per CU, 3 x 51.7 KB of LDS, <= 168 VGPRs) and its persistent grid (256 CUs x that)
+#ifndef USV_SWEEP_WAVES
+#define USV_SWEEP_WAVES 2
+#endif
+constexpr int kPackGrid = 256 * USV_SWEEP_WAVES;
 
 // slot_stats layout (per reset slot)
 enum {
@@ -424,7 +430,7 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
 }
 
 __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) { field_wave_body<true>(c, b); }
-__global__ __launch_bounds__(kWaveThreads, 2) void k_field_wave_pack(usv_cfg_t c, usv_bufs_t b) {
+__global__ __launch_bounds__(kWaveThreads, USV_SWEEP_WAVES) void k_field_wave_pack(usv_cfg_t c, usv_bufs_t b) {
   field_wave_body<false>(c, b);
 }
 
@@ -772,7 +778,8 @@ int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream
     return 0;
   }
   if (stage == 2 || stage == 3) {
-    hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
+    const int grid_w = b->n < kPackGrid ? b->n : kPackGrid;
+    hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_w), dim3(kWaveThreads), 0, s, *cfg, *b);
     USV_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
     USV_CHECK_LAUNCH();
@@ -823,7 +830,8 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
     hipLaunchKernelGGL(k_field_place, dim3(grid_p), dim3(kPlaceTB), 0, s, *cfg, *b);
     USV_CHECK_LAUNCH();
   }
-  if (pack) hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
+  if (pack) hipLaunchKernelGGL(k_field_wave_pack, dim3(b->n < kPackGrid ? b->n : kPackGrid), dim3(kWaveThreads), 0, s,
+                              *cfg, *b);
   else hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
