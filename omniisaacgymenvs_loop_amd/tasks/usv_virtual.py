@@ -158,6 +158,7 @@ class USVVirtual:
         self._side = None
         self._ev_stats = None
         self._step_pending = False
+        self._late_pending = False   # USV_LATE_ON_JOIN: an overlapped step's deferred reward waits for join_step
         self._host_dirty = True   # host-side buffer writes since the last join (the allocation's fills)
         self._side_tail_late = False   # the side stream's last work is an overlapped step's deferred reward
         self.lut = Z((2, 1000), **f32)
@@ -425,19 +426,31 @@ class USVVirtual:
                    self.seed, k, _capi.ptr(u_step), 3, main.cuda_stream)
         if stats_first:
             main.wait_event(self._ev_stats)
-        self._ev_early.record(main)
-        side.wait_event(self._ev_early)
-        _capi.call("usv_env_step_late", cfg, b, side.cuda_stream)
-        self._ev_join.record(side)
+        # USV_LATE_ON_JOIN=1: the deferred reward runs on the joining stream right after its wait for the fields
+        # (one cross-stream wait per step fewer on the critical path); 0: on the side stream behind part 3
+        late_on_join = os.getenv("USV_LATE_ON_JOIN", "0") == "1"
+        if late_on_join:
+            self._ev_join.record(side)
+            self._late_pending = True
+        else:
+            self._ev_early.record(main)
+            side.wait_event(self._ev_early)
+            _capi.call("usv_env_step_late", cfg, b, side.cuda_stream)
+            self._ev_join.record(side)
         self._step_pending = True
-        self._side_tail_late = True
+        self._side_tail_late = not late_on_join
         return self.obs_view, self.rew_buf, self.dones
 
     def join_step(self) -> None:
-        """Make the current stream wait for an overlapped step's side stream (rewards, fields final)."""
+        """Make the current stream wait for an overlapped step's side stream (rewards, fields final); with
+        USV_LATE_ON_JOIN the step's deferred reward then runs on this stream."""
         if self._step_pending:
-            torch.cuda.current_stream(self._device).wait_event(self._ev_join)
+            cur = torch.cuda.current_stream(self._device)
+            cur.wait_event(self._ev_join)
             self._step_pending = False
+            if self._late_pending:
+                self._late_pending = False
+                _capi.call("usv_env_step_late", _capi.byref(self.cfg), _capi.byref(self._bufs), cur.cuda_stream)
 
     def _f32(self, actions: torch.Tensor) -> torch.Tensor:
         if actions.dtype != torch.float32 or not actions.is_contiguous():

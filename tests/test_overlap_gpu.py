@@ -41,8 +41,8 @@ def test_overlapped_env_step_equals_plain_step(n):
             np.testing.assert_array_equal(so[k], sp[k], err_msg=f"{k} step {t}")
 
 
-@pytest.mark.parametrize("reset_on_side", ["0", "1"])
-def test_overlapped_rollout_equals_sequential(monkeypatch, reset_on_side):
+@pytest.mark.parametrize("reset_on_side,late_on_join", [("0", "0"), ("1", "0"), ("0", "1")])
+def test_overlapped_rollout_equals_sequential(monkeypatch, reset_on_side, late_on_join):
     """A2CAgent.play_steps with the overlapped env step (policy n+1 beside step n's field kernels) vs the
     sequential loop: every experience buffer, the meters and the env state bit-identical after two epochs
     of rollouts (the first from the all-env reset); also with the chained steps' reset and obstacle placement
@@ -50,6 +50,7 @@ def test_overlapped_rollout_equals_sequential(monkeypatch, reset_on_side):
     import os
     from tests.test_train_gpu import _agent_env
     monkeypatch.setenv("USV_RESET_ON_SIDE", reset_on_side)
+    monkeypatch.setenv("USV_LATE_ON_JOIN", late_on_join)
     runs = []
     for ov in ("0", "1"):
         os.environ["USV_STEP_OVERLAP"] = ov
