@@ -498,15 +498,20 @@ __device__ __forceinline__ BatchK batch_k(const usv_cfg_t &c, const usv_bufs_t &
 // the batch constant inf_val (known only when every env is done) enters
 // through one monotone scalar per batch.  Partials at slot_stats[slot][16 + 12 band].
 // The SDF is formed separably with cell_sdf's rounded operations: a thread owns two
-// adjacent columns, keeps (gx - ox)^2 of both for the 16 obstacles in registers and,
+// adjacent columns, keeps (gx - ox)^2 of both for the obstacles in registers and,
 // per row, forms gy - oy once for the two cells -- fmaf(dy, dy, dx * dx), the same
 // min tree, sqrt, minus the radius: the same bits in about half the instructions.
-// Every statistic is a min / max (any grouping gives the same value).
+// Every statistic is a min / max (any grouping gives the same value), so the cells can be
+// dealt to threads in any shape: each wave owns a compact 38-column x 30-row block of the band
+// (19 column pairs x 3 row groups), so the obstacles that can reach it are few (a per-wave mask)
+// and many of its row strips lie out of every obstacle's reach, where the SDF cannot enter the
+// statistics and a cell contributes only through its cost (the "far" path below).
 constexpr int kBandRows = 30, kBands = G / kBandRows;       // row bands of a slot
-constexpr int kColPairs = G / 2, kRowGroups = 3;            // 75 column pairs x 3 row groups = 225 threads
+constexpr int kRowGroups = 3;                               // row groups per wave (rows rg, rg + 3, ...)
+constexpr int kWavePairs = 19;                              // column pairs per wave: 4 waves x 38 >= 150 columns
 constexpr int kBandIters = kBandRows / kRowGroups;          // rows per thread and band
-static_assert(G % kBandRows == 0 && kBandRows % kRowGroups == 0 && kColPairs * kRowGroups <= 256 && G % 2 == 0,
-              "k_field_stats geometry");
+static_assert(G % kBandRows == 0 && kBandRows % kRowGroups == 0 && kWavePairs * kRowGroups <= 64 &&
+              4 * 2 * kWavePairs >= G && G % 2 == 0, "k_field_stats geometry");
 static_assert(kSlotObst >= 16 + 12 * kBands, "slot_stats band partials");
 __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
   __shared__ float red[10][4];
@@ -515,12 +520,20 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   __shared__ float so[2 * USV_NOBST];
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const bool act = tid < kColPairs * kRowGroups;          // threads 225-255 only join the reductions
-  const int cp = act ? tid % kColPairs : 0, rg = act ? tid / kColPairs : 0;
-  const int c0 = 2 * cp;
+  const int cbase = wid * 2 * kWavePairs;                    // first column of this wave's block
+  const int cpl = lane % kWavePairs, rg = lane / kWavePairs;
+  const int c0u = cbase + 2 * cpl;
+  const bool act = rg < kRowGroups && c0u < G;               // other lanes only join the reductions
+  const int c0 = act ? c0u : 0;                              // (even: the pair is one tile row)
+  const int rgc = act ? rg : 0;
+  const int chi = min(cbase + 2 * kWavePairs - 1, G - 1);    // last column of the block
   const float cell = (float)((double)c.map_size / G);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
   const float inv_safe = 1.0f / c.safe_radius;   // goal_mask's quotient as div_rn (field_value's form)
+  // a cell whose squared distance to every obstacle in reach is >= far_d^2 has dte >= R + 1e-3 (jr = 0, not
+  // inside) whatever the rounding of the sqrt and the two subtractions: it enters only through its cost
+  const float far_d = c.influence_radius + 2.0f * c.obstacle_radius + 0.01f * cell + 1e-3f;
+  const uint32_t far2 = __float_as_uint(far_d * far_d);
   const int items = count * kBands;
   if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
   for (int w = blockIdx.x; w < items; w += gridDim.x) {
@@ -534,8 +547,8 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
     float2 gv[kBandIters];
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
-      const int r = band * kBandRows + rg + kRowGroups * k;
-      gv[k] = *reinterpret_cast<const float2 *>(Fe + field_idx(r, c0));   // (c0 even: one tile row)
+      const int r = band * kBandRows + rgc + kRowGroups * k;
+      gv[k] = *reinterpret_cast<const float2 *>(Fe + field_idx(r, c0));
     }
     float dxa[USV_NOBST], dxb[USV_NOBST], oy[USV_NOBST];
     {
@@ -549,19 +562,19 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
         oy[o] = so[2 * o + 1];
       }
     }
-    // Obstacles that can matter to this band: the SDF enters the field only through j_raw (0 unless
-    // dist - 2 r_obs < influence_radius) and the inside test (dist <= 2 r_obs), so an obstacle whose
-    // row distance to the whole band exceeds far_d can only be the minimum of a cell whose SDF is
-    // irrelevant (jr = 0, not inside, with the exact SDF and with the smaller set alike).  Every wave
-    // forms the same mask from the LDS centres (no barrier); a band with no obstacle in reach writes
-    // +inf (jr = 0, not inside: the same statistics and the same final field).
+    // Obstacles that can matter to this wave's block: the SDF enters the statistics only through j_raw (0
+    // unless dist - 2 r_obs < influence_radius) and the inside test (dist <= 2 r_obs), so an obstacle farther
+    // than far_d from the whole block (in x or in y) can only be the minimum of a cell whose SDF is irrelevant
+    // (jr = 0, not inside, with the exact SDF and with the smaller set alike).  Uniform per wave.
     uint32_t omask;
     {
       const float ylo = slin[band * kBandRows], yhi = slin[band * kBandRows + kBandRows - 1];
-      const float far_d = c.influence_radius + 2.0f * c.obstacle_radius + 0.01f * cell + 1e-3f;
-      const float oyl = so[2 * (lane & (USV_NOBST - 1)) + 1];
+      const float xlo = slin[cbase], xhi = slin[chi];
+      const int ol = lane & (USV_NOBST - 1);
+      const float oxl = so[2 * ol], oyl = so[2 * ol + 1];
       const float dyb = fmaxf(fmaxf(ylo - oyl, oyl - yhi), 0.f);
-      omask = (uint32_t)(__ballot(lane < USV_NOBST && !(dyb > far_d)) & 0xFFFFull);
+      const float dxb_ = fmaxf(fmaxf(xlo - oxl, oxl - xhi), 0.f);
+      omask = (uint32_t)(__ballot(lane < USV_NOBST && !(dyb > far_d) && !(dxb_ > far_d)) & 0xFFFFull);
       omask = __builtin_amdgcn_readfirstlane(omask);
     }
     float gmin = INFINITY, gmax = -INFINITY, jmin_f = INFINITY, jmax_f = -INFINITY, jall_f = 0.f;
@@ -587,13 +600,25 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       jmin_f = fminf(jmin_f, (!gi && !ins) ? j : INFINITY);
       jmax_f = fmaxf(jmax_f, (!gi && !ins) ? j : -INFINITY);
     };
+    // the same statistics for a cell out of every obstacle's reach (jr = +0, not inside): what stat() gives
+    // there, without the sqrt and the divisions (jall_f and jrall_i take max(., +0), a no-op from their +0 start)
+    const auto stat_far = [&](float g) {
+      const bool gi = isinf(g);
+      any_inf |= gi;
+      jrmin_i = fminf(jrmin_i, gi ? 0.f : INFINITY);
+      jrmax_i = fmaxf(jrmax_i, gi ? 0.f : -INFINITY);
+      gmin = fminf(gmin, gi ? INFINITY : g);
+      gmax = fmaxf(gmax, gi ? -INFINITY : g);
+      jmin_f = fminf(jmin_f, gi ? INFINITY : 0.f);
+      jmax_f = fmaxf(jmax_f, gi ? -INFINITY : 0.f);
+    };
     // squared distances (non-negative: u32 min of the bit patterns is the float min, exact in any
-    // order), obstacle-outer so a skipped obstacle is one scalar branch for the band's rows
+    // order), obstacle-outer so a skipped obstacle is one scalar branch for the block's rows
     float gy[kBandIters];
     uint32_t a[kBandIters], bb[kBandIters];
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
-      gy[k] = slin[band * kBandRows + rg + kRowGroups * k];
+      gy[k] = slin[band * kBandRows + rgc + kRowGroups * k];
       a[k] = bb[k] = 0x7F800000u;
     }
 #pragma unroll
@@ -608,12 +633,18 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
     }
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
-      const int r = band * kBandRows + rg + kRowGroups * k;
-      const float sva = sqrtf(__uint_as_float(a[k])) - c.obstacle_radius;
-      const float svb = sqrtf(__uint_as_float(bb[k])) - c.obstacle_radius;
-      if (act) {
-        stat(gv[k].x, sva);
-        stat(gv[k].y, svb);
+      // a row strip of the block whose cells all lie out of reach takes the far path (uniform branch)
+      const bool near = act && (a[k] < far2 || bb[k] < far2);
+      if (__ballot(near) != 0ull) {
+        const float sva = sqrtf(__uint_as_float(a[k])) - c.obstacle_radius;
+        const float svb = sqrtf(__uint_as_float(bb[k])) - c.obstacle_radius;
+        if (act) {
+          stat(gv[k].x, sva);
+          stat(gv[k].y, svb);
+        }
+      } else if (act) {
+        stat_far(gv[k].x);
+        stat_far(gv[k].y);
       }
     }
     float vals[9] = {wave_min(gmin), wave_max(gmax), wave_min(jmin_f), wave_max(jmax_f), wave_max(jall_f),
