@@ -246,21 +246,23 @@ def _rew_diag(task, E, got, dpot, dpot_prev, k=4):
     return "\n".join(out)
 
 
-def test_philox_mode_matches_oracle():
-    """In-kernel Philox draws == the oracle's restatement of the same streams."""
+@pytest.mark.parametrize("n,T", [(2048, 24), (1000, 12), (33, 12)])
+def test_philox_mode_matches_oracle(n, T):
+    """In-kernel Philox draws == the oracle's restatement of the same streams; also at ragged sizes (1000: a
+    partial last workgroup and wave; 33: one wave with a single lane past 32, the slab's smallest row stride)."""
     task_cfg = load_yaml(TEST_YAML)
-    n, T = 2048, 24
     task = _task(task_cfg, n)
     E = _oracle_for(task.cfg, n, task_cfg)
     rng = np.random.default_rng(0)
     dp = np.zeros(n)
+    tn = "philox" if n == 2048 else f"philox_{n}"
     for t in range(T):
         a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
         bias = task.current_action_bias()
         obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
         E.full_step(a, bias, t, seed=task.seed)
         torch.cuda.synchronize()
-        dp = _vs_oracle("philox", task, E, obs, rew, dones, t, dp)
+        dp = _vs_oracle(tn, task, E, obs, rew, dones, t, dp)
     # per-episode parameters drawn by the reset kernel
     np.testing.assert_allclose(task.params[0].cpu().numpy(), E.mass, rtol=1e-6)
     np.testing.assert_allclose(task.obst.cpu().numpy().reshape(16, 2, n), E.obst, rtol=1e-6, atol=1e-5)
