@@ -48,7 +48,7 @@ class AverageMeter:
     def update_stats(self, new_mean: float, size: int) -> None:
         if size == 0:
             return
-        size = int(np.clip(size, 0, self.max_size))
+        size = min(max(int(size), 0), self.max_size)   # np.clip on an int, without its per-call overhead
         old_size = min(self.max_size - size, self.current_size)
         size_sum = old_size + size
         self.current_size = size_sum
