@@ -36,8 +36,8 @@ def _dataset(rows, seed=5):
 
 
 def _rank_rows(rank, world):
-    """Rank r's local batch: minibatch i of rank r = rows [i*MB + r*MB/2 .. ) of the union layout
-    the single-rank run sees (each union minibatch = rank 0's half, then rank 1's half)."""
+    """Rank r's local batch: minibatch i of rank r = rows [i*MB + r*MB/world .. ) of the union layout
+    the single-rank run sees (each union minibatch = rank 0's share, then rank 1's, ...)."""
     half = MB // world
     idx = [np.arange(i * MB + rank * half, i * MB + (rank + 1) * half) for i in range(N * H * world // MB)]
     return np.concatenate(idx)
@@ -144,6 +144,30 @@ def test_two_ranks_equal_single_rank_on_the_union(two_ranks):
     ET.check("dist_2ranks", "params", r0["p"], single.model_params.cpu().numpy(), 1e-5, 1e-5)
     ET.check("dist_2ranks", "kl", r0["kls"], single.kls.cpu().numpy(), 1e-4, 1e-7)
     assert r0["lr"] == pytest.approx(float(single.opt[0].item()), rel=1e-6)
+
+
+def test_four_ranks_peer_exchange_match_union(tmp_path_factory):
+    """World size 4 through the peer exchange (four processes on one device: each maps three peers' buffers,
+    every chunk waits for four senders' flags and sums them in rank order): all ranks end with bit-identical
+    weights and LR, equal to a single rank trained on the union of the four batches up to summation order."""
+    import torch.multiprocessing as mp
+    world = 4
+    out = tmp_path_factory.mktemp("dist_gpu_peer4")
+    mp.spawn(_worker, args=(world, _port(), str(out), "peer"), nprocs=world, join=True)
+    rs = [np.load(out / f"r{r}.npz") for r in range(world)]
+    for r in rs[1:]:
+        np.testing.assert_array_equal(rs[0]["p0"], r["p0"])
+        np.testing.assert_array_equal(rs[0]["p"], r["p"])
+        assert rs[0]["lr"] == r["lr"]
+    assert len({int(r["env_seed"]) for r in rs}) == world
+    single = _agent(world * N, MB, False, params_seed=11)
+    _load(single, _dataset(N * H * world), np.arange(world * N * H))
+    single.update_epoch_minibatches()
+    torch.cuda.synchronize()
+    from tests import errtab as ET
+    ET.check("dist_4ranks", "params", rs[0]["p"], single.model_params.cpu().numpy(), 1e-5, 1e-5)
+    ET.check("dist_4ranks", "kl", rs[0]["kls"], single.kls.cpu().numpy(), 1e-4, 1e-7)
+    assert rs[0]["lr"] == pytest.approx(float(single.opt[0].item()), rel=1e-6)
 
 
 def test_ranks_draw_different_env_streams(two_ranks):
