@@ -156,12 +156,14 @@ def _pe_worker(rank, world, port, out_dir, fail_alloc, fail_open):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail_alloc,fail_open", [((1,), ()), ((), (1,)), ((0, 1), ())])
-def test_peer_exchange_setup_failure_is_agreed_and_frees_after_the_barrier(tmp_path, fail_alloc, fail_open):
-    """A failed allocation or mapping on ONE rank: every rank still runs the same collectives (handle exchange,
-    agreement), every rank raises, and each frees its own buffer only after unmapping the peers' (ADVICE r3)."""
-    mp.spawn(_pe_worker, args=(2, _port(), str(tmp_path), fail_alloc, fail_open), nprocs=2, join=True)
-    for r in range(2):
+@pytest.mark.parametrize("world,fail_alloc,fail_open", [(2, (1,), ()), (2, (), (1,)), (2, (0, 1), ()),
+                                                          (4, (), (2,)), (4, (3,), ())])
+def test_peer_exchange_setup_failure_is_agreed_and_frees_after_the_barrier(tmp_path, world, fail_alloc, fail_open):
+    """A failed allocation or mapping on ONE rank (of two or four): every rank still runs the same collectives
+    (handle exchange, agreement), every rank raises, and each frees its own buffer only after unmapping the
+    peers' (ADVICE r3)."""
+    mp.spawn(_pe_worker, args=(world, _port(), str(tmp_path), fail_alloc, fail_open), nprocs=world, join=True)
+    for r in range(world):
         z = np.load(tmp_path / f"pe{r}.npz")
         assert "PeerExchange" in str(z["msg"]), (r, z["msg"])
         log = list(z["log"])
