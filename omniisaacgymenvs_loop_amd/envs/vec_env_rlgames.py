@@ -23,6 +23,7 @@ class VecEnvRLGames:
         self._task = None
         self._world = None
         self.sim_frame_count = 0
+        self._ctl_staged = None   # pinned copy of the task's control words (stage_errors)
 
     # omni.isaac.gym VecEnvBase.set_task
     def set_task(self, task, backend: str = "torch", sim_params: Optional[dict] = None, init_sim: bool = True) -> None:
@@ -74,11 +75,19 @@ class VecEnvRLGames:
         """Raise the errors the device path flags instead of raising mid-step (a host sync; called
         by the trainer after each epoch, outside graph capture): scene replay past its last scene
         with cycle off -> IndexError, as USV_Virtual.py:1386-1390; a non-finite action, state, reward or
-        observation -> the USV_NAN_PROBE RuntimeError (USV_Virtual.py:57-95, vec_env_rlgames.py:41-80)."""
+        observation -> the USV_NAN_PROBE RuntimeError (USV_Virtual.py:57-95, vec_env_rlgames.py:41-80).
+        After stage_errors() and a stream synchronisation the flags come from its pinned host copy."""
+        ctl, self._ctl_staged = self._ctl_staged, None
         for name in ("check_scene_replay", "check_nan"):
             chk = getattr(self._task, name, None)
             if chk is not None:
-                chk()
+                chk(ctl)
+
+    def stage_errors(self) -> None:
+        """Enqueue the error flags' copy to pinned host memory behind the work on the current stream; the next
+        check_errors() (after the caller synchronises that stream) reads the copy, not the device."""
+        st = getattr(self._task, "stage_ctl", None)
+        self._ctl_staged = st() if st is not None else None
 
     def advance_host_clock(self, steps: int) -> None:
         """A captured rollout graph was replayed: the device step clock advanced by `steps`."""

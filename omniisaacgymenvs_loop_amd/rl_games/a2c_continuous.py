@@ -290,6 +290,14 @@ class A2CAgent:
         self.loss_log = torch.zeros((self.mini_epochs_num * self.num_minibatches, 8), **f32)
         self.nan_flag = torch.zeros(1, device=dev, dtype=torch.int32)
         self.cfg.nan_flag = self.nan_flag.data_ptr()
+        # the epoch's host-side tail (meters, LR, NaN flag) as pinned copies enqueued behind the update
+        # (_stage_tail): the epoch-end synchronisation covers them, no blocking device read each
+        pin = torch.device(dev).type == "cuda"
+        self._h_meter = torch.empty(self.meter.shape, dtype=torch.float32, pin_memory=pin)
+        self._h_lr = torch.empty(1, dtype=torch.float32, pin_memory=pin)
+        self._h_nan = torch.empty(1, dtype=torch.int32, pin_memory=pin)
+        self._h_dp_err = None
+        self._tail_staged = False
         self._dp = self._peer_exchange() if self.multi_gpu and self.rank_size > 1 else None
 
     def _peer_exchange(self):
@@ -548,33 +556,53 @@ class A2CAgent:
         if pev is not None:
             pev[2].record()
             self.phase_events.append(tuple(pev))
+        stage = getattr(self.vec_env, "stage_errors", None)
+        if stage is not None:
+            stage()
+        self._stage_tail()
         torch.cuda.current_stream().synchronize()
         update_time_end = time.time()
-        chk = getattr(self.vec_env, "check_errors", None)   # device-flagged env errors (scene replay, NaN probe)
-        if chk is not None:
-            chk()
-        self._check_nan()
-        if self._dp is not None:
-            self._dp.check()
-        self._eager_epochs += 1
-        self._replay_meters()
-        self.last_lr = float(self.opt[0].item())
+        try:
+            chk = getattr(self.vec_env, "check_errors", None)   # device-flagged env errors (scene replay, NaN probe)
+            if chk is not None:
+                chk()
+            self._check_nan()
+            if self._dp is not None:
+                self._dp.check(self._h_dp_err if self._tail_staged else None)
+            self._eager_epochs += 1
+            self._replay_meters()
+            self.last_lr = float(self._h_lr[0])
+        finally:
+            self._tail_staged = False
         step_time = batch["step_time"]
         if step_time != step_time:   # graph replay: no per-step host timing
             step_time = play_time_end - play_time_start
         return (step_time, play_time_end - play_time_start, update_time_end - play_time_end,
                 update_time_end - play_time_start)
 
+    def _stage_tail(self):
+        """Enqueue the epoch tail's device -> pinned host copies behind the update on the current stream (read
+        by _check_nan, _replay_meters and the LR after the epoch-end synchronisation)."""
+        self._h_meter.copy_(self.meter, non_blocking=True)
+        self._h_lr.copy_(self.opt[:1], non_blocking=True)
+        if self.cfg.nan_probe:
+            self._h_nan.copy_(self.nan_flag, non_blocking=True)
+        if self._dp is not None:
+            if self._h_dp_err is None:
+                self._h_dp_err = torch.empty(self._dp.err.shape, dtype=self._dp.err.dtype, pin_memory=True)
+            self._h_dp_err.copy_(self._dp.err, non_blocking=True)
+        self._tail_staged = True
+
     def _check_nan(self):
         """USV_NAN_PROBE for the policy side: a non-finite mu / value in the rollout's forward."""
         if self.cfg.nan_probe:
-            bits = int(self.nan_flag.item())
+            bits = int(self._h_nan[0]) if self._tail_staged else int(self.nan_flag.item())
             if bits:
                 self.nan_flag.zero_()
                 raise_nan_flag(bits, f"rollout of epoch {self.epoch_num}")
 
     def _replay_meters(self):
-        m = self.meter.cpu().numpy()
+        m = self._h_meter.numpy() if self._tail_staged else self.meter.cpu().numpy()
         for t in range(m.shape[0]):
             cnt = int(round(m[t, 3]))
             if cnt > 0:

@@ -168,9 +168,10 @@ class PeerExchange:
     def own_ptr(self) -> int:
         return self._own.value
 
-    def check(self) -> None:
-        """A peer's chunk missed the kernel's wall-clock bound (a lost or diverged rank): raise."""
-        if int(self.err.item()):
+    def check(self, err_host=None) -> None:
+        """A peer's chunk missed the kernel's wall-clock bound (a lost or diverged rank): raise.  `err_host`: a
+        pinned copy of `err` enqueued behind the update, read after the stream synchronisation."""
+        if int(err_host[0] if err_host is not None else self.err.item()):
             raise RuntimeError("[ppo_dp] a peer's gradient chunk did not arrive within the timeout "
                                "(a rank died or the ranks' minibatch sequences diverged)")
 

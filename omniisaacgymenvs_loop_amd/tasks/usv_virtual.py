@@ -140,6 +140,7 @@ class USVVirtual:
         self.ibuf[2] = 1                               # RLTask.cleanup: reset_buf = ones
         self.just_reset.fill_(1)
         self.ctl = Z(CTL_N, **i32)
+        self._ctl_host = None   # pinned copy of ctl (stage_ctl)
         self.fscratch = Z(16, **f32)
         self.extras_buf = Z(NSTAT, **f32)
         self.extras_acc = Z(((n + 255) // 256) * NSTAT, **f32)   # per reset-kernel workgroup (256 envs)
@@ -198,19 +199,31 @@ class USVVirtual:
             return torch.full((self._num_envs,), -1, dtype=torch.long)
         return self.scene_last.long().cpu()
 
-    def check_scene_replay(self) -> None:
-        """Raise the reference's IndexError if a reset ran past the scenes with cycle off (host sync)."""
-        if self.scene is not None and int(self.ctl[DEFINES["USV_CTL_SCENE_ERR"]].item()):
+    def stage_ctl(self):
+        """Enqueue a copy of the control words into pinned host memory on the current stream (behind the work
+        already queued) and return it: after the caller's stream synchronisation the check_* methods read it
+        from host memory instead of one blocking device read each."""
+        if self._ctl_host is None or self._ctl_host.shape != self.ctl.shape:
+            self._ctl_host = torch.empty(self.ctl.shape, dtype=self.ctl.dtype, pin_memory=True)
+        self._ctl_host.copy_(self.ctl, non_blocking=True)
+        return self._ctl_host
+
+    def check_scene_replay(self, ctl=None) -> None:
+        """Raise the reference's IndexError if a reset ran past the scenes with cycle off (host sync, or `ctl`:
+        stage_ctl's copy once the stream has been synchronised)."""
+        i = DEFINES["USV_CTL_SCENE_ERR"]
+        if self.scene is not None and int(ctl[i] if ctl is not None else self.ctl[i].item()):
             raise IndexError(f"scene_replay index out of range: num_scenes={self.scene_replay_num_scenes}")
 
-    def check_nan(self) -> None:
+    def check_nan(self, ctl=None) -> None:
         """The reference's USV_NAN_PROBE fail-fast (USV_Virtual.py:57-95, vec_env_rlgames.py:41-80) for the
         steps since the last check: the step kernels OR the stage of any non-finite clamped action, state,
-        reward or observation into ctl[USV_CTL_NAN_FLAG] (no per-step host sync); one read here."""
+        reward or observation into ctl[USV_CTL_NAN_FLAG] (no per-step host sync); one read here (or `ctl`, as
+        check_scene_replay)."""
         if not self.cfg.nan_probe:
             return
         i = DEFINES["USV_CTL_NAN_FLAG"]
-        bits = int(self.ctl[i].item())
+        bits = int(ctl[i] if ctl is not None else self.ctl[i].item())
         if bits:
             self.ctl[i] = 0
             raise_nan_flag(bits, "env step")
