@@ -157,10 +157,14 @@ __global__ __launch_bounds__(kPlaceTB) void k_field_place(usv_cfg_t c, usv_bufs_
 // USV_SWEEP_CHG 1: a sweep notes a lowered cell by OR-ing the old ^ new bit patterns into a per-lane VGPR
 // (updates only ever lower a value, so the tile changed iff the OR is non-zero); 0: a per-cell compare into a
 // lane mask (one VALU compare + one SALU OR per cell, the SALU op waiting on the compare)
+// 2: the same OR as ONE v_bitop3_b32 per cell (chg | (old ^ new), truth table 0xF6 over the operand constants
+// 0xF0 / 0xCC / 0xAA) where the compiler emits an XOR per cell plus an OR3 per two cells
 #ifndef USV_SWEEP_CHG
-#define USV_SWEEP_CHG 1
+#define USV_SWEEP_CHG 2
 #endif
-#if USV_SWEEP_CHG
+#if USV_SWEEP_CHG == 2
+#define USV_SWEEP_NOTE(hb, m) (chg = __builtin_amdgcn_bitop3_b32(chg, (uint32_t)(hb), (uint32_t)(m), 0xF6))
+#elif USV_SWEEP_CHG
 #define USV_SWEEP_NOTE(hb, m) (chg |= (uint32_t)((hb) ^ (m)))
 #else
 #define USV_SWEEP_NOTE(hb, m) (changed |= (m) < (hb))
