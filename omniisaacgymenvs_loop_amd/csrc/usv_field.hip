@@ -441,7 +441,8 @@ __global__ __launch_bounds__(kWaveThreads, USV_SWEEP_WAVES) void k_field_wave_pa
 // The reference's literal sweeps for the slots k_field_wave could not certify (SS_EXACT):
 // one workgroup per such slot, the occupancy bit map rebuilt from the slot's obstacles
 // exactly as k_field_wave builds it.  A separate launch keeps the sweep kernel's registers
-// untouched; with nothing flagged every workgroup exits after one load per slot.
+// untouched; with nothing flagged every workgroup exits after one round of flag loads (its
+// threads read the flags of all its slots at once: one load latency, not one per slot).
 __global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_bufs_t b) {
   __shared__ uint32_t occ[G * kOccColWords];
   __shared__ float so[2 * USV_NOBST];
@@ -449,6 +450,10 @@ __global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_b
   const int n = b.n;
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);
   const int tid = threadIdx.x;
+  bool any = false;
+  for (int slot = blockIdx.x + tid * gridDim.x; slot < count; slot += kWaveThreads * gridDim.x)
+    any |= b.slot_stats[(size_t)slot * kSlotStride + SS_EXACT] != 0.f;
+  if (!__syncthreads_or(any)) return;   // uniform per workgroup
   for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
     const float *st = b.slot_stats + (size_t)slot * kSlotStride;
     if (st[SS_EXACT] == 0.f) continue;   // uniform per workgroup
@@ -682,42 +687,70 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
 // ------------------------------------------------------------- pass C2 ---
 // fold each slot's chunk partials (chunk order), then the batch maxima: the max of
 // finite costs (d_multi_gemini.py:205-210), J.max() (:257-260) and the any-inside
-// flag.  One wave per slot (lane q folds statistic q over the chunks: one cache line
-// per chunk row instead of a scattered load per statistic and slot), waves of
+// flag.  Six slots per wave (lane 10 g + q folds statistic q of the wave's slot g over the chunks: one cache
+// line per chunk row instead of a scattered load per statistic and slot), waves of
 // kBatchBlocks workgroups loop over the slots; the batch maxima leave through max
 // atomics (exact in any order, one set per workgroup) and the last workgroup forms
 // J.max() = max(J over finite cells, mask(inf_val) * raw J over infinite cells) --
 // the multiplication by the non-negative mask is monotone, so the max of the
 // products is the product with the max.
-constexpr int kBatchBlocks = 64;
+// USV_BATCH_BLOCKS: the batch fold's workgroups (64; 256 measured slower: the per-workgroup max atomics
+// contend).  USV_BATCH_SLOTS_PER_WAVE: slots per wave and round (6: lanes 0-59; 1: lanes 0-9, one dependent round of
+// band-partial loads per slot, ~8 rounds at ~2,000 resets per step)
+#ifndef USV_BATCH_BLOCKS
+#define USV_BATCH_BLOCKS 64
+#endif
+#ifndef USV_BATCH_SLOTS_PER_WAVE
+#define USV_BATCH_SLOTS_PER_WAVE 6
+#endif
+constexpr int kBatchBlocks = USV_BATCH_BLOCKS;
+constexpr int kBatchSpw = USV_BATCH_SLOTS_PER_WAVE;
+static_assert(kBatchSpw >= 1 && 10 * kBatchSpw <= 64, "k_field_batch lane groups");
 __global__ __launch_bounds__(256) void k_field_batch(usv_cfg_t c, usv_bufs_t b) {
   __shared__ float wred[4][4];
   __shared__ bool last;
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], b.n);
   if (count <= 0) return;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int grp = lane / 10, q = lane % 10, l0 = 10 * grp;   // slot group of this lane, its statistic
   const int nw = (int)gridDim.x * 4;
+  // the lane's running maxima over its groups' slots (max-neutral starts: costs and J are >= 0)
   float gfin = -INFINITY, jf = 0.f, jr = 0.f, ins = 0.f;
-  const bool is_min = lane == SS_GMIN_F || lane == SS_JMIN_F_NI || lane == SS_JRMIN_I_NI;
-  for (int sl = (int)blockIdx.x * 4 + wid; sl < count; sl += nw) {
-    float *st = b.slot_stats + (size_t)sl * kSlotStride;
+  const bool is_min = q == SS_GMIN_F || q == SS_JMIN_F_NI || q == SS_JRMIN_I_NI;
+  for (int sl0 = ((int)blockIdx.x * 4 + wid) * kBatchSpw; sl0 < count; sl0 += nw * kBatchSpw) {
+    const int sl = sl0 + grp;
+    const bool ok = grp < kBatchSpw && sl < count;
     float a = 0.f;
-    if (lane < 10) {
+    if (ok) {
+      float *st = b.slot_stats + (size_t)sl * kSlotStride;
       float x[kBands];
 #pragma unroll
-      for (int ch = 0; ch < kBands; ++ch) x[ch] = st[16 + 12 * ch + lane];
+      for (int ch = 0; ch < kBands; ++ch) x[ch] = st[16 + 12 * ch + q];
       a = x[0];
 #pragma unroll
       for (int ch = 1; ch < kBands; ++ch) a = is_min ? fminf(a, x[ch]) : fmaxf(a, x[ch]);
-      st[lane] = a;
+      st[q] = a;
     }
-    const float s_gmax = __shfl(a, SS_GMAX_F, 64), s_anyinf = __shfl(a, SS_ANY_INF, 64);
-    const float s_jf = __shfl(a, SS_JMAX_F_ALL, 64), s_jr = __shfl(a, SS_JRMAX_I_ALL, 64);
-    const float s_in = __shfl(a, SS_INSIDE, 64);
-    gfin = fmaxf(gfin, s_gmax);             // -inf: no finite cell in the slot
-    jf = fmaxf(jf, s_jf);
-    if (s_anyinf != 0.f) jr = fmaxf(jr, s_jr);
-    ins = fmaxf(ins, s_in);
+    // the slot's folded statistics from its group's lanes (lanes without a slot read themselves, unused)
+    const float s_gmax = __shfl(a, ok ? l0 + SS_GMAX_F : lane, 64);
+    const float s_anyinf = __shfl(a, ok ? l0 + SS_ANY_INF : lane, 64);
+    const float s_jf = __shfl(a, ok ? l0 + SS_JMAX_F_ALL : lane, 64);
+    const float s_jr = __shfl(a, ok ? l0 + SS_JRMAX_I_ALL : lane, 64);
+    const float s_in = __shfl(a, ok ? l0 + SS_INSIDE : lane, 64);
+    if (ok) {
+      gfin = fmaxf(gfin, s_gmax);             // -inf: no finite cell in the slot
+      jf = fmaxf(jf, s_jf);
+      if (s_anyinf != 0.f) jr = fmaxf(jr, s_jr);
+      ins = fmaxf(ins, s_in);
+    }
+  }
+  // wave maxima over the lanes (max is exact in any order)
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    gfin = fmaxf(gfin, __shfl_xor(gfin, off, 64));
+    jf = fmaxf(jf, __shfl_xor(jf, off, 64));
+    jr = fmaxf(jr, __shfl_xor(jr, off, 64));
+    ins = fmaxf(ins, __shfl_xor(ins, off, 64));
   }
   if (lane == 0) { wred[wid][0] = gfin; wred[wid][1] = jf; wred[wid][2] = jr; wred[wid][3] = ins; }
   __syncthreads();
