@@ -178,9 +178,12 @@ __device__ __forceinline__ float2 place_obstacles(const usv_cfg_t &c, int ee, fl
       const float dt = tnorm2(ox - tx, oy - ty);
       bool bad = (ds < c.min_dist_safe) || (dt < c.min_dist_safe);
       const bool vo = ox < 900.f;
+      // the four groups hold the same obstacles, so obstacle i is lane i's value: a scalar read of the lane
+      // (v_readlane) instead of a per-lane LDS permute
 #pragma unroll
       for (int i = 0; i < USV_NOBST - 1; ++i) {
-        const float xi = __shfl(ox, gbase + i, 64), yi = __shfl(oy, gbase + i, 64);
+        const float xi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ox), i));
+        const float yi = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(oy), i));
         const float ddx = xi - ox, ddy = yi - oy;
         if (i < o && vo && (xi < 900.f) && (ddx * ddx + ddy * ddy) < sep2) bad = true;
       }
