@@ -169,14 +169,21 @@ __global__ __launch_bounds__(kPlaceTB) void k_field_place(usv_cfg_t c, usv_bufs_
 #else
 #define USV_SWEEP_NOTE(hb, m) (changed |= (m) < (hb))
 #endif
-template <bool kPlace>
+// TH x TW tiles (10 x 10: the packed and plain kernels; 10 x 5: the small-batch kernel, two waves per SIMD for one
+// env) over NTHR threads; the field buffer keeps its 10 x 10 tiles (a 10 x 5 tile stores into half of one)
+template <bool kPlace, int TH = T, int TW = T, int NTHR = kWaveThreads>
 __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bufs_t &b) {
+  constexpr int NTR = G / TH, NTC = G / TW;        // tile rows / columns
+  constexpr int NPR = NTR + 2, NPC = NTC + 2;      // with the +inf ring
+  constexpr int WC = NTHR / 128;                   // wave regions per band (two bands of <= 8 tile rows)
+  static_assert(G % TH == 0 && G % TW == 0 && NTR <= 16 && NTC <= 8 * WC && NTHR % 128 == 0, "sweep tiling");
+  static_assert(USV_FIELD_TH == TH && USV_FIELD_TW % TW == 0, "sweep tiles inside the field tiles");
   __shared__ uint32_t occ[G * kOccColWords];
-  __shared__ float edge[4][NTP * NTP][T];
-  __shared__ int lastc[NTP * NTP];
+  __shared__ float edgeh[2][NPR * NPC][TW];   // top / bottom row of every tile
+  __shared__ float edgev[2][NPR * NPC][TH];   // left / right column
+  __shared__ int lastc[NPR * NPC];
   __shared__ float so[2 * USV_NOBST];
   __shared__ float slin[G];
-  __shared__ float red[12][kWaveThreads / 64];
   const int n = b.n;
   const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);   // slots index reset_ids[0, n)
   const int tid = threadIdx.x;
@@ -195,23 +202,28 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
   // 8x7, 7x8, 7x7 tiles) so a wave idles as a whole while its region is ahead
   // of / behind the front
   const int quad = tid >> 6, qk = tid & 63;
-  const int qr = quad >> 1, qc = quad & 1;
-  const int qw = qc ? NT - 8 : 8, qh = qr ? NT - 8 : 8;
+  const int qr = quad / WC, qc = quad % WC;
+  const int qw = min(8, NTC - 8 * qc), qh = min(8, NTR - 8 * qr);
   const bool tile_ok = qk < qw * qh;
   const int tr = tile_ok ? qr * 8 + qk / qw : 0;
   const int tc = tile_ok ? qc * 8 + qk % qw : 0;
-  const int r0 = tr * T, c0 = tc * T;
-  const int tp = (tr + 1) * NTP + tc + 1;
+  const int r0 = tr * TH, c0 = tc * TW;
+  const int tp = (tr + 1) * NPC + tc + 1;
   const float cell = (float)((double)c.map_size / G);
   const float half_map = (float)((double)c.map_size / 2);
   const float inv_r = (float)(1.0 / (double)c.influence_radius);
   // the +inf ring of tiles (constant for the launch)
-  for (int q = tid; q < 4 * NTP * NTP * T; q += kWaveThreads) {
-    const int t = (q / T) % (NTP * NTP);
-    const int rr = t / NTP, cc = t % NTP;
-    if (rr == 0 || rr == NTP - 1 || cc == 0 || cc == NTP - 1) (&edge[0][0][0])[q] = INFINITY;
+  for (int q = tid; q < 2 * NPR * NPC * TW; q += NTHR) {
+    const int t = (q / TW) % (NPR * NPC);
+    const int rr = t / NPC, cc = t % NPC;
+    if (rr == 0 || rr == NPR - 1 || cc == 0 || cc == NPC - 1) (&edgeh[0][0][0])[q] = INFINITY;
   }
-  for (int q = tid; q < NTP * NTP; q += kWaveThreads) lastc[q] = -1000;
+  for (int q = tid; q < 2 * NPR * NPC * TH; q += NTHR) {
+    const int t = (q / TH) % (NPR * NPC);
+    const int rr = t / NPC, cc = t % NPC;
+    if (rr == 0 || rr == NPR - 1 || cc == 0 || cc == NPC - 1) (&edgev[0][0][0])[q] = INFINITY;
+  }
+  for (int q = tid; q < NPR * NPC; q += NTHR) lastc[q] = -1000;
   for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
     USV_PHASE(field, 0);
     const int e = b.reset_ids[slot];
@@ -234,7 +246,7 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
       so[tid] = b.obst[(size_t)tid * n + e];
     }
     if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
-    for (int q = tid; q < G * kOccColWords; q += kWaveThreads) occ[q] = 0u;
+    for (int q = tid; q < G * kOccColWords; q += NTHR) occ[q] = 0u;
     __syncthreads();
 #ifdef USV_PHASE_PROBE
     if (tid == 0 && blockIdx.x < 4096) g_probe_field[blockIdx.x][12] = wall_clock64();
@@ -248,7 +260,7 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
       const float cellf = (float)((double)c.map_size / G);
       const int reach = (int)ceilf(c.obstacle_radius / cellf) + 2;   // cells either side, with margin
       const int bw = 2 * reach + 1;
-      for (int q = tid; q < USV_NOBST * bw * bw; q += kWaveThreads) {
+      for (int q = tid; q < USV_NOBST * bw * bw; q += NTHR) {
         const int o = q / (bw * bw), k = q % (bw * bw);
         const float ox = so[2 * o], oy = so[2 * o + 1];
         const float ic = (ox + half_m) / cellf - 0.5f, jc = (oy + half_m) / cellf - 0.5f;
@@ -278,12 +290,12 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
     // its own min, so it keeps itself with no extra instruction, and neighbours
     // read it as |h| + w -- a positive NaN whatever payload the add returns, above
     // +inf, so it drops out of their min.  Updates only ever lower a value.
-    float h[T + 2][T + 2];
+    float h[TH + 2][TW + 2];
     if (tile_ok) {
 #pragma unroll
-      for (int i = 0; i < T; ++i)
+      for (int i = 0; i < TH; ++i)
 #pragma unroll
-        for (int j = 0; j < T; ++j) {
+        for (int j = 0; j < TW; ++j) {
           const int r = r0 + i, cc = c0 + j;
           const bool border = r == 0 || r == G - 1 || cc == 0 || cc == G - 1;
           const bool o = border || occ_bit(occ, r, cc);
@@ -300,11 +312,14 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
           h[i + 1][j + 1] = init;
         }
 #pragma unroll
-      for (int k = 0; k < T; ++k) {
-        edge[E_TOP][tp][k] = h[1][k + 1];
-        edge[E_BOT][tp][k] = h[T][k + 1];
-        edge[E_LEFT][tp][k] = h[k + 1][1];
-        edge[E_RIGHT][tp][k] = h[k + 1][T];
+      for (int k = 0; k < TW; ++k) {
+        edgeh[E_TOP][tp][k] = h[1][k + 1];
+        edgeh[E_BOT][tp][k] = h[TH][k + 1];
+      }
+#pragma unroll
+      for (int k = 0; k < TH; ++k) {
+        edgev[E_LEFT - 2][tp][k] = h[k + 1][1];
+        edgev[E_RIGHT - 2][tp][k] = h[k + 1][TW];
       }
       lastc[tp] = 0;
     }
@@ -320,20 +335,23 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
 #pragma unroll
         for (int dr = -1; dr <= 1; ++dr)
 #pragma unroll
-          for (int dc = -1; dc <= 1; ++dc) dirty |= lastc[tp + dr * NTP + dc] >= it - 1;
+          for (int dc = -1; dc <= 1; ++dc) dirty |= lastc[tp + dr * NPC + dc] >= it - 1;
       }
       if (dirty) {
 #pragma unroll
-        for (int k = 0; k < T; ++k) {
-          h[0][k + 1] = edge[E_BOT][tp - NTP][k];
-          h[T + 1][k + 1] = edge[E_TOP][tp + NTP][k];
-          h[k + 1][0] = edge[E_RIGHT][tp - 1][k];
-          h[k + 1][T + 1] = edge[E_LEFT][tp + 1][k];
+        for (int k = 0; k < TW; ++k) {
+          h[0][k + 1] = edgeh[E_BOT][tp - NPC][k];
+          h[TH + 1][k + 1] = edgeh[E_TOP][tp + NPC][k];
         }
-        h[0][0] = edge[E_BOT][tp - NTP - 1][T - 1];
-        h[0][T + 1] = edge[E_BOT][tp - NTP + 1][0];
-        h[T + 1][0] = edge[E_TOP][tp + NTP - 1][T - 1];
-        h[T + 1][T + 1] = edge[E_TOP][tp + NTP + 1][0];
+#pragma unroll
+        for (int k = 0; k < TH; ++k) {
+          h[k + 1][0] = edgev[E_RIGHT - 2][tp - 1][k];
+          h[k + 1][TW + 1] = edgev[E_LEFT - 2][tp + 1][k];
+        }
+        h[0][0] = edgeh[E_BOT][tp - NPC - 1][TW - 1];
+        h[0][TW + 1] = edgeh[E_BOT][tp - NPC + 1][0];
+        h[TH + 1][0] = edgeh[E_TOP][tp + NPC - 1][TW - 1];
+        h[TH + 1][TW + 1] = edgeh[E_TOP][tp + NPC + 1][0];
         // forward raster sweep (up-left, up, up-right, left), then backward (mirror).
         // Cell (i, j) of the forward sweep depends on (i, j-1) and row i-1 up to
         // column j+1, so cells with equal 2i + j are independent: emitting the
@@ -342,11 +360,11 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
         // independent one ~4).  Same updates in a dependency-respecting order
         // (each cell still sees exactly the raster sweep's operands).
 #pragma unroll
-        for (int L = 0; L < 3 * T - 2; ++L)
+        for (int L = 0; L < 2 * TH + TW - 2; ++L)
 #pragma unroll
-          for (int i = 1; i <= T; ++i) {
+          for (int i = 1; i <= TH; ++i) {
             const int j = L - 2 * (i - 1) + 1;
-            if (j < 1 || j > T) continue;
+            if (j < 1 || j > TW) continue;
             const int32_t hb = __float_as_int(h[i][j]);
             int32_t m = min(hb, __float_as_int(fabsf(h[i - 1][j - 1]) + 1.414f));
             m = min(m, __float_as_int(fabsf(h[i - 1][j]) + 1.0f));
@@ -356,11 +374,11 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
             h[i][j] = __int_as_float(m);
           }
 #pragma unroll
-        for (int L = 0; L < 3 * T - 2; ++L)
+        for (int L = 0; L < 2 * TH + TW - 2; ++L)
 #pragma unroll
-          for (int i = T; i >= 1; --i) {
-            const int j = T - (L - 2 * (T - i));
-            if (j < 1 || j > T) continue;
+          for (int i = TH; i >= 1; --i) {
+            const int j = TW - (L - 2 * (TH - i));
+            if (j < 1 || j > TW) continue;
             const int32_t hb = __float_as_int(h[i][j]);
             int32_t m = min(hb, __float_as_int(fabsf(h[i + 1][j + 1]) + 1.414f));
             m = min(m, __float_as_int(fabsf(h[i + 1][j]) + 1.0f));
@@ -376,11 +394,14 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
 #endif
         if (changed) {
 #pragma unroll
-          for (int k = 0; k < T; ++k) {
-            edge[E_TOP][tp][k] = h[1][k + 1];
-            edge[E_BOT][tp][k] = h[T][k + 1];
-            edge[E_LEFT][tp][k] = h[k + 1][1];
-            edge[E_RIGHT][tp][k] = h[k + 1][T];
+          for (int k = 0; k < TW; ++k) {
+            edgeh[E_TOP][tp][k] = h[1][k + 1];
+            edgeh[E_BOT][tp][k] = h[TH][k + 1];
+          }
+#pragma unroll
+          for (int k = 0; k < TH; ++k) {
+            edgev[E_LEFT - 2][tp][k] = h[k + 1][1];
+            edgev[E_RIGHT - 2][tp][k] = h[k + 1][TW];
           }
           lastc[tp] = it;
         }
@@ -400,9 +421,9 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
     float hmax = 0.f;
     if (tile_ok) {
 #pragma unroll
-      for (int i = 0; i < T; ++i)
+      for (int i = 0; i < TH; ++i)
 #pragma unroll
-        for (int j = 0; j < T; ++j) {
+        for (int j = 0; j < TW; ++j) {
           const uint32_t hb = __float_as_uint(h[i + 1][j + 1]);
           if (hb < kInfBits) hmax = fmaxf(hmax, h[i + 1][j + 1]);
         }
@@ -411,14 +432,17 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
     // ---- 3. raw cost out (occupied marker -> +inf) into the env's field tile: the field's 10 x 10 tiles are
     // these threads' tiles, so the 100 stores are immediate offsets of one base (no per-thread offsets, no
     // scratch copy).  Statistics and the SDF in k_field_stats, the constants in k_field_norm ----
-    static_assert(USV_FIELD_TH == T && USV_FIELD_TW == T && USV_FIELD_TCOLS == NT, "field tiles = sweep tiles");
+    // (a TH x TW sweep tile is the column part (tc % kSub) of field tile (tr, tc / kSub))
+    constexpr int kSub = USV_FIELD_TW / TW;
+    static_assert(USV_FIELD_TCOLS * USV_FIELD_TW == G && USV_FIELD_TCOLS == NTC / kSub, "field tiles = sweep tiles");
     if (tile_ok) {
-      float *Ft = b.field + (size_t)e * FS + (tr * NT + tc) * (T * T);
+      float *Ft = b.field + (size_t)e * FS + (tr * USV_FIELD_TCOLS + tc / kSub) * (USV_FIELD_TH * USV_FIELD_TW) +
+                  (tc % kSub) * TW;
 #pragma unroll
-      for (int i = 0; i < T; ++i)
+      for (int i = 0; i < TH; ++i)
 #pragma unroll
-        for (int j = 0; j < T; ++j)
-          Ft[i * T + j] = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
+        for (int j = 0; j < TW; ++j)
+          Ft[i * USV_FIELD_TW + j] = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
     }
     if (tile_ok) lastc[tp] = -1000;   // ready for the next slot
     if (tid == 0) {
@@ -436,6 +460,12 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
 __global__ __launch_bounds__(kWaveThreads) void k_field_wave(usv_cfg_t c, usv_bufs_t b) { field_wave_body<true>(c, b); }
 __global__ __launch_bounds__(kWaveThreads, USV_SWEEP_WAVES) void k_field_wave_pack(usv_cfg_t c, usv_bufs_t b) {
   field_wave_body<false>(c, b);
+}
+// small batches (fewer reset envs than CUs): one env per CU either way, so 10 x 5 tiles over 450 threads (two waves
+// per SIMD instead of one) trade more tile hops per sweep for twice the issue rate (USV_FIELD_HALF)
+constexpr int kHalfThreads = 512;
+__global__ __launch_bounds__(kHalfThreads) void k_field_wave_half(usv_cfg_t c, usv_bufs_t b) {
+  field_wave_body<false, T, T / 2, kHalfThreads>(c, b);
 }
 
 // The reference's literal sweeps for the slots k_field_wave could not certify (SS_EXACT):
@@ -846,8 +876,15 @@ int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream
     return 0;
   }
   if (stage == 2 || stage == 3) {
-    const int grid_w = b->n < kPackGrid ? b->n : kPackGrid;
-    hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_w), dim3(kWaveThreads), 0, s, *cfg, *b);
+    // USV_FIELD_HALF=1/0 forces the small-batch sweep kernel on / off; unset: on below kFieldPackMinEnvs envs
+    const char *half_env = getenv("USV_FIELD_HALF");
+    const bool half = half_env ? atoi(half_env) != 0 : b->n < kFieldPackMinEnvs;
+    if (half) {
+      hipLaunchKernelGGL(k_field_wave_half, dim3(b->n < 256 ? b->n : 256), dim3(kHalfThreads), 0, s, *cfg, *b);
+    } else {
+      const int grid_w = b->n < kPackGrid ? b->n : kPackGrid;
+      hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_w), dim3(kWaveThreads), 0, s, *cfg, *b);
+    }
     USV_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
     USV_CHECK_LAUNCH();

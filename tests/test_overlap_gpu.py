@@ -19,11 +19,15 @@ def _snap(task):
             "sdf": task.field.cpu().numpy(), "cost": task.sdf.cpu().numpy(), "fnorm": task.fnorm.cpu().numpy()}
 
 
+@pytest.mark.parametrize("half", ["0", "1"])
 @pytest.mark.parametrize("n", [1024, 8192])
-def test_overlapped_env_step_equals_plain_step(n):
+def test_overlapped_env_step_equals_plain_step(monkeypatch, n, half):
     """Eight steps from the first (every env reset: the 8,192-env case runs k_field_place's grid stride and
     several rounds of the sweep grid on the side stream), random actions, Philox draws: state, obs, reward,
-    dones, history, episode sums, obstacles, extras and every field bit-identical after each step."""
+    dones, history, episode sums, obstacles, extras and every field bit-identical after each step.  half: the
+    side stream's sweeps as the packed 10 x 10-tile kernel ("0") or the small-batch 10 x 5-tile kernel ("1",
+    USV_FIELD_HALF) against the plain step's 10 x 10-tile k_field_wave."""
+    monkeypatch.setenv("USV_FIELD_HALF", half)
     from omniisaacgymenvs_loop_amd.tasks.usv_config import load_yaml
     from tests.test_oracle_golden import TEST_YAML
     from omniisaacgymenvs_loop_amd.tasks.usv_virtual import USVVirtual
