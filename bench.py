@@ -8,7 +8,9 @@ reference's "fps total" (rl_games a2c_common.py:46-60).  Workload: the north
 star's USV_Virtual_CaptureXY at 2^20 envs over 8 GPUs (BASELINE.json configs[4]),
 i.e. 131072 envs per GPU, PPO-MLP fp32; with --gpus N each rank owns 131072 envs
 (weak scaling) and gradients are all-reduced over RCCL every minibatch.  The
-4096-env BASELINE configs[1] line is reported as a secondary field (extra.c2).
+4096-env BASELINE configs[1] line is reported as a secondary field (extra.c2), and on one GPU
+configs[2] (65536 envs, bf16 GEMMs: extra.c3) and configs[3]'s per-GPU share of each task (extra.c4_pose,
+extra.c4_track) too.
 
     python bench.py [--gpus N --steps K --warmup W --envs 131072]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
@@ -220,9 +222,11 @@ def cpu_baseline(shapes=((32, 512, 4.0), (4096, 8192, 20.0))):
 C2_ENVS = 4096                 # BASELINE configs[1]: secondary line of the same run
 HEADLINE_ENVS = 131072         # BASELINE configs[4] per GPU: 2^20 envs over 8 GPUs
 REWARD_TARGET = 30.0           # BASELINE metric, half 2: wall-clock to rewards/step >= 30
-# 30 is about the untrained policy's level (the first full 100-episode meter of a random-init policy reads
-# ~30); learning milestones of the same rewards/step meter, reported beside it
+# the random-init policy's first full 100-episode meter reads about -99 (early collisions), so 30 marks learned
+# behaviour; further milestones of the same rewards/step meter are reported beside it
 MILESTONES = (30.0, 60.0, 80.0, 100.0)
+C3_ENVS = 65536                # BASELINE configs[2]: CaptureXY SysID DR, bf16 (mixed_precision) on one GPU
+C4_ENVS = 65536                # BASELINE configs[3]: 262144 envs over 4 GPUs -> 65536 per GPU, per task
 
 
 def phase_split(timed_events, ms_per_step, minibatches, last_epoch):
@@ -239,6 +243,36 @@ def phase_split(timed_events, ms_per_step, minibatches, last_epoch):
             "phase_method": f"HIP events recorded on the stream inside each of the {len(rp)} timed epochs "
                             f"(epochs {last_epoch - len(rp) + 1}-{last_epoch}) around the rollout (+ GAE / prepare) "
                             "and the update; mean over the timed epochs"}
+
+
+def rank_record(rank, device, task_name, dp_status, elapsed_local, steps, phase):
+    """This rank's part of a multi-rank line: its device, task, the gradient exchange that ran and its start-up
+    self-test (A2CAgent.dp_status), its own timed-epoch time and its phase split."""
+    from omniisaacgymenvs_loop_amd.rl_games.dist_util import device_identity
+    return {"rank": rank, "device": device_identity(device), "task": task_name,
+            "exchange": dp_status["exchange"], "selftest": dp_status["selftest"], "exchange_error": dp_status["error"],
+            "epoch_ms": elapsed_local / steps * 1e3, "rollout_ms": phase.get("rollout_ms"),
+            "update_us_per_minibatch": phase.get("update_us_per_minibatch")}
+
+
+def rank_records(rec, world):
+    """Every rank's record in rank order (all_gather_object over the process group: RCCL or gloo); [rec] alone."""
+    if world == 1:
+        return [rec]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, rec)
+    return out
+
+
+def dp_fields(records):
+    """config.exchange and the per-rank extras of a multi-rank line: which gradient exchange ran (peer: the
+    in-kernel IPC exchange of ppo_minibatch_fused_dp; collective: torch.distributed all-reduces), each rank's
+    start-up self-test outcome, epoch time and minibatch update time -- so a scaling record says what it measured."""
+    ex = sorted({r["exchange"] for r in records})
+    return (ex[0] if len(ex) == 1 else "mixed: " + ", ".join(ex)), {
+        "dp_selftest": {str(r["rank"]): r["selftest"] for r in records},
+        "ranks": records}
 
 
 def time_epochs(agent, steps, world, local):
@@ -278,6 +312,9 @@ def main():
                          "mixed_precision; BASELINE configs[2] at --envs 65536); physics stays fp32")
     ap.add_argument("--c2-steps", type=int, default=10,
                     help="epochs of the secondary BASELINE configs[1] line (4096 envs/GPU; 0 = skip)")
+    ap.add_argument("--extra-steps", type=int, default=10,
+                    help="one GPU: epochs of each of the configs[2] / configs[3] lines (extra.c3, extra.c4_pose, "
+                         "extra.c4_track; 0 = skip)")
     ap.add_argument("--milestone-seconds", type=float, default=30.0,
                     help="one GPU: keep training after the measurements until rewards/step >= the last milestone "
                          "or this many seconds (wall-clock to learning milestones; 0 = skip)")
@@ -359,6 +396,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_local = elapsed
     t = torch.tensor([elapsed], device=f"cuda:{local}", dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -377,6 +415,9 @@ def main():
     # (the epoch-end synchronisation, meters, the next submission), >= 0 by construction
     phase = phase_split(timed_events, elapsed / args.steps * 1e3, agent.mini_epochs_num * agent.num_minibatches,
                         epoch_timed_last)
+    records = rank_records(rank_record(rank, f"cuda:{local}", task_name, agent.dp_status, elapsed_local, args.steps,
+                                       phase), world)
+    exchange, dp_extra = dp_fields(records)
     # the same two graphs replayed behind a spin kernel after the timed epochs: device time only (no host
     # submission inside the pairs), at a later training state (more resets per step as the policy learns)
     if agent._graph_play is not None and agent._graph_update is not None:
@@ -466,7 +507,7 @@ def main():
                        + (" [mixed_precision: bf16 GEMMs]" if args.mixed_precision else ""),
                        "num_envs_per_gpu": args.envs, "horizon_length": agent.horizon_length,
                        "minibatch_size": agent.minibatch_size, "mini_epochs": agent.mini_epochs_num,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}", "exchange": exchange},
             "fps_step_inference": play_fps, "fps_step_env_only": env_fps,
             "roofline": {"bound": "hbm", "kernel": step_kernel,
                          "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -503,11 +544,13 @@ def main():
                                                     "all-reduce and k_apply follow outside the pair)")
                                                  + " of one eager epoch, minus the empty pair"},
             "wall_clock_to_reward": dict(to_reward, unit="s", since="first env reset of this run (random-init policy)",
-                                         note="30 is about the untrained policy's level: see first_full_meter "
-                                              "and the learning milestones",
+                                         note="the BASELINE metric's target on the reference's rewards/step meter "
+                                              "(last 100 finished episodes); the random-init policy's first full "
+                                              "meter reads first_full_meter (about -99: early collisions), so 30 "
+                                              "is learned behaviour; 60 / 80 / 100 are further milestones",
                                          first_full_meter=first_full or None, milestones=miles,
                                          last100_mean_at_end=float(agent.game_rewards.get_mean())),
-            "extra": dict(phase),
+            "extra": dict(phase, **(dp_extra if world > 1 else {})),
         }
         tf = os.path.join(ROOT, "profiles", f"env_step_traffic_{args.envs}.json")
         if not os.path.exists(tf) and args.envs == C2_ENVS:
@@ -520,22 +563,46 @@ def main():
                 out["roofline"]["traffic_read"] = tr.get("read_bytes_per_launch")
                 out["roofline"]["traffic_write"] = tr.get("write_bytes_per_launch")
                 out["roofline"]["traffic_source"] = tr.get("source")
-    # secondary line: BASELINE configs[1] (4096 envs/GPU), same code path, graph-replayed epochs
-    if args.c2_steps and args.envs != C2_ENVS and task_name == "CaptureXY":
+    # secondary lines, same code path, graph-replayed epochs: BASELINE configs[1] (4096 envs/GPU) on any number
+    # of ranks; on one GPU also configs[2] (65536 envs, bf16 GEMMs) and configs[3]'s per-GPU share of each task
+    if args.envs != HEADLINE_ENVS or task_name != "CaptureXY" or args.mixed_precision:
+        secondary = []
+    else:
+        secondary = [("c2", C2_ENVS, "CaptureXY", False, args.c2_steps,
+                      f"USV_Virtual_CaptureXY num_envs={C2_ENVS}/GPU PPO-MLP fp32 (BASELINE configs[1])")]
+        if world == 1:
+            secondary += [
+                ("c3", C3_ENVS, "CaptureXY", True, args.extra_steps,
+                 f"USV_Virtual_CaptureXY_SysID num_envs={C3_ENVS}/GPU PPO-MLP, bf16 GEMM operands / fp32 "
+                 "accumulate (train config mixed_precision; BASELINE configs[2])"),
+                ("c4_pose", C4_ENVS, "GoToPose", False, args.extra_steps,
+                 f"USV_Virtual_GoToPose num_envs={C4_ENVS}/GPU PPO-MLP fp32 (BASELINE configs[3]'s per-GPU share, "
+                 "the GoToPose ranks)"),
+                ("c4_track", C4_ENVS, "TrackXYOVelocity", False, args.extra_steps,
+                 f"USV_Virtual_TrackXYOVelocity num_envs={C4_ENVS}/GPU PPO-MLP fp32 (BASELINE configs[3]'s "
+                 "per-GPU share, the TrackXYOVelocity ranks)")]
+    if any(st for *_, st, _ in secondary):
         del agent, env, task
         torch.cuda.empty_cache()
-        env2, task2, agent2 = build(C2_ENVS, local, world, args.seed, task_name)
+    for key, n2, task2_name, mixed, st2, workload in secondary:
+        if not st2:
+            continue
+        env2, task2, agent2 = build(n2, local, world, args.seed, task2_name, mixed)
         agent2.use_graph = not args.no_graph
         agent2.obs = agent2.env_reset()
         for _ in range(3):
             agent2.train_epoch()
-        el2 = time_epochs(agent2, args.c2_steps, world, local)
+        el2 = time_epochs(agent2, st2, world, local)
         if out is not None:
-            out["extra"]["c2"] = {"workload": f"USV_Virtual_CaptureXY num_envs={C2_ENVS}/GPU PPO-MLP fp32 "
-                                              "(BASELINE configs[1])",
-                                  "value": world * C2_ENVS * agent2.horizon_length * args.c2_steps / el2,
-                                  "unit": "env-steps/s", "ms_per_step": el2 / args.c2_steps * 1e3,
-                                  "steps": args.c2_steps}
+            out["extra"][key] = {"workload": workload,
+                                 "value": world * n2 * agent2.horizon_length * st2 / el2,
+                                 "unit": "env-steps/s", "ms_per_step": el2 / st2 * 1e3, "steps": st2,
+                                 "n_gpus": world}
+        if agent2._dp is not None:
+            torch.cuda.synchronize()
+            agent2._dp.release()
+        del agent2, env2, task2
+        torch.cuda.empty_cache()
     if rank == 0:
         if not args.no_cpu_baseline and world == 1 and args.task == "CaptureXY":
             print("[bench] cpu baseline ...", file=sys.stderr, flush=True)

@@ -206,7 +206,7 @@ typedef struct usv_cfg {
    * reward or observation into ctl[USV_CTL_NAN_FLAG]; the host raises after the epoch ---- */
   int   nan_probe;
   /* ---- GoToPose spawn curriculum (GoToPoseTask.get_spawns / update_kills, USV_go_to_pose.py:183-209,
-   * 256-300; GoToPoseParameters.spawn_curriculum*, USV_task_parameters.py:70-76): the spawn disk and the kill
+   * 256-300; GoToPoseParameters.spawn_curriculum*, USV_task_parameters.py:107-113): the spawn disk and the kill
    * distance move linearly from the curriculum values to the task's as the reference's USVVirtual.step (a
    * Python float += 1 / horizon_length per calculate_metrics, USV_Virtual.py:1633) goes from warmup to end;
    * get_spawns sees the value at the step's reset, update_kills the value after its calculate_metrics

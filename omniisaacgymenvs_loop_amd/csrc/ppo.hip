@@ -1028,6 +1028,7 @@ constexpr int AUX_SC1 = 16;   // sc1: write-through (the in-launch group fold re
 // one 128-B line holding the arrival counter (monotonic: a member's arrival value tells its launch generation)
 // and 32 slice words (the generation whose fold wrote slice m).
 constexpr int FOLD_G = 8;
+static_assert(RD_G >= FOLD_G, "k_reduce_partials(fold = 1) reads one group row per row group");
 constexpr int FOLD_MAX_M = 32;                      // nblk <= 256: the grid is resident at one workgroup per CU
 constexpr int FOLD_CTL_STRIDE = 64;                 // u32 words per group: [0] counter, [32 + m] slice gens
 constexpr uint64_t FOLD_WAIT_TICKS = 10000;         // 100 us at the 100 MHz wall clock
@@ -1523,13 +1524,16 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     const int nblk = (int)gridDim.x, M = nblk / FOLD_G, g = blockIdx.x % FOLD_G, m = blockIdx.x / FOLD_G;
     uint32_t *ctl = fold_ctl(partials, nblk) + g * FOLD_CTL_STRIDE;
     if (tid == 0) {
+      // release: the members may sit on other XCDs (separate L2s); the memory model, not the write-through
+      // stores' drain alone, then orders this workgroup's row before its arrival
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       const uint32_t old = __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t gen = old / (uint32_t)M + 1u, target = gen * (uint32_t)M;
       const uint64_t t0 = wall_clock64();
       int ok = 0;
       while (true) {
         const uint32_t v = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 poll
-        if ((int32_t)(v - target) >= 0) { ok = 1; break; }
+        if ((int32_t)(v - target) >= 0) { ok = 1; __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); break; }
         if (wall_clock64() - t0 > FOLD_WAIT_TICKS) break;
         __builtin_amdgcn_s_sleep(1);
       }

@@ -298,13 +298,17 @@ class A2CAgent:
         self._h_nan = torch.empty(1, dtype=torch.int32, pin_memory=pin)
         self._h_dp_err = None
         self._tail_staged = False
+        self.dp_status = {"exchange": "none (one rank)", "selftest": "not run", "error": None}
         self._dp = self._peer_exchange() if self.multi_gpu and self.rank_size > 1 else None
 
     def _peer_exchange(self):
         """Several ranks: the one-shot peer exchange of ppo_minibatch_fused_dp (dist_util.PeerExchange) unless
         USV_DP_EXCHANGE=collective; every rank must map every other rank's buffer, otherwise all ranks fall
         back to torch.distributed all-reduces (eager, the three-launch split)."""
+        # what ran, for the bench line (config.exchange, extra.ranks): exchange, the start-up self-test's outcome
+        self.dp_status = {"exchange": "collective", "selftest": "not run", "error": None}
         if os.getenv("USV_DP_EXCHANGE", "peer") == "collective":
+            self.dp_status["error"] = "USV_DP_EXCHANGE=collective"
             return None
         ex, err = None, None
         try:   # every rank succeeds or every rank raises (PeerExchange agrees over the ranks itself)
@@ -315,10 +319,15 @@ class A2CAgent:
         if not self._ranks_agree(ex is not None):
             if ex is not None:
                 ex.close()
+            self.dp_status["error"] = str(err) if err is not None else "failed on another rank"
+            if err is not None and "start-up exchange test failed" in str(err):
+                self.dp_status["selftest"] = "fail"
             if self.rank == 0:
                 print(f"peer exchange unavailable ({err or 'on another rank'}); gradients go through "
                       f"torch.distributed all-reduces")
             return None
+        self.dp_status.update(exchange="peer", selftest="pass" if ex.selftest_bits == 0 else
+                              ("not run" if ex.selftest_bits is None else f"fail (bits {ex.selftest_bits})"))
         return ex
 
     # ------------------------------------------------------------- rollout

@@ -57,6 +57,39 @@ def max_over_ranks(x: float, device) -> float:
     return float(t.item())
 
 
+# Ranks per device the peer exchange can train with: the waiting ranks' spinning reduction workgroups (8 KB of
+# LDS each, up to one per CU per rank) must leave every CU the 146 KB a gradient workgroup of the last rank needs.
+# Two ranks on one device fit (the one-GPU rehearsals); four stall until the exchange timeout.
+PEER_MAX_RANKS_PER_DEVICE = 2
+
+
+def device_identity(device) -> str:
+    """Host + PCI location of this rank's GPU (the physical device, whatever HIP_VISIBLE_DEVICES maps it to);
+    without a GPU (CPU tests) host + device string."""
+    import socket
+    host = socket.gethostname()
+    try:
+        if torch.cuda.is_available():
+            p = torch.cuda.get_device_properties(torch.device(device))
+            return f"{host}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    except (RuntimeError, AssertionError, AttributeError):
+        pass
+    return f"{host}/{device}"
+
+
+def shared_device_refusal(idents, limit: int = PEER_MAX_RANKS_PER_DEVICE):
+    """None if no device holds more than `limit` ranks, else the refusal message naming the device and ranks."""
+    by_dev = {}
+    for r, d in enumerate(idents):
+        by_dev.setdefault(d, []).append(r)
+    worst = max(by_dev.items(), key=lambda kv: len(kv[1]))
+    if len(worst[1]) <= limit:
+        return None
+    return (f"ranks {worst[1]} share device {worst[0]}: the peer exchange trains with at most {limit} ranks per "
+            f"device (the waiting ranks' reduction workgroups would hold the LDS the last rank's gradient kernel "
+            f"needs, a stall until the exchange timeout); use one process per GPU, or USV_DP_EXCHANGE=collective")
+
+
 class PeerExchange:
     """The one-shot gradient all-reduce of ppo_minibatch_fused_dp (include/usv_hip.h ppo_dp_t): every rank
     allocates one receive buffer (ppo_dp_alloc), the 64-byte IPC handles go around once through the process
@@ -81,6 +114,16 @@ class PeerExchange:
         from .._abi import DEFINES, PpoDp
         if not 1 <= world_size <= DEFINES["PPO_DP_MAX"]:
             raise RuntimeError(f"PeerExchange: world size {world_size} > PPO_DP_MAX")
+        self.selftest_bits = None
+        if peers is None and world_size > 1:
+            # forward progress needs few enough ranks per device (PEER_MAX_RANKS_PER_DEVICE): every rank sees the
+            # same gathered identities, so every rank refuses together, before anything is allocated
+            idents = [None] * world_size
+            dist.all_gather_object(idents, device_identity(device))
+            why = shared_device_refusal(idents)
+            if why is not None and os.getenv("USV_DP_SHARED_DEVICE_SETUP") != "1":
+                raise RuntimeError(f"PeerExchange: {why}")
+            self.shared_device = why is not None
         lib = _capi.lib()
         self.rank, self.world, self.device = rank, world_size, device
         self._lib = lib
@@ -154,11 +197,12 @@ class PeerExchange:
                        _capi.stream_ptr())
             torch.cuda.synchronize()
             bits = int(self.err.item())
-        except RuntimeError:
-            pass
-        self.clock.fill_(self.SELFTEST_ROUNDS)     # the flags hold the last test key: real keys continue after it
-        self.err.zero_()
-        torch.cuda.synchronize()
+            self.clock.fill_(self.SELFTEST_ROUNDS)  # the flags hold the last test key: real keys continue after it
+            self.err.zero_()
+            torch.cuda.synchronize()
+        except Exception:   # noqa: BLE001 -- a faulted kernel also fails the fills / sync: still reach agree()
+            bits |= 4
+        self.selftest_bits = bits
         if not agree(bits == 0, self.device):
             what = ("a flag did not arrive" if bits & 1 else "a payload arrived wrong or stale" if bits & 2
                     else "the test kernel failed to launch" if bits & 4 else "it failed on another rank")
@@ -174,6 +218,15 @@ class PeerExchange:
         if int(err_host[0] if err_host is not None else self.err.item()):
             raise RuntimeError("[ppo_dp] a peer's gradient chunk did not arrive within the timeout "
                                "(a rank died or the ranks' minibatch sequences diverged)")
+
+    def release(self) -> None:
+        """Collective teardown (every rank, kernels finished): unmap the peers' buffers, barrier, free our own."""
+        for p in self._opened:
+            self._lib.ppo_dp_close(ctypes_void(p))
+        self._opened = []
+        if dist.is_available() and dist.is_initialized():
+            dist.barrier()
+        self.close()
 
     def close(self) -> None:
         for p in self._opened:

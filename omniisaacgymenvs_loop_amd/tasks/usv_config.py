@@ -351,9 +351,12 @@ TASK_KINDS = {"CaptureXY": 0, "GoToPose": 1, "TrackXYOVelocity": 2}   # USV_TASK
 _MODES = {"linear": 0, "square": 1, "exponential": 2}
 # GoToPoseParameters / TrackXYOVelocityParameters and their reward dataclasses
 # (USV_task_parameters.py:74-148, USV_task_rewards.py:160-393)
+# GoToPoseParameters (USV_task_parameters.py:95-113), its own curriculum defaults (not GoToXYParameters' :70-76)
 _POSE_DEFAULTS = dict(position_tolerance=0.01, heading_tolerance=0.025, kill_after_n_steps_in_tolerance=500,
                       goal_random_position=0.0, max_spawn_dist=3.0, min_spawn_dist=0.5, kill_dist=10.0,
-                      spawn_curriculum=False)
+                      spawn_curriculum=False, spawn_curriculum_min_dist=0.5, spawn_curriculum_max_dist=2.5,
+                      spawn_curriculum_kill_dist=3.0, spawn_curriculum_mode="linear", spawn_curriculum_warmup=250,
+                      spawn_curriculum_end=750)
 _POSE_REWARD = dict(position_reward_mode="exponential", heading_reward_mode="exponential",
                     position_exponential_reward_coeff=0.25, heading_exponential_reward_coeff=0.25,
                     position_scale=1.0, heading_scale=5.0, sig_gain=3.0)
@@ -380,15 +383,15 @@ def _pose_task_cfg(c: UsvCfg, name: str, env: Dict[str, Any]) -> Dict[str, Any]:
         rp = dict(_POSE_REWARD)
         rp.update(env.get("reward_parameters", {}) or {})
         if bool(tp.get("spawn_curriculum", False)):
-            # GoToPoseParameters (USV_task_parameters.py:70-92): linear mode only, as the reference asserts
-            if str(tp.get("spawn_curriculum_mode", "linear")).lower() != "linear":
+            # GoToPoseParameters (USV_task_parameters.py:107-128): linear mode only, as the reference asserts
+            if str(tp["spawn_curriculum_mode"]).lower() != "linear":
                 raise AssertionError("Linear is the only currently supported mode.")
             c.curriculum_on = 1
-            c.cur_min_dist = float(tp.get("spawn_curriculum_min_dist", 0.2))
-            c.cur_max_dist = float(tp.get("spawn_curriculum_max_dist", 3.0))
-            c.cur_kill_dist = float(tp.get("spawn_curriculum_kill_dist", 30.0))
-            c.cur_warmup = float(int(tp.get("spawn_curriculum_warmup", 250)))
-            c.cur_end = float(int(tp.get("spawn_curriculum_end", 1000)))
+            c.cur_min_dist = float(tp["spawn_curriculum_min_dist"])
+            c.cur_max_dist = float(tp["spawn_curriculum_max_dist"])
+            c.cur_kill_dist = float(tp["spawn_curriculum_kill_dist"])
+            c.cur_warmup = float(int(tp["spawn_curriculum_warmup"]))
+            c.cur_end = float(int(tp["spawn_curriculum_end"]))
             c.min_spawn_d, c.max_spawn_d = float(tp["min_spawn_dist"]), float(tp["max_spawn_dist"])
             c.kill_dist_d = float(tp["kill_dist"])
         c.tk_mode[0], c.tk_mode[1] = _mode(rp["position_reward_mode"]), _mode(rp["heading_reward_mode"])

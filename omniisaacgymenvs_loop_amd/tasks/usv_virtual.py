@@ -285,13 +285,13 @@ class USVVirtual:
         self._side_tail_late = False
 
     def set_env_origins(self, org: torch.Tensor) -> None:
-        self._touch()
         """World x, y of each env's origin ([2][n]; RLTask._env_pos from the stage)."""
+        self._touch()
         self.env_org.copy_(org.to(self._device, torch.float32).reshape(2, self._num_envs))
 
     def set_grid_lin(self, lin: torch.Tensor) -> None:
-        self._touch()
         """Override the field grid's cell centres (parity tests vs CPU fixtures)."""
+        self._touch()
         self.grid_lin = lin.to(self._device, torch.float32).contiguous()
         self._bufs = self._make_bufs()
 

@@ -22,6 +22,7 @@ LIB_PATH = os.path.join(HERE, "build", "libusv_oracle_omp.so" if os.environ.get(
 NOBS, NOBST, GRID, NSTAT = 33, 16, 150, 28
 NU_RESET, NU_STEP = 712, 8
 NDIST = 11
+NDBG = 20          # usv_oracle.c USV_ORACLE_NDBG: per-env diagnostics of the last step
 CTL_POT_VALID, CTL_PEN_VALID, CTL_REW_VALID = 1, 2, 3
 
 _lib = None
@@ -78,7 +79,8 @@ class _OracleEnvC(ctypes.Structure):
     _fields_ = ([("n", ctypes.c_int)] + [(k, ctypes.c_void_p) for k in _PTR_FIELDS] +
                 [("ctl", ctypes.c_int32 * 20), ("extras", ctypes.c_float * NSTAT), ("dbg", ctypes.c_void_p),
                  ("tmp", ctypes.c_void_p), ("grid_lin", ctypes.c_void_p), ("dist", ctypes.c_void_p),
-                 ("env_org", ctypes.c_void_p), ("tgt_h", ctypes.c_void_p), ("step_f", ctypes.c_double)])
+                 ("env_org", ctypes.c_void_p), ("tgt_h", ctypes.c_void_p), ("step_f", ctypes.c_double),
+                 ("pot_in", ctypes.c_void_p), ("pos_in", ctypes.c_void_p)])
 
 
 class OracleEnv:
@@ -108,7 +110,7 @@ class OracleEnv:
         self.prev_cmd = np.zeros((2, n), np.float32)
         self.stats = np.zeros((NSTAT, n), np.float32)
         self.obs = np.zeros((n, NOBS), np.float32)
-        self.dbg = np.zeros((n, 16), np.float32)
+        self.dbg = np.zeros((n, NDBG), np.float32)
         self.tmp = np.zeros((n, 8), np.float32)
         self.grid_lin = None
         self.lin_damp = np.zeros((3, n), np.float32) if cfg.drag_rand_on else None
@@ -177,8 +179,9 @@ class OracleEnv:
         lib().oracle_step(ctypes.byref(self.cfg), ctypes.byref(self.c), _p(actions), _p(self.lut),
                           ctypes.c_float(bias), _p(U))
 
-    def full_step(self, actions, bias, step_idx, seed=0, U_step=None, U_reset=None):
-        """reset_idx (if any) + step, drawing Philox uniforms unless injected."""
+    def full_step(self, actions, bias, step_idx, seed=0, U_step=None, U_reset=None, pot_in=None, pos_in=None):
+        """reset_idx (if any) + step, drawing Philox uniforms unless injected.  pot_in / pos_in: the parity
+        harness's device potential samples [n] and post-integration positions [2][n] (see set_device_samples)."""
         ids = self.compact()
         if len(ids):
             if U_reset is None:
@@ -186,8 +189,19 @@ class OracleEnv:
             self.reset(ids, U_reset)
         if U_step is None:
             U_step = step_uniforms(seed, step_idx, self.n)
+        self.set_device_samples(pot_in, pos_in)
         self.step(actions, bias, U_step)
+        self.set_device_samples(None, None)
         return ids
+
+    def set_device_samples(self, pot_in=None, pos_in=None):
+        """Feed the device's potential samples to the next step's CaptureXY reward (the oracle's own samples go
+        to dbg[:, 14]) and have the oracle sample its own field at the device's positions into dbg[:, 15]: the
+        reward is then checked at 1e-5 with no potential-sample allowance, the sample itself separately."""
+        self._pot_in = None if pot_in is None else np.ascontiguousarray(pot_in, np.float32).reshape(self.n)
+        self._pos_in = None if pos_in is None else np.ascontiguousarray(pos_in, np.float32).reshape(2, self.n)
+        self.c.pot_in = _p(self._pot_in) if self._pot_in is not None else None
+        self.c.pos_in = _p(self._pos_in) if self._pos_in is not None else None
 
     def set_grid_lin(self, lin):
         self.grid_lin = np.ascontiguousarray(lin, np.float32)

@@ -122,6 +122,7 @@ static inline int lut_index(float cmd, int n) {
 /* ------------------------------------------------------------------------ */
 /* Env state (SoA, host memory)                                             */
 /* ------------------------------------------------------------------------ */
+#define USV_ORACLE_NDBG 20
 typedef struct oracle_env {
   int n;
   float *px, *py, *yaw, *vx, *vy, *wz, *fl, *fr;
@@ -141,8 +142,10 @@ typedef struct oracle_env {
   int32_t ctl[USV_CTL_N];
   float extras[USV_NSTAT];
   /* diagnostics of the last step (for parity tests) */
-  float *dbg;                       /* [n][16]: u_l, u_r, target_l, target_r, pot, danger, total, pens, shaping, dist_r, align_r,
-                                       praw (before the dead zone), ppos, ggate */
+  float *dbg;                       /* [n][USV_ORACLE_NDBG]: u_l, u_r, target_l, target_r, pot (the sample the reward used), danger, total,
+                                       pens, shaping, dist_r, align_r, praw (before the dead zone), ppos, ggate, the oracle's
+                                       own sample, its sample at pos_in, 1 where prev_pot was replaced by this step's sample
+                                       (a reset env or the global None after any reset) */
   float *tmp;                       /* [n][8]: cmd[2], thrust[2], unit[2], target force[2] */
   const float *grid_lin;            /* [150] potential-field cell centres, NULL => linspace formula */
   float *dist;                      /* [USV_NDIST][n] disturbance parameters or NULL */
@@ -150,6 +153,12 @@ typedef struct oracle_env {
   float *tgt_h;                     /* [n] GoToPose target heading / TrackXYO target yaw rate */
   double step_f;                    /* USVVirtual.step (+= 1 / horizon_length per calculate_metrics,
                                        USV_Virtual.py:1633): the GoToPose curriculum's clock */
+  /* parity harness (tests only): the device's potential samples and post-integration positions.  With
+     pot_in the CaptureXY reward uses pot_in[e] as this step's potential sample instead of the oracle's own
+     (which is kept in dbg[14]); prev_pot then carries the device's samples from step to step too.  With
+     pos_in the oracle also samples its own field at the device's position (+ the same noise) into dbg[15]. */
+  const float *pot_in;              /* [n] or NULL */
+  const float *pos_in;              /* [2][n] or NULL */
 } oracle_env_t;
 
 /* GoToPoseTask spawn curriculum (USV_go_to_pose.py:188-202 kill distance, :266-290 spawn radii): linear in
@@ -771,7 +780,7 @@ void oracle_step_pre(const usv_cfg_t *c, oracle_env_t *E, const float *actions, 
   for (int e = 0; e < n; ++e) {
     const float *u = U + (size_t)e * USV_NU_STEP;
     const int was_reset = E->just_reset[e];
-    float *dbg = E->dbg ? E->dbg + (size_t)e * 16 : NULL;
+    float *dbg = E->dbg ? E->dbg + (size_t)e * USV_ORACLE_NDBG : NULL;
     float *tmp = E->tmp + (size_t)e * 8;
     /* ---- VecEnvRLGames.step: clamp actions (:136-140) ---- */
     float cmd[2], thrust[2], uu[2], unit[2], tgt[2];
@@ -896,7 +905,7 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
   for (int e = 0; e < n; ++e) {
     const float *u = U + (size_t)e * USV_NU_STEP;
     const int was_reset = E->just_reset[e];
-    float *dbg = E->dbg ? E->dbg + (size_t)e * 16 : NULL;
+    float *dbg = E->dbg ? E->dbg + (size_t)e * USV_ORACLE_NDBG : NULL;
     const float *tmp = E->tmp + (size_t)e * 8;
     const float cmd[2] = {tmp[0], tmp[1]}, thrust[2] = {tmp[2], tmp[3]}, unit[2] = {tmp[4], tmp[5]};
     /* ---- post_physics_step (rl_task.py:283-303) ---- */
@@ -989,7 +998,18 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
     float align_r = c->align_la1 * (expf(c->align_la2 * (h2 * h2)) + expf(c->align_la3 * h2));
     if (was_reset) dist_r = 0.f;                                          /* :374 */
     const float prev_dist = was_reset ? dist : (rew_valid ? E->prev_dist[e] : dist);  /* :361-380 */
-    const float pot = sample_field(E->field + (size_t)e * USV_GRID2, c->map_size, px, py);
+    float pot = sample_field(E->field + (size_t)e * USV_GRID2, c->map_size, px, py);
+    if (dbg) dbg[14] = pot;
+    if (E->pos_in && dbg) {   /* the oracle's field at the device's integrated position, same noise as above */
+      float qx = E->pos_in[e], qy = E->pos_in[n + e];
+      if (c->pos_noise_on) {
+        const float rng = (float)((double)c->pos_noise_max - (double)c->pos_noise_min);
+        qx = qx + (u[SU_PX] * rng + c->pos_noise_min);
+        qy = qy + (u[SU_PX + 1] * rng + c->pos_noise_min);
+      }
+      dbg[15] = sample_field(E->field + (size_t)e * USV_GRID2, c->map_size, qx, qy);
+    }
+    if (E->pot_in) pot = E->pot_in[e];
     const float pn = clampf_(pot, 0.f, 1.f);
     const float xs = clampf_((pn - 0.6f) / (0.3f + 1e-6f), 0.f, 1.f);
     const float danger = xs * xs * (3.0f - 2.0f * xs);
@@ -1080,7 +1100,7 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
 #undef ADDS
     }
     if (dbg) { dbg[4] = pot; dbg[5] = danger; dbg[6] = total; dbg[7] = pens; dbg[8] = shaping; dbg[9] = dist_r; dbg[10] = align_r;
-               dbg[11] = praw_in; dbg[12] = ppos; dbg[13] = ggate; }
+               dbg[11] = praw_in; dbg[12] = ppos; dbg[13] = ggate; dbg[16] = (float)(any_reset_none || was_reset); }
     /* ---- _process_data: clamp obs (vec_env_rlgames.py:85-95) ---- */
     for (int q = 0; q < USV_NOBS; ++q) E->obs[(size_t)e * USV_NOBS + q] = clampf_(obs[q], -c->clip_obs, c->clip_obs);
     E->just_reset[e] = 0;

@@ -60,3 +60,36 @@ def test_phase_split_from_timed_epoch_events():
     assert ph["update_us_per_minibatch"] == pytest.approx(51.0e3 / 2048)
     assert ph["rollout_ms_min_max"] == [10.0, 12.0] and "epochs 29-30" in ph["phase_method"]
     assert bench.phase_split([], 65.0, 2048, 30) == {}
+
+
+def test_multi_rank_line_fields_under_torchrun_gloo(tmp_path):
+    """A two-rank torchrun (gloo, CPU): the line's config.exchange, extra.dp_selftest per rank and extra.ranks with
+    each rank's device, task, epoch ms and minibatch update time, gathered in rank order."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = 29000 + os.getpid() % 2000
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port),
+                          os.path.join(root, "tests", "_bench_ranks_worker.py")],
+                         capture_output=True, text=True, timeout=240, cwd=str(tmp_path))
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["config"]["exchange"] == "peer"
+    assert line["extra"]["dp_selftest"] == {"0": "pass", "1": "pass"}
+    ranks = line["extra"]["ranks"]
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert [r["task"] for r in ranks] == ["GoToPose", "TrackXYOVelocity"]
+    assert ranks[1]["epoch_ms"] == pytest.approx(65.0) and ranks[0]["epoch_ms"] == pytest.approx(60.0)
+    assert [r["update_us_per_minibatch"] for r in ranks] == [25.0, 26.0]
+    assert all(r["device"].endswith("/cpu") for r in ranks)
+
+
+def test_dp_fields_names_a_mixed_exchange():
+    bench = pytest.importorskip("bench")
+    recs = [{"rank": 0, "exchange": "peer", "selftest": "pass"},
+            {"rank": 1, "exchange": "collective", "selftest": "fail"}]
+    ex, extra = bench.dp_fields(recs)
+    assert ex == "mixed: collective, peer" and extra["dp_selftest"] == {"0": "pass", "1": "fail"}

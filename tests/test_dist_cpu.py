@@ -136,7 +136,7 @@ class _FakeDpLib:
         return 0
 
 
-def _pe_worker(rank, world, port, out_dir, fail_alloc, fail_open):
+def _pe_worker(rank, world, port, out_dir, fail_alloc, fail_open, shared=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -145,6 +145,8 @@ def _pe_worker(rank, world, port, out_dir, fail_alloc, fail_open):
         from omniisaacgymenvs_loop_amd.rl_games import dist_util
         fake = _FakeDpLib(rank, fail_alloc, fail_open)
         _capi.lib = lambda: fake
+        # one device per rank (what torchrun gives on a node), or every rank on one device
+        dist_util.device_identity = (lambda d: "host/0000:75:00") if shared else (lambda d: f"host/0000:{rank:02x}:00")
         msg = ""
         try:
             dist_util.PeerExchange(rank, world, "cpu")
@@ -173,6 +175,28 @@ def test_peer_exchange_setup_failure_is_agreed_and_frees_after_the_barrier(tmp_p
                 assert log.index("close") < log.index("free")
         else:
             assert "free" not in log
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_peer_exchange_refuses_more_than_two_ranks_per_device(tmp_path, world, monkeypatch):
+    """More ranks on one device than the exchange can make progress with (PEER_MAX_RANKS_PER_DEVICE: the waiting
+    ranks' spinning reduction workgroups would starve the last rank's gradient kernel of LDS) is refused on every
+    rank with a message naming the device and ranks, before anything is allocated (A2CAgent then falls back to
+    collectives); USV_DP_SHARED_DEVICE_SETUP=1 lets the set-up and self-test rehearsal through."""
+    from omniisaacgymenvs_loop_amd.rl_games.dist_util import shared_device_refusal
+    assert shared_device_refusal(["a", "a"]) is None and shared_device_refusal(["a", "b", "c", "d"]) is None
+    assert "ranks [0, 2, 3] share device a" in shared_device_refusal(["a", "b", "a", "a"])
+    monkeypatch.delenv("USV_DP_SHARED_DEVICE_SETUP", raising=False)
+    mp.spawn(_pe_worker, args=(world, _port(), str(tmp_path), (), (), True), nprocs=world, join=True)
+    for r in range(world):
+        z = np.load(tmp_path / f"pe{r}.npz")
+        assert "share device host/0000:75:00" in str(z["msg"]) and "USV_DP_EXCHANGE=collective" in str(z["msg"])
+        assert list(z["log"]) == []      # nothing allocated or mapped
+    monkeypatch.setenv("USV_DP_SHARED_DEVICE_SETUP", "1")
+    mp.spawn(_pe_worker, args=(world, _port(), str(tmp_path), (), (), True), nprocs=world, join=True)
+    for r in range(world):
+        z = np.load(tmp_path / f"pe{r}.npz")
+        assert "share device" not in str(z["msg"]) and list(z["log"])[:1] == ["alloc"]
 
 
 def test_update_capturable_gates_on_the_path_that_runs(monkeypatch):

@@ -151,7 +151,7 @@ def _worker_setup_only(rank, world, port, out_dir):
     every sender's flags and payload slots) without training."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), LOCAL_RANK=str(rank),
                       WORLD_SIZE=str(world), USV_RANKS_SHARE_DEVICE="0", USV_DIST_BACKEND="gloo",
-                      USV_DP_EXCHANGE="peer", USV_DP_TIMEOUT_MS="10000")
+                      USV_DP_EXCHANGE="peer", USV_DP_TIMEOUT_MS="10000", USV_DP_SHARED_DEVICE_SETUP="1")
     import sys
     sys.path.insert(0, ROOT)
     import torch.distributed as dist

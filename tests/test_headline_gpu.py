@@ -22,7 +22,7 @@ from oracle import oracle as O
 from oracle import ppo_oracle as PO
 from omniisaacgymenvs_loop_amd.tasks.usv_config import load_yaml
 from tests import errtab as ET
-from tests.test_env_gpu import _oracle_for, _run_field, _task, _vs_oracle
+from tests.test_env_gpu import _oracle_for, _run_field, _task, _vs_oracle, device_samples, oracle_step
 from tests.test_oracle_golden import TEST_YAML
 from tests.test_ppo_gpu import _agent
 
@@ -176,8 +176,7 @@ def test_philox_placement_8192_resets_vs_oracle(monkeypatch):
         a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
         bias = task.current_action_bias()
         obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
-        ids = E.full_step(a, bias, t, seed=task.seed)
-        torch.cuda.synchronize()
+        ids = oracle_step(task, E, a, bias, t)
         if t == 0:
             assert len(ids) == n
             np.testing.assert_array_equal(task.obst.cpu().numpy().reshape(16, 2, n), E.obst)
@@ -238,7 +237,8 @@ def test_full_size_131072_step_vs_oracle():
     Philox draws: every env reset on the first step -- DR parameters, spawns and obstacles bit-exact for all
     131,072 envs, the raw cost-to-go of 64 sampled envs bit-exact against the oracle's wavefront, the batch's
     inf_val equal to 1.5 x the largest finite cost over all 131,072 fields -- then three steps with obs /
-    state at 1e-5, dones exact and the reward within 1e-5 + the potential-sample bound (test_env_gpu.py).
+    state at 1e-5, dones exact, the potential samples against the oracle's field at the device's positions and
+    the reward at 1e-5 against the oracle fed those samples (test_env_gpu._vs_oracle).
     The oracle's reset skips its own 131,072 fields (oracle_set_skip_field: hours of CPU) and steps on the
     device's fields, whose texels are checked above and at 8,192 resets in
     test_philox_placement_8192_resets_vs_oracle; later resets (few envs) build their fields in the oracle."""
@@ -278,10 +278,10 @@ def test_full_size_131072_step_vs_oracle():
             for c0 in range(0, n, 16384):
                 idx = torch.arange(c0, min(c0 + 16384, n), device=DEV)
                 E.field[c0:c0 + len(idx)] = task.field_rowmajor(idx).cpu().numpy()
+            E.set_device_samples(*device_samples(task))
             E.step(a, bias, O.step_uniforms(task.seed, 0, n))
         else:
-            E.full_step(a, bias, t, seed=task.seed)
-        torch.cuda.synchronize()
+            oracle_step(task, E, a, bias, t)
         dp = _vs_oracle("full_size_131072", task, E, obs, rew, dones, t, dp)
         st = task.state.cpu().numpy()
         for j, k in enumerate(("px", "py", "yaw", "vx", "vy", "wz", "fl", "fr")):

@@ -9,6 +9,7 @@ from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg
 from omniisaacgymenvs_loop_amd.utils import hydra_cfg as HC
 
 REF_CFG = "/root/reference/omniisaacgymenvs/cfg"
+CFG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "omniisaacgymenvs_loop_amd", "cfg")
 
 
 def test_relative_absolute_and_resolvers():
@@ -77,3 +78,19 @@ def test_reference_yamls_unmodified():
     for name, _ in a._fields_:
         assert getattr(a, name) == getattr(b, name) or (
             hasattr(getattr(a, name), "__len__") and list(getattr(a, name)) == list(getattr(b, name))), name
+
+
+def test_gotopose_curriculum_defaults_are_gotopose_parameters():
+    """spawn_curriculum=True with no other curriculum key takes GoToPoseParameters' defaults
+    (USV_task_parameters.py:107-113: 0.5 / 2.5 / 3.0 / 250 / 750), not GoToXYParameters' (:70-76)."""
+    from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg, load_yaml
+    y = load_yaml(os.path.join(CFG, "task", "USV", "USV_Virtual_GoToPose.yaml"))
+    tp = y["env"]["task_parameters"]
+    for k in list(tp):
+        if k.startswith("spawn_curriculum"):
+            del tp[k]
+    tp["spawn_curriculum"] = True
+    c = build_usv_cfg(y)
+    assert c.curriculum_on == 1
+    assert (c.cur_min_dist, c.cur_max_dist, c.cur_kill_dist, c.cur_warmup, c.cur_end) == \
+        pytest.approx((0.5, 2.5, 3.0, 250.0, 750.0))
