@@ -821,6 +821,17 @@ __global__ __launch_bounds__(RS_TB) void k_obs_rms_seq(ppo_cfg_t c, const double
 // 16 dW2 tiles go two per wave; the row inputs of the losses are loaded with the
 // weights, so nothing in the loss phase waits on memory.
 constexpr int GTB = 512;          // threads per workgroup
+// USV_PPO_BWD2: the backward in two concurrent wave groups without barriers (dh1 -> dz1 -> dW1 on waves 0-3,
+// dW2 + head gradients on waves 4-7, dz2 formed on the fly); 0 = the one-group form (K-half exchanges, A/B builds)
+#ifndef USV_PPO_BWD2
+#define USV_PPO_BWD2 1
+#endif
+#ifndef USV_PPO_HL
+#define USV_PPO_HL 1     // heads and losses in one phase (0: heads, barrier, losses on two waves; A/B builds)
+#endif
+#ifndef USV_BWD_PRIO
+#define USV_BWD_PRIO 1   // s_setprio of the dh1 -> dz1 -> dW1 waves in the two-group backward (A/B builds override it)
+#endif
 
 // k_reduce_partials geometry (RED_BLOCKS chunk squares follow the gradient in grad[])
 #ifndef USV_RD_P
@@ -944,6 +955,7 @@ struct GradSmem {
   float b1[NH];
   float tail[TAIL + 1];
   float nrm[4];                   // chained update: wave sums of the chunk squares
+  float lsum[8][4];               // per-wave loss / sigma-gradient row sums (USV_PPO_HL)
   int fold[2];                    // group fold: all members arrived, this launch's generation
 };
 
@@ -1129,7 +1141,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // per-row loss inputs, lane = row (waves 0 and 1 use them: the actor / the critic side)
   RowIn ri;
   {
+#if USV_PPO_HL
+    const size_t row = (size_t)rb0 + 8 * (w & 3) + (lane >> 3);   // the row this lane's loss terms take
+#else
     const size_t row = (size_t)rb0 + (lane & (RB - 1));
+#endif
     ri.act0 = row_ld(&e_act[row * 2]); ri.act1 = row_ld(&e_act[row * 2 + 1]);
     ri.nlp = row_ld(&e_nlp[row]); ri.adv = row_ld(&e_adv[row]);
     ri.val = row_ld(&e_val[row]); ri.ret = row_ld(&e_ret[row]);
@@ -1262,6 +1278,9 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
   __syncthreads();
   USV_PHASE(ppo, 12);
+  const PartOutT<kFold ? AUX_SC1 : USV_PART_AUX> part_st{
+      __builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4, 0x00020000)};
+#if !USV_PPO_HL
   // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (16 threads per row, k = part + 16 kk: the 16
   // threads of a row read 16 consecutive words -- no 4-way LDS bank conflicts) ----
   {
@@ -1289,8 +1308,6 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
   __syncthreads();
   USV_PHASE(ppo, 2);
-  const PartOutT<kFold ? AUX_SC1 : USV_PART_AUX> part_st{
-      __builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4, 0x00020000)};
   // ---- per-row losses and output gradients (lane = row < RB): wave 0 the actor side (ratio, clipped
   // surrogate, dnlp, dmu, dlogstd), wave 1 in parallel the critic, bound, entropy and KL terms and the
   // mu / sigma write-back (the same per-row arithmetic and lane sums as one wave doing both) ----
@@ -1380,8 +1397,245 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
       }
     }
   }
+#else
+  // ---- heads and per-row losses in one phase: waves 0-3 and waves 4-7 each form the heads of all 32 rows (8
+  // threads per row, k = part + 8 kk), then the actor side (ratio, clipped surrogate, dnlp, dmu, dlogstd) runs on
+  // waves 0-3 and the critic, bound, entropy and KL terms and the mu / sigma write-back on waves 4-7, row
+  // r = 8 (w & 3) + lane / 8 on lane part 0 (the heads-to-losses barrier and the out[] round trip are gone) ----
+  {
+    const int r = 8 * (w & 3) + (lane >> 3), part = lane & 7;
+    float a0 = 0.f, a1 = 0.f, av = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < NH / 8; ++kk) {
+      const int k = part + 8 * kk;
+      const float hv = s.h2[r * HS + k];
+      a0 = fmaf(s.tail[T_WMU + k], hv, a0);
+      a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
+      av = fmaf(s.tail[T_WV + k], hv, av);
+    }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      a0 += __shfl_xor(a0, m, 64);
+      a1 += __shfl_xor(a1, m, 64);
+      av += __shfl_xor(av, m, 64);
+    }
+    USV_PHASE(ppo, 2);
+    const bool rowok = part == 0;
+    const size_t row = (size_t)rb0 + r;
+    const float mu0 = a0 + s.tail[T_BMU], mu1 = a1 + s.tail[T_BMU + 1], v = av + s.tail[T_BV];
+    if (!slow) {
+      lsig0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lsv), 0));
+      lsig1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lsv), 1));
+    }
+    const float ls0 = mu0 * 0.f + lsig0, ls1 = mu1 * 0.f + lsig1;
+    const float sg0 = expf(ls0), sg1 = expf(ls1);
+    const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
+    const float bh1 = fmaxf(mu1 - 1.1f, 0.f), bl1 = fminf(mu1 + 1.1f, 0.f);
+    if (w < 4) {
+      float la = 0.f, gs0 = 0.f, gs1 = 0.f;
+      if (rowok) {
+        const float z0 = (ri.act0 - mu0) / sg0, z1 = (ri.act1 - mu1) / sg1;
+        const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
+        const float A = ri.adv;
+        // actor_loss (common_losses.py:36-46)
+        const float ratio = expf(ri.nlp - nlp);
+        const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
+        const float rc = clampt(ratio, lo, hi);
+        const float s1 = -(A * ratio), s2 = -(A * rc);
+        const float a_loss = fmaxf(s1, s2);
+        const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
+        const float g1 = -A, g2 = -A * inr;                // d(-A r)/dr, d(-A clip(r))/dr
+        const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
+        const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
+        // + bound_loss (a2c_continuous.py:209-217)
+        const float bc = c.bounds_loss_coef * invB;
+        const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
+        const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
+        // d nlp / d logstd = 1 - z^2; - entropy_coef * mean(entropy): d entropy / d logstd = 1 per row
+        const float dent = -c.entropy_coef * invB;
+        gs0 = dnlp * (1.f - z0 * z0) + dent;
+        gs1 = dnlp * (1.f - z1 * z1) + dent;
+        la = a_loss;
+        s.g[r * 4 + 0] = dmu0;
+        s.g[r * 4 + 1] = dmu1;
+        s.g[r * 4 + 3] = dnlp;
+      }
+      la = wave_sum(la); gs0 = wave_sum(gs0); gs1 = wave_sum(gs1);
+      if (lane == 0) { s.lsum[w][0] = la; s.lsum[w][1] = gs0; s.lsum[w][2] = gs1; }
+    } else {
+      float lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f;
+      if (rowok) {
+        // critic_loss (common_losses.py:10-19)
+        const float vo = ri.val, R = ri.ret;
+        float dv, c_loss;
+        if (c.clip_value) {
+          const float dvr = v - vo;
+          const float dvc = clampt(dvr, -c.e_clip, c.e_clip);
+          const float vc = vo + dvc;
+          const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
+          c_loss = fmaxf(l1, l2);
+          const float d1 = 2.f * (v - R);
+          const float d2 = 2.f * (vc - R) * ((dvr >= -c.e_clip && dvr <= c.e_clip) ? 1.f : 0.f);
+          dv = (l1 > l2) ? d1 : ((l1 < l2) ? d2 : 0.5f * (d1 + d2));
+        } else {
+          c_loss = (R - v) * (R - v);
+          dv = 2.f * (v - R);
+        }
+        dv *= 0.5f * c.critic_coef * invB;
+        const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
+        const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
+        // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
+        const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
+        const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
+        const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
+        e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
+        e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
+        lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
+        s.g[r * 4 + 2] = dv;
+      }
+      lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
+      if (lane == 0) { s.lsum[w][0] = lc; s.lsum[w][1] = le; s.lsum[w][2] = lb; s.lsum[w][3] = lkl; }
+    }
+  }
+#endif
   __syncthreads();
   USV_PHASE(ppo, 3);
+#if USV_PPO_HL
+  if (tid < 7) {   // the loss sums: the four waves' row sums of each quantity in wave order
+    const int wb = tid < 3 ? 0 : 4, q = tid < 3 ? tid : tid - 3;
+    const float v = ((s.lsum[wb][q] + s.lsum[wb + 1][q]) + s.lsum[wb + 2][q]) + s.lsum[wb + 3][q];
+    const int slot = tid == 0 ? P_LOSS + 0 : tid < 3 ? S_SIG + tid - 1 : P_LOSS + tid - 2;
+    part_st(slot, v);
+  }
+#endif
+#if USV_PPO_BWD2
+  // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 (quarter qq: 8 rows) ----
+  {
+    const int j = tid & (NH - 1), qq = tid >> 7;
+    const float wm0 = s.tail[T_WMU + j], wm1 = s.tail[T_WMU + NH + j], wv = s.tail[T_WV + j];
+    float gw0 = 0.f, gw1 = 0.f, gwv = 0.f, db = 0.f;
+#pragma unroll
+    for (int q = 0; q < RB / 4; ++q) {
+      const int rr = qq * (RB / 4) + q;
+      const float hv = s.h2[rr * HS + j];
+      const float d0 = s.g[rr * 4], d1 = s.g[rr * 4 + 1], dvv = s.g[rr * 4 + 2];
+      gw0 = fmaf(d0, hv, gw0); gw1 = fmaf(d1, hv, gw1); gwv = fmaf(dvv, hv, gwv);
+      const float dz = (d0 * wm0 + d1 * wm1 + dvv * wv) * (1.f - hv * hv);
+      s.h2[rr * HS + j] = dz;
+      db += dz;
+    }
+    s.hg[qq][0][j] = gw0; s.hg[qq][1][j] = gw1; s.hg[qq][2][j] = gwv; s.hg[qq][3][j] = db;
+  }
+  __syncthreads();
+  USV_PHASE(ppo, 4);
+  // ---- the rest of the backward in two concurrent wave groups, no further barrier:
+  //   waves 0-3 (column block cb): dh1 = dz2 W2 over the full K = 128 (one accumulator chain), dz1 = dh1 (1 - h1^2)
+  //     in registers, then dW1[j in cb][k] = sum_r dz1[r][j] x[r][k] straight from those registers (the A operand's
+  //     32 rows are the lane's own accumulator rows), db1 and W1's last column by lane sums;
+  //   waves 4-7 (row block t of dW2): the head-weight / b2 / bmu / bv sums, then dW2[n in t][k] = sum_r dz2[r][n]
+  //     h1[r][k] (4 tiles, each tile's 16-B partial stores spread over the next tile's chain).
+  // Each SIMD's two waves keep its matrix core busy through dz1's VALU and the partial stores; the K-half exchange
+  // and the dz1 barrier of the one-group form are gone ----
+  if (w < 4) {
+    // the critical chain (dh1 -> dz1 -> dW1) first on the matrix core; dW2 fills the gaps
+    if constexpr (USV_BWD_PRIO > 0) __builtin_amdgcn_s_setprio(USV_BWD_PRIO);
+    float dz1[16];
+    {
+      f32x16 dh = {};
+      if constexpr (kBf) {
+#pragma unroll
+        for (int st = 0; st < NH / 16; ++st) {
+          const int j0 = 16 * st + 8 * h;
+          dh = mfma_bf16(ld8(&s.h2[i * HS + j0]), ld8s(&s.w2[j0 * HS + n0 + i], HS), dh);
+        }
+      } else {
+#pragma unroll 16
+        for (int st = 0; st < NH / 2; ++st) {
+          const int j = 2 * st + h;
+          dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + n0 + i], dh);
+        }
+      }
+      USV_PHASE(ppo, 6);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float hv = s.h1[crow(q, h) * HS + n0 + i];
+        dz1[q] = dh[q] * (1.f - hv * hv);
+      }
+    }
+    USV_PHASE(ppo, 7);
+    // dW1[n0 + crow(.., h)][k = i]: step q pairs rows crow(q, 0) (lanes h = 0) and crow(q, 1) (h = 1)
+    f32x16 acc = {};
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc = mfma32(dz1[q], s.x[crow(q, h) * XS + i], acc);
+    float sb = 0.f, sc = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      sb += dz1[q];
+      sc = fmaf(dz1[q], s.x[crow(q, h) * XS + NIN - 1], sc);
+    }
+    sb += __shfl_xor(sb, 32, 64);   // rows of h = 0 + rows of h = 1 (the same sum in both lanes)
+    sc += __shfl_xor(sc, 32, 64);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      part_st.x4(acc_slot(S_W1, cb, a, lane), acc[4 * a], acc[4 * a + 1], acc[4 * a + 2], acc[4 * a + 3]);
+    if (h == 0) {
+      part_st(S_B1 + n0 + i, sb);
+      part_st(S_W1C + n0 + i, sc);
+    }
+  } else {
+    const int t = w - 4, tt = tid - 256;
+    if (tt < NH) {   // head-weight and b2 gradients: quarter sums in a fixed order
+      const int j = tt;
+      part_st(tail_slot(PPO_OFF_WMU + j), ((s.hg[0][0][j] + s.hg[1][0][j]) + s.hg[2][0][j]) + s.hg[3][0][j]);
+      part_st(tail_slot(PPO_OFF_WMU + NH + j), ((s.hg[0][1][j] + s.hg[1][1][j]) + s.hg[2][1][j]) + s.hg[3][1][j]);
+      part_st(tail_slot(PPO_OFF_WV + j), ((s.hg[0][2][j] + s.hg[1][2][j]) + s.hg[2][2][j]) + s.hg[3][2][j]);
+      part_st(tail_slot(PPO_OFF_B2 + j), ((s.hg[0][3][j] + s.hg[1][3][j]) + s.hg[2][3][j]) + s.hg[3][3][j]);
+    } else if (tt < NH + 3) {   // bmu0, bmu1, bv: the row sums of dmu / dv
+      const int q = tt - NH;
+      float sacc = 0.f;
+      for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
+      part_st(tail_slot(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV), sacc);
+    }
+    const int nt0 = 32 * t;
+    f32x16 prev = {};
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      f32x16 d = {};
+      if constexpr (kBf) {
+#pragma unroll
+        for (int st = 0; st < RB / 16; ++st) {
+          const int r0 = 16 * st + 8 * h;
+          d = mfma_bf16(ld8s(&s.h2[r0 * HS + nt0 + i], HS), ld8s(&s.h1[r0 * HS + 32 * kb + i], HS), d);
+          if (kb > 0) {
+#pragma unroll
+            for (int a = 2 * st; a < 2 * st + 2; ++a)
+              part_st.x4(acc_slot(S_W2, 4 * t + kb - 1, a, lane), prev[4 * a], prev[4 * a + 1], prev[4 * a + 2],
+                         prev[4 * a + 3]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int st = 0; st < RB / 2; ++st) {
+          const int r = st + 16 * h;
+          d = mfma32(s.h2[r * HS + nt0 + i], s.h1[r * HS + 32 * kb + i], d);
+          if (kb > 0 && (st & 3) == 1) {
+            const int a = st >> 2;
+            part_st.x4(acc_slot(S_W2, 4 * t + kb - 1, a, lane), prev[4 * a], prev[4 * a + 1], prev[4 * a + 2],
+                       prev[4 * a + 3]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+      prev = d;
+    }
+    USV_PHASE_T(ppo, 13, 256);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      part_st.x4(acc_slot(S_W2, 4 * t + 3, a, lane), prev[4 * a], prev[4 * a + 1], prev[4 * a + 2], prev[4 * a + 3]);
+    USV_PHASE_T(ppo, 5, 256);
+  }
+#else
   // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 (quarter qq: 8 rows) ----
   {
     const int j = tid & (NH - 1), qq = tid >> 7;
@@ -1516,6 +1770,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
       part_st(S_B1 + j, a);
     }
   }
+#endif
   USV_PHASE(ppo, 8);
   if constexpr (kFold) {
     // ---- the group fold (see FOLD_G): arrive once every wave's write-through stores are drained ----

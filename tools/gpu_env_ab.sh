@@ -1,20 +1,36 @@
 #!/bin/bash
-# GPU box: env parity (fixture replays, Philox vs oracle, fields) + bench line + kernel trace/stats and the
-# two PMC passes (FETCH_SIZE, WRITE_SIZE) on k_env_step at 131072 envs.     TAG=r03d bash tools/gpu_env_ab.sh
+# GPU box: env-step A/B of library variants in the sequential step (USV_STEP_OVERLAP=0: k_env_step alone on the
+# GPU): rocprofv3 kernel-trace stats of a short bench per variant (twice, interleaved), plus one FETCH_SIZE pass
+# each.   VARIANTS="base pf0" TAG=r05d bash tools/gpu_env_ab.sh
 set -uo pipefail
 R=$GRAFT_REPO_ROOT
-TAG=${TAG:-r03d}
-O=$R/gpurun_out/$TAG
-mkdir -p $O
-cd $R
-timeout -k 10 900 python3 -u -m pytest ${TESTS:-tests/test_env_gpu.py tests/test_headline_gpu.py} -m gpu -x -q --timeout 300 \
-  --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
-tail -2 $O/pytest_gpu.log
-cp gpurun_out/parity_errors.json $O/ 2>/dev/null
-timeout -k 10 600 python3 bench.py --no-cpu-baseline --steps 10 --milestone-seconds 0 --c2-steps 0 > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-python3 -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['extra'].get('update_us_per_minibatch'),d['extra'].get('rollout_ms'),d['roofline']['frac'],d['roofline']['launch_ms'],d['roofline_ppo']['frac'])"
-bash profiles/run_profiles.sh $TAG 131072 || exit 1
-python3 profiles/pmc_traffic.py $TAG 131072 $O/env_step_traffic_131072.json || exit 1
-cp profiles/${TAG}_* $O/ || exit 1
-cat $O/env_step_traffic_131072.json
-exit 0
+O=$R/gpurun_out/${TAG:-envab}; mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+B="$R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --c2-steps 0 --milestone-seconds 0 --extra-steps 0"
+export USV_STEP_OVERLAP=0
+for rep in 1 2; do
+  for v in $VARIANTS; do
+    lib=""; [ "$v" != "base" ] && lib="$v.so"
+    USV_HIP_LIB=$lib timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$v.$rep -o t -- python3 $B > $O/$v.$rep.log 2>&1 || { tail $O/$v.$rep.log; exit 1; }
+    python3 - "$O/$v.$rep/t_kernel_stats.csv" "$v" "$rep" <<'PY'
+import csv, sys
+for r in csv.DictReader(open(sys.argv[1])):
+    if "k_env_step<" in r["Name"] and "FixedWin<19>" in r["Name"]:
+        print(sys.argv[2], sys.argv[3], "k_env_step calls", r["Calls"], "avg_us %.2f" % (float(r["AverageNs"]) / 1e3))
+PY
+  done
+done
+for v in $VARIANTS; do
+  lib=""; [ "$v" != "base" ] && lib="$v.so"
+  USV_HIP_LIB=$lib timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_env_step --output-format csv -d $O/$v.fetch -o p -- python3 $B > $O/$v.fetch.log 2>&1 || { tail $O/$v.fetch.log; exit 1; }
+  python3 - $O/$v.fetch "$v" <<'PY'
+import csv, glob, sys
+vals = []
+for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
+    for r in csv.DictReader(open(f)):
+        if "FixedWin<19>" in r.get("Kernel_Name", ""):
+            vals.append(float(r["Counter_Value"]))
+if vals:
+    print(sys.argv[2], "FETCH_SIZE per launch (x1024 x2) MB %.1f over %d" % (sum(vals) / len(vals) * 2048 / 1e6, len(vals)))
+PY
+done
