@@ -36,14 +36,19 @@ constexpr int RB = 32;          // rows per block
 constexpr int TB = 256;         // threads per block (4 waves; wave w owns output columns 32w..32w+31)
 constexpr int XS = 35;          // row stride of x / W1 in LDS (k 33, 34 zero; odd: the layer-1 operand
                                 // reads x[i][k] / W1[i][k] of 32 lanes i hit 32 different banks)
-constexpr int HS = 129;         // row stride of h1 / h2 / W2 in LDS (odd: the matrix-core operand reads of
-                                // a column, 32 lanes = 32 rows, hit 32 different banks)
+#ifndef USV_PPO_L2F
+#define USV_PPO_L2F 1   // the gradient kernel's layer 2 on 16 x 16 tiles without a K split (0: 32 x 32, K halves)
+#endif
+// row stride of h1 / h2 / W2 in LDS: a column read by 32 lanes (32 rows, the 32x32 operands) hits 32 banks at
+// both; 130 (= 2 mod 64) also puts the 16x16x4 operand reads (16 rows x 2 k per 32 lanes) on 32 banks
+constexpr int HS = USV_PPO_L2F ? 130 : 129;
 constexpr int NPART = PPO_NPARAM + 8;   // partial row: params + loss sums
 constexpr int NPART_PAD = (NPART + 3) & ~3;   // partial row stride (16-B aligned rows)
 constexpr int P_LOSS = PPO_NPARAM;      // a, c, entropy, b, kl sums
 constexpr float kLog2Pi = 1.8378770664093453f;  // 0.5*log(2*pi)*2 (models.py:400)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
@@ -1010,18 +1015,30 @@ struct RowIn {
 #ifndef USV_PART_AUX
 #define USV_PART_AUX 2   // cache-policy bits of the partial stores: nt (A/B builds override it)
 #endif
-template <int kAux>
+// Partial layout.  Row-major (kCM false; the group fold's): row b = [NPART_PAD] at b NPART_PAD.  Chunk-major
+// (USV_PART_CM, the default otherwise): the reduction's chunks of RD_P slots are the outer index, [chunk][nblk][RD_P],
+// so each reduction workgroup reads one contiguous nblk x RD_P block (128 KB at 8192 rows) instead of 256
+// segments 85 KB apart; a gradient workgroup writes its row as RED_BLOCKS segments of 512 B.
+template <int kAux, bool kCM>
 struct PartOutT {
   __amdgpu_buffer_rsrc_t r;
+  uint32_t cs;   // chunk-major: bytes from one chunk of a row to the next (nblk RD_P 4)
+  __device__ __forceinline__ uint32_t off(int idx) const {
+    if constexpr (kCM) return (uint32_t)(idx / RD_P) * cs + (uint32_t)(idx % RD_P) * 4u;
+    else return (uint32_t)idx * 4u;
+  }
   __device__ __forceinline__ void operator()(int idx, float v) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (uint32_t)idx * 4u, 0, kAux);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, off(idx), 0, kAux);
   }
   __device__ __forceinline__ void x4(int idx, float a, float b, float c, float d) const {
     const u32x4_t v = {__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b), __builtin_bit_cast(uint32_t, c),
                        __builtin_bit_cast(uint32_t, d)};
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, (uint32_t)idx * 4u, 0, kAux);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off(idx), 0, kAux);   // idx % 4 == 0: inside one chunk
   }
 };
+#ifndef USV_PART_CM
+#define USV_PART_CM 1
+#endif
 constexpr int AUX_SC1 = 16;   // sc1: write-through (the in-launch group fold reads the rows from another CU)
 
 // ---- The XCD-group fold of the partial rows (kFold launches of k_mb_grad; k_reduce_partials(fold = 1)) ----
@@ -1250,6 +1267,40 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // finishes sit in accumulator registers 0-7 and the rows it hands over in 8-15: every register
   // index is a constant (no per-wave select, no dynamic register indexing) ----
   const int ra = (i + 16 * kh) & (RB - 1);
+#if USV_PPO_L2F
+  // ---- layer 2 on 16 x 16 tiles, no K split: wave w owns output columns 16 w .. 16 w + 15 of both 16-row
+  // blocks (two accumulators) over the full K = 128, so its tanh epilogue needs no exchange and no barrier
+  // before it.  16x16x4 f32: lane l supplies A[row l & 15][k = 4 st + (l >> 4)] and B[k][col l & 15] and holds
+  // C[row 4 (l >> 4) + v][col l & 15]; the bf16 mode's 16x16x32 takes 8 consecutive k per lane ----
+  {
+    const int il = lane & 15, kq = lane >> 4, nc = 16 * w + il;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+    if constexpr (kBf) {
+#pragma unroll
+      for (int st = 0; st < NH / 32; ++st) {
+        const int k0 = 32 * st + 8 * kq;
+        const bf16x8 bv = ld8(&s.w2[nc * HS + k0]);
+        a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld8(&s.h1[il * HS + k0]), bv, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld8(&s.h1[(16 + il) * HS + k0]), bv, a1, 0, 0, 0);
+      }
+    } else {
+#pragma unroll 16
+      for (int st = 0; st < NH / 4; ++st) {
+        const int k = 4 * st + kq;
+        const float bv = s.w2[nc * HS + k];
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.h1[il * HS + k], bv, a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.h1[(16 + il) * HS + k], bv, a1, 0, 0, 0);
+      }
+    }
+    USV_PHASE(ppo, 11);
+    const float bj = s.tail[T_B2 + nc];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      s.h2[(4 * kq + v) * HS + nc] = fast_tanh(a0[v] + bj);
+      s.h2[(16 + 4 * kq + v) * HS + nc] = fast_tanh(a1[v] + bj);
+    }
+  }
+#else
   {
     f32x16 acc = {};
     if constexpr (kBf) {
@@ -1276,10 +1327,15 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     for (int q = 0; q < 8; ++q)
       s.h2[(crow(q, h) + 16 * kh) * HS + n0 + i] = fast_tanh((acc[q] + s.xch[cb][8 - 8 * kh + q][lane]) + bj);
   }
+#endif
   __syncthreads();
   USV_PHASE(ppo, 12);
-  const PartOutT<kFold ? AUX_SC1 : USV_PART_AUX> part_st{
-      __builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4, 0x00020000)};
+  constexpr bool kCM = USV_PART_CM != 0 && !kFold;
+  const PartOutT<kFold ? AUX_SC1 : USV_PART_AUX, kCM> part_st{
+      kCM ? __builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * RD_P, 0,
+                                              (int)(((size_t)RED_BLOCKS * gridDim.x - blockIdx.x) * RD_P * 4), 0x00020000)
+          : __builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4, 0x00020000),
+      (uint32_t)gridDim.x * RD_P * 4u};
 #if !USV_PPO_HL
   // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (16 threads per row, k = part + 16 kk: the 16
   // threads of a row read 16 consecutive words -- no 4-way LDS bank conflicts) ----
@@ -2049,7 +2105,9 @@ __global__ __launch_bounds__(RD_TB) void k_reduce_partials(const float *__restri
     float4 x[RD_KB];
 #pragma unroll
     for (int k = 0; k < RD_KB; ++k) {
-      const float4 *src = P4 + (size_t)min(b0 + RD_G * k, nblk - 1) * (NPART_PAD / 4) + p4c;
+      const int row = min(b0 + RD_G * k, nblk - 1);
+      const float4 *src = USV_PART_CM ? P4 + ((size_t)blockIdx.x * nblk + row) * RD_L + col
+                                      : P4 + (size_t)row * (NPART_PAD / 4) + p4c;
 #if USV_RD_NT
       const f32x4v v = __builtin_nontemporal_load(reinterpret_cast<const f32x4v *>(src));   // read once
       x[k] = make_float4(v[0], v[1], v[2], v[3]);
@@ -2478,7 +2536,13 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
 }
 
 // per-workgroup rows, the fold's group rows and its control lines (zero-initialised by the caller)
-int ppo_partials_floats(int minibatch) { return (minibatch / RB + FOLD_G) * NPART_PAD + FOLD_G * FOLD_CTL_STRIDE; }
+int ppo_partials_floats(int minibatch) {
+  // the chunk-major rows (RED_BLOCKS x RD_P >= NPART_PAD floats per row) must stay below the fold control words
+  static_assert(RED_BLOCKS * RD_P >= NPART_PAD, "chunk-major rows cover a partial row");
+  const int nblk = minibatch / RB;
+  if ((long long)nblk * RED_BLOCKS * RD_P > (long long)(nblk + FOLD_G) * NPART_PAD) return -1;
+  return (nblk + FOLD_G) * NPART_PAD + FOLD_G * FOLD_CTL_STRIDE;
+}
 int ppo_grad_floats(void) { return PPO_NPARAM + 8 + RED_BLOCKS; }
 int ppo_meter_floats(int n_envs, int horizon) {
   return horizon * 4 + horizon * ((n_envs + kStoreTB - 1) / kStoreTB) * 4;
