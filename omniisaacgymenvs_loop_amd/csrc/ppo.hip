@@ -946,11 +946,17 @@ struct ChainIn {
 
 // x rows of the gradient kernel padded to whole staging passes: every thread stores its slots
 // unconditionally (see the obs staging in mb_grad8w)
-constexpr int GX = ((RB * XS + GTB - 1) / GTB) * GTB;
+#ifndef USV_PPO_L1F
+#define USV_PPO_L1F 1   // the gradient kernel's layer 1 on 16 x 16 tiles over all 8 waves (0: 32 x 32 on waves 0-3)
+#endif
+// row stride of x / W1 in the gradient kernel's LDS: 36 (K padded to 36 for the 16x16x4 layer 1, = 4 mod 64: the
+// 16 rows x 2 k of 32 lanes hit 32 banks); 35 with the 32x32 layer 1 (odd: its 32-row operand reads hit 32 banks)
+constexpr int XG = USV_PPO_L1F ? 36 : XS;
+constexpr int GX = ((RB * XG + GTB - 1) / GTB) * GTB;
 struct GradSmem {
   float w2[NH * HS];              // W2[j][k]
-  float w1[NH * XS];              // W1[j][k], k 33, 34 = 0
-  float x[GX];                    // normalised obs (dW1 operand); [RB * XS, GX) staging overflow slots
+  float w1[NH * XG];              // W1[j][k], k 33, 34 = 0
+  float x[GX];                    // normalised obs (dW1 operand); [RB * XG, GX) staging overflow slots
   float h1[RB * HS];              // tanh layer 1, later dz1
   float h2[RB * HS];              // tanh layer 2, later dz2
   float xch[4][16][64];           // upper-K partial accumulators of layer 2 / dh1 (per wave, register, lane)
@@ -1039,6 +1045,9 @@ struct PartOutT {
 #ifndef USV_PART_CM
 #define USV_PART_CM 1
 #endif
+#ifndef USV_STAGE16
+#define USV_STAGE16 1   // the gradient kernel stages W2 with 16-byte loads (0: 4-byte loads, 32 per thread)
+#endif
 constexpr int AUX_SC1 = 16;   // sc1: write-through (the in-launch group fold reads the rows from another CU)
 
 // ---- The XCD-group fold of the partial rows (kFold launches of k_mb_grad; k_reduce_partials(fold = 1)) ----
@@ -1093,7 +1102,7 @@ __device__ __forceinline__ void redo_step(const ppo_cfg_t &c, const ChainIn &ch,
       s.b1[q - PPO_OFF_B1] = pn;
     } else if (q >= PPO_OFF_W1) {
       const int e = q - PPO_OFF_W1;
-      s.w1[(e / NIN) * XS + e % NIN] = pn;
+      s.w1[(e / NIN) * XG + e % NIN] = pn;
     }
   }
   float pn, mn, vn;
@@ -1127,9 +1136,13 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // ---- every global load issued up front (compile-time trip counts) ----
   // W2 element tid + u GTB per thread (4-byte loads): each wave's LDS commit is 64 consecutive words
   // of one row, conflict-free at the odd row stride (16-byte loads would leave 4-word strided writes)
-  constexpr int NW1G = (NH * XS + GTB - 1) / GTB, NTLG = (TAIL + GTB - 1) / GTB, NW2F = NH * NH / GTB;
+  constexpr int NW1G = (NH * XG + GTB - 1) / GTB, NTLG = (TAIL + GTB - 1) / GTB, NW2F = NH * NH / GTB;
   static_assert(NH * NH % GTB == 0, "staging trip counts");
+#if !USV_STAGE16
   float w2f[NW2F];
+#else
+  constexpr int NW2Q = (NH * NH + 2 + 3) / 4, NW2V = (NW2Q + GTB - 1) / GTB;   // float4s covering W2 (+2), per thread
+#endif
   float w1r[NW1G], tlr[NTLG];
   // chained update: minibatch k-1's optimiser scalars (lanes 0-7) and KL (lane 8) as VECTOR loads,
   // the first in flight -- scalar loads here would share lgkmcnt with the LDS staging writes and
@@ -1142,7 +1155,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   {
 #pragma unroll
     for (int u = 0; u < NW1G; ++u) {
-      const int q = min(tid + u * GTB, NH * XS - 1), j = q / XS, k = q % XS;
+      const int q = min(tid + u * GTB, NH * XG - 1), j = q / XG, k = q % XG;
       w1r[u] = P[PPO_OFF_W1 + j * NIN + min(k, NIN - 1)];
     }
 #pragma unroll
@@ -1170,24 +1183,34 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     ri.sg0 = row_ld(&e_sigma[row * 2]); ri.sg1 = row_ld(&e_sigma[row * 2 + 1]);
   }
   // obs rows and the running statistics (always loaded; obs_rms is non-null, checked on the host)
-  constexpr int NU = (RB * XS + GTB - 1) / GTB;
+  constexpr int NU = (RB * XG + GTB - 1) / GTB;
   float xo[NU];
   double mu[NU], var[NU];
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
-    const int q = min(tid + u * GTB, RB * XS - 1), r = q / XS, kc = min(q % XS, NIN - 1);
+    const int q = min(tid + u * GTB, RB * XG - 1), r = q / XG, kc = min(q % XG, NIN - 1);
     xo[u] = row_ld(&e_obs[(size_t)(rb0 + r) * NIN + kc]);
     mu[u] = obs_rms[kc];
     var[u] = obs_rms[NIN + kc];
   }
   // W2 (64 KB of the 85 KB) issued LAST: the staging of x / W1 / biases and layer 1 wait only for the
   // loads ahead of it (counted vmcnt waits), W2 lands during layer 1 and is committed after it
+#if !USV_STAGE16
 #pragma unroll
   for (int u = 0; u < NW2F; ++u) w2f[u] = P[PPO_OFF_W2 + tid + u * GTB];
+#else
+  // W2 as 16-byte loads from the 16-B aligned float index W2A = PPO_OFF_W2 - 2 (P is 16-B aligned, checked on
+  // the host): float4 f holds W2 elements 4 f - 2 .. 4 f + 1; 9 loads per thread instead of 32
+  static_assert((PPO_OFF_W2 - 2) % 4 == 0, "W2 staging alignment");
+  float4 w2v[NW2V];
+#pragma unroll
+  for (int u = 0; u < NW2V; ++u)
+    w2v[u] = reinterpret_cast<const float4 *>(P + PPO_OFF_W2 - 2)[min(tid + u * GTB, NW2Q - 1)];
+#endif
   __builtin_amdgcn_sched_barrier(0);   // every load above is issued before anything waits
 #pragma unroll
   for (int u = 0; u < NW1G; ++u)
-    if ((tid + u * GTB) % XS >= NIN) w1r[u] = 0.f;
+    if ((tid + u * GTB) % XG >= NIN) w1r[u] = 0.f;
   if (kChain && tid >= RED_BLOCKS) csq = 0.f;
   {   // obs rows, normalised on the way into LDS: every value formed unconditionally and selected, so no
       // load is sunk into a branch (a load issued there would come after W2's and wait for all of them)
@@ -1195,15 +1218,15 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int q = tid + u * GTB;
-      const int k = q % XS;
+      const int k = q % XG;
       const float xn = rms_norm(xo[u], mu[u], var[u], c.rms_eps);
-      const float xv = (k < NIN && q < RB * XS) ? (norm ? xn : xo[u]) : 0.f;
-      s.x[q] = xv;   // q < GX: the slots past RB * XS are never read
+      const float xv = (k < NIN && q < RB * XG) ? (norm ? xn : xo[u]) : 0.f;
+      s.x[q] = xv;   // q < GX: the slots past RB * XG are never read
     }
   }
 #pragma unroll
   for (int u = 0; u < NW1G; ++u)
-    if (tid + u * GTB < NH * XS) s.w1[tid + u * GTB] = w1r[u];
+    if (tid + u * GTB < NH * XG) s.w1[tid + u * GTB] = w1r[u];
 #pragma unroll
   for (int u = 0; u < NTLG; ++u)
     if (tid + u * GTB < TAIL) s.tail[tid + u * GTB] = tlr[u];
@@ -1239,26 +1262,61 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     }
   }
   USV_PHASE(ppo, 1);
+#if USV_PPO_L1F
+  {
+    // ---- layer 1 on 16 x 16 tiles: wave w owns columns 16 w .. 16 w + 15 of both 16-row blocks, K = 36 (33 .. 35
+    // zero); the tanh epilogue is spread over all 8 waves (8 values per lane) ----
+    const int il = lane & 15, kq = lane >> 4, nc = 16 * w + il;
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+#pragma unroll
+    for (int st = 0; st < XG / 4; ++st) {
+      const int k = 4 * st + kq;
+      const float bv = s.w1[nc * XG + k];
+      a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.x[il * XG + k], bv, a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.x[(16 + il) * XG + k], bv, a1, 0, 0, 0);
+    }
+    const float bj = s.b1[nc];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      s.h1[(4 * kq + v) * HS + nc] = fast_tanh(a0[v] + bj);
+      s.h1[(16 + 4 * kq + v) * HS + nc] = fast_tanh(a1[v] + bj);
+    }
+  }
+#else
   if (kh == 0) {
     // ---- layer 1 (waves 0-3): h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero) ----
     f32x16 acc = {};
 #pragma unroll
     for (int st = 0; st < 17; ++st) {
       const int k = 2 * st + h;
-      acc = mfma32(s.x[i * XS + k], s.w1[(n0 + i) * XS + k], acc);
+      acc = mfma32(s.x[i * XG + k], s.w1[(n0 + i) * XG + k], acc);
     }
     const float bj = s.b1[n0 + i];
 #pragma unroll
     for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
   }
+#endif
   USV_PHASE(ppo, 9);
   // W2 into LDS (waves 4-7 do it while 0-3 run layer 1; each thread commits its own loads)
   if (!slow) {
+#if !USV_STAGE16
 #pragma unroll
     for (int u = 0; u < NW2F; ++u) {
       const int e = tid + u * GTB;
       s.w2[(e >> 7) * HS + (e & (NH - 1))] = w2f[u];
     }
+#else
+#pragma unroll
+    for (int u = 0; u < NW2V; ++u) {
+      const int f = tid + u * GTB;
+      const float v4[4] = {w2v[u].x, w2v[u].y, w2v[u].z, w2v[u].w};
+#pragma unroll
+      for (int c4 = 0; c4 < 4; ++c4) {
+        const int e = 4 * f + c4 - 2;
+        if (f < NW2Q && e >= 0 && e < NH * NH) s.w2[(e >> 7) * HS + (e & (NH - 1))] = v4[c4];
+      }
+    }
+#endif
   }
   __syncthreads();
   USV_PHASE(ppo, 10);
@@ -1622,12 +1680,12 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     // dW1[n0 + crow(.., h)][k = i]: step q pairs rows crow(q, 0) (lanes h = 0) and crow(q, 1) (h = 1)
     f32x16 acc = {};
 #pragma unroll
-    for (int q = 0; q < 16; ++q) acc = mfma32(dz1[q], s.x[crow(q, h) * XS + i], acc);
+    for (int q = 0; q < 16; ++q) acc = mfma32(dz1[q], s.x[crow(q, h) * XG + i], acc);
     float sb = 0.f, sc = 0.f;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       sb += dz1[q];
-      sc = fmaf(dz1[q], s.x[crow(q, h) * XS + NIN - 1], sc);
+      sc = fmaf(dz1[q], s.x[crow(q, h) * XG + NIN - 1], sc);
     }
     sb += __shfl_xor(sb, 32, 64);   // rows of h = 0 + rows of h = 1 (the same sum in both lanes)
     sc += __shfl_xor(sc, 32, 64);
@@ -1807,7 +1865,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
 #pragma unroll
     for (int st = 0; st < RB / 2; ++st) {
       const int r = st + (RB / 2) * h;
-      acc = mfma32(s.h1[r * HS + n0 + i], s.x[r * XS + i], acc);
+      acc = mfma32(s.h1[r * HS + n0 + i], s.x[r * XG + i], acc);
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -1817,7 +1875,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     if (t < NH) {
       const int j = t;
       float a = 0.f;
-      for (int r = 0; r < RB; ++r) a = fmaf(s.h1[r * HS + j], s.x[r * XS + NIN - 1], a);
+      for (int r = 0; r < RB; ++r) a = fmaf(s.h1[r * HS + j], s.x[r * XG + NIN - 1], a);
       part_st(S_W1C + j, a);
     } else {
       const int j = t - NH;
