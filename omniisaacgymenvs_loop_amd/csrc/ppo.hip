@@ -832,7 +832,11 @@ constexpr int GTB = 512;          // threads per workgroup
 #define USV_PPO_BWD2 1
 #endif
 #ifndef USV_PPO_HL
-#define USV_PPO_HL 1     // heads and losses in one phase (0: heads, barrier, losses on two waves; A/B builds)
+#define USV_PPO_HL 0     // 1: heads and losses in one phase (actor rows on waves 0-3, critic on 4-7); measured +0.4 us
+                         // in the phase probe against heads, barrier, losses on two waves
+#endif
+#ifndef USV_BWD_SYNC
+#define USV_BWD_SYNC 1   // dh1 alone on the matrix core, then dW2 beside dz1 -> dW1 (0: dh1 and dW2 concurrently)
 #endif
 #ifndef USV_BWD_PRIO
 #define USV_BWD_PRIO 1   // s_setprio of the dh1 -> dz1 -> dW1 waves in the two-group backward (A/B builds override it)
@@ -947,7 +951,7 @@ struct ChainIn {
 // x rows of the gradient kernel padded to whole staging passes: every thread stores its slots
 // unconditionally (see the obs staging in mb_grad8w)
 #ifndef USV_PPO_L1F
-#define USV_PPO_L1F 1   // the gradient kernel's layer 1 on 16 x 16 tiles over all 8 waves (0: 32 x 32 on waves 0-3)
+#define USV_PPO_L1F 0   // 1: the gradient kernel's layer 1 on 16 x 16 tiles over all 8 waves (measured neutral); 0: 32 x 32 on waves 0-3
 #endif
 // row stride of x / W1 in the gradient kernel's LDS: 36 (K padded to 36 for the 16x16x4 layer 1, = 4 mod 64: the
 // 16 rows x 2 k of 32 lanes hit 32 banks); 35 with the 32x32 layer 1 (odd: its 32-row operand reads hit 32 banks)
@@ -1046,7 +1050,8 @@ struct PartOutT {
 #define USV_PART_CM 1
 #endif
 #ifndef USV_STAGE16
-#define USV_STAGE16 1   // the gradient kernel stages W2 with 16-byte loads (0: 4-byte loads, 32 per thread)
+#define USV_STAGE16 0   // 1: the gradient kernel stages W2 with 16-byte loads (9 per thread instead of 32): measured
+                        // +0.5 us per minibatch (the W2 commit's scattered LDS writes), off
 #endif
 constexpr int AUX_SC1 = 16;   // sc1: write-through (the in-launch group fold reads the rows from another CU)
 
@@ -1650,31 +1655,49 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   //     h1[r][k] (4 tiles, each tile's 16-B partial stores spread over the next tile's chain).
   // Each SIMD's two waves keep its matrix core busy through dz1's VALU and the partial stores; the K-half exchange
   // and the dz1 barrier of the one-group form are gone ----
+  // dh1 = dz2 W2 on waves 0-3 over the full K = 128 (one accumulator chain per wave) with the matrix core to
+  // itself (USV_BWD_SYNC: waves 4-7 store the head gradients and wait at a barrier; sharing the core with dW2
+  // doubles the chain's time and leaves dz1 -> dW1 alone on it at the end), then dW2 on waves 4-7 beside
+  // dz1 -> dW1 on waves 0-3
+  f32x16 dh = {};
   if (w < 4) {
-    // the critical chain (dh1 -> dz1 -> dW1) first on the matrix core; dW2 fills the gaps
     if constexpr (USV_BWD_PRIO > 0) __builtin_amdgcn_s_setprio(USV_BWD_PRIO);
-    float dz1[16];
-    {
-      f32x16 dh = {};
-      if constexpr (kBf) {
+    if constexpr (kBf) {
 #pragma unroll
-        for (int st = 0; st < NH / 16; ++st) {
-          const int j0 = 16 * st + 8 * h;
-          dh = mfma_bf16(ld8(&s.h2[i * HS + j0]), ld8s(&s.w2[j0 * HS + n0 + i], HS), dh);
-        }
-      } else {
+      for (int st = 0; st < NH / 16; ++st) {
+        const int j0 = 16 * st + 8 * h;
+        dh = mfma_bf16(ld8(&s.h2[i * HS + j0]), ld8s(&s.w2[j0 * HS + n0 + i], HS), dh);
+      }
+    } else {
 #pragma unroll 16
-        for (int st = 0; st < NH / 2; ++st) {
-          const int j = 2 * st + h;
-          dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + n0 + i], dh);
-        }
+      for (int st = 0; st < NH / 2; ++st) {
+        const int j = 2 * st + h;
+        dh = mfma32(s.h2[i * HS + j], s.w2[j * HS + n0 + i], dh);
       }
-      USV_PHASE(ppo, 6);
+    }
+    USV_PHASE(ppo, 6);
+  } else {
+    const int tt = tid - 256;
+    if (tt < NH) {   // head-weight and b2 gradients: quarter sums in a fixed order
+      const int j = tt;
+      part_st(tail_slot(PPO_OFF_WMU + j), ((s.hg[0][0][j] + s.hg[1][0][j]) + s.hg[2][0][j]) + s.hg[3][0][j]);
+      part_st(tail_slot(PPO_OFF_WMU + NH + j), ((s.hg[0][1][j] + s.hg[1][1][j]) + s.hg[2][1][j]) + s.hg[3][1][j]);
+      part_st(tail_slot(PPO_OFF_WV + j), ((s.hg[0][2][j] + s.hg[1][2][j]) + s.hg[2][2][j]) + s.hg[3][2][j]);
+      part_st(tail_slot(PPO_OFF_B2 + j), ((s.hg[0][3][j] + s.hg[1][3][j]) + s.hg[2][3][j]) + s.hg[3][3][j]);
+    } else if (tt < NH + 3) {   // bmu0, bmu1, bv: the row sums of dmu / dv
+      const int q = tt - NH;
+      float sacc = 0.f;
+      for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
+      part_st(tail_slot(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV), sacc);
+    }
+  }
+  if constexpr (USV_BWD_SYNC != 0) __syncthreads();
+  if (w < 4) {
+    float dz1[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const float hv = s.h1[crow(q, h) * HS + n0 + i];
-        dz1[q] = dh[q] * (1.f - hv * hv);
-      }
+    for (int q = 0; q < 16; ++q) {
+      const float hv = s.h1[crow(q, h) * HS + n0 + i];
+      dz1[q] = dh[q] * (1.f - hv * hv);
     }
     USV_PHASE(ppo, 7);
     // dW1[n0 + crow(.., h)][k = i]: step q pairs rows crow(q, 0) (lanes h = 0) and crow(q, 1) (h = 1)
@@ -1697,19 +1720,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
       part_st(S_W1C + n0 + i, sc);
     }
   } else {
-    const int t = w - 4, tt = tid - 256;
-    if (tt < NH) {   // head-weight and b2 gradients: quarter sums in a fixed order
-      const int j = tt;
-      part_st(tail_slot(PPO_OFF_WMU + j), ((s.hg[0][0][j] + s.hg[1][0][j]) + s.hg[2][0][j]) + s.hg[3][0][j]);
-      part_st(tail_slot(PPO_OFF_WMU + NH + j), ((s.hg[0][1][j] + s.hg[1][1][j]) + s.hg[2][1][j]) + s.hg[3][1][j]);
-      part_st(tail_slot(PPO_OFF_WV + j), ((s.hg[0][2][j] + s.hg[1][2][j]) + s.hg[2][2][j]) + s.hg[3][2][j]);
-      part_st(tail_slot(PPO_OFF_B2 + j), ((s.hg[0][3][j] + s.hg[1][3][j]) + s.hg[2][3][j]) + s.hg[3][3][j]);
-    } else if (tt < NH + 3) {   // bmu0, bmu1, bv: the row sums of dmu / dv
-      const int q = tt - NH;
-      float sacc = 0.f;
-      for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
-      part_st(tail_slot(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV), sacc);
-    }
+    const int t = w - 4;
     const int nt0 = 32 * t;
     f32x16 prev = {};
 #pragma unroll

@@ -728,8 +728,12 @@ __device__ __forceinline__ StepCfg step_cfg_reload() {
 #endif
 }
 
+// USV_FIELD_PREFETCH: 1 = the env's field constants in the first load burst; 2 = also a load of the texel rows
+// at the pre-step position before the substeps (measured: 28.6 vs 26.7 us per launch and FETCH 86 vs 77 MB at
+// 131,072 envs -- the lines it pulls are often not the ones the sample at the integrated position reads);
+// 0 = the constants with the texels after the substeps
 #ifndef USV_FIELD_PREFETCH
-#define USV_FIELD_PREFETCH 1
+#define USV_FIELD_PREFETCH 0
 #endif
 template <bool kStats, bool kInj, bool kDist, class Win>
 __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, Win w,
@@ -905,7 +909,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     // lines land during the substeps; the boat moves about one cell per control step, so the sample at the
     // integrated position mostly reads the same lines, from L2, instead of a second HBM round trip)
     float pf0 = 0.f, pf1 = 0.f;
-    if constexpr (USV_FIELD_PREFETCH != 0) {
+    if constexpr (USV_FIELD_PREFETCH >= 2) {
       const float *Fe = b.field + (size_t)ec * USV_FIELD_STRIDE;
       pf0 = Fe[field_nw_idx(c.map_size, px, py, 0)];
       pf1 = Fe[field_nw_idx(c.map_size, px, py, 1)];
@@ -975,7 +979,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     FieldTaps taps;
     if constexpr (USV_FIELD_PREFETCH != 0) {
       taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, fn0, fn1, c.map_size, pxn, pyn);
-      __asm__ volatile("" ::"v"(pf0), "v"(pf1));   // the prefetch's registers stay allocated until it landed
+      if constexpr (USV_FIELD_PREFETCH >= 2)
+        __asm__ volatile("" ::"v"(pf0), "v"(pf1));   // the prefetch's registers stay allocated until it landed
     } else {
       taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, FNe, c.map_size, pxn, pyn);
     }
