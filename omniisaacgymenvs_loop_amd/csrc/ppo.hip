@@ -36,19 +36,14 @@ constexpr int RB = 32;          // rows per block
 constexpr int TB = 256;         // threads per block (4 waves; wave w owns output columns 32w..32w+31)
 constexpr int XS = 35;          // row stride of x / W1 in LDS (k 33, 34 zero; odd: the layer-1 operand
                                 // reads x[i][k] / W1[i][k] of 32 lanes i hit 32 different banks)
-#ifndef USV_PPO_L2F
-#define USV_PPO_L2F 1   // the gradient kernel's layer 2 on 16 x 16 tiles without a K split (0: 32 x 32, K halves)
-#endif
-// row stride of h1 / h2 / W2 in LDS: a column read by 32 lanes (32 rows, the 32x32 operands) hits 32 banks at
-// both; 130 (= 2 mod 64) also puts the 16x16x4 operand reads (16 rows x 2 k per 32 lanes) on 32 banks
-constexpr int HS = USV_PPO_L2F ? 130 : 129;
+constexpr int HS = 129;         // row stride of h1 / h2 / W2 in LDS (odd: the matrix-core operand reads of
+                                // a column, 32 lanes = 32 rows, hit 32 different banks)
 constexpr int NPART = PPO_NPARAM + 8;   // partial row: params + loss sums
 constexpr int NPART_PAD = (NPART + 3) & ~3;   // partial row stride (16-B aligned rows)
 constexpr int P_LOSS = PPO_NPARAM;      // a, c, entropy, b, kl sums
 constexpr float kLog2Pi = 1.8378770664093453f;  // 0.5*log(2*pi)*2 (models.py:400)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
@@ -826,20 +821,12 @@ __global__ __launch_bounds__(RS_TB) void k_obs_rms_seq(ppo_cfg_t c, const double
 // 16 dW2 tiles go two per wave; the row inputs of the losses are loaded with the
 // weights, so nothing in the loss phase waits on memory.
 constexpr int GTB = 512;          // threads per workgroup
-// USV_PPO_BWD2: the backward in two concurrent wave groups without barriers (dh1 -> dz1 -> dW1 on waves 0-3,
-// dW2 + head gradients on waves 4-7, dz2 formed on the fly); 0 = the one-group form (K-half exchanges, A/B builds)
-#ifndef USV_PPO_BWD2
-#define USV_PPO_BWD2 1
-#endif
-#ifndef USV_PPO_HL
-#define USV_PPO_HL 0     // 1: heads and losses in one phase (actor rows on waves 0-3, critic on 4-7); measured +0.4 us
-                         // in the phase probe against heads, barrier, losses on two waves
-#endif
 #ifndef USV_BWD_SYNC
-#define USV_BWD_SYNC 1   // dh1 alone on the matrix core, then dW2 beside dz1 -> dW1 (0: dh1 and dW2 concurrently)
+#define USV_BWD_SYNC 0   // 1: dh1 alone on the matrix core, then dW2 beside dz1 -> dW1: measured +1.1 us per minibatch
+                         // (dW2's 64 KB of partial stores then leave in 1.7 us and meet the write bandwidth)
 #endif
 #ifndef USV_BWD_PRIO
-#define USV_BWD_PRIO 1   // s_setprio of the dh1 -> dz1 -> dW1 waves in the two-group backward (A/B builds override it)
+#define USV_BWD_PRIO 0   // s_setprio of the dh1 -> dz1 -> dW1 waves in the two-group backward (1: measured the same)
 #endif
 
 // k_reduce_partials geometry (RED_BLOCKS chunk squares follow the gradient in grad[])
@@ -950,12 +937,7 @@ struct ChainIn {
 
 // x rows of the gradient kernel padded to whole staging passes: every thread stores its slots
 // unconditionally (see the obs staging in mb_grad8w)
-#ifndef USV_PPO_L1F
-#define USV_PPO_L1F 0   // 1: the gradient kernel's layer 1 on 16 x 16 tiles over all 8 waves (measured neutral); 0: 32 x 32 on waves 0-3
-#endif
-// row stride of x / W1 in the gradient kernel's LDS: 36 (K padded to 36 for the 16x16x4 layer 1, = 4 mod 64: the
-// 16 rows x 2 k of 32 lanes hit 32 banks); 35 with the 32x32 layer 1 (odd: its 32-row operand reads hit 32 banks)
-constexpr int XG = USV_PPO_L1F ? 36 : XS;
+constexpr int XG = XS;          // row stride of x / W1 in the gradient kernel's LDS
 constexpr int GX = ((RB * XG + GTB - 1) / GTB) * GTB;
 struct GradSmem {
   float w2[NH * HS];              // W2[j][k]
@@ -970,7 +952,6 @@ struct GradSmem {
   float b1[NH];
   float tail[TAIL + 1];
   float nrm[4];                   // chained update: wave sums of the chunk squares
-  float lsum[8][4];               // per-wave loss / sigma-gradient row sums (USV_PPO_HL)
   int fold[2];                    // group fold: all members arrived, this launch's generation
 };
 
@@ -1048,10 +1029,6 @@ struct PartOutT {
 };
 #ifndef USV_PART_CM
 #define USV_PART_CM 1
-#endif
-#ifndef USV_STAGE16
-#define USV_STAGE16 0   // 1: the gradient kernel stages W2 with 16-byte loads (9 per thread instead of 32): measured
-                        // +0.5 us per minibatch (the W2 commit's scattered LDS writes), off
 #endif
 constexpr int AUX_SC1 = 16;   // sc1: write-through (the in-launch group fold reads the rows from another CU)
 
@@ -1143,11 +1120,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // of one row, conflict-free at the odd row stride (16-byte loads would leave 4-word strided writes)
   constexpr int NW1G = (NH * XG + GTB - 1) / GTB, NTLG = (TAIL + GTB - 1) / GTB, NW2F = NH * NH / GTB;
   static_assert(NH * NH % GTB == 0, "staging trip counts");
-#if !USV_STAGE16
   float w2f[NW2F];
-#else
-  constexpr int NW2Q = (NH * NH + 2 + 3) / 4, NW2V = (NW2Q + GTB - 1) / GTB;   // float4s covering W2 (+2), per thread
-#endif
   float w1r[NW1G], tlr[NTLG];
   // chained update: minibatch k-1's optimiser scalars (lanes 0-7) and KL (lane 8) as VECTOR loads,
   // the first in flight -- scalar loads here would share lgkmcnt with the LDS staging writes and
@@ -1176,11 +1149,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // per-row loss inputs, lane = row (waves 0 and 1 use them: the actor / the critic side)
   RowIn ri;
   {
-#if USV_PPO_HL
-    const size_t row = (size_t)rb0 + 8 * (w & 3) + (lane >> 3);   // the row this lane's loss terms take
-#else
     const size_t row = (size_t)rb0 + (lane & (RB - 1));
-#endif
     ri.act0 = row_ld(&e_act[row * 2]); ri.act1 = row_ld(&e_act[row * 2 + 1]);
     ri.nlp = row_ld(&e_nlp[row]); ri.adv = row_ld(&e_adv[row]);
     ri.val = row_ld(&e_val[row]); ri.ret = row_ld(&e_ret[row]);
@@ -1200,18 +1169,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
   // W2 (64 KB of the 85 KB) issued LAST: the staging of x / W1 / biases and layer 1 wait only for the
   // loads ahead of it (counted vmcnt waits), W2 lands during layer 1 and is committed after it
-#if !USV_STAGE16
 #pragma unroll
   for (int u = 0; u < NW2F; ++u) w2f[u] = P[PPO_OFF_W2 + tid + u * GTB];
-#else
-  // W2 as 16-byte loads from the 16-B aligned float index W2A = PPO_OFF_W2 - 2 (P is 16-B aligned, checked on
-  // the host): float4 f holds W2 elements 4 f - 2 .. 4 f + 1; 9 loads per thread instead of 32
-  static_assert((PPO_OFF_W2 - 2) % 4 == 0, "W2 staging alignment");
-  float4 w2v[NW2V];
-#pragma unroll
-  for (int u = 0; u < NW2V; ++u)
-    w2v[u] = reinterpret_cast<const float4 *>(P + PPO_OFF_W2 - 2)[min(tid + u * GTB, NW2Q - 1)];
-#endif
   __builtin_amdgcn_sched_barrier(0);   // every load above is issued before anything waits
 #pragma unroll
   for (int u = 0; u < NW1G; ++u)
@@ -1267,27 +1226,6 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     }
   }
   USV_PHASE(ppo, 1);
-#if USV_PPO_L1F
-  {
-    // ---- layer 1 on 16 x 16 tiles: wave w owns columns 16 w .. 16 w + 15 of both 16-row blocks, K = 36 (33 .. 35
-    // zero); the tanh epilogue is spread over all 8 waves (8 values per lane) ----
-    const int il = lane & 15, kq = lane >> 4, nc = 16 * w + il;
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
-#pragma unroll
-    for (int st = 0; st < XG / 4; ++st) {
-      const int k = 4 * st + kq;
-      const float bv = s.w1[nc * XG + k];
-      a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.x[il * XG + k], bv, a0, 0, 0, 0);
-      a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.x[(16 + il) * XG + k], bv, a1, 0, 0, 0);
-    }
-    const float bj = s.b1[nc];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      s.h1[(4 * kq + v) * HS + nc] = fast_tanh(a0[v] + bj);
-      s.h1[(16 + 4 * kq + v) * HS + nc] = fast_tanh(a1[v] + bj);
-    }
-  }
-#else
   if (kh == 0) {
     // ---- layer 1 (waves 0-3): h1 = tanh(x W1^T + b1), K = 34 (k = 33 is zero) ----
     f32x16 acc = {};
@@ -1300,28 +1238,14 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
 #pragma unroll
     for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
   }
-#endif
   USV_PHASE(ppo, 9);
   // W2 into LDS (waves 4-7 do it while 0-3 run layer 1; each thread commits its own loads)
   if (!slow) {
-#if !USV_STAGE16
 #pragma unroll
     for (int u = 0; u < NW2F; ++u) {
       const int e = tid + u * GTB;
       s.w2[(e >> 7) * HS + (e & (NH - 1))] = w2f[u];
     }
-#else
-#pragma unroll
-    for (int u = 0; u < NW2V; ++u) {
-      const int f = tid + u * GTB;
-      const float v4[4] = {w2v[u].x, w2v[u].y, w2v[u].z, w2v[u].w};
-#pragma unroll
-      for (int c4 = 0; c4 < 4; ++c4) {
-        const int e = 4 * f + c4 - 2;
-        if (f < NW2Q && e >= 0 && e < NH * NH) s.w2[(e >> 7) * HS + (e & (NH - 1))] = v4[c4];
-      }
-    }
-#endif
   }
   __syncthreads();
   USV_PHASE(ppo, 10);
@@ -1330,40 +1254,6 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   // finishes sit in accumulator registers 0-7 and the rows it hands over in 8-15: every register
   // index is a constant (no per-wave select, no dynamic register indexing) ----
   const int ra = (i + 16 * kh) & (RB - 1);
-#if USV_PPO_L2F
-  // ---- layer 2 on 16 x 16 tiles, no K split: wave w owns output columns 16 w .. 16 w + 15 of both 16-row
-  // blocks (two accumulators) over the full K = 128, so its tanh epilogue needs no exchange and no barrier
-  // before it.  16x16x4 f32: lane l supplies A[row l & 15][k = 4 st + (l >> 4)] and B[k][col l & 15] and holds
-  // C[row 4 (l >> 4) + v][col l & 15]; the bf16 mode's 16x16x32 takes 8 consecutive k per lane ----
-  {
-    const int il = lane & 15, kq = lane >> 4, nc = 16 * w + il;
-    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
-    if constexpr (kBf) {
-#pragma unroll
-      for (int st = 0; st < NH / 32; ++st) {
-        const int k0 = 32 * st + 8 * kq;
-        const bf16x8 bv = ld8(&s.w2[nc * HS + k0]);
-        a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld8(&s.h1[il * HS + k0]), bv, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ld8(&s.h1[(16 + il) * HS + k0]), bv, a1, 0, 0, 0);
-      }
-    } else {
-#pragma unroll 16
-      for (int st = 0; st < NH / 4; ++st) {
-        const int k = 4 * st + kq;
-        const float bv = s.w2[nc * HS + k];
-        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.h1[il * HS + k], bv, a0, 0, 0, 0);
-        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(s.h1[(16 + il) * HS + k], bv, a1, 0, 0, 0);
-      }
-    }
-    USV_PHASE(ppo, 11);
-    const float bj = s.tail[T_B2 + nc];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      s.h2[(4 * kq + v) * HS + nc] = fast_tanh(a0[v] + bj);
-      s.h2[(16 + 4 * kq + v) * HS + nc] = fast_tanh(a1[v] + bj);
-    }
-  }
-#else
   {
     f32x16 acc = {};
     if constexpr (kBf) {
@@ -1390,7 +1280,6 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     for (int q = 0; q < 8; ++q)
       s.h2[(crow(q, h) + 16 * kh) * HS + n0 + i] = fast_tanh((acc[q] + s.xch[cb][8 - 8 * kh + q][lane]) + bj);
   }
-#endif
   __syncthreads();
   USV_PHASE(ppo, 12);
   constexpr bool kCM = USV_PART_CM != 0 && !kFold;
@@ -1399,7 +1288,6 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
                                               (int)(((size_t)RED_BLOCKS * gridDim.x - blockIdx.x) * RD_P * 4), 0x00020000)
           : __builtin_amdgcn_make_buffer_rsrc(partials + (size_t)blockIdx.x * NPART_PAD, 0, NPART * 4, 0x00020000),
       (uint32_t)gridDim.x * RD_P * 4u};
-#if !USV_PPO_HL
   // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (16 threads per row, k = part + 16 kk: the 16
   // threads of a row read 16 consecutive words -- no 4-way LDS bank conflicts) ----
   {
@@ -1516,118 +1404,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
       }
     }
   }
-#else
-  // ---- heads and per-row losses in one phase: waves 0-3 and waves 4-7 each form the heads of all 32 rows (8
-  // threads per row, k = part + 8 kk), then the actor side (ratio, clipped surrogate, dnlp, dmu, dlogstd) runs on
-  // waves 0-3 and the critic, bound, entropy and KL terms and the mu / sigma write-back on waves 4-7, row
-  // r = 8 (w & 3) + lane / 8 on lane part 0 (the heads-to-losses barrier and the out[] round trip are gone) ----
-  {
-    const int r = 8 * (w & 3) + (lane >> 3), part = lane & 7;
-    float a0 = 0.f, a1 = 0.f, av = 0.f;
-#pragma unroll
-    for (int kk = 0; kk < NH / 8; ++kk) {
-      const int k = part + 8 * kk;
-      const float hv = s.h2[r * HS + k];
-      a0 = fmaf(s.tail[T_WMU + k], hv, a0);
-      a1 = fmaf(s.tail[T_WMU + NH + k], hv, a1);
-      av = fmaf(s.tail[T_WV + k], hv, av);
-    }
-#pragma unroll
-    for (int m = 1; m < 8; m <<= 1) {
-      a0 += __shfl_xor(a0, m, 64);
-      a1 += __shfl_xor(a1, m, 64);
-      av += __shfl_xor(av, m, 64);
-    }
-    USV_PHASE(ppo, 2);
-    const bool rowok = part == 0;
-    const size_t row = (size_t)rb0 + r;
-    const float mu0 = a0 + s.tail[T_BMU], mu1 = a1 + s.tail[T_BMU + 1], v = av + s.tail[T_BV];
-    if (!slow) {
-      lsig0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lsv), 0));
-      lsig1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lsv), 1));
-    }
-    const float ls0 = mu0 * 0.f + lsig0, ls1 = mu1 * 0.f + lsig1;
-    const float sg0 = expf(ls0), sg1 = expf(ls1);
-    const float bh0 = fmaxf(mu0 - 1.1f, 0.f), bl0 = fminf(mu0 + 1.1f, 0.f);
-    const float bh1 = fmaxf(mu1 - 1.1f, 0.f), bl1 = fminf(mu1 + 1.1f, 0.f);
-    if (w < 4) {
-      float la = 0.f, gs0 = 0.f, gs1 = 0.f;
-      if (rowok) {
-        const float z0 = (ri.act0 - mu0) / sg0, z1 = (ri.act1 - mu1) / sg1;
-        const float nlp = 0.5f * (z0 * z0 + z1 * z1) + kLog2Pi + (ls0 + ls1);
-        const float A = ri.adv;
-        // actor_loss (common_losses.py:36-46)
-        const float ratio = expf(ri.nlp - nlp);
-        const float lo = 1.0f - c.e_clip, hi = 1.0f + c.e_clip;
-        const float rc = clampt(ratio, lo, hi);
-        const float s1 = -(A * ratio), s2 = -(A * rc);
-        const float a_loss = fmaxf(s1, s2);
-        const float inr = (ratio >= lo && ratio <= hi) ? 1.f : 0.f;
-        const float g1 = -A, g2 = -A * inr;                // d(-A r)/dr, d(-A clip(r))/dr
-        const float g_r = (s1 > s2) ? g1 : ((s1 < s2) ? g2 : 0.5f * (g1 + g2));
-        const float dnlp = invB * g_r * (-ratio);          // dr/dnlp = -r
-        // + bound_loss (a2c_continuous.py:209-217)
-        const float bc = c.bounds_loss_coef * invB;
-        const float dmu0 = dnlp * (-z0 / sg0) + bc * 2.f * (bh0 + bl0);
-        const float dmu1 = dnlp * (-z1 / sg1) + bc * 2.f * (bh1 + bl1);
-        // d nlp / d logstd = 1 - z^2; - entropy_coef * mean(entropy): d entropy / d logstd = 1 per row
-        const float dent = -c.entropy_coef * invB;
-        gs0 = dnlp * (1.f - z0 * z0) + dent;
-        gs1 = dnlp * (1.f - z1 * z1) + dent;
-        la = a_loss;
-        s.g[r * 4 + 0] = dmu0;
-        s.g[r * 4 + 1] = dmu1;
-        s.g[r * 4 + 3] = dnlp;
-      }
-      la = wave_sum(la); gs0 = wave_sum(gs0); gs1 = wave_sum(gs1);
-      if (lane == 0) { s.lsum[w][0] = la; s.lsum[w][1] = gs0; s.lsum[w][2] = gs1; }
-    } else {
-      float lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f;
-      if (rowok) {
-        // critic_loss (common_losses.py:10-19)
-        const float vo = ri.val, R = ri.ret;
-        float dv, c_loss;
-        if (c.clip_value) {
-          const float dvr = v - vo;
-          const float dvc = clampt(dvr, -c.e_clip, c.e_clip);
-          const float vc = vo + dvc;
-          const float l1 = (v - R) * (v - R), l2 = (vc - R) * (vc - R);
-          c_loss = fmaxf(l1, l2);
-          const float d1 = 2.f * (v - R);
-          const float d2 = 2.f * (vc - R) * ((dvr >= -c.e_clip && dvr <= c.e_clip) ? 1.f : 0.f);
-          dv = (l1 > l2) ? d1 : ((l1 < l2) ? d2 : 0.5f * (d1 + d2));
-        } else {
-          c_loss = (R - v) * (R - v);
-          dv = 2.f * (v - R);
-        }
-        dv *= 0.5f * c.critic_coef * invB;
-        const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
-        const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
-        // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
-        const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
-        const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
-        const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
-        e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
-        e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
-        lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
-        s.g[r * 4 + 2] = dv;
-      }
-      lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
-      if (lane == 0) { s.lsum[w][0] = lc; s.lsum[w][1] = le; s.lsum[w][2] = lb; s.lsum[w][3] = lkl; }
-    }
-  }
-#endif
   __syncthreads();
   USV_PHASE(ppo, 3);
-#if USV_PPO_HL
-  if (tid < 7) {   // the loss sums: the four waves' row sums of each quantity in wave order
-    const int wb = tid < 3 ? 0 : 4, q = tid < 3 ? tid : tid - 3;
-    const float v = ((s.lsum[wb][q] + s.lsum[wb + 1][q]) + s.lsum[wb + 2][q]) + s.lsum[wb + 3][q];
-    const int slot = tid == 0 ? P_LOSS + 0 : tid < 3 ? S_SIG + tid - 1 : P_LOSS + tid - 2;
-    part_st(slot, v);
-  }
-#endif
-#if USV_PPO_BWD2
   // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 (quarter qq: 8 rows) ----
   {
     const int j = tid & (NH - 1), qq = tid >> 7;
@@ -1647,18 +1425,15 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
   __syncthreads();
   USV_PHASE(ppo, 4);
-  // ---- the rest of the backward in two concurrent wave groups, no further barrier:
+  // ---- the rest of the backward in two concurrent wave groups, no further barrier (round 5; the one-group form
+  // before it: K-half exchanges for dh1, a dz1 barrier, dW1 on waves 0-3 after it):
   //   waves 0-3 (column block cb): dh1 = dz2 W2 over the full K = 128 (one accumulator chain), dz1 = dh1 (1 - h1^2)
   //     in registers, then dW1[j in cb][k] = sum_r dz1[r][j] x[r][k] straight from those registers (the A operand's
   //     32 rows are the lane's own accumulator rows), db1 and W1's last column by lane sums;
   //   waves 4-7 (row block t of dW2): the head-weight / b2 / bmu / bv sums, then dW2[n in t][k] = sum_r dz2[r][n]
   //     h1[r][k] (4 tiles, each tile's 16-B partial stores spread over the next tile's chain).
-  // Each SIMD's two waves keep its matrix core busy through dz1's VALU and the partial stores; the K-half exchange
-  // and the dz1 barrier of the one-group form are gone ----
-  // dh1 = dz2 W2 on waves 0-3 over the full K = 128 (one accumulator chain per wave) with the matrix core to
-  // itself (USV_BWD_SYNC: waves 4-7 store the head gradients and wait at a barrier; sharing the core with dW2
-  // doubles the chain's time and leaves dz1 -> dW1 alone on it at the end), then dW2 on waves 4-7 beside
-  // dz1 -> dW1 on waves 0-3
+  // The two groups share each SIMD's matrix core, so dW2's 64 KB of partial stores leave over the whole backward
+  // (USV_BWD_SYNC = 1 runs dh1 alone first and measured slower: the stores then meet the write bandwidth) ----
   f32x16 dh = {};
   if (w < 4) {
     if constexpr (USV_BWD_PRIO > 0) __builtin_amdgcn_s_setprio(USV_BWD_PRIO);
@@ -1722,6 +1497,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   } else {
     const int t = w - 4;
     const int nt0 = 32 * t;
+    {
     f32x16 prev = {};
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
@@ -1759,143 +1535,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     for (int a = 0; a < 4; ++a)
       part_st.x4(acc_slot(S_W2, 4 * t + 3, a, lane), prev[4 * a], prev[4 * a + 1], prev[4 * a + 2], prev[4 * a + 3]);
     USV_PHASE_T(ppo, 5, 256);
-  }
-#else
-  // ---- heads' grads and dz2 = (dmu Wmu + dv Wv) (1 - h2^2), in place over h2 (quarter qq: 8 rows) ----
-  {
-    const int j = tid & (NH - 1), qq = tid >> 7;
-    const float wm0 = s.tail[T_WMU + j], wm1 = s.tail[T_WMU + NH + j], wv = s.tail[T_WV + j];
-    float gw0 = 0.f, gw1 = 0.f, gwv = 0.f, db = 0.f;
-#pragma unroll
-    for (int q = 0; q < RB / 4; ++q) {
-      const int rr = qq * (RB / 4) + q;
-      const float hv = s.h2[rr * HS + j];
-      const float d0 = s.g[rr * 4], d1 = s.g[rr * 4 + 1], dvv = s.g[rr * 4 + 2];
-      gw0 = fmaf(d0, hv, gw0); gw1 = fmaf(d1, hv, gw1); gwv = fmaf(dvv, hv, gwv);
-      const float dz = (d0 * wm0 + d1 * wm1 + dvv * wv) * (1.f - hv * hv);
-      s.h2[rr * HS + j] = dz;
-      db += dz;
-    }
-    s.hg[qq][0][j] = gw0; s.hg[qq][1][j] = gw1; s.hg[qq][2][j] = gwv; s.hg[qq][3][j] = db;
-  }
-  __syncthreads();
-  if (tid < NH) {
-    const int j = tid;
-    part_st(tail_slot(PPO_OFF_WMU + j), ((s.hg[0][0][j] + s.hg[1][0][j]) + s.hg[2][0][j]) + s.hg[3][0][j]);
-    part_st(tail_slot(PPO_OFF_WMU + NH + j), ((s.hg[0][1][j] + s.hg[1][1][j]) + s.hg[2][1][j]) + s.hg[3][1][j]);
-    part_st(tail_slot(PPO_OFF_WV + j), ((s.hg[0][2][j] + s.hg[1][2][j]) + s.hg[2][2][j]) + s.hg[3][2][j]);
-    part_st(tail_slot(PPO_OFF_B2 + j), ((s.hg[0][3][j] + s.hg[1][3][j]) + s.hg[2][3][j]) + s.hg[3][3][j]);
-  } else if (tid < NH + 3) {
-    const int q = tid - NH;
-    float sacc = 0.f;
-    for (int r = 0; r < RB; ++r) sacc += s.g[r * 4 + q];
-    part_st(tail_slot(q < 2 ? PPO_OFF_BMU + q : PPO_OFF_BV), sacc);
-  }
-  USV_PHASE(ppo, 4);
-  // ---- dW2[n][k] = sum_r dz2[r][n] h1[r][k]: wave (kh, cb) owns n block cb, k blocks 2 kh, 2 kh + 1.
-  // The dW2 partial (64 KB per workgroup) is bound by the chip's write bandwidth, so its 16-byte
-  // stores are spread over the matrix-core chains that follow (the k block 2 kh tile's during the
-  // second tile's chain, the second tile's during dh1); sched_barrier keeps them there ----
-  const int tile0 = 4 * cb + 2 * kh;
-  f32x16 dw0 = {}, dw1 = {};
-  if constexpr (kBf) {   // K = the 32 rows: r = 16 st + 8 h + j
-#pragma unroll
-    for (int st = 0; st < RB / 16; ++st) {
-      const int r0 = 16 * st + 8 * h;
-      dw0 = mfma_bf16(ld8s(&s.h2[r0 * HS + n0 + i], HS), ld8s(&s.h1[r0 * HS + 32 * (2 * kh) + i], HS), dw0);
-    }
-#pragma unroll
-    for (int st = 0; st < RB / 16; ++st) {
-      const int r0 = 16 * st + 8 * h;
-      dw1 = mfma_bf16(ld8s(&s.h2[r0 * HS + n0 + i], HS), ld8s(&s.h1[r0 * HS + 32 * (2 * kh + 1) + i], HS), dw1);
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-      part_st.x4(acc_slot(S_W2, tile0, a, lane), dw0[4 * a], dw0[4 * a + 1], dw0[4 * a + 2], dw0[4 * a + 3]);
-  } else {
-#pragma unroll
-    for (int st = 0; st < RB / 2; ++st) {
-      const int r = st + (RB / 2) * h;
-      dw0 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh) + i], dw0);
-    }
-#pragma unroll
-    for (int st = 0; st < RB / 2; ++st) {
-      const int r = st + (RB / 2) * h;
-      dw1 = mfma32(s.h2[r * HS + n0 + i], s.h1[r * HS + 32 * (2 * kh + 1) + i], dw1);
-      if ((st & 3) == 1) {
-        const int a = st >> 2;
-        part_st.x4(acc_slot(S_W2, tile0, a, lane), dw0[4 * a], dw0[4 * a + 1], dw0[4 * a + 2], dw0[4 * a + 3]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
     }
   }
-  USV_PHASE(ppo, 13);
-  USV_PHASE(ppo, 5);
-  // ---- dh1[r][k] = sum_n dz2[r][n] W2[n][k]: wave (kh, cb) owns columns k in block cb, n in half kh
-  // (A-operand rows rotated as in layer 2) ----
-  {
-    f32x16 dh = {};
-    if constexpr (kBf) {
-#pragma unroll
-      for (int st = 0; st < NH / 32; ++st) {
-        const int j0 = 64 * kh + 16 * st + 8 * h;
-        dh = mfma_bf16(ld8(&s.h2[ra * HS + j0]), ld8s(&s.w2[j0 * HS + n0 + i], HS), dh);
-        part_st.x4(acc_slot(S_W2, tile0 + 1, st, lane), dw1[4 * st], dw1[4 * st + 1], dw1[4 * st + 2],
-                   dw1[4 * st + 3]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-#pragma unroll
-      for (int st = 0; st < NH / 4; ++st) {
-        const int j = 64 * kh + 2 * st + h;
-        dh = mfma32(s.h2[ra * HS + j], s.w2[j * HS + n0 + i], dh);
-        if ((st & 3) == 1 && st < 16) {
-          const int a = st >> 2;
-          part_st.x4(acc_slot(S_W2, tile0 + 1, a, lane), dw1[4 * a], dw1[4 * a + 1], dw1[4 * a + 2], dw1[4 * a + 3]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-    }
-    USV_PHASE(ppo, 6);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) s.xch[cb][8 * kh + q][lane] = dh[8 + q];
-    __syncthreads();   // every read of h1 (dW2 operand) is done; the halves are published
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int idx = (crow(q, h) + 16 * kh) * HS + n0 + i;
-      const float hv = s.h1[idx];
-      s.h1[idx] = (dh[q] + s.xch[cb][8 - 8 * kh + q][lane]) * (1.f - hv * hv);   // h1 := dz1
-    }
-  }
-  __syncthreads();
-  USV_PHASE(ppo, 7);
-  // ---- dW1[j][k] = sum_r dz1[r][j] x[r][k]: waves 0-3 on the matrix cores (k < 32); waves 4-7 the
-  // last column (k = 32) and db1 ----
-  if (kh == 0) {
-    f32x16 acc = {};
-#pragma unroll
-    for (int st = 0; st < RB / 2; ++st) {
-      const int r = st + (RB / 2) * h;
-      acc = mfma32(s.h1[r * HS + n0 + i], s.x[r * XG + i], acc);
-    }
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-      part_st.x4(acc_slot(S_W1, cb, a, lane), acc[4 * a], acc[4 * a + 1], acc[4 * a + 2], acc[4 * a + 3]);
-  } else {
-    const int t = tid - 256;
-    if (t < NH) {
-      const int j = t;
-      float a = 0.f;
-      for (int r = 0; r < RB; ++r) a = fmaf(s.h1[r * HS + j], s.x[r * XG + NIN - 1], a);
-      part_st(S_W1C + j, a);
-    } else {
-      const int j = t - NH;
-      float a = 0.f;
-      for (int r = 0; r < RB; ++r) a += s.h1[r * HS + j];
-      part_st(S_B1 + j, a);
-    }
-  }
-#endif
   USV_PHASE(ppo, 8);
   if constexpr (kFold) {
     // ---- the group fold (see FOLD_G): arrive once every wave's write-through stores are drained ----

@@ -458,8 +458,8 @@ struct FieldTaps {
   int i0, i1c, j0, j1c;
   bool i_out, j_out;
 };
-// F: the env's cost tiles, fn0 / fn1: its USV_FNORM constants (loaded by the caller)
-__device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, float4 fn0, float4 fn1,
+// F: the env's cost tiles, FN: its USV_FNORM constants
+__device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, const float *__restrict__ FN,
                                                 float map_size, float x, float y) {
   constexpr int G = USV_GRID;
   const float gx = 2.0f * x / map_size, gy = 2.0f * y / map_size;
@@ -481,25 +481,12 @@ __device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, flo
   t.g_ne = F[field_idx(j0, i1c)];
   t.g_sw = F[field_idx(j1c, i0)];
   t.g_se = F[field_idx(j1c, i1c)];
-  t.fn0 = fn0;
-  t.fn1 = fn1;
+  t.fn0 = reinterpret_cast<const float4 *>(FN)[0];
+  t.fn1 = reinterpret_cast<const float4 *>(FN)[1];
   t.i0 = i0; t.i1c = i1c; t.j0 = j0; t.j1c = j1c;
   t.i_out = i1 >= G;
   t.j_out = j1 >= G;
   return t;
-}
-__device__ __forceinline__ FieldTaps field_taps(const float *__restrict__ F, const float *__restrict__ FN,
-                                                float map_size, float x, float y) {
-  return field_taps(F, reinterpret_cast<const float4 *>(FN)[0], reinterpret_cast<const float4 *>(FN)[1], map_size,
-                    x, y);
-}
-// the texel offset of the NW tap of a position (field_taps' index arithmetic)
-__device__ __forceinline__ int field_nw_idx(float map_size, float x, float y, int drow) {
-  constexpr int G = USV_GRID;
-  const float half = (float)G / 2.0f;
-  const float ix = minf((float)(G - 1), maxf(fmaf(2.0f * x / map_size + 1.f, half, -0.5f), 0.f));
-  const float iy = minf((float)(G - 1), maxf(fmaf(2.0f * y / map_size + 1.f, half, -0.5f), 0.f));
-  return field_idx(min((int)iy + drow, G - 1), (int)ix);
 }
 // the field's grid coordinates from the host-derived (start, end, step) or the override table
 struct GridK {
@@ -728,13 +715,6 @@ __device__ __forceinline__ StepCfg step_cfg_reload() {
 #endif
 }
 
-// USV_FIELD_PREFETCH: 1 = the env's field constants in the first load burst; 2 = also a load of the texel rows
-// at the pre-step position before the substeps (measured: 28.6 vs 26.7 us per launch and FETCH 86 vs 77 MB at
-// 131,072 envs -- the lines it pulls are often not the ones the sample at the integrated position reads);
-// 0 = the constants with the texels after the substeps
-#ifndef USV_FIELD_PREFETCH
-#define USV_FIELD_PREFETCH 0
-#endif
 template <bool kStats, bool kInj, bool kDist, class Win>
 __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, Win w,
                                                      const char *__restrict__ wbase, const float *__restrict__ actions,
@@ -842,14 +822,6 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
 #pragma unroll
       for (int q = 0; q < 25; ++q) sums[q] = bld(R, w.stats + (uint32_t)kSum[q] * w.n4, v4);
     }
-    // the env's field constants (32 B) do not depend on the step: with USV_FIELD_PREFETCH they leave the second
-    // load round trip (the texels at the integrated position) and ride in this burst
-    const float *FNe = b.fnorm + (size_t)ec * USV_FNORM;
-    float4 fn0 = make_float4(0.f, 0.f, 0.f, 0.f), fn1 = fn0;
-    if constexpr (USV_FIELD_PREFETCH != 0) {
-      fn0 = reinterpret_cast<const float4 *>(FNe)[0];
-      fn1 = reinterpret_cast<const float4 *>(FNe)[1];
-    }
     // ---- uniforms of this step (SU_* layout; the second Philox block only when drawn from) ----
     float u[USV_NU_STEP];
     if (kInj) {
@@ -905,16 +877,6 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     const float al = c.thr_alpha, oma = 1.0f - c.thr_alpha;
     const float dt = c.dt;
     const float arm_l = -(c.thr_y - comy), arm_r = c.thr_y + comy;
-    // USV_FIELD_PREFETCH: the two texel rows of the bilinear sample at the pre-step position, loaded now (their
-    // lines land during the substeps; the boat moves about one cell per control step, so the sample at the
-    // integrated position mostly reads the same lines, from L2, instead of a second HBM round trip)
-    float pf0 = 0.f, pf1 = 0.f;
-    if constexpr (USV_FIELD_PREFETCH >= 2) {
-      const float *Fe = b.field + (size_t)ec * USV_FIELD_STRIDE;
-      pf0 = Fe[field_nw_idx(c.map_size, px, py, 0)];
-      pf1 = Fe[field_nw_idx(c.map_size, px, py, 1)];
-      __builtin_amdgcn_sched_barrier(0);
-    }
     for (int s = 0; s < c.substeps; ++s) {
       fl = fl * al + oma * tgt0;                      // ThrusterDynamics.py:133-136
       fr = fr * al + oma * tgt1;
@@ -976,14 +938,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
       pyn = pyn + (u[SU_PX + 1] * K.pos_rng + c.pos_noise_min);
     }
     // the potential sample only needs the position: issue its 4 texel loads now
-    FieldTaps taps;
-    if constexpr (USV_FIELD_PREFETCH != 0) {
-      taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, fn0, fn1, c.map_size, pxn, pyn);
-      if constexpr (USV_FIELD_PREFETCH >= 2)
-        __asm__ volatile("" ::"v"(pf0), "v"(pf1));   // the prefetch's registers stay allocated until it landed
-    } else {
-      taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, FNe, c.map_size, pxn, pyn);
-    }
+    const FieldTaps taps = field_taps(b.field + (size_t)ec * USV_FIELD_STRIDE, b.fnorm + (size_t)ec * USV_FNORM,
+                                      c.map_size, pxn, pyn);
     float vxn = vx, vyn = vy, wzn = wz;
     if (c.vel_noise_on) {
       vxn = vxn + (u[SU_VX] * K.vel_rng + c.vel_noise_min);

@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/variants
 mkdir -p $O
 cd $R
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in $VARIANTS; do
     lib=""; [ "$v" != "base" ] && lib="$v.so"
     USV_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --no-cpu-baseline --c2-steps 0 ${BENCH_ARGS:-} \
