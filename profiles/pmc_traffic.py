@@ -31,8 +31,10 @@ KEEP = ["Dispatch_Id", "Grid_Size", "Kernel_Name", "Workgroup_Size", "LDS_Block_
         "VGPR_Count", "SGPR_Count", "Counter_Name", "Counter_Value"]
 
 
-def trim(src, dst):
-    rows = [r for r in csv.DictReader(open(src)) if "k_env_step" in r["Kernel_Name"]]
+def trim(src, dst, envs=None):
+    # the fused CaptureXY step at this size only (the grid is one thread per env, rounded to whole 256-thread blocks)
+    rows = [r for r in csv.DictReader(open(src)) if "k_env_step" in r["Kernel_Name"] and "task" not in r["Kernel_Name"]
+            and (envs is None or int(r["Grid_Size"]) == (envs + 255) // 256 * 256)]
     with open(dst, "w", newline="") as f:
         w = csv.DictWriter(f, fieldnames=KEEP)
         w.writeheader()
@@ -46,9 +48,9 @@ def main(tag, envs, out_json=None):
     dst = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(src, "trace_kernel_stats.csv"), os.path.join(dst, f"{tag}_kernel_stats.csv"))
     fetch = trim(os.path.join(src, "pmc_fetch_counter_collection.csv"),
-                 os.path.join(dst, f"{tag}_pmc_fetch_k_env_step.csv"))
+                 os.path.join(dst, f"{tag}_pmc_fetch_k_env_step.csv"), envs)
     write = trim(os.path.join(src, "pmc_write_counter_collection.csv"),
-                 os.path.join(dst, f"{tag}_pmc_write_k_env_step.csv"))
+                 os.path.join(dst, f"{tag}_pmc_write_k_env_step.csv"), envs)
     fk = sum(fetch) / len(fetch)
     wk = sum(write) / len(write)
     seq = {}

@@ -13,5 +13,6 @@ bash profiles/run_profiles.sh ${TAG}_131072 131072 || exit $?
 python3 profiles/pmc_traffic.py ${TAG}_131072 131072 || exit $?
 mkdir -p gpurun_out/$TAG
 cp profiles/${TAG}_* profiles/env_step_traffic*.json gpurun_out/$TAG/ || exit $?
+rm -rf gpurun_out/prof_${TAG} gpurun_out/prof_${TAG}_131072   # raw traces: condensed above (the merge-back cap is 64 MiB)
 timeout -k 10 600 python3 bench.py > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || exit $?
 cat gpurun_out/$TAG/bench.json
