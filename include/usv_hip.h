@@ -673,7 +673,9 @@ int ppo_minibatch_fused_dp(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, 
                            const float *exp_adv, float *exp_mu, float *exp_sigma, float *grad, float *losses,
                            float *partials, double *work, float *kl_prev_out, void *stream);
 
-/* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad (16-byte aligned) */
+/* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad (16-byte aligned): one row per
+ * 32-row workgroup, chunk-major ([128-slot chunk][workgroup][128]) for the reduction's contiguous reads, then the
+ * group fold's rows and control words; <= 0 when the chunk-major rows would not fit in front of the fold words */
 int ppo_partials_floats(int minibatch);
 /* size (floats) of the grad buffer of ppo_minibatch_grad / ppo_minibatch_apply */
 int ppo_grad_floats(void);

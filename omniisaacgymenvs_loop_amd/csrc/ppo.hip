@@ -1316,9 +1316,9 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   __syncthreads();
   USV_PHASE(ppo, 2);
   // ---- per-row losses and output gradients (lane = row < RB): wave 0 the actor side (ratio, clipped
-  // surrogate, dnlp, dmu, dlogstd), wave 1 in parallel the critic, bound, entropy and KL terms and the
-  // mu / sigma write-back (the same per-row arithmetic and lane sums as one wave doing both) ----
-  if (tid < 128) {
+  // surrogate, dnlp, dmu, dlogstd), wave 1 in parallel the critic loss and dv, wave 2 the bound, entropy and KL
+  // terms and the mu / sigma write-back (the same per-row arithmetic and lane sums as one wave doing all) ----
+  if (tid < 192) {
     const int r = lane;
     const bool rowok = r < RB;
     const int rr = rowok ? r : 0;
@@ -1366,8 +1366,27 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
         part_st(P_LOSS + 0, la);
         part_st(S_SIG, gs0); part_st(S_SIG + 1, gs1);
       }
+    } else if (w == 2) {
+      // the KL, entropy and bound terms and the mu / sigma write-back on a wave of their own: they feed the
+      // loss sums and the adaptive LR only, not this minibatch's backward
+      float le = 0.f, lb = 0.f, lkl = 0.f;
+      if (rowok) {
+        const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
+        const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
+        // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
+        const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
+        const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
+        const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
+        e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
+        e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
+        le = ent; lb = b_loss; lkl = kl0 + kl1;
+      }
+      le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
+      if (lane == 0) {
+        part_st(P_LOSS + 2, le); part_st(P_LOSS + 3, lb); part_st(P_LOSS + 4, lkl);
+      }
     } else {
-      float lc = 0.f, le = 0.f, lb = 0.f, lkl = 0.f;
+      float lc = 0.f;
       if (rowok) {
         // critic_loss (common_losses.py:10-19)
         const float vo = ri.val, R = ri.ret;
@@ -1386,22 +1405,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
           dv = 2.f * (v - R);
         }
         dv *= 0.5f * c.critic_coef * invB;
-        const float b_loss = (bl0 * bl0 + bh0 * bh0) + (bl1 * bl1 + bh1 * bh1);
-        const float ent = (0.5f + 0.5f * logf(USV_2PI_F) + ls0) + (0.5f + 0.5f * logf(USV_2PI_F) + ls1);
-        // policy_kl (torch_ext.py:27-36) vs the dataset's mu/sigma, then update_mu_sigma
-        const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
-        const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
-        const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
-        e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
-        e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
-        lc = c_loss; le = ent; lb = b_loss; lkl = kl0 + kl1;
+        lc = c_loss;
         s.g[r * 4 + 2] = dv;
       }
-      lc = wave_sum(lc); le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
-      if (lane == 0) {
-        part_st(P_LOSS + 1, lc); part_st(P_LOSS + 2, le); part_st(P_LOSS + 3, lb);
-        part_st(P_LOSS + 4, lkl);
-      }
+      lc = wave_sum(lc);
+      if (lane == 0) part_st(P_LOSS + 1, lc);
     }
   }
   __syncthreads();

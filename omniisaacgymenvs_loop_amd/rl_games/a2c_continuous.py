@@ -260,7 +260,10 @@ class A2CAgent:
         self.val_rms = torch.tensor([0.0, 1.0, 1.0], **f64)
         self.grad = torch.zeros(_capi.lib().ppo_grad_floats(), **f32)
         self.losses = torch.zeros(8, **f32)
-        self.partials = torch.zeros(_capi.lib().ppo_partials_floats(self.minibatch_size), **f32)
+        n_part = _capi.lib().ppo_partials_floats(self.minibatch_size)
+        if n_part <= 0:   # the chunk-major partial rows of this many workgroups would overrun the fold words
+            raise ValueError(f"minibatch_size {self.minibatch_size}: no partial-gradient layout (ppo_partials_floats)")
+        self.partials = torch.zeros(n_part, **f32)
         self.work = torch.zeros(8 + 8 * 4096 + N // 2 + 64, **f64)
         B = N * H
         self.exp_obs = torch.zeros((B, NIN), **f32)
