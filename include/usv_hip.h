@@ -216,6 +216,13 @@ typedef struct usv_cfg {
   double step_inc;          /* 1 / horizon_length (the increment of USVVirtual.step) */
   double cur_min_dist, cur_max_dist, cur_kill_dist, cur_warmup, cur_end;
   double min_spawn_d, max_spawn_d, kill_dist_d;   /* the task's min_spawn_dist, max_spawn_dist, kill_dist */
+  /* ---- the first substep after a reset computes the drag and the disturbances from the
+   * reference's CACHED root state, which still holds the pre-reset pose and velocity (apply_forces reads
+   * root_pos / root_quats / root_velocities, USV_Virtual.py:1103-1117, refreshed only by update_state,
+   * :771-813, which runs after each world step, vec_env_rlgames.py:154-171).  usv_reset keeps those inputs
+   * in usv_bufs_t.stale; 0 = the first substep uses the new state instead. ---- */
+  int   stale_root;
+  int   pad_stale;
 } usv_cfg_t;
 
 /* stage bits of ctl[USV_CTL_NAN_FLAG] / ppo_cfg_t.nan_flag (the reference's probe names) */
@@ -307,7 +314,18 @@ typedef struct usv_bufs {
      batch's inside value `high` (> 0; negated when no cell of the batch is inside an obstacle),
      RN(1 / cost range), RN(1 / J range) */
   float *fnorm;
+  /* [USV_STALE_ROWS][n] the hydrodynamic / disturbance inputs of a reset env's first substep (cfg.stale_root):
+     usv_reset writes them from the pre-reset state before it spawns the env -- the water-relative body
+     velocity R(yaw)^T (v - flow) (Hydrodynamics.py:207-245), the yaw rate, and the local position at which
+     the disturbance sinusoids are evaluated (USV_disturbances.py:386-410, 510-530) */
+  float *stale;
 } usv_bufs_t;
+#define USV_STALE_UB 0
+#define USV_STALE_VB 1
+#define USV_STALE_RB 2
+#define USV_STALE_PX 3
+#define USV_STALE_PY 4
+#define USV_STALE_ROWS 5
 #define USV_FNORM 8
 #define USV_RSTASH_ROWS 14
 #define USV_CLOCK_WORDS 6
@@ -422,7 +440,8 @@ int usv_env_step(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *actions
 #define USV_SLAB_DIST    136    /* USV_NDIST rows */
 #define USV_SLAB_ENV_ORG 147    /* 2 */
 #define USV_SLAB_TGT_H   149
-#define USV_SLAB_ROWS    150
+#define USV_SLAB_STALE   150    /* USV_STALE_ROWS rows */
+#define USV_SLAB_ROWS    155
 
 /* usv_env_step split in two so the non-reset envs can run while the reset envs'
  * potential fields are built: part 1 = envs not reset this step (needs only

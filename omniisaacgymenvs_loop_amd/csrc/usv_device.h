@@ -63,6 +63,31 @@ __device__ __forceinline__ float div_rn(float x, float b, float y) {
   return fmaf(r, y, q);
 }
 
+// sin and cos of the integrator's angles (yaw, spawn and disturbance phases): this build's own definition (the
+// reference's PhysX step has none), restated operation for operation by the C oracle
+// (oracle/usv_oracle.c:usv_sincos), so the device and the oracle integrate the same bits.  Reduction by pi/2 in
+// three Cody-Waite parts (k * part exact for |k| < 2^13), Cephes' single-precision minimax polynomials on
+// [-pi/4, pi/4]; plain IEEE multiplies and adds (the library is built with -ffp-contract=off)
+__device__ __forceinline__ void usv_sincos(float x, float *s, float *c) {
+  const float k = rintf(x * 0.63661977236758134f);
+  float r = x - k * 1.5703125f;
+  r = r - k * 4.837512969970703125e-4f;
+  r = r - k * 7.54978995489188216e-8f;
+  const float z = r * r;
+  const float sp = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
+  const float cp = 1.0f - 0.5f * z + z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f +
+                                                                            z * 2.443315711809948e-5f));
+  const int q = (int)k & 3;
+  const float sa = (q & 1) ? cp : sp, ca = (q & 1) ? sp : cp;
+  *s = (q & 2) ? -sa : sa;
+  *c = ((q + 1) & 2) ? -ca : ca;
+}
+__device__ __forceinline__ float usv_sin(float x) {
+  float s, c;
+  usv_sincos(x, &s, &c);
+  return s;
+}
+
 // cell centre i of the potential field's grid (BatchedMapGPU's torch.linspace of the cell centres,
 // d_multi_gemini.py:40-48), or the override table (parity tests)
 __device__ __forceinline__ float grid_coord_k(float start, float end, float step, int i) {

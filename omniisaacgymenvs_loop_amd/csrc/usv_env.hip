@@ -203,8 +203,10 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
       } else if (c.mass_dr_on && c.com_mode == 2 && c.com_legacy_r > 0.f) {
         const float r = U(RU_COM) * c.com_legacy_r;
         const float th = U(RU_COM + 1) * USV_PI_F * 2.0f;
-        cx = c.base_com[0] + cosf(th) * r;
-        cy = c.base_com[1] + sinf(th) * r;
+        float sth, cth;
+        usv_sincos(th, &sth, &cth);
+        cx = c.base_com[0] + cth * r;
+        cy = c.base_com[1] + sth * r;
       }
       b.mass[e] = mass;
       b.com_x[e] = cx;
@@ -254,8 +256,10 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         if (c.fdist_on && c.fconst_on) {
           const float r = U(RU_FCONST) * (float)((double)c.fconst_max - (double)c.fconst_min) + c.fconst_min;
           const float th = U(RU_FCONST + 1) * USV_PI_F * 2.0f;
-          D[DI_FCX * nn + e] = cosf(th) * r;
-          D[DI_FCY * nn + e] = sinf(th) * r;
+          float sth, cth;
+          usv_sincos(th, &sth, &cth);
+          D[DI_FCX * nn + e] = cth * r;
+          D[DI_FCY * nn + e] = sth * r;
         }
         if (c.tdist_on && c.tsin_on) {
           D[DI_TF * nn + e] = U(RU_TSIN) * (float)((double)c.tfreq_max - (double)c.tfreq_min) + c.tfreq_min;
@@ -289,8 +293,10 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
       if (c.task_kind == USV_TASK_CAPTURE_XY) {   // CaptureXYTask.get_spawns (static_obs.py:936-1060)
         const float r = U(RU_SPAWN_R) * (c.spawn_rmax - c.spawn_rmin) + c.spawn_rmin;
         const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
-        sx = r * cosf(th);
-        sy = r * sinf(th);
+        float sth, cth;
+        usv_sincos(th, &sth, &cth);
+        sx = r * cth;
+        sy = r * sth;
         b.field_old_tgt[e] = tx;
         b.field_old_tgt[n + e] = ty;
       } else if (c.task_kind == USV_TASK_GO_TO_POSE) {   // GoToPoseTask.get_spawns (USV_go_to_pose.py:256-319)
@@ -302,12 +308,32 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         }
         const float r = U(RU_SPAWN_R) * (float)(rmax - rmin) + (float)rmin;
         const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
-        sx = r * cosf(th) + tx;
-        sy = r * sinf(th) + ty;
+        float sth, cth;
+        usv_sincos(th, &sth, &cth);
+        sx = r * cth + tx;
+        sy = r * sth + ty;
         b.prev_dist[e] = 0.f;                            // GoToPoseTask.reset: prev_position_dist = 0 (:227)
       } else {                                           // TrackXYOVelocityTask.get_spawns (:203-219): env origin
         sx = 0.f;
         sy = 0.f;
+      }
+      // ---- the reference's cached root state still holds this pre-reset pose when the first substep
+      // computes its drag and disturbances (USV_Virtual.py:1103-1117): keep those inputs ----
+      if (c.stale_root) {
+        const float opx = b.px[e], opy = b.py[e], ovx = b.vx[e], ovy = b.vy[e];
+        float so, co;
+        usv_sincos(b.yaw[e], &so, &co);
+        float ub = co * ovx + so * ovy;               // R^T v (Utils.py:8-12)
+        float vb = -so * ovx + co * ovy;
+        if (c.current_on) {                           // relative to the water (Hydrodynamics.py:224-237)
+          ub = ub - (co * c.flow_vel[0] + so * c.flow_vel[1]);
+          vb = vb - (-so * c.flow_vel[0] + co * c.flow_vel[1]);
+        }
+        b.stale[USV_STALE_UB * (size_t)n + e] = ub;
+        b.stale[USV_STALE_VB * (size_t)n + e] = vb;
+        b.stale[USV_STALE_RB * (size_t)n + e] = b.wz[e];
+        b.stale[USV_STALE_PX * (size_t)n + e] = opx;
+        b.stale[USV_STALE_PY * (size_t)n + e] = opy;
       }
       // ---- pose / velocities / bookkeeping (USV_Virtual.py:1541-1579) ----
       if (b.scene) {
@@ -565,7 +591,7 @@ struct StepWin {
   uint32_t px, py, yaw, vx, vy, wz, fl, fr, mass, k_iz, k_drag, thr_l, thr_r, com_x, com_y, com_z;
   uint32_t lin_damp, quad_damp, progress, tgt_x, tgt_y, obst, goal_cnt, prev_dist, prev_head, prev_pot, prev_wz;
   uint32_t stats, prev_cmd, rew, reset_buf, dones, done_coll, done_succ, just_reset, obs;
-  uint32_t dist, env_org;
+  uint32_t dist, env_org, stale;
   uint32_t n4;      // bytes of one [n] f32 row
   uint32_t bytes;   // window size
 };
@@ -591,7 +617,7 @@ struct FixedWin {
                             done_coll = R(USV_SLAB_IBUF + 4);
   static constexpr uint32_t just_reset = R(USV_SLAB_JUST_RESET), stats = R(USV_SLAB_STATS), obs = R(USV_SLAB_OBS),
                             rew = R(USV_SLAB_REW), dones = R(USV_SLAB_DONES), dist = R(USV_SLAB_DIST),
-                            env_org = R(USV_SLAB_ENV_ORG);
+                            env_org = R(USV_SLAB_ENV_ORG), stale = R(USV_SLAB_STALE);
   static constexpr uint32_t n4 = 1u << kShift;
   static constexpr uint32_t bytes = (uint32_t)USV_SLAB_ROWS << kShift;
   static_assert((unsigned long long)USV_SLAB_ROWS << kShift < 0x80000000ull, "window < 2 GiB");
@@ -793,6 +819,17 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
       orgx = b.env_org ? ox_ : 0.f;
       orgy = b.env_org ? oy_ : 0.f;
     }
+    // a reset env's first substep: the pre-reset inputs usv_reset kept; the other lanes
+    // read past the window (no memory access, 0)
+    const bool stl = c.stale_root && was_reset;
+    const uint32_t vst = stl ? v4 : kDrop;
+    const float st_ub = bld(R, w.stale + USV_STALE_UB * w.n4, vst), st_vb = bld(R, w.stale + USV_STALE_VB * w.n4, vst);
+    const float st_rb = bld(R, w.stale + USV_STALE_RB * w.n4, vst);
+    float st_px = 0.f, st_py = 0.f;
+    if (kDist) {
+      st_px = bld(R, w.stale + USV_STALE_PX * w.n4, vst);
+      st_py = bld(R, w.stale + USV_STALE_PY * w.n4, vst);
+    }
     __builtin_amdgcn_sched_barrier(0);   // keep the substep inputs ahead of the loads below
     const int progress0 = bldi(R, w.progress, v4);
     const float tgx = bld(R, w.tgt_x, v4), tgy = bld(R, w.tgt_y, v4);
@@ -881,26 +918,34 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
       fl = fl * al + oma * tgt0;                      // ThrusterDynamics.py:133-136
       fr = fr * al + oma * tgt1;
       float sy_, cy_;
-      sincosf(yaw, &sy_, &cy_);
+      usv_sincos(yaw, &sy_, &cy_);
       float ub = cy_ * vx + sy_ * vy;                 // R^T v (Utils.py:8-12)
       float vb = -sy_ * vx + cy_ * vy;
-      const float rb = wz;
+      float rb = wz;
+      float hpx = px, hpy = py;
+      if (kDist && c.current_on) {                    // relative to the water (Hydrodynamics.py:224-237)
+        ub = ub - (cy_ * c.flow_vel[0] + sy_ * c.flow_vel[1]);
+        vb = vb - (-sy_ * c.flow_vel[0] + cy_ * c.flow_vel[1]);
+      }
+      if (s == 0) {                                   // the cached pre-reset root state
+        ub = stl ? st_ub : ub;
+        vb = stl ? st_vb : vb;
+        rb = stl ? st_rb : rb;
+        hpx = stl ? st_px : hpx;
+        hpy = stl ? st_py : hpy;
+      }
       float dfx = 0.f, dfy = 0.f, dtz = 0.f;
       if (kDist) {
-        if (c.current_on) {                           // relative to the water (Hydrodynamics.py:224-237)
-          ub = ub - (cy_ * c.flow_vel[0] + sy_ * c.flow_vel[1]);
-          vb = vb - (-sy_ * c.flow_vel[0] + cy_ * c.flow_vel[1]);
-        }
         // get_disturbance_forces / get_torque_disturbance at root_pos (USV_disturbances.py:386-410,510-530)
-        const float wx = px + orgx, wy = py + orgy;
+        const float wx = hpx + orgx, wy = hpy + orgy;
         dfx = dp[DI_FCX];
         dfy = dp[DI_FCY];
         dtz = dp[DI_TC];
         if (c.fsin_on) {
-          dfx = dfx + sinf(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
-          dfy = dfy + sinf(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
+          dfx = dfx + usv_sin(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
+          dfy = dfy + usv_sin(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
         }
-        if (c.tsin_on) dtz = dtz + sinf((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
+        if (c.tsin_on) dtz = dtz + usv_sin((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
       }
       float D0 = lin0 + qd0 * fabsf(ub), D1 = lin1 + qd1 * fabsf(vb), D2 = lin2 + qd2 * fabsf(rb);
       D0 = D0 * c.scaling_damping; D1 = D1 * c.scaling_damping; D2 = D2 * c.scaling_damping;
@@ -1262,6 +1307,16 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
   const int progress0 = b.progress[ec], goal_cnt0 = b.goal_cnt[ec];
   const float tgx = b.tgt_x[ec], tgy = b.tgt_y[ec], tgh = b.tgt_h[ec];
   const float prev_pd = b.prev_dist[ec], prev_wz_mem = b.prev_wz[ec];
+  // a reset env's first substep: the pre-reset inputs usv_reset kept
+  const bool stl = c.stale_root && was_reset;
+  float st_ub = 0.f, st_vb = 0.f, st_rb = 0.f, st_px = 0.f, st_py = 0.f;
+  if (stl) {
+    st_ub = b.stale[USV_STALE_UB * nn + ec];
+    st_vb = b.stale[USV_STALE_VB * nn + ec];
+    st_rb = b.stale[USV_STALE_RB * nn + ec];
+    st_px = b.stale[USV_STALE_PX * nn + ec];
+    st_py = b.stale[USV_STALE_PY * nn + ec];
+  }
   float sums[USV_NSTAT];
   if (kStats) {
 #pragma unroll
@@ -1310,25 +1365,27 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
     fl = fl * al + oma * tgt0;
     fr = fr * al + oma * tgt1;
     float sy_, cy_;
-    sincosf(yaw, &sy_, &cy_);
+    usv_sincos(yaw, &sy_, &cy_);
     float ub = cy_ * vx + sy_ * vy;
     float vb = -sy_ * vx + cy_ * vy;
-    const float rb = wz;
+    float rb = wz;
+    float hpx = px, hpy = py;
+    if (has_dist && c.current_on) {
+      ub = ub - (cy_ * c.flow_vel[0] + sy_ * c.flow_vel[1]);
+      vb = vb - (-sy_ * c.flow_vel[0] + cy_ * c.flow_vel[1]);
+    }
+    if (s == 0 && stl) { ub = st_ub; vb = st_vb; rb = st_rb; hpx = st_px; hpy = st_py; }
     float dfx = 0.f, dfy = 0.f, dtz = 0.f;
     if (has_dist) {
-      if (c.current_on) {
-        ub = ub - (cy_ * c.flow_vel[0] + sy_ * c.flow_vel[1]);
-        vb = vb - (-sy_ * c.flow_vel[0] + cy_ * c.flow_vel[1]);
-      }
-      const float wx = px + orgx, wy = py + orgy;
+      const float wx = hpx + orgx, wy = hpy + orgy;
       dfx = dp[DI_FCX];
       dfy = dp[DI_FCY];
       dtz = dp[DI_TC];
       if (c.fsin_on) {
-        dfx = dfx + sinf(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
-        dfy = dfy + sinf(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
+        dfx = dfx + usv_sin(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
+        dfy = dfy + usv_sin(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
       }
-      if (c.tsin_on) dtz = dtz + sinf((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
+      if (c.tsin_on) dtz = dtz + usv_sin((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
     }
     float D0 = lin0 + qd0 * fabsf(ub), D1 = lin1 + qd1 * fabsf(vb), D2 = lin2 + qd2 * fabsf(rb);
     D0 = D0 * c.scaling_damping; D1 = D1 * c.scaling_damping; D2 = D2 * c.scaling_damping;
@@ -1620,7 +1677,7 @@ __global__ void k_forces(usv_cfg_t c, usv_bufs_t b, float *__restrict__ out) {
   const int n = b.n;
   if (e >= n) return;
   float sy_, cy_;
-  sincosf(b.yaw[e], &sy_, &cy_);
+  usv_sincos(b.yaw[e], &sy_, &cy_);
   const float vx = b.vx[e], vy = b.vy[e], wz = b.wz[e];
   float ub = cy_ * vx + sy_ * vy, vb = -sy_ * vx + cy_ * vy;
   if (c.current_on) {   // relative to the water (Hydrodynamics.py:224-237)
@@ -1670,7 +1727,8 @@ int step_window(const usv_cfg_t &c, const usv_bufs_t &b, const char **base, Step
       {b.dones, 2 * f, &w->dones, true}, {b.done_coll, f, &w->done_coll, true},
       {b.done_succ, f, &w->done_succ, true}, {b.just_reset, n, &w->just_reset, true},
       {b.obs, USV_NOBS * f, &w->obs, true}, {b.dist, USV_NDIST * f, &w->dist, false},
-      {b.dist ? b.env_org : nullptr, 2 * f, &w->env_org, false}};
+      {b.dist ? b.env_org : nullptr, 2 * f, &w->env_org, false},
+      {c.stale_root ? b.stale : nullptr, USV_STALE_ROWS * f, &w->stale, c.stale_root != 0}};
   uintptr_t lo = UINTPTR_MAX, hi = 0;
   for (const Arr &a : arr) {
     if (!a.p) {
@@ -1716,7 +1774,8 @@ int fixed_slab_shift(const usv_cfg_t &c, const usv_bufs_t &b) {
       {b.done_coll, USV_SLAB_IBUF + 4, true}, {b.just_reset, USV_SLAB_JUST_RESET, true},
       {c.stats_on ? b.stats : nullptr, USV_SLAB_STATS, c.stats_on != 0}, {b.obs, USV_SLAB_OBS, true},
       {b.rew, USV_SLAB_REW, true}, {b.dones, USV_SLAB_DONES, true}, {b.dist, USV_SLAB_DIST, false},
-      {b.dist ? b.env_org : nullptr, USV_SLAB_ENV_ORG, false}};
+      {b.dist ? b.env_org : nullptr, USV_SLAB_ENV_ORG, false},
+      {c.stale_root ? b.stale : nullptr, USV_SLAB_STALE, c.stale_root != 0}};
   for (const Row &r : rows) {
     if (!r.p) {
       if (r.required) return -1;
@@ -1826,6 +1885,7 @@ int usv_reset_part(const usv_cfg_t *cfg, const usv_bufs_t *b, uint64_t seed, uin
   if (!cfg || !b || b->n <= 0 || part < 0 || part > 2) return 1;
   if (b->scene && (b->n_scenes <= 0 || !b->scene_next || !b->scene_last || cfg->task_kind != USV_TASK_CAPTURE_XY))
     return 1;
+  if (cfg->stale_root && !b->stale) return 1;   // the first substep's cached-state inputs have nowhere to go
   hipStream_t s = (hipStream_t)stream;
   const int grid = (b->n + kBlock - 1) / kBlock;
   if (part != 2) {

@@ -56,6 +56,12 @@
   X(USV_TS_LIN_OK, "USV_TS_LIN_OK") \
   X(USV_TS_POS_KILL, "USV_TS_POS_KILL") \
   X(USV_TS_ROWS, "USV_TS_ROWS") \
+  X(USV_STALE_UB, "USV_STALE_UB") \
+  X(USV_STALE_VB, "USV_STALE_VB") \
+  X(USV_STALE_RB, "USV_STALE_RB") \
+  X(USV_STALE_PX, "USV_STALE_PX") \
+  X(USV_STALE_PY, "USV_STALE_PY") \
+  X(USV_STALE_ROWS, "USV_STALE_ROWS") \
   X(USV_FNORM, "USV_FNORM") \
   X(USV_RSTASH_ROWS, "USV_RSTASH_ROWS") \
   X(USV_CLOCK_WORDS, "USV_CLOCK_WORDS") \
@@ -105,6 +111,7 @@
   X(USV_SLAB_DIST, "USV_SLAB_DIST") \
   X(USV_SLAB_ENV_ORG, "USV_SLAB_ENV_ORG") \
   X(USV_SLAB_TGT_H, "USV_SLAB_TGT_H") \
+  X(USV_SLAB_STALE, "USV_SLAB_STALE") \
   X(USV_SLAB_ROWS, "USV_SLAB_ROWS") \
   X(PPO_NIN, "PPO_NIN") \
   X(PPO_NH, "PPO_NH") \
@@ -335,6 +342,8 @@
   X(offsetof(usv_cfg_t, min_spawn_d), "usv_cfg.min_spawn_d") \
   X(offsetof(usv_cfg_t, max_spawn_d), "usv_cfg.max_spawn_d") \
   X(offsetof(usv_cfg_t, kill_dist_d), "usv_cfg.kill_dist_d") \
+  X(offsetof(usv_cfg_t, stale_root), "usv_cfg.stale_root") \
+  X(offsetof(usv_cfg_t, pad_stale), "usv_cfg.pad_stale") \
   X(sizeof(usv_bufs_t), "sizeof usv_bufs") \
   X(offsetof(usv_bufs_t, n), "usv_bufs.n") \
   X(offsetof(usv_bufs_t, pad0), "usv_bufs.pad0") \
@@ -397,6 +406,7 @@
   X(offsetof(usv_bufs_t, clock), "usv_bufs.clock") \
   X(offsetof(usv_bufs_t, rstash), "usv_bufs.rstash") \
   X(offsetof(usv_bufs_t, fnorm), "usv_bufs.fnorm") \
+  X(offsetof(usv_bufs_t, stale), "usv_bufs.stale") \
   X(sizeof(usv_hydro_t), "sizeof usv_hydro") \
   X(offsetof(usv_hydro_t, water_density), "usv_hydro.water_density") \
   X(offsetof(usv_hydro_t, gravity), "usv_hydro.gravity") \

@@ -324,6 +324,9 @@ def build_usv_cfg(task_cfg: Dict[str, Any]) -> UsvCfg:
     # the reference's fail-fast probe toggle (USV_Virtual.py:57-59): on unless USV_NAN_PROBE=0
     c.nan_probe = nan_probe_enabled()
     c.step_inc = 1 / int(env.get("horizon_length", 16))   # USVVirtual.step += 1 / horizon_length (:1633)
+    # the first substep after a reset sees the cached pre-reset root state, as the reference's
+    # apply_forces does (USV_Virtual.py:1103-1117).  Not a reference yaml key: this build's switch, on by default
+    c.stale_root = int(bool(env.get("stale_root_after_reset", True)))
     return c
 
 

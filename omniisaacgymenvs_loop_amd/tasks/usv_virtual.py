@@ -107,7 +107,8 @@ class USVVirtual:
                      ("obs_buf_t", (n, NOBS), torch.float32, "OBS"), ("rew_buf", (n,), torch.float32, "REW"),
                      ("dones", (n,), torch.int64, "DONES"), ("field_old_tgt", (2, n), torch.float32, "FIELD_OLD_TGT"),
                      ("reset_ids", (n,), torch.int32, "RESET_IDS"), ("dist", (NDIST, n), torch.float32, "DIST"),
-                     ("env_org", (2, n), torch.float32, "ENV_ORG"), ("tgt_h", (n,), torch.float32, "TGT_H")]
+                     ("env_org", (2, n), torch.float32, "ENV_ORG"), ("tgt_h", (n,), torch.float32, "TGT_H"),
+                     ("stale", (DEFINES["USV_STALE_ROWS"], n), torch.float32, "STALE")]
         sizes = [int(np.prod(shape)) * torch.empty((), dtype=dt).element_size() for _, shape, dt, _ in slab_spec]
         if n % 64 == 0:
             rb = 4 * n
@@ -259,6 +260,7 @@ class USVVirtual:
         b.dist = p(self.dist) if self.dist is not None else None
         b.env_org = p(self.env_org)
         b.tgt_h = p(self.tgt_h)
+        b.stale = p(self.stale)
         b.task_scratch = p(self.task_scratch) if self.task_scratch is not None else None
         if self.scene is not None:
             b.scene, b.scene_next, b.scene_last = p(self.scene), p(self.scene_next), p(self.scene_last)

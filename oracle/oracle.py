@@ -80,7 +80,7 @@ class _OracleEnvC(ctypes.Structure):
                 [("ctl", ctypes.c_int32 * 20), ("extras", ctypes.c_float * NSTAT), ("dbg", ctypes.c_void_p),
                  ("tmp", ctypes.c_void_p), ("grid_lin", ctypes.c_void_p), ("dist", ctypes.c_void_p),
                  ("env_org", ctypes.c_void_p), ("tgt_h", ctypes.c_void_p), ("step_f", ctypes.c_double),
-                 ("pot_in", ctypes.c_void_p), ("pos_in", ctypes.c_void_p)])
+                 ("pot_in", ctypes.c_void_p), ("pos_in", ctypes.c_void_p), ("root_cache", ctypes.c_void_p)])
 
 
 class OracleEnv:
@@ -125,6 +125,9 @@ class OracleEnv:
             setattr(self.c, k, _p(getattr(self, k)))
         self.c.dbg = _p(self.dbg)
         self.c.tmp = _p(self.tmp)
+        # the reference's cached root state (px, py, yaw, vx, vy, wz) at a reset env's first substep (App. C.1)
+        self.root_cache = np.zeros((6, n), np.float32)
+        self.c.root_cache = _p(self.root_cache)
         self.c.lin_damp = _p(self.lin_damp) if self.lin_damp is not None else None
         self.c.quad_damp = _p(self.quad_damp) if self.quad_damp is not None else None
         # disturbance parameters (zeros until drawn at reset) and env origins
@@ -279,6 +282,14 @@ def reset_uniforms(seed, step, ids):
     u = np.zeros((len(ids), NU_RESET), np.float32)
     lib().oracle_reset_uniforms(seed, step, len(ids), _p(ids), _p(u))
     return u
+
+
+def sincos(x):
+    """The integrator's sin / cos (usv_oracle.c:usv_sincos) of a float32 array."""
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib().oracle_sincos(_p(x), ctypes.c_int(x.size), _p(s), _p(c))
+    return s, c
 
 
 def philox(ctr, key):

@@ -62,6 +62,32 @@ static inline float minf_(float a, float b) { return a < b ? a : b; }
  * plain x*x + y*y. */
 static inline float tnorm2(float x, float y) { return sqrtf(fmaf(y, y, x * x)); }
 
+/* sin / cos of the integrator's angles (yaw, spawn and disturbance phases).  The reference's PhysX step has no
+ * restatable integrator: this build defines it, and its sin / cos are part of that definition --
+ * restated here operation for operation (csrc/usv_device.h:usv_sincos; plain IEEE float multiplies and adds,
+ * both sides built with -ffp-contract=off), so the oracle integrates the device's bits.  Reduction by pi/2 in
+ * three Cody-Waite parts, Cephes' single-precision minimax polynomials on [-pi/4, pi/4]; the accuracy against
+ * libm is a CPU test (tests/test_oracle_golden.py::test_integrator_sincos_accuracy). */
+void usv_sincos(float x, float *s, float *c) {
+  const float k = rintf(x * 0.63661977236758134f);
+  float r = x - k * 1.5703125f;
+  r = r - k * 4.837512969970703125e-4f;
+  r = r - k * 7.54978995489188216e-8f;
+  const float z = r * r;
+  const float sp = r + r * z * (-1.6666654611e-1f + z * (8.3321608736e-3f + z * -1.9515295891e-4f));
+  const float cp = 1.0f - 0.5f * z + z * z * (4.166664568298827e-2f + z * (-1.388731625493765e-3f +
+                                                                            z * 2.443315711809948e-5f));
+  const int q = (int)k & 3;
+  const float sa = (q & 1) ? cp : sp, ca = (q & 1) ? sp : cp;
+  *s = (q & 2) ? -sa : sa;
+  *c = ((q + 1) & 2) ? -ca : ca;
+}
+void oracle_sincos(const float *x, int n, float *s, float *c) {
+  for (int i = 0; i < n; ++i) usv_sincos(x[i], s + i, c + i);
+}
+static inline float usv_sin(float x) { float s, c; usv_sincos(x, &s, &c); return s; }
+static inline float usv_cos(float x) { float s, c; usv_sincos(x, &s, &c); return c; }
+
 /* ------------------------------------------------------------------------ */
 /* Philox streams (same mapping as the kernels)                              */
 /* ------------------------------------------------------------------------ */
@@ -159,6 +185,11 @@ typedef struct oracle_env {
      pos_in the oracle also samples its own field at the device's position (+ the same noise) into dbg[15]. */
   const float *pot_in;              /* [n] or NULL */
   const float *pos_in;              /* [2][n] or NULL */
+  /* [6][n] (px, py, yaw, vx, vy, wz) or NULL: the reference's cached root_pos / root_quats / root_velocities
+     as the first substep after a reset reads them (apply_forces, USV_Virtual.py:1103-1117,
+     reads the values of the last update_state, :771-813) -- the pre-reset state, kept by oracle_reset when
+     cfg.stale_root is on */
+  float *root_cache;
 } oracle_env_t;
 
 /* GoToPoseTask spawn curriculum (USV_go_to_pose.py:188-202 kill distance, :266-290 spawn radii): linear in
@@ -175,10 +206,11 @@ static double curriculum_lerp(const usv_cfg_t *c, double st, double cur, double 
  * (Hydrodynamics.py:176-245) restricted to the planar DOFs u, v, r; thrusters
  * at the heron.usd lever arms.                           */
 /* ------------------------------------------------------------------------ */
-static void planar_forces(const usv_cfg_t *c, const oracle_env_t *E, int e, float cy, float sy,
-                          float fl, float fr, const float *dist3 /* disturbance fx, fy, tz or NULL */,
+static void planar_forces(const usv_cfg_t *c, const oracle_env_t *E, int e, float cy, float sy, float vx, float vy,
+                          float wz, float fl, float fr, const float *dist3 /* disturbance fx, fy, tz or NULL */,
                           float *X, float *Y, float *N) {
-  const float vx = E->vx[e], vy = E->vy[e], wz = E->wz[e];
+  /* (cy, sy, vx, vy, wz): the root state apply_forces reads (the current one, or the cached pre-reset one
+     in a reset env's first substep) */
   /* getLocalLinearVelocities: R^T v  (Utils.py:8-12) */
   float u = cy * vx + sy * vy;
   float v = -sy * vx + cy * vy;
@@ -216,26 +248,27 @@ static void planar_forces(const usv_cfg_t *c, const oracle_env_t *E, int e, floa
  * (USV_disturbances.py:386-410, 510-530) at the world root position (root_pos =
  * local + RLTask._env_pos); body-frame base force / yaw torque (is_global=False,
  * USV_Virtual.py:1118-1125). */
-static void disturbance(const usv_cfg_t *c, const oracle_env_t *E, int e, float *fx, float *fy, float *tz) {
+static void disturbance(const usv_cfg_t *c, const oracle_env_t *E, int e, float px, float py, float *fx, float *fy,
+                        float *tz) {
   const int n = E->n;
   const float *D = E->dist;
-  const float wx = E->px[e] + (E->env_org ? E->env_org[e] : 0.f);
-  const float wy = E->py[e] + (E->env_org ? E->env_org[n + e] : 0.f);
+  const float wx = px + (E->env_org ? E->env_org[e] : 0.f);
+  const float wy = py + (E->env_org ? E->env_org[n + e] : 0.f);
   *fx = D[DI_FCX * n + e];
   *fy = D[DI_FCY * n + e];
   *tz = D[DI_TC * n + e];
   if (c->fsin_on) {
-    *fx = *fx + sinf(wx * D[DI_FXF * n + e] + D[DI_FXS * n + e]) * D[DI_FAMP * n + e];
-    *fy = *fy + sinf(wy * D[DI_FYF * n + e] + D[DI_FYS * n + e]) * D[DI_FAMP * n + e];
+    *fx = *fx + usv_sin(wx * D[DI_FXF * n + e] + D[DI_FXS * n + e]) * D[DI_FAMP * n + e];
+    *fy = *fy + usv_sin(wy * D[DI_FYF * n + e] + D[DI_FYS * n + e]) * D[DI_FAMP * n + e];
   }
-  if (c->tsin_on) *tz = *tz + sinf((wx + wy) * D[DI_TF * n + e] + D[DI_TS * n + e]) * D[DI_TAMP * n + e];
+  if (c->tsin_on) *tz = *tz + usv_sin((wx + wy) * D[DI_TF * n + e] + D[DI_TS * n + e]) * D[DI_TAMP * n + e];
 }
 
 void oracle_forces(const usv_cfg_t *c, oracle_env_t *E, float *out /*[n][3]*/) {
   for (int e = 0; e < E->n; ++e) {
-    const float cy = cosf(E->yaw[e]), sy = sinf(E->yaw[e]);
+    const float cy = usv_cos(E->yaw[e]), sy = usv_sin(E->yaw[e]);
     float X, Y, N;
-    planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], NULL, &X, &Y, &N);
+    planar_forces(c, E, e, cy, sy, E->vx[e], E->vy[e], E->wz[e], E->fl[e], E->fr[e], NULL, &X, &Y, &N);
     out[e * 3 + 0] = X; out[e * 3 + 1] = Y; out[e * 3 + 2] = N;
   }
 }
@@ -517,6 +550,12 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
   for (int s = 0; s < k; ++s) {
     const int e = ids[s];
     const float *u = U + (size_t)s * USV_NU_RESET;
+    /* the cached root state keeps the pre-reset pose until the next update_state */
+    if (c->stale_root && E->root_cache) {
+      float *rc = E->root_cache;
+      rc[0 * n + e] = E->px[e]; rc[1 * n + e] = E->py[e]; rc[2 * n + e] = E->yaw[e];
+      rc[3 * n + e] = E->vx[e]; rc[4 * n + e] = E->vy[e]; rc[5 * n + e] = E->wz[e];
+    }
     /* CaptureXYTask.reset (static_obs.py:767-778) */
     E->goal_cnt[e] = 0; E->done_succ[e] = 0; E->done_coll[e] = 0;
     E->just_reset[e] = 1;
@@ -533,8 +572,8 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
     } else if (c->mass_dr_on && c->com_mode == 2 && c->com_legacy_r > 0.f) {  /* legacy disk (:112-124) */
       const float r = u[RU_COM] * c->com_legacy_r;
       const float th = u[RU_COM + 1] * (float)OPI * 2.0f;
-      E->com_x[e] = c->base_com[0] + cosf(th) * r;
-      E->com_y[e] = c->base_com[1] + sinf(th) * r;
+      E->com_x[e] = c->base_com[0] + usv_cos(th) * r;
+      E->com_y[e] = c->base_com[1] + usv_sin(th) * r;
       E->com_z[e] = c->base_com[2];
     } else {
       E->com_x[e] = c->base_com[0]; E->com_y[e] = c->base_com[1]; E->com_z[e] = c->base_com[2];
@@ -584,8 +623,8 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
       if (c->fdist_on && c->fconst_on) {
         const float rr = u[RU_FCONST] * (float)((double)c->fconst_max - (double)c->fconst_min) + c->fconst_min;
         const float tt = u[RU_FCONST + 1] * (float)OPI * 2.0f;
-        D[DI_FCX * n + e] = cosf(tt) * rr;
-        D[DI_FCY * n + e] = sinf(tt) * rr;
+        D[DI_FCX * n + e] = usv_cos(tt) * rr;
+        D[DI_FCY * n + e] = usv_sin(tt) * rr;
       }
       if (c->tdist_on && c->tsin_on) {
         D[DI_TF * n + e] = u[RU_TSIN] * (float)((double)c->tfreq_max - (double)c->tfreq_min) + c->tfreq_min;
@@ -628,15 +667,15 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
       }
       const float r = u[RU_SPAWN_R] * (float)(dmax - dmin) + (float)dmin;
       const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
-      sx = r * cosf(th) + E->tgt_x[e];
-      sy = r * sinf(th) + E->tgt_y[e];
+      sx = r * usv_cos(th) + E->tgt_x[e];
+      sy = r * usv_sin(th) + E->tgt_y[e];
       E->prev_dist[e] = 0.f;   /* GoToPoseTask.reset: prev_position_dist = 0 (:227) */
     } else if (c->task_kind == USV_TASK_TRACK_XYO) {
       sx = 0.f; sy = 0.f;      /* TrackXYOVelocityTask.get_spawns (:203-219): heading only */
     } else {
       const float r = u[RU_SPAWN_R] * (rmax - rmin) + rmin;
       const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
-      sx = r * cosf(th); sy = r * sinf(th);
+      sx = r * usv_cos(th); sy = r * usv_sin(th);
     }
     if (c->task_kind != USV_TASK_CAPTURE_XY) {
       E->px[e] = sx; E->py[e] = sy; E->yaw[e] = yaw0;
@@ -813,6 +852,7 @@ void oracle_step_pre(const usv_cfg_t *c, oracle_env_t *E, const float *actions, 
 
 void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E) {
   const float PI_F = (float)OPI, TWO_PI_F = (float)(2.0 * OPI);
+  const int n = E->n;
   OMP_FOR
   for (int e = 0; e < E->n; ++e) {
     const float *tmp = E->tmp + (size_t)e * 8;
@@ -824,10 +864,18 @@ void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E) {
       /* DynamicsFirstOrder.update (ThrusterDynamics.py:132-136) */
       E->fl[e] = E->fl[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[0];
       E->fr[e] = E->fr[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[1];
-      const float cy = cosf(E->yaw[e]), sy = sinf(E->yaw[e]);
+      const float cy = usv_cos(E->yaw[e]), sy = usv_sin(E->yaw[e]);
+      /* apply_forces reads the cached root state: the pre-reset one in a reset env's first substep (C.1) */
+      const int cached = s == 0 && c->stale_root && E->just_reset[e] && E->root_cache;
+      const float *rc = E->root_cache;
+      const float hpx = cached ? rc[0 * n + e] : E->px[e], hpy = cached ? rc[1 * n + e] : E->py[e];
+      const float hcy = cached ? usv_cos(rc[2 * n + e]) : cy, hsy = cached ? usv_sin(rc[2 * n + e]) : sy;
+      const float hvx = cached ? rc[3 * n + e] : E->vx[e], hvy = cached ? rc[4 * n + e] : E->vy[e];
+      const float hwz = cached ? rc[5 * n + e] : E->wz[e];
       float X, Y, N, d3[3];
-      if (E->dist) disturbance(c, E, e, &d3[0], &d3[1], &d3[2]);
-      planar_forces(c, E, e, cy, sy, E->fl[e], E->fr[e], E->dist ? d3 : NULL, &X, &Y, &N);
+      if (E->dist) disturbance(c, E, e, hpx, hpy, &d3[0], &d3[1], &d3[2]);
+      planar_forces(c, E, e, hcy, hsy, hvx, hvy, hwz, E->fl[e], E->fr[e], E->dist ? d3 : NULL, &X, &Y, &N);
+      /* PhysX applies the body-frame wrench in the body's CURRENT frame (is_global=False) */
       /* build's 3-DoF semi-implicit Euler (no reference: PhysX) */
       const float ax = (cy * X - sy * Y) / m;
       const float ay = (sy * X + cy * Y) / m;

@@ -15,10 +15,12 @@ pytorch3d, none of which exist offline, so:
     semi-implicit Euler (the reference has no integrator of its own);
   * every torch.rand / torch.rand_like call is recorded with its call site so
     the oracle/kernels can replay the exact draws.
-Deviation (documented in DESIGN.md): right after reset_idx the fake view's
-fresh pose is pushed into the task's cached root_* tensors, so the first
-substep after a reset uses the new state (reference quirk App. C.1 is a PhysX
-artefact and is not reproduced).
+The task's cached root_* tensors are left as the reference leaves them: the
+first substep after a reset computes drag and disturbances from the pre-reset
+state.  The one harness step: update_state() runs once after
+post_reset, so the very first step's cache holds the initial pose (the
+reference zero-initialises root_quats, USV_Virtual.py:605, and
+quaternion_to_matrix of a zero quaternion is 0/0).
 """
 from __future__ import annotations
 
@@ -824,19 +826,12 @@ def gen_episode(torch, variant, n, steps, seed):
     usv, heron, world, task_cfg = build_usv(torch, n, variant)
     ve = make_vecenv(torch, usv, world)
     rec = RandRecorder(torch)
-    orig_reset_idx = type(usv).reset_idx
-
-    def reset_idx_refresh(self, env_ids):
-        orig_reset_idx(self, env_ids)
-        # push the fresh pose into the cached root_* state (see module doc)
-        self.root_pos, self.root_quats = self._heron.get_world_poses()
-        self.root_velocities = self._heron.get_velocities()
-
-    usv.reset_idx = types.MethodType(reset_idx_refresh, usv)
     rng = np.random.default_rng(seed)
     with rec:
         usv.post_reset()
         init_draws = rec.take()
+        usv.update_state()   # the cached root_* state of the first step (see module doc)
+        rec.take()
         init_tgt = _task_targets(usv.task)[0]
         usv.task.reset(torch.arange(n))   # flags only (reset via VecEnv.reset below)
         rec.take()

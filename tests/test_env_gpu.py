@@ -231,10 +231,11 @@ POT_ATOL = 1e-6   # the device's bilinear sample vs the oracle's field sampled a
 
 
 def _vs_oracle(tn, task, E, obs, rew, dones, t, prev_own, w=None, ties=False):
-    """GPU step vs the C oracle on the same Philox draws (the oracle stepped by oracle_step): dones exact, obs at
-    1e-5 (ties: obstacle order may differ where two distances tie), and the reward in two exact parts:
+    """GPU step vs the C oracle on the same Philox draws (the oracle stepped by oracle_step): the integrated state
+    (px, py, yaw, vx, vy, wz, fl, fr) bit-exact, dones exact, obs at 1e-5 (ties: obstacle order may differ where two
+    distances tie), and the reward in two exact parts:
       * the potential sample: the device's value equals the oracle's bit-exact field sampled at the device's
-        own integrated position within POT_ATOL (the position itself is checked at 1e-5 by the state checks);
+        own integrated position within POT_ATOL (the position itself is bit-exact, above);
       * the reward: the oracle's compute_reward fed the device's samples (this step's and, through prev_pot,
         the previous step's) within 1e-5 -- no potential-sample allowance.
     The sample difference to the oracle's own position and the envs whose shaping branch would differ there
@@ -242,6 +243,9 @@ def _vs_oracle(tn, task, E, obs, rew, dones, t, prev_own, w=None, ties=False):
     o = obs.cpu().numpy()
     w = w or o.shape[1]
     np.testing.assert_array_equal(dones.cpu().numpy(), E.reset_buf, err_msg=f"{tn} dones t={t}")
+    # the integrator is restated operation for operation (usv_sincos, div_rn == IEEE division): state bit-exact
+    ET.check(tn, "state", task.state.cpu().numpy().T, np.stack([getattr(E, k) for k in STATE_KEYS]).T, 0.0, 0.0,
+             list(STATE_KEYS), f"{tn} state t={t}")
     if ties:
         ET.record(tn, "obs", o, E.obs[:, :w], ET.obs_cols(w), tol=(1e-5, 1e-5))
         assert_obs_close(o, E.obs[:, :w], 1e-5, msg=f"{tn} obs t={t}")
