@@ -18,6 +18,7 @@ for r in csv.DictReader(open(sys.argv[1])):
     if "k_env_step<" in r["Name"] and "FixedWin<19>" in r["Name"]:
         print(sys.argv[2], sys.argv[3], "k_env_step calls", r["Calls"], "avg_us %.2f" % (float(r["AverageNs"]) / 1e3))
 PY
+    rm -rf $O/$v.$rep   # traces stay on the box (the merge-back cap)
   done
 done
 for v in $VARIANTS; do
@@ -33,4 +34,5 @@ for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
 if vals:
     print(sys.argv[2], "FETCH_SIZE per launch (x1024 x2) MB %.1f over %d" % (sum(vals) / len(vals) * 2048 / 1e6, len(vals)))
 PY
+  rm -rf $O/$v.fetch
 done
