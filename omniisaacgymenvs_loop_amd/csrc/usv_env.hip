@@ -1914,6 +1914,7 @@ int usv_env_step_part(const usv_cfg_t *cfg, const usv_bufs_t *b, const float *ac
                       void *stream) {
   if (!cfg || !b || !actions || !lut_dev || b->n <= 0 || part < 0 || part > 3) return 1;
   if (part == 3 && (cfg->task_kind != USV_TASK_CAPTURE_XY || !b->rstash)) return 1;
+  if (cfg->stale_root && !b->stale) return 1;   // a reset env's first substep reads usv_reset's cached inputs
   // CaptureXY samples the potential field from its parts (SDF tiles, cost rows, constants)
   if (cfg->task_kind == USV_TASK_CAPTURE_XY && (!b->field || !b->sdf || !b->fnorm)) return 7;
   if (cfg->priv_dim != 4 && cfg->priv_dim != 8) return 3;
