@@ -90,3 +90,23 @@ def test_layout_key_changes_with_any_entry():
         mod = list(ent)
         mod[i] = (expr, name, v)
         assert _abi.layout_key_of(mod) != k0
+
+
+def test_stale_root_needs_its_rows():
+    """cfg.stale_root (on by default) without usv_bufs_t.stale: usv_reset and usv_env_step
+    refuse the call with status 1 before touching the device (argument checks only: no GPU here)."""
+    from omniisaacgymenvs_loop_amd import _capi
+    from omniisaacgymenvs_loop_amd._abi import UsvBufs
+    from omniisaacgymenvs_loop_amd.tasks.usv_config import build_usv_cfg, load_yaml
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("libusv_hip.so not built (run __graft_entry__.build())")
+    cfg = build_usv_cfg(load_yaml(os.path.join(ROOT, "omniisaacgymenvs_loop_amd", "cfg", "task", "USV", "IROS2024",
+                                               "USV_Virtual_CaptureXY_SysID-TEST.yaml")))
+    assert cfg.stale_root == 1
+    b = UsvBufs()
+    b.n = 64
+    dummy = ctypes.create_string_buffer(64)
+    lib = _capi.lib()
+    assert lib.usv_reset(_capi.byref(cfg), _capi.byref(b), 0, 0, None, None) == 1
+    assert lib.usv_env_step(_capi.byref(cfg), _capi.byref(b), ctypes.addressof(dummy), ctypes.addressof(dummy),
+                            ctypes.c_float(0.0), 0, 0, None, None) == 1
