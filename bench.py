@@ -582,6 +582,9 @@ def main():
                  f"USV_Virtual_TrackXYOVelocity num_envs={C4_ENVS}/GPU PPO-MLP fp32 (BASELINE configs[3]'s "
                  "per-GPU share, the TrackXYOVelocity ranks)")]
     if any(st for *_, st, _ in secondary):
+        if agent._dp is not None:   # every rank: the headline agent's peer buffers, before the next agent maps its own
+            torch.cuda.synchronize()
+            agent._dp.release()
         del agent, env, task
         torch.cuda.empty_cache()
     for key, n2, task2_name, mixed, st2, workload in secondary:
