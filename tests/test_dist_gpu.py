@@ -219,3 +219,27 @@ def test_dp_selftest_passes_alone_and_fails_fast_without_the_peer():
         ex._selftest(300)
     assert time.time() - t0 < 5.0
     lost.close()
+
+
+def test_bench_two_ranks_on_one_device(tmp_path):
+    """The driver's multi-GPU bench path end to end on the one-GPU box: `torch.distributed.run --nproc-per-node 2
+    bench.py --gpus 2` with both ranks on cuda:0 (gloo for the host-side collectives), the update's gradient
+    exchange through the in-kernel peer path.  Rank 0 prints one line with n_gpus 2, the peer exchange on every
+    rank, both start-up self-tests passing, per-rank records and a finite whole-job value."""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ, USV_RANKS_SHARE_DEVICE="0", USV_DIST_BACKEND="gloo", USV_DP_EXCHANGE="peer",
+               USV_DP_TIMEOUT_MS="10000")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_port()),
+                          os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+                          "--envs", "8192", "--no-cpu-baseline", "--c2-steps", "0", "--milestone-seconds", "0"],
+                         capture_output=True, text=True, timeout=240, cwd=str(tmp_path), env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["steps"] == 2
+    assert line["config"]["exchange"] == "peer"
+    assert line["extra"]["dp_selftest"] == {"0": "pass", "1": "pass"}
+    assert [r["rank"] for r in line["extra"]["ranks"]] == [0, 1]
+    assert np.isfinite(line["value"]) and line["value"] > 0
