@@ -87,6 +87,58 @@ __device__ __forceinline__ float usv_sin(float x) {
   usv_sincos(x, &s, &c);
   return s;
 }
+// exp, tanh and atan2 of the observation / reward formulas, by the same rule (oracle/usv_oracle.c restates them):
+// Cephes' single-precision reductions and minimax polynomials in plain IEEE multiplies, adds and divisions, the
+// power of two by ldexpf (exact).  Within 2 ulp of float64 libm on the ranges the step uses (CPU tests).
+__device__ __forceinline__ float usv_exp(float x) {
+  if (x != x) return x;
+  if (x > 88.72283f) return INFINITY;
+  if (x < -103.97208f) return 0.f;
+  const float k = rintf(x * 1.44269504088896341f);
+  float r = x - k * 0.693359375f;
+  r = r - k * -2.12194440e-4f;
+  const float z = r * r;
+  float p = 1.9875691500e-4f;
+  p = p * r + 1.3981999507e-3f;
+  p = p * r + 8.3334519073e-3f;
+  p = p * r + 4.1665795894e-2f;
+  p = p * r + 1.6666665459e-1f;
+  p = p * r + 5.0000001201e-1f;
+  p = p * z + r + 1.0f;
+  return ldexpf(p, (int)k);
+}
+__device__ __forceinline__ float usv_tanh(float x) {
+  const float ax = fabsf(x);
+  float y;
+  if (ax < 0.625f) {
+    const float z = x * x;
+    y = ((((-5.70498872745e-3f * z + 2.06390887954e-2f) * z - 5.37397155531e-2f) * z + 1.33314422036e-1f) * z -
+         3.33332819422e-1f) * z * x + x;
+  } else {
+    y = ax > 9.0f ? 1.0f : 1.0f - 2.0f / (usv_exp(ax + ax) + 1.0f);
+    y = copysignf(y, x);
+  }
+  return y;
+}
+__device__ __forceinline__ float usv_atan2(float y, float x) {
+  if (x != x || y != y) return x + y;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float r;
+  if (ax == 0.f && ay == 0.f) {
+    r = signbit(x) ? 3.14159265358979323846f : 0.f;
+  } else {
+    const float a = ay / ax;   // +inf where x = 0
+    float t, base, blo;       // base = hi + lo parts of 0, pi / 4, pi / 2
+    if (a > 2.414213562373095f) { t = -1.0f / a; base = 1.57079637f; blo = -4.371139e-08f; }
+    else if (a > 0.4142135623730950f) { t = (a - 1.0f) / (a + 1.0f); base = 0.785398185f; blo = -2.1855694e-08f; }
+    else { t = a; base = 0.f; blo = 0.f; }
+    const float z = t * t;
+    r = base + (((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) *
+                 z * t + t) + blo);
+    if (signbit(x)) r = (3.14159274f - r) + -8.742278e-08f;
+  }
+  return copysignf(r, y);
+}
 
 // cell centre i of the potential field's grid (BatchedMapGPU's torch.linspace of the cell centres,
 // d_multi_gemini.py:40-48), or the override table (parity tests)

@@ -539,7 +539,7 @@ __device__ __forceinline__ float field_blend(const usv_cfg_t &c, const FieldTaps
 
 __device__ __forceinline__ float pen_scalar(int kind, float k, float x0, float cc, float x) {
   if (kind == PEN_DEADZONE) return -maxf(fabsf(x) - x0, 0.f) * k + cc;
-  if (kind == PEN_EXPABS) return (expf(x0 * fabsf(x)) - 1.0f) * k + cc;
+  if (kind == PEN_EXPABS) return (usv_exp(x0 * fabsf(x)) - 1.0f) * k + cc;
   return 0.f;
 }
 
@@ -572,7 +572,7 @@ __device__ __forceinline__ RewardOut reward_tail(const usv_cfg_t &c, const Rewar
   const float prev_pot = pot_is_prev ? pot : prev_pot_mem;
   float praw = (prev_pot - pot) * 100.0f;
   if (fabsf(praw) < 0.01f) praw = 0.f;
-  const float pa1 = 2.0f * tanhf(div_rn(praw, kPa, 1.0f / kPa));
+  const float pa1 = 2.0f * usv_tanh(div_rn(praw, kPa, 1.0f / kPa));
   const float ppos = maxf(pa1, 0.f), pneg = minf(pa1, 0.f);
   o.gate_pos = (ppos < 0.5f) ? 1.0f : p.ggate;
   o.shaping = o.gate_pos * ppos + pneg;
@@ -994,18 +994,18 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     float yawn = yaw;
     if (c.head_noise_on) yawn = yawn + (u[SU_HEAD] * K.head_rng + c.head_noise_min);
     float hs, hc;
-    sincosf(yawn, &hs, &hc);
+    usv_sincos(yawn, &hs, &hc);
     // ---- get_state_observations (static_obs.py:193-299) ----
     const float ex = tgx - pxn, ey = tgy - pyn;
-    const float theta = atan2f(hs, hc);
-    const float beta = atan2f(ey, ex);
+    const float theta = usv_atan2(hs, hc);
+    const float beta = usv_atan2(ey, ex);
     const float alpha = fmodf((beta - theta) + USV_PI_F, USV_2PI_F) - USV_PI_F;
     const float herr = fabsf(alpha);
     const float dist = sqrtf(ex * ex + ey * ey);
     const float dist_n = tnorm2(ex, ey);
     float st, ct, sa, ca;
-    sincosf(theta, &st, &ct);
-    sincosf(alpha, &sa, &ca);     // cos is even: ca == cosf(herr) as well
+    usv_sincos(theta, &st, &ct);
+    usv_sincos(alpha, &sa, &ca);     // usv_sincos's cos is exactly even: ca == cos(herr) as well
     // 16 obstacle distances; the 5 nearest (torch.topk largest=False, ascending) by a
     // selection network over (distance bits, index) keys -- distances are >= 0 so
     // their bit patterns order like the floats
@@ -1068,10 +1068,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     RewardPre rp;
     if (c.reward_mode == 0) rp.dist_r0 = c.position_scale * (prev_err - dist);
     else if (c.reward_mode == 1) rp.dist_r0 = c.position_scale * (prev_err * prev_err - dist * dist);
-    else rp.dist_r0 = c.position_scale * (expf(div_rn(-dist, c.exp_coeff, K.inv_exp_coeff)) -
-                                          expf(div_rn(-prev_err, c.exp_coeff, K.inv_exp_coeff)));
+    else rp.dist_r0 = c.position_scale * (usv_exp(div_rn(-dist, c.exp_coeff, K.inv_exp_coeff)) -
+                                          usv_exp(div_rn(-prev_err, c.exp_coeff, K.inv_exp_coeff)));
     const float h2 = herr * herr;
-    rp.align0 = c.align_la1 * (expf(c.align_la2 * (h2 * h2)) + expf(c.align_la3 * h2));
+    rp.align0 = c.align_la1 * (usv_exp(c.align_la2 * (h2 * h2)) + usv_exp(c.align_la3 * h2));
     if (was_reset) rp.dist_r0 = 0.f;
     const float prev_dist = was_reset ? dist : (rew_valid ? prev_d_mem : dist);
     rp.g = clampt(ca, 0.f, 1.f);
@@ -1089,11 +1089,11 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     rp.turning = fabsf(wzn) > 0.2f ? 1.f : 0.f;
     const float vfwd = vxn * hc + vyn * hs;
     rp.sf = clampt(div_rn(fabsf(vfwd) - 0.15f, kSf, 1.0f / kSf), 0.f, 1.f);
-    rp.speed_r = (1.0f - expf(div_rn(-vtp, kSp, 1.0f / kSp))) * 0.05f;
+    rp.speed_r = (1.0f - usv_exp(div_rn(-vtp, kSp, 1.0f / kSp))) * 0.05f;
     const float sgn = (alpha > 0.f) ? 1.f : ((alpha < 0.f) ? -1.f : 0.f);
     const float tang = (herr > 1.0f) ? sgn * 1.0f : sgn * 0.2f;
     const float dw = wzn - tang;
-    rp.ang_r = expf(div_rn(-(dw * dw), kAn, 1.0f / kAn)) * 0.03f;
+    rp.ang_r = usv_exp(div_rn(-(dw * dw), kAn, 1.0f / kAn)) * 0.03f;
     rp.goal_r = ((float)goal_cnt * c.goal_reward) * 5.0f;
     rp.coll = coll;
     bst(R, w.prev_dist, vs, dist);
@@ -1259,7 +1259,7 @@ __global__ __launch_bounds__(64) void k_env_reward_late(usv_cfg_t c, usv_bufs_t 
 __device__ __forceinline__ float task_term(int mode, float x, float coeff) {
   if (mode == 0) return 1.0f / (1.0f + x);
   if (mode == 1) return 1.0f / (1.0f + x * x);
-  return expf(-x / coeff);
+  return usv_exp(-x / coeff);
 }
 
 template <int kKind, bool kStats, bool kInj>
@@ -1430,7 +1430,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
   float yawn = yaw;
   if (c.head_noise_on) yawn = yawn + (u[SU_HEAD] * K.head_rng + c.head_noise_min);
   float hs, hc;
-  sincosf(yawn, &hs, &hc);
+  usv_sincos(yawn, &hs, &hc);
   // ---- Core.update_observation_tensor (USV_core.py:55-121) ----
   if (c.obs_local) {
     put(0, hc * vxn + hs * vyn);
@@ -1470,14 +1470,16 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
   if (kKind == USV_TASK_GO_TO_POSE) {
     // GoToPoseTask.get_state_observations (:89-130)
     const float ex = tgx - pxn, ey = tgy - pyn;
-    const float theta = atan2f(hs, hc);
-    const float beta = atan2f(ey, ex);
+    const float theta = usv_atan2(hs, hc);
+    const float beta = usv_atan2(ey, ex);
     const float alpha = fmodf((beta - theta) + USV_PI_F, USV_2PI_F) - USV_PI_F;
     const float hraw = fmodf((tgh - theta) + USV_PI_F, USV_2PI_F) - USV_PI_F;
-    const float herr = atan2f(sinf(hraw), cosf(hraw));
+    float shr, chr;
+    usv_sincos(hraw, &shr, &chr);
+    const float herr = usv_atan2(shr, chr);
     float sa, ca, sh, ch;
-    sincosf(alpha, &sa, &ca);
-    sincosf(herr, &sh, &ch);
+    usv_sincos(alpha, &sa, &ca);
+    usv_sincos(herr, &sh, &ch);
     put(3, ca);
     put(4, sa);
     put(5, tnorm2(ex, ey));
@@ -1492,7 +1494,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
     const int gir = (pdist < c.position_tolerance) & (speed < 0.1f);
     goal_cnt = goal_cnt0 * gir + gir;
     // GoToPoseReward.compute_reward (USV_task_rewards.py:190-233)
-    const float hw = 1.0f - 1.0f / (1.0f + expf(-c.sig_gain * (pdist - 2.0f)));
+    const float hw = 1.0f - 1.0f / (1.0f + usv_exp(-c.sig_gain * (pdist - 2.0f)));
     const float pos_r = c.tk_scale[0] * task_term(c.tk_mode[0], pdist, c.tk_coeff[0]);
     const float head_r = hw * c.tk_scale[1] * task_term(c.tk_mode[1], hdist, c.tk_coeff[1]);
     const float act_pen = -0.05f * (fabsf(cmd0) + fabsf(cmd1));

@@ -292,6 +292,16 @@ def sincos(x):
     return s, c
 
 
+def math3(x, y):
+    """The observation / reward functions (usv_oracle.c:usv_exp, usv_tanh, usv_atan2) of float32 arrays:
+    (exp(x), tanh(x), atan2(y, x))."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.ascontiguousarray(y, np.float32)
+    e, t, a = np.empty_like(x), np.empty_like(x), np.empty_like(x)
+    lib().oracle_math(_p(x), _p(y), ctypes.c_int(x.size), _p(e), _p(t), _p(a))
+    return e, t, a
+
+
 def philox(ctr, key):
     c = np.ascontiguousarray(ctr, np.uint32)
     k = np.ascontiguousarray(key, np.uint32)

@@ -88,6 +88,67 @@ void oracle_sincos(const float *x, int n, float *s, float *c) {
 static inline float usv_sin(float x) { float s, c; usv_sincos(x, &s, &c); return s; }
 static inline float usv_cos(float x) { float s, c; usv_sincos(x, &s, &c); return c; }
 
+/* exp, tanh and atan2 of the observation / reward formulas (the reference's torch.exp / torch.tanh / torch.atan2 in
+ * float32), by the same rule as usv_sincos: this build's functions, restated operation for operation from
+ * csrc/usv_device.h (Cephes' single-precision reductions and polynomials; the power of two by ldexpf, exact), so the
+ * device's observations and rewards are the oracle's bits.  Accuracy against float64 libm: CPU tests. */
+float usv_exp(float x) {
+  if (x != x) return x;
+  if (x > 88.72283f) return INFINITY;
+  if (x < -103.97208f) return 0.f;
+  const float k = rintf(x * 1.44269504088896341f);
+  float r = x - k * 0.693359375f;
+  r = r - k * -2.12194440e-4f;
+  const float z = r * r;
+  float p = 1.9875691500e-4f;
+  p = p * r + 1.3981999507e-3f;
+  p = p * r + 8.3334519073e-3f;
+  p = p * r + 4.1665795894e-2f;
+  p = p * r + 1.6666665459e-1f;
+  p = p * r + 5.0000001201e-1f;
+  p = p * z + r + 1.0f;
+  return ldexpf(p, (int)k);
+}
+float usv_tanh(float x) {
+  const float ax = fabsf(x);
+  float y;
+  if (ax < 0.625f) {
+    const float z = x * x;
+    y = ((((-5.70498872745e-3f * z + 2.06390887954e-2f) * z - 5.37397155531e-2f) * z + 1.33314422036e-1f) * z -
+         3.33332819422e-1f) * z * x + x;
+  } else {
+    y = ax > 9.0f ? 1.0f : 1.0f - 2.0f / (usv_exp(ax + ax) + 1.0f);
+    y = copysignf(y, x);
+  }
+  return y;
+}
+float usv_atan2(float y, float x) {
+  if (x != x || y != y) return x + y;
+  const float ax = fabsf(x), ay = fabsf(y);
+  float r;
+  if (ax == 0.f && ay == 0.f) {
+    r = signbit(x) ? 3.14159265358979323846f : 0.f;
+  } else {
+    const float a = ay / ax;   /* +inf where x = 0 */
+    float t, base, blo;       /* base = hi + lo parts of 0, pi / 4, pi / 2 */
+    if (a > 2.414213562373095f) { t = -1.0f / a; base = 1.57079637f; blo = -4.371139e-08f; }
+    else if (a > 0.4142135623730950f) { t = (a - 1.0f) / (a + 1.0f); base = 0.785398185f; blo = -2.1855694e-08f; }
+    else { t = a; base = 0.f; blo = 0.f; }
+    const float z = t * t;
+    r = base + (((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) *
+                 z * t + t) + blo);
+    if (signbit(x)) r = (3.14159274f - r) + -8.742278e-08f;
+  }
+  return copysignf(r, y);
+}
+void oracle_math(const float *x, const float *y, int n, float *e, float *t, float *a) {
+  for (int i = 0; i < n; ++i) {
+    e[i] = usv_exp(x[i]);
+    t[i] = usv_tanh(x[i]);
+    a[i] = usv_atan2(y[i], x[i]);
+  }
+}
+
 /* ------------------------------------------------------------------------ */
 /* Philox streams (same mapping as the kernels)                              */
 /* ------------------------------------------------------------------------ */
@@ -488,7 +549,7 @@ float oracle_sample_field(const float *F, float map_size, float x, float y) { re
 static float pen_scalar(int kind, float k, float x0, float cc, float x) {
   switch (kind) {
     case PEN_DEADZONE: return -maxf_(fabsf(x) - x0, 0.f) * k + cc;
-    case PEN_EXPABS: return (expf(x0 * fabsf(x)) - 1.0f) * k + cc;
+    case PEN_EXPABS: return (usv_exp(x0 * fabsf(x)) - 1.0f) * k + cc;
     default: return 0.f;
   }
 }
@@ -977,13 +1038,13 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
       const float rng = (float)((double)c->head_noise_max - (double)c->head_noise_min);
       yawn = yawn + (u[SU_HEAD] * rng + c->head_noise_min);
     }
-    const float hc = cosf(yawn), hs = sinf(yawn);
+    const float hc = usv_cos(yawn), hs = usv_sin(yawn);
     /* ---- get_observations -> CaptureXYTask.get_state_observations (static_obs.py:193-299) ---- */
     float obs[USV_NOBS];
     memset(obs, 0, sizeof(obs));
     const float ex = E->tgt_x[e] - px, ey = E->tgt_y[e] - py;
-    const float theta = atan2f(hs, hc);
-    const float beta = atan2f(ey, ex);
+    const float theta = usv_atan2(hs, hc);
+    const float beta = usv_atan2(ey, ex);
     const float alpha = fmodf((beta - theta) + PI_F, TWO_PI_F) - PI_F;
     const float herr = fabsf(alpha);
     const float dist = sqrtf(ex * ex + ey * ey);       /* compute_reward :338 */
@@ -1004,10 +1065,10 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
         if (!used[o] && (best < 0 || od[o] < od[best])) best = o;
       used[best] = 1; sel[q] = best;
     }
-    const float ct = cosf(theta), st = sinf(theta);
+    const float ct = usv_cos(theta), st = usv_sin(theta);
     float task[5 + 3 * USV_NCLOSE];
     memset(task, 0, sizeof(task));
-    task[0] = cosf(alpha); task[1] = sinf(alpha); task[2] = dist_n;
+    task[0] = usv_cos(alpha); task[1] = usv_sin(alpha); task[2] = dist_n;
     for (int q = 0; q < USV_NCLOSE; ++q) {
       const int o = sel[q];
       const float bx = orx[o] * ct + ory[o] * st;
@@ -1041,9 +1102,9 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
     float dist_r;
     if (c->reward_mode == 0) dist_r = c->position_scale * (prev_err - dist);
     else if (c->reward_mode == 1) dist_r = c->position_scale * (prev_err * prev_err - dist * dist);
-    else dist_r = c->position_scale * (expf(-dist / c->exp_coeff) - expf(-prev_err / c->exp_coeff));
+    else dist_r = c->position_scale * (usv_exp(-dist / c->exp_coeff) - usv_exp(-prev_err / c->exp_coeff));
     const float h2 = herr * herr;
-    float align_r = c->align_la1 * (expf(c->align_la2 * (h2 * h2)) + expf(c->align_la3 * h2));
+    float align_r = c->align_la1 * (usv_exp(c->align_la2 * (h2 * h2)) + usv_exp(c->align_la3 * h2));
     if (was_reset) dist_r = 0.f;                                          /* :374 */
     const float prev_dist = was_reset ? dist : (rew_valid ? E->prev_dist[e] : dist);  /* :361-380 */
     float pot = sample_field(E->field + (size_t)e * USV_GRID2, c->map_size, px, py);
@@ -1063,7 +1124,7 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
     const float danger = xs * xs * (3.0f - 2.0f * xs);
     align_r = align_r * maxf_(0.3f, 1.0f - danger);
     dist_r = dist_r * maxf_(0.6f, 1.0f - danger * 0.5f);
-    const float g = clampf_(cosf(herr), 0.f, 1.f);
+    const float g = clampf_(usv_cos(herr), 0.f, 1.f);
     dist_r = minf_(dist_r, 0.f) + g * maxf_(dist_r, 0.f);
     float prev_h = (rew_valid && !was_reset) ? E->prev_head[e] : herr;
     float hi = clampf_(prev_h - herr, -0.4f, 0.4f);
@@ -1073,7 +1134,7 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
     float praw = (prev_pot - pot) * 100.0f;
     const float praw_in = praw;   /* before the dead zone (dbg[11]: the tests' discontinuity margins) */
     if (fabsf(praw) < 0.01f) praw = 0.f;
-    const float pa1 = 2.0f * tanhf(praw / (2.0f + 1e-6f));
+    const float pa1 = 2.0f * usv_tanh(praw / (2.0f + 1e-6f));
     const float gdx = ex / (dist + 1e-6f), gdy = ey / (dist + 1e-6f);
     const float vtow = vxn * gdx + vyn * gdy;
     const float vtp = maxf_(vtow, 0.f);
@@ -1092,11 +1153,11 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
     const float sf = clampf_((fabsf(vfwd) - 0.15f) / ((0.60f - 0.15f) + 1e-6f), 0.f, 1.f);
     const float turn_haz = (float)(worsening && turning) * (-10.0f) * (g * g) * sf;
     E->prev_pot[e] = pot;
-    const float speed_r = (1.0f - expf(-vtp / (0.8f + 1e-6f))) * 0.05f;
+    const float speed_r = (1.0f - usv_exp(-vtp / (0.8f + 1e-6f))) * 0.05f;
     float sgn = (alpha > 0.f) ? 1.f : ((alpha < 0.f) ? -1.f : 0.f);
     const float tang = (herr > 1.0f) ? sgn * 1.0f : sgn * 0.2f;
     const float dw = wzn - tang;
-    const float ang_r = expf(-(dw * dw) / 0.2f) * 0.03f;
+    const float ang_r = usv_exp(-(dw * dw) / 0.2f) * 0.03f;
     float coll = 0.f;
     for (int o = 0; o < USV_NOBST; ++o) coll += (float)(od[o] < c->collision_threshold) * (-10.0f) * 10.0f;
     const float goal_r = ((float)E->goal_cnt[e] * c->goal_reward) * 5.0f;
@@ -1170,7 +1231,44 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
 static float task_term(int mode, float x, float coeff) {
   if (mode == 0) return 1.0f / (1.0f + x);
   if (mode == 1) return 1.0f / (1.0f + x * x);
-  return expf(-x / coeff);
+  return usv_exp(-x / coeff);
+}
+
+/* torch.square(ang_err).sum(-1) over ALL envs (USV_track_xyo_velocity.py:121-123): the sum in the order the device
+ * forms it (the reference's reduction order is torch's, unspecified), so the two agree bit for bit -- per 64-env wave
+ * a butterfly (partners 32, 16, .., 1 apart), per 256-env block the four wave sums in order, then thread t of one
+ * 256-thread block adds blocks t, t + 256, .. in order and a halving tree folds the 256 thread sums
+ * (csrc/usv_env.hip: k_env_step_task's wave_sum / block partial, k_track_finish). */
+static float track_ang_sum(const float *sq, int n) {
+  const int nblk = (n + 255) / 256;
+  float *part = (float *)calloc((size_t)nblk, sizeof(float));
+  for (int blk = 0; blk < nblk; ++blk) {
+    float sblk = 0.f;
+    for (int w = 0; w < 4; ++w) {
+      float v[64];
+      for (int l = 0; l < 64; ++l) {
+        const int e = blk * 256 + w * 64 + l;
+        v[l] = e < n ? sq[e] : 0.f;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        float nv[64];
+        for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+        memcpy(v, nv, sizeof(v));
+      }
+      sblk += v[0];
+    }
+    part[blk] = sblk;
+  }
+  float red[256];
+  for (int t = 0; t < 256; ++t) {
+    float acc = 0.f;
+    for (int i = t; i < nblk; i += 256) acc += part[i];
+    red[t] = acc;
+  }
+  for (int w = 128; w > 0; w >>= 1)
+    for (int t = 0; t < w; ++t) red[t] += red[t + w];
+  free(part);
+  return red[0];
 }
 
 static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const float *U) {
@@ -1179,7 +1277,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
   const float PI_F = (float)OPI, TWO_PI_F = (float)(2.0 * OPI);
   const int track = c->task_kind == USV_TASK_TRACK_XYO;
   /* TrackXYOVelocity: torch.square(ang_err).sum(-1) of a 1-D tensor sums over ALL envs (:121-123) */
-  double ang_sq = 0.0;
+  float *ang_sq_e = (float *)calloc((size_t)n, sizeof(float));
   float *lin_r = (float *)malloc(sizeof(float) * (size_t)n), *pen_v = (float *)malloc(sizeof(float) * (size_t)n);
   int *lin_ok = (int *)malloc(sizeof(int) * (size_t)n), *pkill = (int *)malloc(sizeof(int) * (size_t)n);
   for (int e = 0; e < n; ++e) {
@@ -1205,7 +1303,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
       const float rng = (float)((double)c->head_noise_max - (double)c->head_noise_min);
       yawn = yawn + (u[SU_HEAD] * rng + c->head_noise_min);
     }
-    const float hc = cosf(yawn), hs = sinf(yawn);
+    const float hc = usv_cos(yawn), hs = usv_sin(yawn);
     float obs[USV_NOBS];
     memset(obs, 0, sizeof(obs));
     if (c->obs_local) {
@@ -1237,13 +1335,13 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
     if (!track) {
       /* GoToPoseTask.get_state_observations (:89-130) */
       const float ex = E->tgt_x[e] - px, ey = E->tgt_y[e] - py;
-      const float theta = atan2f(hs, hc);
-      const float beta = atan2f(ey, ex);
+      const float theta = usv_atan2(hs, hc);
+      const float beta = usv_atan2(ey, ex);
       const float alpha = fmodf((beta - theta) + PI_F, TWO_PI_F) - PI_F;
       const float hraw = fmodf((E->tgt_h[e] - theta) + PI_F, TWO_PI_F) - PI_F;
-      const float herr = atan2f(sinf(hraw), cosf(hraw));
-      obs[3] = cosf(alpha); obs[4] = sinf(alpha); obs[5] = tnorm2(ex, ey);
-      obs[6] = cosf(herr); obs[7] = sinf(herr);
+      const float herr = usv_atan2(usv_sin(hraw), usv_cos(hraw));
+      obs[3] = usv_cos(alpha); obs[4] = usv_sin(alpha); obs[5] = tnorm2(ex, ey);
+      obs[6] = usv_cos(herr); obs[7] = usv_sin(herr);
       /* compute_reward (:134-181) */
       const float pdist = sqrtf(ex * ex + ey * ey);
       const float hdist = fabsf(herr);
@@ -1252,7 +1350,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
       const float speed = tnorm2(vxn, vyn);
       const int gir = (pdist < c->position_tolerance) && (speed < 0.1f);
       E->goal_cnt[e] = E->goal_cnt[e] * gir + gir;
-      const float hw = 1.0f - 1.0f / (1.0f + expf(-c->sig_gain * (pdist - 2.0f)));
+      const float hw = 1.0f - 1.0f / (1.0f + usv_exp(-c->sig_gain * (pdist - 2.0f)));
       const float pos_r = c->tk_scale[0] * task_term(c->tk_mode[0], pdist, c->tk_coeff[0]);
       const float head_r = hw * c->tk_scale[1] * task_term(c->tk_mode[1], hdist, c->tk_coeff[1]);
       const float act_pen = -0.05f * (fabsf(cmd[0]) + fabsf(cmd[1]));
@@ -1272,7 +1370,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
       obs[3] = lex; obs[4] = ley; obs[5] = aerr;
       const float pos_d = sqrtf(px * px + py * py);
       const float lin_d = sqrtf(lex * lex + ley * ley);
-      ang_sq += (double)(aerr * aerr);
+      ang_sq_e[e] = aerr * aerr;
       lin_r[e] = task_term(c->tk_mode[0], lin_d, c->tk_coeff[0]) * c->tk_scale[0];
       lin_ok[e] = lin_d < c->tk_tol[0];
       pkill[e] = pos_d > c->kill_dist;
@@ -1299,7 +1397,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
     E->just_reset[e] = 0;
   }
   if (track) {   /* TrackXYOVelocityTask.compute_reward / update_kills (:103-166) with the all-env angular distance */
-    const float ang_d = sqrtf((float)ang_sq);
+    const float ang_d = sqrtf(track_ang_sum(ang_sq_e, n));
     const int ang_ok = ang_d < c->tk_tol[1];
     const float ang_r = task_term(c->tk_mode[1], ang_d, c->tk_coeff[1]) * c->tk_scale[1];
     for (int e = 0; e < n; ++e) {
@@ -1315,7 +1413,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
       }
     }
   }
-  free(lin_r); free(pen_v); free(lin_ok); free(pkill);
+  free(lin_r); free(pen_v); free(lin_ok); free(pkill); free(ang_sq_e);
   E->ctl[USV_CTL_POT_VALID] = 1;
   E->ctl[USV_CTL_PEN_VALID] = 1;
   E->ctl[USV_CTL_REW_VALID] = 1;

@@ -258,6 +258,35 @@ def test_integrator_sincos_accuracy(lo, hi):
     assert s0[0] == 0.0 and c0[0] == 1.0
 
 
+def test_obs_reward_math_accuracy():
+    """The observation / reward functions (usv_oracle.c:usv_exp, usv_tanh, usv_atan2 == csrc/usv_device.h) against
+    float64 libm: exp within 1 ulp over its whole normal range, tanh within 1.5 ulp, atan2 within 2.6 ulp (3e-7
+    absolute) on random and unit-circle arguments; IEEE atan2's signed zeros and pi at the origin."""
+    def ulps(got, ref):
+        sp = np.spacing(np.abs(ref.astype(np.float32))).astype(np.float64)
+        return np.abs(got.astype(np.float64) - ref) / np.maximum(sp, 1e-45)
+    x = np.linspace(-87.0, 88.0, 1_000_001).astype(np.float32)
+    e, _, _ = O.math3(x, np.ones_like(x))
+    ref = np.exp(x.astype(np.float64))
+    assert ulps(e[ref > 1.2e-38], ref[ref > 1.2e-38]).max() <= 1.0
+    x = np.linspace(-10.0, 10.0, 1_000_001).astype(np.float32)
+    _, t, _ = O.math3(x, np.ones_like(x))
+    ref = np.tanh(x.astype(np.float64))
+    assert ulps(t[ref != 0], ref[ref != 0]).max() <= 1.5
+    rng = np.random.default_rng(0)
+    xx, yy = rng.normal(0, 10, 1_000_000).astype(np.float32), rng.normal(0, 10, 1_000_000).astype(np.float32)
+    th = np.linspace(-np.pi, np.pi, 1_000_001)
+    xx = np.concatenate([xx, np.cos(th).astype(np.float32)])
+    yy = np.concatenate([yy, np.sin(th).astype(np.float32)])
+    _, _, a = O.math3(xx, yy)
+    ref = np.arctan2(yy.astype(np.float64), xx.astype(np.float64))
+    assert ulps(a, ref).max() <= 2.6 and np.abs(a - ref).max() < 3e-7
+    ys = np.array([0.0, -0.0, 0.0, -0.0, 1.0, -1.0], np.float32)
+    xs = np.array([0.0, 0.0, -0.0, -0.0, 0.0, 0.0], np.float32)
+    np.testing.assert_array_equal(np.signbit(O.math3(xs, ys)[2]), np.signbit(np.arctan2(ys, xs)))
+    np.testing.assert_allclose(O.math3(xs, ys)[2], np.arctan2(ys, xs), rtol=1e-7)
+
+
 def test_penalty_parser():
     c = {"c1": 0.3, "c2": 0.1}
     assert parse_penalty_fn("lambda x,step: -torch.clamp(torch.abs(x) - 0.4, min=0.0) * 0.02", c) == \
