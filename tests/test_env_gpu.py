@@ -289,6 +289,31 @@ def test_philox_mode_matches_oracle(n, T):
     np.testing.assert_array_equal(task.obst.cpu().numpy().reshape(16, 2, n), E.obst)
 
 
+def test_philox_long_horizon_bit_exact():
+    """100 steps at 1,024 envs with 30-step episodes (every env resets three times or more: fresh DR draws,
+    spawns, obstacle placements and potential fields, the cached pre-reset state of C.1, the batch-global field
+    maxima of every reset batch): the device's step stays the oracle's bit for bit throughout (_vs_oracle)."""
+    task_cfg = load_yaml(TEST_YAML)
+    task_cfg["env"]["maxEpisodeLength"] = 30
+    n, T = 1024, 100
+    task = _task(task_cfg, n)
+    E = _oracle_for(task.cfg, n, task_cfg)
+    rng = np.random.default_rng(11)
+    dp = np.zeros(n)
+    resets = 0
+    for t in range(T):
+        a = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        bias = task.current_action_bias()
+        obs, rew, dones = task.env_step(torch.tensor(a, device=DEV))
+        oracle_step(task, E, a, bias, t)
+        torch.cuda.synchronize()
+        dp = _vs_oracle("philox_long", task, E, obs, rew, dones, t, dp)
+        resets += int(E.reset_buf.sum())
+    ET.check("philox_long", "stats", task.stats.cpu().numpy().T, E.stats.T, 0.0, 0.0,
+             [f"s{j}" for j in range(E.stats.shape[0])])
+    assert resets >= 3 * n
+
+
 @pytest.mark.parametrize("frame", ["local", "global"])
 def test_philox_priv4_matches_oracle(frame):
     """priv_dim 4 (every reference yaml but TEST): 29-column rows, the slab's 4 pad columns stay 0."""
