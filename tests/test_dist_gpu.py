@@ -243,3 +243,64 @@ def test_bench_two_ranks_on_one_device(tmp_path):
     assert line["extra"]["dp_selftest"] == {"0": "pass", "1": "pass"}
     assert [r["rank"] for r in line["extra"]["ranks"]] == [0, 1]
     assert np.isfinite(line["value"]) and line["value"] > 0
+
+
+def _worker_rccl_one_rank(rank, port, out_dir):
+    """The nccl (RCCL) backend on the one GPU a box has: world size 1, the split update path (USV_PPO_FUSED=0)
+    with the fallback's collective -- dist_util.allreduce_grad's SUM all-reduce of [grad, kl] -- forced into
+    every minibatch, eagerly and captured in the update's HIP graph (the USV_GRAPH_COLLECTIVES form)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", LOCAL_RANK="0", WORLD_SIZE="1",
+                      USV_DIST_BACKEND="nccl", USV_PPO_FUSED="0")
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import NPARAM
+    try:
+        data, rows = _dataset(N * H), np.arange(N * H)
+        calls = []
+
+        def with_allreduce(ag):
+            def allreduce():   # a2c_common.py:309-323 on one rank: SUM over one rank is the identity, scale 1
+                dist.all_reduce(ag.grad[:NPARAM + 1], op=dist.ReduceOp.SUM)
+                calls.append(1)
+                return 1.0
+            ag._allreduce_grad = allreduce
+            return ag
+
+        eager = with_allreduce(_agent(N, MB, True))
+        assert dist.get_backend() == "nccl" and eager.rank_size == 1
+        _load(eager, data, rows)
+        eager.update_epoch_minibatches()
+        torch.cuda.synchronize()
+        n_eager = len(calls)
+        graph = with_allreduce(_agent(N, MB, True))
+        _load(graph, data, rows)
+        g = graph._graph_capture(graph.update_epoch_minibatches)   # records the all-reduces, runs nothing
+        g.replay()
+        torch.cuda.synchronize()
+        plain = _agent(N, MB, False)          # the same split path without any collective
+        _load(plain, data, rows)
+        plain.update_epoch_minibatches()
+        torch.cuda.synchronize()
+        np.savez(os.path.join(out_dir, "rccl.npz"), eager=eager.model_params.cpu().numpy(),
+                 graph=graph.model_params.cpu().numpy(), plain=plain.model_params.cpu().numpy(),
+                 kl_eager=eager.kls.cpu().numpy(), kl_graph=graph.kls.cpu().numpy(), kl_plain=plain.kls.cpu().numpy(),
+                 n_eager=n_eager, n_capture=len(calls) - n_eager, minibatches=EPOCHS * N * H // MB)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_fallback_collective_on_one_rank(tmp_path):
+    """The RCCL fallback path executes: nccl process group, the flat-gradient SUM all-reduce per minibatch of the
+    split update, eager and inside a captured HIP graph; both leave the weights and KLs bit-identical to the same
+    update without a collective (one rank: the all-reduce is the identity).  Two ranks cannot share one GPU under
+    nccl, so the multi-rank sums stay with the gloo tests above and the driver's multi-GPU run."""
+    import torch.multiprocessing as mp
+    mp.spawn(_worker_rccl_one_rank, args=(_port(), str(tmp_path)), nprocs=1, join=True)
+    r = np.load(tmp_path / "rccl.npz")
+    assert int(r["n_eager"]) == int(r["minibatches"]) == int(r["n_capture"])
+    np.testing.assert_array_equal(r["eager"], r["plain"])
+    np.testing.assert_array_equal(r["graph"], r["plain"])
+    np.testing.assert_array_equal(r["kl_eager"], r["kl_plain"])
+    np.testing.assert_array_equal(r["kl_graph"], r["kl_plain"])
+    assert not np.array_equal(r["plain"], _agent(N, MB, False).model_params.cpu().numpy())   # the update moved them
