@@ -866,6 +866,16 @@ namespace {
 // stage 1: the obstacle placement alone (k_field_place); stage 2: the rest after it (sweeps, exactness
 // fallback, statistics, batch fold, constants) = stage 3 (sweeps, fallback, statistics) + stage 4 (batch fold,
 // constants)
+// k_field_stats' grid: workgroups loop over (slot, band) items; USV_STATS_GRID caps it (default 4096)
+static int stats_grid(int n) {
+  static const int cap = [] {
+    const char *v = getenv("USV_STATS_GRID");
+    const int x = v ? atoi(v) : 0;
+    return x > 0 ? x : 4096;
+  }();
+  return n * kBands < cap ? n * kBands : cap;
+}
+
 int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream_t s) {
   const int grid_b = b->n < 512 ? b->n : 512;
   const int grid_n = (b->n + 255) / 256 < 64 ? (b->n + 255) / 256 : 64;
@@ -888,7 +898,7 @@ int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream
     USV_CHECK_LAUNCH();
     hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
     USV_CHECK_LAUNCH();
-    const int grid_s = b->n * kBands < 4096 ? b->n * kBands : 4096;
+    const int grid_s = stats_grid(b->n);
     hipLaunchKernelGGL(k_field_stats, dim3(grid_s), dim3(256), 0, s, *cfg, *b);
     USV_CHECK_LAUNCH();
   }
@@ -941,7 +951,7 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
-  const int grid_s = b->n * kBands < 4096 ? b->n * kBands : 4096;
+  const int grid_s = stats_grid(b->n);
   hipLaunchKernelGGL(k_field_stats, dim3(grid_s), dim3(256), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_field_batch, dim3(kBatchBlocks), dim3(256), 0, s, *cfg, *b);
