@@ -545,6 +545,14 @@ __device__ __forceinline__ BatchK batch_k(const usv_cfg_t &c, const usv_bufs_t &
 // (19 column pairs x 3 row groups), so the obstacles that can reach it are few (a per-wave mask)
 // and many of its row strips lie out of every obstacle's reach, where the SDF cannot enter the
 // statistics and a cell contributes only through its cost (the "far" path below).
+// USV_STATS_PIPE=1: k_field_stats loads the next item's costs during the current one (0: at the item's start)
+#ifndef USV_STATS_PIPE
+#define USV_STATS_PIPE 0
+#endif
+// USV_STATS_REG_OBST=1: every obstacle's (gx - ox)^2 and oy in registers across the band (0: the mask's from LDS)
+#ifndef USV_STATS_REG_OBST
+#define USV_STATS_REG_OBST 1
+#endif
 constexpr int kBandRows = 30, kBands = G / kBandRows;       // row bands of a slot
 constexpr int kRowGroups = 3;                               // row groups per wave (rows rg, rg + 3, ...)
 constexpr int kWavePairs = 19;                              // column pairs per wave: 4 waves x 38 >= 150 columns
@@ -552,7 +560,11 @@ constexpr int kBandIters = kBandRows / kRowGroups;          // rows per thread a
 static_assert(G % kBandRows == 0 && kBandRows % kRowGroups == 0 && kWavePairs * kRowGroups <= 64 &&
               4 * 2 * kWavePairs >= G && G % 2 == 0, "k_field_stats geometry");
 static_assert(kSlotObst >= 16 + 12 * kBands, "slot_stats band partials");
+#ifdef USV_STATS_WAVES   // (A/B builds: a minimum of waves per SIMD, i.e. a register budget)
+__global__ __launch_bounds__(256, USV_STATS_WAVES) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
+#else
 __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
+#endif
   __shared__ float red[10][4];
   __shared__ int flags[2];
   __shared__ float slin[G];
@@ -575,20 +587,45 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
   const uint32_t far2 = __float_as_uint(far_d * far_d);
   const int items = count * kBands;
   if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
-  for (int w = blockIdx.x; w < items; w += gridDim.x) {
+  // the band's raw costs (two adjacent cells per row: one 8-byte load), all in flight at once
+  const auto load_costs = [&](int wq, int eq, float2 *dst) {
+    const float *F = b.field + (size_t)eq * FS;     // the raw cost tiles (k_field_wave / k_field_exact)
+#pragma unroll
+    for (int k = 0; k < kBandIters; ++k) {
+      const int r = (wq % kBands) * kBandRows + rgc + kRowGroups * k;
+      dst[k] = *reinterpret_cast<const float2 *>(F + field_idx(r, c0));
+    }
+  };
+  // USV_STATS_PIPE: a software pipeline over the workgroup's items -- the next item's obstacle coordinates and slot
+  // index load at the top of an item, its costs after the current SDF, so they arrive during this item's statistics
+  float2 gA[kBandIters], gB[kBandIters];
+  float so_nx = 0.f;
+#if USV_STATS_PIPE
+  if ((int)blockIdx.x < items) {
+    const int sl = (int)blockIdx.x / kBands;
+    load_costs((int)blockIdx.x, b.reset_ids[sl], gA);
+    if (tid < 2 * USV_NOBST) so_nx = b.slot_stats[(size_t)sl * kSlotStride + kSlotObst + tid];
+  }
+#endif
+  // one item: the statistics of band w % kBands of slot w / kBands from the costs in gv (pipelined: loaded by
+  // the previous item) while the next item's costs load into gnx
+  const auto item = [&](const int w, float2 (&gv)[kBandIters], float2 (&gnx)[kBandIters]) {
     const int slot = w / kBands, band = w % kBands;
-    const int e = b.reset_ids[slot];
-    const float *Fe = b.field + (size_t)e * FS;     // the raw cost tiles (k_field_wave / k_field_exact)
+#if USV_STATS_PIPE
+    if (tid < 2 * USV_NOBST) so[tid] = so_nx;
+    if (tid < 2) flags[tid] = 0;
+    __syncthreads();
+    // the next item (this one again after the last: loads without a branch, so the wait counts stay exact)
+    const int wn = w + (int)gridDim.x < items ? w + (int)gridDim.x : w;
+    const int en = b.reset_ids[wn / kBands];
+    if (tid < 2 * USV_NOBST) so_nx = b.slot_stats[(size_t)(wn / kBands) * kSlotStride + kSlotObst + tid];
+#else
     if (tid < 2 * USV_NOBST) so[tid] = b.slot_stats[(size_t)slot * kSlotStride + kSlotObst + tid];
     if (tid < 2) flags[tid] = 0;
     __syncthreads();
-    // the band's raw costs (two adjacent cells per row: one 8-byte load), all in flight at once
-    float2 gv[kBandIters];
-#pragma unroll
-    for (int k = 0; k < kBandIters; ++k) {
-      const int r = band * kBandRows + rgc + kRowGroups * k;
-      gv[k] = *reinterpret_cast<const float2 *>(Fe + field_idx(r, c0));
-    }
+    load_costs(w, b.reset_ids[slot], gv);
+#endif
+#if USV_STATS_REG_OBST
     float dxa[USV_NOBST], dxb[USV_NOBST], oy[USV_NOBST];
     {
       const float gxa = slin[c0], gxb = slin[c0 + 1];
@@ -601,6 +638,9 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
         oy[o] = so[2 * o + 1];
       }
     }
+#else
+    const float gxa = slin[c0], gxb = slin[c0 + 1];
+#endif
     // Obstacles that can matter to this wave's block: the SDF enters the statistics only through j_raw (0
     // unless dist - 2 r_obs < influence_radius) and the inside test (dist <= 2 r_obs), so an obstacle farther
     // than far_d from the whole block (in x or in y) can only be the minimum of a cell whose SDF is irrelevant
@@ -660,6 +700,7 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       gy[k] = slin[band * kBandRows + rgc + kRowGroups * k];
       a[k] = bb[k] = 0x7F800000u;
     }
+#if USV_STATS_REG_OBST
 #pragma unroll
     for (int o = 0; o < USV_NOBST; ++o) {
       if (!((omask >> o) & 1u)) continue;   // uniform
@@ -670,6 +711,25 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
         bb[k] = min(bb[k], __float_as_uint(fmaf(dy, dy, dxb[o])));
       }
     }
+#else
+    // the mask's obstacles only (a scalar loop over its set bits; the coordinates are LDS broadcasts): no
+    // per-obstacle registers
+    for (uint32_t om = omask; om != 0u; om &= om - 1u) {
+      const int o = __builtin_ctz(om);
+      const float ox = so[2 * o], oyo = so[2 * o + 1];
+      const float da = gxa - ox, db = gxb - ox;
+      const float dxa = da * da, dxb = db * db;
+#pragma unroll
+      for (int k = 0; k < kBandIters; ++k) {
+        const float dy = gy[k] - oyo;
+        a[k] = min(a[k], __float_as_uint(fmaf(dy, dy, dxa)));
+        bb[k] = min(bb[k], __float_as_uint(fmaf(dy, dy, dxb)));
+      }
+    }
+#endif
+#if USV_STATS_PIPE
+    load_costs(wn, en, gnx);
+#endif
 #pragma unroll
     for (int k = 0; k < kBandIters; ++k) {
       // a row strip of the block whose cells all lie out of reach takes the far path (uniform branch)
@@ -711,7 +771,19 @@ __global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) 
       // k_field_batch (one atomic per band on a single address serialised this kernel)
     }
     __syncthreads();
+  };
+#if USV_STATS_PIPE
+  // the two cost buffers in turn: no register copies between items (a copy would wait for the loads)
+  for (int w = blockIdx.x; w < items;) {
+    item(w, gA, gB);
+    w += (int)gridDim.x;
+    if (w >= items) break;
+    item(w, gB, gA);
+    w += (int)gridDim.x;
   }
+#else
+  for (int w = blockIdx.x; w < items; w += gridDim.x) item(w, gA, gB);
+#endif
 }
 
 // ------------------------------------------------------------- pass C2 ---
