@@ -549,9 +549,15 @@ __device__ __forceinline__ BatchK batch_k(const usv_cfg_t &c, const usv_bufs_t &
 #ifndef USV_STATS_PIPE
 #define USV_STATS_PIPE 0
 #endif
-// USV_STATS_REG_OBST=1: every obstacle's (gx - ox)^2 and oy in registers across the band (0: the mask's from LDS)
+// USV_STATS_REG_OBST=1: every obstacle's (gx - ox)^2 and oy in registers across the band (0: the mask's from LDS,
+// 48 fewer VGPRs: with USV_STATS_WAVES 5 waves per SIMD instead of 4, -5% on the kernel late in training)
 #ifndef USV_STATS_REG_OBST
-#define USV_STATS_REG_OBST 1
+#define USV_STATS_REG_OBST 0
+#endif
+// USV_STATS_WAVES: k_field_stats' minimum waves per SIMD (its register budget: 5 -> 96 VGPRs, no spills with the LDS
+// obstacles; 6 spills)
+#ifndef USV_STATS_WAVES
+#define USV_STATS_WAVES 5
 #endif
 constexpr int kBandRows = 30, kBands = G / kBandRows;       // row bands of a slot
 constexpr int kRowGroups = 3;                               // row groups per wave (rows rg, rg + 3, ...)
@@ -560,11 +566,7 @@ constexpr int kBandIters = kBandRows / kRowGroups;          // rows per thread a
 static_assert(G % kBandRows == 0 && kBandRows % kRowGroups == 0 && kWavePairs * kRowGroups <= 64 &&
               4 * 2 * kWavePairs >= G && G % 2 == 0, "k_field_stats geometry");
 static_assert(kSlotObst >= 16 + 12 * kBands, "slot_stats band partials");
-#ifdef USV_STATS_WAVES   // (A/B builds: a minimum of waves per SIMD, i.e. a register budget)
 __global__ __launch_bounds__(256, USV_STATS_WAVES) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
-#else
-__global__ __launch_bounds__(256) void k_field_stats(usv_cfg_t c, usv_bufs_t b) {
-#endif
   __shared__ float red[10][4];
   __shared__ int flags[2];
   __shared__ float slin[G];
