@@ -72,7 +72,12 @@ extern "C" {
 #define RU_TSIN     706     /* TorqueDisturbance.generate_torque:484-494 (freq, shift, amp) */
 #define RU_TCONST   709     /* :500-506 (r, sign draw) */
 #define RU_GOAL_H   711     /* GoToPoseTask.get_goals:248 heading / TrackXYOVelocityTask.get_goals:193 angular velocity */
-#define USV_NU_RESET 712
+/* parity tests only (usv_cfg_t.inj_trig with injected uniforms): the reference's own torch.cos / torch.sin values on
+ * the reset's state path -- cos, sin of the spawn angle (static_obs.py:955-956, USV_go_to_pose.py:307-310), cos, sin
+ * of half the spawn / scene yaw (the quaternion, static_obs.py:960-961, USV_Virtual.py:1449-1450), cos, sin of the
+ * constant disturbance's direction (USV_disturbances.py:369-374).  Never drawn. */
+#define RU_TRIG     712
+#define USV_NU_RESET 718
 /* Layout of the uniform draws of one env step (device [n][USV_NU_STEP] when
  * injected; otherwise Philox(ctr={env, step_lo, step_hi, i/4})[i%4]).
  * Only the draws of the LAST update_state of the step reach obs/reward
@@ -222,7 +227,9 @@ typedef struct usv_cfg {
    * :771-813, which runs after each world step, vec_env_rlgames.py:154-171).  usv_reset keeps those inputs
    * in usv_bufs_t.stale; 0 = the first substep uses the new state instead. ---- */
   int   stale_root;
-  int   pad_stale;
+  /* parity tests: with injected reset uniforms, take the spawn / disturbance-direction sin and cos from the
+   * RU_TRIG slots (the reference's recorded CPU values) instead of usv_sincos_cr; 0 in training */
+  int   inj_trig;
 } usv_cfg_t;
 
 /* stage bits of ctl[USV_CTL_NAN_FLAG] / ppo_cfg_t.nan_flag (the reference's probe names) */

@@ -87,6 +87,20 @@ __device__ __forceinline__ float usv_sin(float x) {
   usv_sincos(x, &s, &c);
   return s;
 }
+// The rigid body's attitude as the reference reads it back: PhysX's yaw-only quaternion q = (w, 0, 0, z) =
+// (cos(yaw/2), 0, 0, sin(yaw/2)) (this build's stand-in for the integrator's pose, usv_sincos of yaw / 2), and
+// pytorch3d.transforms.quaternion_to_matrix of it (two_s = 2 / sum(q * q); the reference's drag,
+// Hydrodynamics.py:209-217) -- R = [[C, -S, 0], [S, C, 0], [0, 0, 1]] with C = 1 - two_s z^2, S = two_s (z w), the
+// x = y = 0 terms exact.  getLocalLinearVelocities (Utils.py:10-14, torch.bmm's CPU order: (r0 vx + r1 vy) + r2 vz,
+// no fma) then gives R^T v = (C vx + S vy, -S vx + C vy); the integrator rotates the body-frame wrench with the same
+// R (its own definition, the PhysX step's), so one half-angle sincos per substep serves both
+struct QuatRot { float C, S, w, z; };
+__device__ __forceinline__ QuatRot usv_quat_rot(float yaw) {
+  float z, w;
+  usv_sincos(yaw * 0.5f, &z, &w);
+  const float two_s = 2.0f / (w * w + z * z);   // (q * q).sum(-1) of (w, 0, 0, z); 2.0 / t == reciprocal * 2 (exact)
+  return QuatRot{1.0f - two_s * (z * z), two_s * (z * w), w, z};
+}
 // exp, tanh and atan2 of the observation / reward formulas, by the same rule (oracle/usv_oracle.c restates them):
 // Cephes' single-precision reductions and minimax polynomials in plain IEEE multiplies, adds and divisions, the
 // power of two by ldexpf (exact).  Within 2 ulp of float64 libm on the ranges the step uses (CPU tests).
@@ -138,6 +152,51 @@ __device__ __forceinline__ float usv_atan2(float y, float x) {
     if (signbit(x)) r = (3.14159274f - r) + -8.742278e-08f;
   }
   return copysignf(r, y);
+}
+// update_state's heading (USV_Virtual.py:776-786): arctan2(2 (w z + x y), 1 - 2 (y^2 + z^2)) of the read-back
+// quaternion (usv_quat_rot's), x = y = 0 terms exact
+__device__ __forceinline__ float usv_heading(const QuatRot &q) {
+  return usv_atan2(2.0f * (q.w * q.z), 1.0f - 2.0f * (q.z * q.z));
+}
+// the stand-in's pose from a quaternion set_world_poses receives (w, 0, 0, z): yaw = 2 atan2(z, w)
+__device__ __forceinline__ float usv_yaw_of_quat(float w, float z) { return 2.0f * usv_atan2(z, w); }
+
+// sin and cos where the reference itself calls torch.sin / torch.cos on the state path: spawn positions and
+// quaternions (static_obs.py:955-961, USV_go_to_pose.py:307-318, USV_track_xyo_velocity.py:217-218, scene replay
+// USV_Virtual.py:1447-1450), the constant disturbance direction and the disturbance sinusoids
+// (USV_disturbances.py:369-410, 510-530) and the legacy CoM disk (:121-122).  torch's CPU kernels there are MKL
+// VML HA (within 0.6 ulp: the correctly rounded value for ~95% of arguments), so this is the double-precision
+// value rounded to float: Cody-Waite reduction by pi/2 in three parts (P1, P2 30-bit: k P exact for |k| < 2^23,
+// i.e. every float phase below ~1.3e7, the largest env origin x frequency the step forms), fdlibm's kernel
+// polynomials.  Plain IEEE double operations (-ffp-contract=off), restated by oracle/usv_oracle.c:usv_sincos_cr,
+// so the device and the oracle round the same double.
+__host__ __device__ __forceinline__ void usv_sincos_cr(float xf, float *s, float *c) {
+  const double x = (double)xf;
+  const double k = rint(x * 0x1.45f306dc9c883p-1);
+  double r = x - k * 0x1.921fb54p+0;            // P1 = pi/2 to 30 bits
+  r = r - k * 0x1.10b46118p-30;               // P2: the next 30 bits
+  r = r - k * 0x1.313198a2e037p-61;           // P3: the rest, rounded
+  const double z = r * r;
+  const double sp = r + (z * r) * (-1.66666666666666324348e-01 +
+                                   z * (8.33333333332248946124e-03 +
+                                        z * (-1.98412698298579493134e-04 +
+                                             z * (2.75573137070700676789e-06 +
+                                                  z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)))));
+  const double cr = z * (4.16666666666666019037e-02 +
+                         z * (-1.38888888888741095749e-03 +
+                              z * (2.48015872894767294178e-05 +
+                                   z * (-2.75573143513906633035e-07 +
+                                        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double cp = 1.0 - (0.5 * z - z * cr);
+  const int q = (int)(long long)k & 3;
+  const double sa = (q & 1) ? cp : sp, ca = (q & 1) ? sp : cp;
+  *s = (float)((q & 2) ? -sa : sa);
+  *c = (float)(((q + 1) & 2) ? -ca : ca);
+}
+__host__ __device__ __forceinline__ float usv_sin_cr(float x) {
+  float s, c;
+  usv_sincos_cr(x, &s, &c);
+  return s;
 }
 
 // cell centre i of the potential field's grid (BatchedMapGPU's torch.linspace of the cell centres,

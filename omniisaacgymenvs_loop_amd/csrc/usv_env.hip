@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         const float r = U(RU_COM) * c.com_legacy_r;
         const float th = U(RU_COM + 1) * USV_PI_F * 2.0f;
         float sth, cth;
-        usv_sincos(th, &sth, &cth);
+        usv_sincos_cr(th, &sth, &cth);
         cx = c.base_com[0] + cth * r;
         cy = c.base_com[1] + sth * r;
       }
@@ -257,7 +257,8 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
           const float r = U(RU_FCONST) * (float)((double)c.fconst_max - (double)c.fconst_min) + c.fconst_min;
           const float th = U(RU_FCONST + 1) * USV_PI_F * 2.0f;
           float sth, cth;
-          usv_sincos(th, &sth, &cth);
+          usv_sincos_cr(th, &sth, &cth);
+          if (c.inj_trig && inj) { cth = U(RU_TRIG + 4); sth = U(RU_TRIG + 5); }
           D[DI_FCX * nn + e] = cth * r;
           D[DI_FCY * nn + e] = sth * r;
         }
@@ -289,12 +290,19 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
       // ---- task.get_spawns, previous-episode target (get_goals runs later, USV_Virtual.py:1618) ----
       tx = b.tgt_x[e];
       ty = b.tgt_y[e];
-      const float yaw0 = U(RU_YAW) * USV_PI_F;
+      // the spawn heading reaches the stand-in as the quaternion (cos(yaw0 / 2), 0, 0, sin(yaw0 / 2))
+      // (static_obs.py:959-961) and set_world_poses turns it into its yaw (usv_yaw_of_quat)
+      const bool inj_trig = c.inj_trig && inj;   // parity tests: the reference's recorded torch.cos / sin values
+      float qz0, qw0;
+      usv_sincos_cr(U(RU_YAW) * USV_PI_F * 0.5f, &qz0, &qw0);
+      if (inj_trig) { qw0 = U(RU_TRIG + 2); qz0 = U(RU_TRIG + 3); }
+      const float yaw0 = usv_yaw_of_quat(qw0, qz0);
       if (c.task_kind == USV_TASK_CAPTURE_XY) {   // CaptureXYTask.get_spawns (static_obs.py:936-1060)
         const float r = U(RU_SPAWN_R) * (c.spawn_rmax - c.spawn_rmin) + c.spawn_rmin;
         const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
         float sth, cth;
-        usv_sincos(th, &sth, &cth);
+        usv_sincos_cr(th, &sth, &cth);
+        if (inj_trig) { cth = U(RU_TRIG); sth = U(RU_TRIG + 1); }
         sx = r * cth;
         sy = r * sth;
         b.field_old_tgt[e] = tx;
@@ -309,7 +317,8 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         const float r = U(RU_SPAWN_R) * (float)(rmax - rmin) + (float)rmin;
         const float th = U(RU_SPAWN_TH) * 2.0f * USV_PI_F;
         float sth, cth;
-        usv_sincos(th, &sth, &cth);
+        usv_sincos_cr(th, &sth, &cth);
+        if (inj_trig) { cth = U(RU_TRIG); sth = U(RU_TRIG + 1); }
         sx = r * cth + tx;
         sy = r * sth + ty;
         b.prev_dist[e] = 0.f;                            // GoToPoseTask.reset: prev_position_dist = 0 (:227)
@@ -321,9 +330,9 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
       // computes its drag and disturbances (USV_Virtual.py:1103-1117): keep those inputs ----
       if (c.stale_root) {
         const float opx = b.px[e], opy = b.py[e], ovx = b.vx[e], ovy = b.vy[e];
-        float so, co;
-        usv_sincos(b.yaw[e], &so, &co);
-        float ub = co * ovx + so * ovy;               // R^T v (Utils.py:8-12)
+        const QuatRot qr = usv_quat_rot(b.yaw[e]);
+        const float so = qr.S, co = qr.C;
+        float ub = co * ovx + so * ovy;               // R^T v (Utils.py:10-14, Hydrodynamics.py:209-217)
         float vb = -so * ovx + co * ovy;
         if (c.current_on) {                           // relative to the water (Hydrodynamics.py:224-237)
           ub = ub - (co * c.flow_vel[0] + so * c.flow_vel[1]);
@@ -356,7 +365,12 @@ __global__ __launch_bounds__(kBlock) void k_reset(usv_cfg_t c, usv_bufs_t b, uin
         for (int q = 0; q < 2 * USV_NOBST; ++q) b.obst[(size_t)q * n + e] = sc[USV_SC_OBST + q];
         b.px[e] = sc[USV_SC_START];
         b.py[e] = sc[USV_SC_START + 1];
-        b.yaw[e] = sc[USV_SC_YAW];
+        {   // the yaw-only quaternion of the scene's start yaw (USV_Virtual.py:1447-1450) through set_world_poses
+          float hz, hw;
+          usv_sincos_cr(0.5f * sc[USV_SC_YAW], &hz, &hw);
+          if (inj_trig) { hw = U(RU_TRIG + 2); hz = U(RU_TRIG + 3); }
+          b.yaw[e] = usv_yaw_of_quat(hw, hz);
+        }
         b.vx[e] = sc[USV_SC_VEL];
         b.vy[e] = sc[USV_SC_VEL + 1];
         b.tgt_x[e] = sc[USV_SC_GOAL];
@@ -917,9 +931,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
     for (int s = 0; s < c.substeps; ++s) {
       fl = fl * al + oma * tgt0;                      // ThrusterDynamics.py:133-136
       fr = fr * al + oma * tgt1;
-      float sy_, cy_;
-      usv_sincos(yaw, &sy_, &cy_);
-      float ub = cy_ * vx + sy_ * vy;                 // R^T v (Utils.py:8-12)
+      // the attitude the reference reads back: R = quaternion_to_matrix(q(yaw)) (usv_quat_rot)
+      const QuatRot qr = usv_quat_rot(yaw);
+      const float sy_ = qr.S, cy_ = qr.C;
+      float ub = cy_ * vx + sy_ * vy;                 // R^T v (Utils.py:10-14, Hydrodynamics.py:209-217)
       float vb = -sy_ * vx + cy_ * vy;
       float rb = wz;
       float hpx = px, hpy = py;
@@ -942,10 +957,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
         dfy = dp[DI_FCY];
         dtz = dp[DI_TC];
         if (c.fsin_on) {
-          dfx = dfx + usv_sin(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
-          dfy = dfy + usv_sin(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
+          dfx = dfx + usv_sin_cr(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
+          dfy = dfy + usv_sin_cr(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
         }
-        if (c.tsin_on) dtz = dtz + usv_sin((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
+        if (c.tsin_on) dtz = dtz + usv_sin_cr((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
       }
       float D0 = lin0 + qd0 * fabsf(ub), D1 = lin1 + qd1 * fabsf(vb), D2 = lin2 + qd2 * fabsf(rb);
       D0 = D0 * c.scaling_damping; D1 = D1 * c.scaling_damping; D2 = D2 * c.scaling_damping;
@@ -991,7 +1006,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step(StepCfg ck, usv_bufs_t b, W
       vyn = vyn + (u[SU_VY] * K.vel_rng + c.vel_noise_min);
       wzn = wzn + (u[SU_WZ] * K.vel_rng + c.vel_noise_min);
     }
-    float yawn = yaw;
+    // update_state's heading: atan2 of the read-back quaternion (USV_Virtual.py:776-786), then its noise
+    float yawn = usv_heading(usv_quat_rot(yaw));
     if (c.head_noise_on) yawn = yawn + (u[SU_HEAD] * K.head_rng + c.head_noise_min);
     float hs, hc;
     usv_sincos(yawn, &hs, &hc);
@@ -1364,8 +1380,8 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
   for (int s = 0; s < c.substeps; ++s) {
     fl = fl * al + oma * tgt0;
     fr = fr * al + oma * tgt1;
-    float sy_, cy_;
-    usv_sincos(yaw, &sy_, &cy_);
+    const QuatRot qr = usv_quat_rot(yaw);   // R = quaternion_to_matrix(q(yaw)), as the CaptureXY step
+    const float sy_ = qr.S, cy_ = qr.C;
     float ub = cy_ * vx + sy_ * vy;
     float vb = -sy_ * vx + cy_ * vy;
     float rb = wz;
@@ -1382,10 +1398,10 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
       dfy = dp[DI_FCY];
       dtz = dp[DI_TC];
       if (c.fsin_on) {
-        dfx = dfx + usv_sin(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
-        dfy = dfy + usv_sin(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
+        dfx = dfx + usv_sin_cr(wx * dp[DI_FXF] + dp[DI_FXS]) * dp[DI_FAMP];
+        dfy = dfy + usv_sin_cr(wy * dp[DI_FYF] + dp[DI_FYS]) * dp[DI_FAMP];
       }
-      if (c.tsin_on) dtz = dtz + usv_sin((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
+      if (c.tsin_on) dtz = dtz + usv_sin_cr((wx + wy) * dp[DI_TF] + dp[DI_TS]) * dp[DI_TAMP];
     }
     float D0 = lin0 + qd0 * fabsf(ub), D1 = lin1 + qd1 * fabsf(vb), D2 = lin2 + qd2 * fabsf(rb);
     D0 = D0 * c.scaling_damping; D1 = D1 * c.scaling_damping; D2 = D2 * c.scaling_damping;
@@ -1427,7 +1443,7 @@ __global__ __launch_bounds__(kBlock) void k_env_step_task(StepCfg ck, usv_bufs_t
     vyn = vyn + (u[SU_VY] * K.vel_rng + c.vel_noise_min);
     wzn = wzn + (u[SU_WZ] * K.vel_rng + c.vel_noise_min);
   }
-  float yawn = yaw;
+  float yawn = usv_heading(usv_quat_rot(yaw));   // update_state's heading (USV_Virtual.py:776-786)
   if (c.head_noise_on) yawn = yawn + (u[SU_HEAD] * K.head_rng + c.head_noise_min);
   float hs, hc;
   usv_sincos(yawn, &hs, &hc);
@@ -1678,8 +1694,8 @@ __global__ void k_forces(usv_cfg_t c, usv_bufs_t b, float *__restrict__ out) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = b.n;
   if (e >= n) return;
-  float sy_, cy_;
-  usv_sincos(b.yaw[e], &sy_, &cy_);
+  const QuatRot qr = usv_quat_rot(b.yaw[e]);   // R = quaternion_to_matrix(q(yaw)) (Hydrodynamics.py:209-217)
+  const float sy_ = qr.S, cy_ = qr.C;
   const float vx = b.vx[e], vy = b.vy[e], wz = b.wz[e];
   float ub = cy_ * vx + sy_ * vy, vb = -sy_ * vx + cy_ * vy;
   if (c.current_on) {   // relative to the water (Hydrodynamics.py:224-237)

@@ -34,6 +34,7 @@
   X(RU_TSIN, "RU_TSIN") \
   X(RU_TCONST, "RU_TCONST") \
   X(RU_GOAL_H, "RU_GOAL_H") \
+  X(RU_TRIG, "RU_TRIG") \
   X(USV_NU_RESET, "USV_NU_RESET") \
   X(SU_VX, "SU_VX") \
   X(SU_VY, "SU_VY") \
@@ -343,7 +344,7 @@
   X(offsetof(usv_cfg_t, max_spawn_d), "usv_cfg.max_spawn_d") \
   X(offsetof(usv_cfg_t, kill_dist_d), "usv_cfg.kill_dist_d") \
   X(offsetof(usv_cfg_t, stale_root), "usv_cfg.stale_root") \
-  X(offsetof(usv_cfg_t, pad_stale), "usv_cfg.pad_stale") \
+  X(offsetof(usv_cfg_t, inj_trig), "usv_cfg.inj_trig") \
   X(sizeof(usv_bufs_t), "sizeof usv_bufs") \
   X(offsetof(usv_bufs_t, n), "usv_bufs.n") \
   X(offsetof(usv_bufs_t, pad0), "usv_bufs.pad0") \

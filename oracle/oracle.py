@@ -20,7 +20,8 @@ LIB_PATH = os.path.join(HERE, "build", "libusv_oracle_omp.so" if os.environ.get(
                         else "libusv_oracle.so")
 
 NOBS, NOBST, GRID, NSTAT = 33, 16, 150, 28
-NU_RESET, NU_STEP = 712, 8
+NU_RESET, NU_STEP = 718, 8
+RU_TRIG = 712      # include/usv_hip.h: the recorded reference sin / cos of the reset (cfg.inj_trig)
 NDIST = 11
 NDBG = 20          # usv_oracle.c USV_ORACLE_NDBG: per-env diagnostics of the last step
 CTL_POT_VALID, CTL_PEN_VALID, CTL_REW_VALID = 1, 2, 3
@@ -50,6 +51,9 @@ def lib():
         _lib.oracle_grid_lin.argtypes = [ctypes.c_float, P]
         _lib.oracle_lut.argtypes = [P, ctypes.c_int, ctypes.c_int, P]
         _lib.oracle_forces.argtypes = [P, P, P]
+        _lib.oracle_forces_q.argtypes = [P, P, P, P]
+        _lib.oracle_sincos_cr.argtypes = [P, ctypes.c_int, P, P]
+        _lib.oracle_quat.argtypes = [P, ctypes.c_int, P]
         _lib.oracle_hydrostatics.argtypes = [P, ctypes.c_int, P, P, P, P, P]
         _lib.oracle_compact.argtypes = [P, P]
         _lib.oracle_compact.restype = ctypes.c_int
@@ -223,9 +227,12 @@ class OracleEnv:
         self._U = np.ascontiguousarray(U, np.float32)
         lib().oracle_step_post(ctypes.byref(self.cfg), ctypes.byref(self.c), _p(self._U))
 
-    def forces(self):
+    def forces(self, quat=None):
+        """Planar X, Y, N of the env state; quat [n][4] (w, 0, 0, z): the drag's attitude given as the reference's
+        own quaternions instead of the stand-in's quaternion of the yaw."""
         out = np.zeros((self.n, 3), np.float32)
-        lib().oracle_forces(ctypes.byref(self.cfg), ctypes.byref(self.c), _p(out))
+        q = None if quat is None else np.ascontiguousarray(quat, np.float32).reshape(self.n, 4)
+        lib().oracle_forces_q(ctypes.byref(self.cfg), ctypes.byref(self.c), _p(q) if q is not None else None, _p(out))
         return out
 
 
@@ -290,6 +297,24 @@ def sincos(x):
     s, c = np.empty_like(x), np.empty_like(x)
     lib().oracle_sincos(_p(x), ctypes.c_int(x.size), _p(s), _p(c))
     return s, c
+
+
+def sincos_cr(x):
+    """sin / cos where the reference calls torch.sin / torch.cos on the state path (usv_oracle.c:usv_sincos_cr: a
+    double evaluation rounded to float)."""
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib().oracle_sincos_cr(_p(x), ctypes.c_int(x.size), _p(s), _p(c))
+    return s, c
+
+
+def quat(yaw):
+    """Per yaw: (C, S) of quaternion_to_matrix of the stand-in's quaternion, the update_state heading and the yaw
+    set_world_poses recovers from that quaternion (usv_oracle.c:oracle_quat) -> [n][4] float32."""
+    yaw = np.ascontiguousarray(yaw, np.float32)
+    out = np.empty((yaw.size, 4), np.float32)
+    lib().oracle_quat(_p(yaw), ctypes.c_int(yaw.size), _p(out))
+    return out
 
 
 def math3(x, y):

@@ -88,6 +88,67 @@ void oracle_sincos(const float *x, int n, float *s, float *c) {
 static inline float usv_sin(float x) { float s, c; usv_sincos(x, &s, &c); return s; }
 static inline float usv_cos(float x) { float s, c; usv_sincos(x, &s, &c); return c; }
 
+/* The attitude the reference reads back (csrc/usv_device.h:usv_quat_rot): the stand-in's yaw-only quaternion
+ * q = (w, 0, 0, z) = (cos(yaw/2), 0, 0, sin(yaw/2)) by usv_sincos, pytorch3d.transforms.quaternion_to_matrix of it
+ * (two_s = 2 / (q * q).sum(-1); Hydrodynamics.py:209-217): R = [[C, -S, 0], [S, C, 0], [0, 0, 1]] with
+ * C = 1 - two_s * (z * z), S = two_s * (z * w).  The drag's R^T v in torch.bmm's CPU order
+ * ((r0 vx + r1 vy) + r2 vz, no fma: checked on random batches) is (C vx + S vy, -S vx + C vy); the integrator
+ * rotates the body-frame wrench with the same R. */
+typedef struct { float C, S, w, z; } quat_rot_t;
+static inline quat_rot_t usv_quat_rot(float yaw) {
+  float z, w;
+  usv_sincos(yaw * 0.5f, &z, &w);
+  const float two_s = 2.0f / (w * w + z * z);
+  quat_rot_t q = {1.0f - two_s * (z * z), two_s * (z * w), w, z};
+  return q;
+}
+/* update_state's heading (USV_Virtual.py:776-786): arctan2(2 (w z + x y), 1 - 2 (y^2 + z^2)) of that quaternion */
+float usv_atan2(float y, float x);
+static inline float usv_heading(quat_rot_t q) { return usv_atan2(2.0f * (q.w * q.z), 1.0f - 2.0f * (q.z * q.z)); }
+/* the stand-in's pose from a quaternion set_world_poses receives (w, 0, 0, z) */
+static inline float usv_yaw_of_quat(float w, float z) { return 2.0f * usv_atan2(z, w); }
+
+/* sin / cos where the reference calls torch.sin / torch.cos on the state path (spawn angle and quaternion, scene
+ * yaw, constant-disturbance direction, disturbance sinusoids, legacy CoM disk): torch's CPU kernels there are MKL
+ * VML HA (within 0.6 ulp, the correctly rounded value for ~95% of float arguments), so this build rounds a double
+ * evaluation (csrc/usv_device.h:usv_sincos_cr, restated operation for operation): Cody-Waite by pi/2 in three
+ * parts (P1, P2 of 30 bits, exact k * P for |k| < 2^23), fdlibm's kernel polynomials. */
+void usv_sincos_cr(float xf, float *s, float *c) {
+  const double x = (double)xf;
+  const double k = rint(x * 0x1.45f306dc9c883p-1);
+  double r = x - k * 0x1.921fb54p+0;
+  r = r - k * 0x1.10b46118p-30;
+  r = r - k * 0x1.313198a2e037p-61;
+  const double z = r * r;
+  const double sp = r + (z * r) * (-1.66666666666666324348e-01 +
+                                   z * (8.33333333332248946124e-03 +
+                                        z * (-1.98412698298579493134e-04 +
+                                             z * (2.75573137070700676789e-06 +
+                                                  z * (-2.50507602534068634195e-08 + z * 1.58969099521155010221e-10)))));
+  const double cr = z * (4.16666666666666019037e-02 +
+                         z * (-1.38888888888741095749e-03 +
+                              z * (2.48015872894767294178e-05 +
+                                   z * (-2.75573143513906633035e-07 +
+                                        z * (2.08757232129817482790e-09 + z * -1.13596475577881948265e-11)))));
+  const double cp = 1.0 - (0.5 * z - z * cr);
+  const int q = (int)(long long)k & 3;
+  const double sa = (q & 1) ? cp : sp, ca = (q & 1) ? sp : cp;
+  *s = (float)((q & 2) ? -sa : sa);
+  *c = (float)(((q + 1) & 2) ? -ca : ca);
+}
+static inline float usv_sin_cr(float x) { float s, c; usv_sincos_cr(x, &s, &c); return s; }
+void oracle_sincos_cr(const float *x, int n, float *s, float *c) {
+  for (int i = 0; i < n; ++i) usv_sincos_cr(x[i], s + i, c + i);
+}
+/* [n][4] per yaw: C, S (usv_quat_rot), the heading (usv_heading) and the yaw back from (w, z) (usv_yaw_of_quat) */
+void oracle_quat(const float *yaw, int n, float *out) {
+  for (int i = 0; i < n; ++i) {
+    const quat_rot_t q = usv_quat_rot(yaw[i]);
+    out[4 * i + 0] = q.C; out[4 * i + 1] = q.S; out[4 * i + 2] = usv_heading(q);
+    out[4 * i + 3] = usv_yaw_of_quat(q.w, q.z);
+  }
+}
+
 /* exp, tanh and atan2 of the observation / reward formulas (the reference's torch.exp / torch.tanh / torch.atan2 in
  * float32), by the same rule as usv_sincos: this build's functions, restated operation for operation from
  * csrc/usv_device.h (Cephes' single-precision reductions and polynomials; the power of two by ldexpf, exact), so the
@@ -271,8 +332,8 @@ static void planar_forces(const usv_cfg_t *c, const oracle_env_t *E, int e, floa
                           float wz, float fl, float fr, const float *dist3 /* disturbance fx, fy, tz or NULL */,
                           float *X, float *Y, float *N) {
   /* (cy, sy, vx, vy, wz): the root state apply_forces reads (the current one, or the cached pre-reset one
-     in a reset env's first substep) */
-  /* getLocalLinearVelocities: R^T v  (Utils.py:8-12) */
+     in a reset env's first substep); cy, sy = C, S of quaternion_to_matrix (usv_quat_rot) */
+  /* getLocalLinearVelocities: R^T v  (Utils.py:10-14) in torch.bmm's order */
   float u = cy * vx + sy * vy;
   float v = -sy * vx + cy * vy;
   const float r = wz;
@@ -319,20 +380,32 @@ static void disturbance(const usv_cfg_t *c, const oracle_env_t *E, int e, float 
   *fy = D[DI_FCY * n + e];
   *tz = D[DI_TC * n + e];
   if (c->fsin_on) {
-    *fx = *fx + usv_sin(wx * D[DI_FXF * n + e] + D[DI_FXS * n + e]) * D[DI_FAMP * n + e];
-    *fy = *fy + usv_sin(wy * D[DI_FYF * n + e] + D[DI_FYS * n + e]) * D[DI_FAMP * n + e];
+    *fx = *fx + usv_sin_cr(wx * D[DI_FXF * n + e] + D[DI_FXS * n + e]) * D[DI_FAMP * n + e];
+    *fy = *fy + usv_sin_cr(wy * D[DI_FYF * n + e] + D[DI_FYS * n + e]) * D[DI_FAMP * n + e];
   }
-  if (c->tsin_on) *tz = *tz + usv_sin((wx + wy) * D[DI_TF * n + e] + D[DI_TS * n + e]) * D[DI_TAMP * n + e];
+  if (c->tsin_on) *tz = *tz + usv_sin_cr((wx + wy) * D[DI_TF * n + e] + D[DI_TS * n + e]) * D[DI_TAMP * n + e];
 }
 
-void oracle_forces(const usv_cfg_t *c, oracle_env_t *E, float *out /*[n][3]*/) {
+/* quat: NULL => the stand-in's quaternion of E->yaw (usv_quat_rot); else [n][4] (w, x, y, z) yaw-only quaternions
+ * (x = y = 0) given by the caller -- the reference's own, so the drag is checked bit for bit against it */
+void oracle_forces_q(const usv_cfg_t *c, oracle_env_t *E, const float *quat, float *out /*[n][3]*/) {
   for (int e = 0; e < E->n; ++e) {
-    const float cy = usv_cos(E->yaw[e]), sy = usv_sin(E->yaw[e]);
+    float C, S;
+    if (quat) {
+      const float w = quat[4 * e], z = quat[4 * e + 3];
+      const float two_s = 2.0f / (w * w + z * z);
+      C = 1.0f - two_s * (z * z);
+      S = two_s * (z * w);
+    } else {
+      const quat_rot_t q = usv_quat_rot(E->yaw[e]);
+      C = q.C; S = q.S;
+    }
     float X, Y, N;
-    planar_forces(c, E, e, cy, sy, E->vx[e], E->vy[e], E->wz[e], E->fl[e], E->fr[e], NULL, &X, &Y, &N);
+    planar_forces(c, E, e, C, S, E->vx[e], E->vy[e], E->wz[e], E->fl[e], E->fr[e], NULL, &X, &Y, &N);
     out[e * 3 + 0] = X; out[e * 3 + 1] = Y; out[e * 3 + 2] = N;
   }
 }
+void oracle_forces(const usv_cfg_t *c, oracle_env_t *E, float *out /*[n][3]*/) { oracle_forces_q(c, E, NULL, out); }
 
 /* Hydrostatic wrench: USVVirtual.update_state volume (USV_Virtual.py:791-798), get_euler_angles
  * (:815-835), HydrostaticsObject.compute_archimedes_metacentric_local (Hydrostatics.py:63-133) */
@@ -633,8 +706,10 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
     } else if (c->mass_dr_on && c->com_mode == 2 && c->com_legacy_r > 0.f) {  /* legacy disk (:112-124) */
       const float r = u[RU_COM] * c->com_legacy_r;
       const float th = u[RU_COM + 1] * (float)OPI * 2.0f;
-      E->com_x[e] = c->base_com[0] + usv_cos(th) * r;
-      E->com_y[e] = c->base_com[1] + usv_sin(th) * r;
+      float sth, cth;
+      usv_sincos_cr(th, &sth, &cth);
+      E->com_x[e] = c->base_com[0] + cth * r;
+      E->com_y[e] = c->base_com[1] + sth * r;
       E->com_z[e] = c->base_com[2];
     } else {
       E->com_x[e] = c->base_com[0]; E->com_y[e] = c->base_com[1]; E->com_z[e] = c->base_com[2];
@@ -684,8 +759,11 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
       if (c->fdist_on && c->fconst_on) {
         const float rr = u[RU_FCONST] * (float)((double)c->fconst_max - (double)c->fconst_min) + c->fconst_min;
         const float tt = u[RU_FCONST + 1] * (float)OPI * 2.0f;
-        D[DI_FCX * n + e] = usv_cos(tt) * rr;
-        D[DI_FCY * n + e] = usv_sin(tt) * rr;
+        float st, ct;
+        usv_sincos_cr(tt, &st, &ct);
+        if (c->inj_trig) { ct = u[RU_TRIG + 4]; st = u[RU_TRIG + 5]; }   /* the reference's recorded values */
+        D[DI_FCX * n + e] = ct * rr;
+        D[DI_FCY * n + e] = st * rr;
       }
       if (c->tdist_on && c->tsin_on) {
         D[DI_TF * n + e] = u[RU_TSIN] * (float)((double)c->tfreq_max - (double)c->tfreq_min) + c->tfreq_min;
@@ -716,7 +794,18 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
      * obstacle box use the target of the PREVIOUS episode: get_goals runs later
      * in set_targets (USV_Virtual.py:1618). */
     const float rmin = c->spawn_rmin, rmax = c->spawn_rmax;
-    const float yaw0 = u[RU_YAW] * (float)OPI;
+    /* the spawn heading reaches the stand-in as the quaternion (cos(yaw0 / 2), 0, 0, sin(yaw0 / 2))
+       (static_obs.py:959-961), which set_world_poses turns into its yaw; c->inj_trig: the parity harness's
+       recorded torch.cos / torch.sin values (RU_TRIG) instead of usv_sincos_cr */
+    float qz0, qw0;
+    usv_sincos_cr(u[RU_YAW] * (float)OPI * 0.5f, &qz0, &qw0);
+    if (c->inj_trig) { qw0 = u[RU_TRIG + 2]; qz0 = u[RU_TRIG + 3]; }
+    const float yaw0 = usv_yaw_of_quat(qw0, qz0);
+    float cth = 0.f, sth = 0.f;
+    if (c->task_kind != USV_TASK_TRACK_XYO) {
+      usv_sincos_cr(u[RU_SPAWN_TH] * 2.0f * (float)OPI, &sth, &cth);
+      if (c->inj_trig) { cth = u[RU_TRIG]; sth = u[RU_TRIG + 1]; }
+    }
     float sx, sy;
     if (c->task_kind == USV_TASK_GO_TO_POSE) {
       /* GoToPoseTask.get_spawns (USV_go_to_pose.py:256-319): disk around the previous target, radii from the
@@ -727,16 +816,14 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
         dmin = curriculum_lerp(c, E->step_f, c->cur_min_dist, c->min_spawn_d);
       }
       const float r = u[RU_SPAWN_R] * (float)(dmax - dmin) + (float)dmin;
-      const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
-      sx = r * usv_cos(th) + E->tgt_x[e];
-      sy = r * usv_sin(th) + E->tgt_y[e];
+      sx = r * cth + E->tgt_x[e];
+      sy = r * sth + E->tgt_y[e];
       E->prev_dist[e] = 0.f;   /* GoToPoseTask.reset: prev_position_dist = 0 (:227) */
     } else if (c->task_kind == USV_TASK_TRACK_XYO) {
       sx = 0.f; sy = 0.f;      /* TrackXYOVelocityTask.get_spawns (:203-219): heading only */
     } else {
       const float r = u[RU_SPAWN_R] * (rmax - rmin) + rmin;
-      const float th = u[RU_SPAWN_TH] * 2.0f * (float)OPI;
-      sx = r * usv_cos(th); sy = r * usv_sin(th);
+      sx = r * cth; sy = r * sth;
     }
     if (c->task_kind != USV_TASK_CAPTURE_XY) {
       E->px[e] = sx; E->py[e] = sy; E->yaw[e] = yaw0;
@@ -772,7 +859,13 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
         }
       E->tgt_x[e] = sc[USV_SC_GOAL]; E->tgt_y[e] = sc[USV_SC_GOAL + 1];
       tgt_k[s * 2 + 0] = sc[USV_SC_GOAL]; tgt_k[s * 2 + 1] = sc[USV_SC_GOAL + 1];
-      E->px[e] = sc[USV_SC_START]; E->py[e] = sc[USV_SC_START + 1]; E->yaw[e] = sc[USV_SC_YAW];
+      E->px[e] = sc[USV_SC_START]; E->py[e] = sc[USV_SC_START + 1];
+      {  /* the yaw-only quaternion of the start yaw (USV_Virtual.py:1447-1450) through set_world_poses */
+        float hz, hw;
+        usv_sincos_cr(0.5f * sc[USV_SC_YAW], &hz, &hw);
+        if (c->inj_trig) { hw = u[RU_TRIG + 2]; hz = u[RU_TRIG + 3]; }
+        E->yaw[e] = usv_yaw_of_quat(hw, hz);
+      }
       E->vx[e] = sc[USV_SC_VEL]; E->vy[e] = sc[USV_SC_VEL + 1];
       E->wz[e] = 0.f;
       E->reset_buf[e] = 0; E->progress[e] = 0;
@@ -780,7 +873,6 @@ void oracle_reset_scene(const usv_cfg_t *c, oracle_env_t *E, int k, const int32_
       for (int q = 0; q < USV_NSTAT; ++q) E->stats[q * n + e] = 0.f;
       continue;
     }
-    /* quaternion (cos(yaw/2),0,0,sin(yaw/2)) -> yaw: identical in the planar state */
     const float tx = E->tgt_x[e], ty = E->tgt_y[e];
     float oc[USV_NOBST][2];
     const float mn[2] = {tx - c->obst_box, ty - c->obst_box};
@@ -925,12 +1017,15 @@ void oracle_step_physics(const usv_cfg_t *c, oracle_env_t *E) {
       /* DynamicsFirstOrder.update (ThrusterDynamics.py:132-136) */
       E->fl[e] = E->fl[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[0];
       E->fr[e] = E->fr[e] * c->thr_alpha + (1.0f - c->thr_alpha) * tgt[1];
-      const float cy = usv_cos(E->yaw[e]), sy = usv_sin(E->yaw[e]);
+      /* the read-back attitude R = quaternion_to_matrix(q(yaw)) (usv_quat_rot) */
+      const quat_rot_t qr = usv_quat_rot(E->yaw[e]);
+      const float cy = qr.C, sy = qr.S;
       /* apply_forces reads the cached root state: the pre-reset one in a reset env's first substep (C.1) */
       const int cached = s == 0 && c->stale_root && E->just_reset[e] && E->root_cache;
       const float *rc = E->root_cache;
       const float hpx = cached ? rc[0 * n + e] : E->px[e], hpy = cached ? rc[1 * n + e] : E->py[e];
-      const float hcy = cached ? usv_cos(rc[2 * n + e]) : cy, hsy = cached ? usv_sin(rc[2 * n + e]) : sy;
+      const quat_rot_t qc = usv_quat_rot(cached ? rc[2 * n + e] : E->yaw[e]);
+      const float hcy = qc.C, hsy = qc.S;
       const float hvx = cached ? rc[3 * n + e] : E->vx[e], hvy = cached ? rc[4 * n + e] : E->vy[e];
       const float hwz = cached ? rc[5 * n + e] : E->wz[e];
       float X, Y, N, d3[3];
@@ -1033,7 +1128,7 @@ static void oracle_step_post_impl(const usv_cfg_t *c, oracle_env_t *E, const flo
       vyn = vyn + (u[SU_VY] * rng + c->vel_noise_min);
       wzn = wzn + (u[SU_WZ] * rng + c->vel_noise_min);
     }
-    float yawn = E->yaw[e];
+    float yawn = usv_heading(usv_quat_rot(E->yaw[e]));   /* update_state's heading (USV_Virtual.py:776-786) */
     if (c->head_noise_on) {
       const float rng = (float)((double)c->head_noise_max - (double)c->head_noise_min);
       yawn = yawn + (u[SU_HEAD] * rng + c->head_noise_min);
@@ -1298,7 +1393,7 @@ static void oracle_step_post_task(const usv_cfg_t *c, oracle_env_t *E, const flo
       vyn = vyn + (u[SU_VY] * rng + c->vel_noise_min);
       wzn = wzn + (u[SU_WZ] * rng + c->vel_noise_min);
     }
-    float yawn = E->yaw[e];
+    float yawn = usv_heading(usv_quat_rot(E->yaw[e]));   /* update_state's heading (USV_Virtual.py:776-786) */
     if (c->head_noise_on) {
       const float rng = (float)((double)c->head_noise_max - (double)c->head_noise_min);
       yawn = yawn + (u[SU_HEAD] * rng + c->head_noise_min);

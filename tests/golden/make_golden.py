@@ -163,6 +163,66 @@ class RandRecorder:
 
 
 # --------------------------------------------------------------------------
+# torch.cos / torch.sin recorder: the reference's own values on the reset's state path
+# --------------------------------------------------------------------------
+# (file, line) of the reference call -> offset in the RU_TRIG slots (include/usv_hip.h)
+TRIG_SITES = {("USV_capture_xy_static_obs.py", 955): 0, ("USV_capture_xy_static_obs.py", 956): 1,
+              ("USV_capture_xy_static_obs.py", 960): 2, ("USV_capture_xy_static_obs.py", 961): 3,
+              ("USV_go_to_pose.py", 307): 0, ("USV_go_to_pose.py", 310): 1,
+              ("USV_go_to_pose.py", 317): 2, ("USV_go_to_pose.py", 318): 3,
+              ("USV_track_xyo_velocity.py", 217): 2, ("USV_track_xyo_velocity.py", 218): 3,
+              ("USV_Virtual.py", 1449): 2, ("USV_Virtual.py", 1450): 3,
+              ("USV_disturbances.py", 380): 4, ("USV_disturbances.py", 381): 5}
+
+
+class TrigRecorder:
+    """Records torch.cos / torch.sin at TRIG_SITES: on the CPU they are MKL VML HA (closed source, within 0.6 ulp),
+    which the build cannot restate bit for bit; the parity tests inject these values (usv_cfg_t.inj_trig) to follow
+    the reference's state exactly, and check the build's own usv_sincos_cr against them separately."""
+
+    def __init__(self, torch):
+        self.torch = torch
+        self.log = []
+        self._cos, self._sin = torch.cos, torch.sin
+
+    def _wrap(self, fn):
+        rec = self
+
+        def g(x, *a, **k):
+            t = fn(x, *a, **k)
+            f = sys._getframe(1)
+            site = (os.path.basename(f.f_code.co_filename), f.f_lineno)
+            if site in TRIG_SITES:
+                rec.log.append((TRIG_SITES[site], t.detach().clone()))
+            return t
+        return g
+
+    def __enter__(self):
+        self.torch.cos, self.torch.sin = self._wrap(self._cos), self._wrap(self._sin)
+        return self
+
+    def __exit__(self, *exc):
+        self.torch.cos, self.torch.sin = self._cos, self._sin
+
+    def take(self):
+        out, self.log = self.log, []
+        return out
+
+
+_ORACLE = None
+
+
+def _oracle():
+    """This build's C oracle (its usv_sincos / usv_atan2 define the stand-in's quaternion and yaw)."""
+    global _ORACLE
+    if _ORACLE is None:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+        from oracle import oracle as O
+        _ORACLE = O
+    return _ORACLE
+
+
+# --------------------------------------------------------------------------
 # fake Isaac Sim articulation view + world (planar, this build's integrator)
 # --------------------------------------------------------------------------
 HERON_Y = 0.37765
@@ -221,10 +281,13 @@ class FakeHeron:
         self.f_base = self.t_base = self.f_left = self.f_right = None
 
     def quat(self):
+        """The stand-in's pose as PhysX returns it: (cos(yaw/2), 0, 0, sin(yaw/2)) by this build's usv_sincos
+        (oracle.sincos == csrc/usv_device.h:usv_quat_rot's half-angle sincos)."""
         t = self.t
+        s, c = _oracle().sincos((self.yaw * 0.5).numpy())
         q = t.zeros(self.n, 4)
-        q[:, 0] = t.cos(self.yaw * 0.5)
-        q[:, 3] = t.sin(self.yaw * 0.5)
+        q[:, 0] = t.from_numpy(c)
+        q[:, 3] = t.from_numpy(s)
         return q
 
     def get_world_poses(self, clone=True):
@@ -254,8 +317,10 @@ class FakeHeron:
         self.px[idx] = pos[:, 0].float()
         self.py[idx] = pos[:, 1].float()
         self.pz[idx] = pos[:, 2].float()
-        w, z = rot[:, 0].float(), rot[:, 3].float()
-        self.yaw[idx] = 2.0 * self.t.atan2(z, w)
+        w, z = rot[:, 0].float().numpy(), rot[:, 3].float().numpy()
+        # the stand-in keeps a yaw: 2 atan2(z, w) by this build's usv_atan2 (csrc/usv_device.h:usv_yaw_of_quat)
+        a = _oracle().math3(np.ascontiguousarray(w), np.ascontiguousarray(z))[2]
+        self.yaw[idx] = self.t.from_numpy(np.float32(2.0) * a)
 
     def set_velocities(self, vel, indices=None):
         idx = indices.long()
@@ -268,11 +333,17 @@ class FakeHeron:
         t = self.t
         fl = self.f_left[:, 0]
         fr = self.f_right[:, 0]
-        X = self.f_base[:, 0] + fl + fr
+        X = (fl + fr) + self.f_base[:, 0]   # csrc/usv_env.hip k_env_step: thrusters, then the base wrench
         Y = self.f_base[:, 1]
         comy = self.com[:, 1]
         N = self.t_base[:, 2] + (-(HERON_Y - comy) * fl + (HERON_Y + comy) * fr)
-        c, s = t.cos(self.yaw), t.sin(self.yaw)
+        # the body-frame wrench rotated by R = quaternion_to_matrix(quat()) (csrc/usv_device.h:usv_quat_rot): the
+        # integrator's own definition, the same R the reference's drag reads back
+        q = self.quat()
+        w, z = q[:, 0], q[:, 3]
+        two_s = 2.0 / (w * w + z * z)
+        c = 1.0 - two_s * (z * z)
+        s = two_s * (z * w)
         m = self.mass
         izz = self.inertia[:, 8]
         ax = (c * X - s * Y) / m
@@ -449,8 +520,9 @@ def make_vecenv(torch, usv, world):
 # --------------------------------------------------------------------------
 RU = dict(MASS=0, COM=1, KIZ=4, KDRAG=5, THR=6, DRAG=8, SPAWN_R=20, SPAWN_TH=21, YAW=22, OBST=23,
           RESAMPLE=55, VX=695, VY=696, GOAL=697, FSIN=699, FCONST=704, TSIN=706, TCONST=709)
-NU_RESET, NU_STEP = 712, 8
+NU_RESET, NU_STEP = 718, 8
 RU["GOAL_H"] = 711
+RU["TRIG"] = 712
 # draw sites of the GoToPose / TrackXYOVelocity spawn + goal generators
 POSE_SITES = {("USV_go_to_pose.py", 240): RU["GOAL"], ("USV_go_to_pose.py", 248): RU["GOAL_H"],
               ("USV_go_to_pose.py", 305): RU["SPAWN_R"], ("USV_go_to_pose.py", 306): RU["SPAWN_TH"],
@@ -509,6 +581,14 @@ def map_reset_draws(draws, k):
         else:
             raise RuntimeError(f"unmapped reset draw site {fn}:{line} ({fname})")
     return U
+
+
+def map_reset_trig(trig, k):
+    """The recorded torch.cos / torch.sin values of one reset batch -> [k][6] (RU_TRIG offsets; NaN: not called)."""
+    T = np.full((k, 6), np.nan, np.float32)
+    for off, t in trig:
+        T[:, off] = t.numpy().astype(np.float32).reshape(k)
+    return T
 
 
 def map_step_draws(draws, n):
@@ -826,8 +906,9 @@ def gen_episode(torch, variant, n, steps, seed):
     usv, heron, world, task_cfg = build_usv(torch, n, variant)
     ve = make_vecenv(torch, usv, world)
     rec = RandRecorder(torch)
+    trec = TrigRecorder(torch)
     rng = np.random.default_rng(seed)
-    with rec:
+    with rec, trec:
         usv.post_reset()
         init_draws = rec.take()
         usv.update_state()   # the cached root_* state of the first step (see module doc)
@@ -835,12 +916,13 @@ def gen_episode(torch, variant, n, steps, seed):
         init_tgt = _task_targets(usv.task)[0]
         usv.task.reset(torch.arange(n))   # flags only (reset via VecEnv.reset below)
         rec.take()
+        trec.take()
     data = {k: [] for k in ("actions", "obs", "rew", "reset", "progress", "px", "py", "yaw", "vx", "vy", "wz",
                             "fl", "fr", "reset_mask", "u_step", "mass", "com", "k_drag", "thr_l", "thr_r",
                             "k_iz", "obst", "tgt", "extras", "goal_cnt", "bias", "terms")}
     reset_U = []
     usv.task.just_had_been_reset = torch.arange(n)
-    with rec:
+    with rec, trec:
         for t in range(steps):
             reset_mask = usv.reset_buf.numpy().astype(bool).copy() if t > 0 else np.ones(n, bool)
             if t == 0:
@@ -856,10 +938,13 @@ def gen_episode(torch, variant, n, steps, seed):
                                                              "add_noise_on_pos", "add_noise_on_act")]
             Us, _ = map_step_draws(draws, n)
             k = int(reset_mask.sum())
+            trig = trec.take()
             if k:
-                reset_U.append(map_reset_draws(reset_draws, k))
+                Ur = map_reset_draws(reset_draws, k)
+                Ur[:, RU["TRIG"]:RU["TRIG"] + 6] = map_reset_trig(trig, k)
+                reset_U.append(Ur)
             else:
-                assert not reset_draws, reset_draws
+                assert not reset_draws and not trig, (reset_draws, trig)
             data["actions"].append(act)
             data["bias"].append(np.float32(usv._initial_action_bias if bias_active else 0.0))
             data["obs"].append(obs_dict["obs"]["state"].numpy().copy())
