@@ -699,9 +699,26 @@ int ppo_minibatch_fused_dp(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, 
                            const float *exp_adv, float *exp_mu, float *exp_sigma, float *grad, float *losses,
                            float *partials, double *work, float *kl_prev_out, void *stream);
 
+/* Several ranks WITHOUT the peer exchange (its set-up or start-up test failed, or USV_DP_EXCHANGE=collective): the
+ * RCCL fallback, still two launches per minibatch.  The caller SUM-all-reduces grad[0, PPO_NPARAM] (gradient + KL,
+ * a2c_common.py:308-323, 1218-1222) in stream order after each ppo_minibatch_coll; minibatch seq's gradient kernel
+ * then takes minibatch seq - 1's clip + Adam + LR step itself in every workgroup (the all-reduced gradient x
+ * grad_scale = 1 / world, ppo_minibatch_apply's norm of it) from bank (seq - 1) % 2 into bank seq % 2 and trains on
+ * the result; ppo_minibatch_coll_finish takes the last minibatch's step.  Same bits as ppo_minibatch_grad +
+ * all-reduce + ppo_minibatch_apply(grad_scale, norm_from_partials = 0) per minibatch; banks / opt / kl outputs as
+ * ppo_minibatch_fused (state in bank count % 2).  Graph-capturable with the collectives (nccl). */
+int ppo_minibatch_coll(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int seq, float grad_scale,
+                       double *obs_rms, int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+                       const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
+                       float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
+                       float *kl_prev_out, void *stream);
+int ppo_minibatch_coll_finish(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int count, const float *grad,
+                              float grad_scale, float *kl_out, void *stream);
+
 /* size (floats) of the per-block partial-gradient scratch of ppo_minibatch_grad (16-byte aligned): one row per
  * 32-row workgroup, chunk-major ([128-slot chunk][workgroup][128]) for the reduction's contiguous reads, then the
- * group fold's rows and control words; <= 0 when the chunk-major rows would not fit in front of the fold words */
+ * group fold's rows and control words (after the larger of the two row layouts); <= 0 when minibatch is not a
+ * positive multiple of 32 or the buffer would pass 2^31 floats -- the minibatch entry points return 2 then */
 int ppo_partials_floats(int minibatch);
 /* size (floats) of the grad buffer of ppo_minibatch_grad / ppo_minibatch_apply */
 int ppo_grad_floats(void);

@@ -78,6 +78,8 @@ def _declare(lib):
         "ppo_minibatch_apply": [P, P, P, P, P, P, I, F, P, I, P],
         "ppo_minibatch_fused": [P, P, I, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_minibatch_finish": [P, P, I, P, P, P],
+        "ppo_minibatch_coll": [P, P, I, F, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+        "ppo_minibatch_coll_finish": [P, P, I, P, F, P, P],
         "ppo_minibatch_fused_dp": [P, P, P, I, P, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
         "ppo_dp_alloc": [P, P],
         "ppo_dp_open": [P, P],

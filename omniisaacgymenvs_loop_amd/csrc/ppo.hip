@@ -933,6 +933,7 @@ struct ChainIn {
   uint32_t *dp_clock;                      // several ranks: the minibatch counter the next reduction keys its
                                            // exchange on (advanced here, by workgroup 0; nullable)
   int fold_skip;                           // group fold: arrive but fold nothing (tests: the reduction's raw-row path)
+  float gscale;                            // collective chain (kColl): 1 / world, the all-reduced gradient's scale
 };
 
 // x rows of the gradient kernel padded to whole staging passes: every thread stores its slots
@@ -1052,11 +1053,17 @@ static_assert(RD_G >= FOLD_G, "k_reduce_partials(fold = 1) reads one group row p
 constexpr int FOLD_MAX_M = 32;                      // nblk <= 256: the grid is resident at one workgroup per CU
 constexpr int FOLD_CTL_STRIDE = 64;                 // u32 words per group: [0] counter, [32 + m] slice gens
 constexpr uint64_t FOLD_WAIT_TICKS = 10000;         // 100 us at the 100 MHz wall clock
+// floats in front of the fold control words: the larger of the chunk-major rows (RED_BLOCKS x RD_P per row, 112
+// floats more than a row-major row) and the row-major rows + the group rows, so every minibatch size has a layout
+__host__ __device__ constexpr size_t part_body_floats(int nblk) {
+  return (size_t)nblk * RED_BLOCKS * RD_P > (size_t)(nblk + FOLD_G) * NPART_PAD ? (size_t)nblk * RED_BLOCKS * RD_P
+                                                                                 : (size_t)(nblk + FOLD_G) * NPART_PAD;
+}
 __device__ __forceinline__ uint32_t *fold_ctl(float *partials, int nblk) {
-  return reinterpret_cast<uint32_t *>(partials + (size_t)(nblk + FOLD_G) * NPART_PAD);
+  return reinterpret_cast<uint32_t *>(partials + part_body_floats(nblk));
 }
 __device__ __forceinline__ const uint32_t *fold_ctl(const float *partials, int nblk) {
-  return reinterpret_cast<const uint32_t *>(partials + (size_t)(nblk + FOLD_G) * NPART_PAD);
+  return reinterpret_cast<const uint32_t *>(partials + part_body_floats(nblk));
 }
 __device__ __forceinline__ f32x4v ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return __builtin_bit_cast(f32x4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, AUX_SC1));
@@ -1066,12 +1073,13 @@ __device__ __forceinline__ f32x4v ld4_sc1(__amdgpu_buffer_rsrc_t r, uint32_t byt
 // coefficient, straight into this workgroup's LDS weights (and sigma into ls0 / ls1);
 // workgroup (q / GTB) % grid writes parameter chunk q / GTB of the redone state over bank cur
 // (no workgroup of this launch reads bank cur after its first barrier)
+// (scale: 1 on one rank; the collective chain's 1 / world -- k_apply's g * grad_scale * coef)
 __device__ __forceinline__ void redo_step(const ppo_cfg_t &c, const ChainIn &ch, const float (&op)[8], float coef,
-                                          GradSmem &s, float &ls0, float &ls1) {
+                                          float scale, GradSmem &s, float &ls0, float &ls1) {
   const AdamK ak = adam_consts_tagged(c, op[0], op[1] + 1.0f, op[4], op[5], op[6], op[7]);
   for (int q = threadIdx.x; q < PPO_NPARAM; q += GTB) {
     float pn, mn, vn;
-    adam_one(c, ak, ch.grad[q] * 1.0f * coef, ch.P_prev[q], ch.m_prev[q], ch.v_prev[q], pn, mn, vn);
+    adam_one(c, ak, ch.grad[q] * scale * coef, ch.P_prev[q], ch.m_prev[q], ch.v_prev[q], pn, mn, vn);
     if ((q / GTB) % gridDim.x == blockIdx.x) {
       ch.P_cur[q] = pn; ch.m_cur[q] = mn; ch.v_cur[q] = vn;
     }
@@ -1088,15 +1096,42 @@ __device__ __forceinline__ void redo_step(const ppo_cfg_t &c, const ChainIn &ch,
     }
   }
   float pn, mn, vn;
-  adam_one(c, ak, ch.grad[PPO_OFF_SIGMA] * 1.0f * coef, ch.P_prev[PPO_OFF_SIGMA], ch.m_prev[PPO_OFF_SIGMA],
+  adam_one(c, ak, ch.grad[PPO_OFF_SIGMA] * scale * coef, ch.P_prev[PPO_OFF_SIGMA], ch.m_prev[PPO_OFF_SIGMA],
            ch.v_prev[PPO_OFF_SIGMA], pn, mn, vn);
   ls0 = pn;
-  adam_one(c, ak, ch.grad[PPO_OFF_SIGMA + 1] * 1.0f * coef, ch.P_prev[PPO_OFF_SIGMA + 1],
+  adam_one(c, ak, ch.grad[PPO_OFF_SIGMA + 1] * scale * coef, ch.P_prev[PPO_OFF_SIGMA + 1],
            ch.m_prev[PPO_OFF_SIGMA + 1], ch.v_prev[PPO_OFF_SIGMA + 1], pn, mn, vn);
   ls1 = pn;
 }
 
-template <bool kBf, bool kChain, bool kFold>
+// The norm of the all-reduced, scaled gradient as k_apply<false, ..> forms it (the same 256 threads, float4
+// order, fma chain, wave sums and wave order), so the collective chain's step is the split path's bit for bit
+constexpr int APN_TB = 256;
+__device__ __forceinline__ float apply_norm_part(const float *__restrict__ grad_in, float grad_scale, int tid) {
+  constexpr int N4 = PPO_NPARAM / 4, U = (N4 + APN_TB - 1) / APN_TB;
+  const float4 *g4 = reinterpret_cast<const float4 *>(grad_in);
+  float4 gv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) gv[u] = g4[min(tid + u * APN_TB, N4 - 1)];
+  float ss = 0.f;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (tid + u * APN_TB >= N4) continue;
+    const float x = gv[u].x * grad_scale, y = gv[u].y * grad_scale;
+    const float z = gv[u].z * grad_scale, w = gv[u].w * grad_scale;
+    ss = fmaf(x, x, ss); ss = fmaf(y, y, ss); ss = fmaf(z, z, ss); ss = fmaf(w, w, ss);
+  }
+  for (int r = 4 * N4 + tid; r < PPO_NPARAM; r += APN_TB) {
+    const float g = grad_in[r] * grad_scale;
+    ss = fmaf(g, g, ss);
+  }
+  return ss;
+}
+
+// kColl (several ranks without the peer exchange: ppo_minibatch_coll): ch.grad holds minibatch k-1's gradient and
+// KL after the host's in-stream SUM all-reduce; nothing was stepped speculatively, so every workgroup takes that
+// step itself (redo_step from bank prev with coefficient and scale, k_apply's norm of the scaled gradient).
+template <bool kBf, bool kChain, bool kFold, bool kColl = false>
 __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch, const float *__restrict__ P,
                                           const double *__restrict__ obs_rms, int row0,
                                           const float *__restrict__ e_obs, const float *__restrict__ e_act,
@@ -1195,11 +1230,18 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   for (int u = 0; u < NTLG; ++u)
     if (tid + u * GTB < TAIL) s.tail[tid + u * GTB] = tlr[u];
   if (tid < NH) s.b1[tid] = b1r;
-  if (kChain && w < 4) {   // k_apply's norm: the same lanes, the same order
+  if (kChain && !kColl && w < 4) {   // k_apply's norm: the same lanes, the same order
     const float t = wave_sum(csq);
     if (lane == 0) s.nrm[w] = t;
   }
   __syncthreads();
+  if constexpr (kColl) {   // k_apply<false, ..>'s norm of the all-reduced gradient (waves 0-3)
+    if (w < 4) {
+      const float t = wave_sum(apply_norm_part(ch.grad, ch.gscale, tid));
+      if (lane == 0) s.nrm[w] = t;
+    }
+    __syncthreads();
+  }
   bool slow = false;
   if constexpr (kChain) {
     // (the scalars are read out of ov's lanes only where they are used: readlane ignores exec)
@@ -1208,20 +1250,21 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
     };
     const float total_norm = sqrtf(((s.nrm[0] + s.nrm[1]) + s.nrm[2]) + s.nrm[3]);
     const float coef = clip_coef(c, total_norm);
+    const float gscale = kColl ? ch.gscale : 1.0f;
     // (wave 4 of workgroup 0: the kh = 1 waves only commit W2 while layer 1 runs)
     if (blockIdx.x == 0 && tid == 256) {
       float op[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) op[q] = lane_of(q);
-      const float kl_prev = lane_of(8);
+      const float kl_prev = kColl ? lane_of(8) * gscale : lane_of(8);   // k_apply: grad[NPARAM] * grad_scale
       opt_store(c, opt_next(c, op, kl_prev), ch.opt_cur, total_norm, kl_prev, ch.kl_out);
     }
-    if (coef < 1.0f) {   // uniform over the launch
+    if (kColl || coef < 1.0f) {   // uniform over the launch
       slow = true;
       float op[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) op[q] = lane_of(q);
-      redo_step(c, ch, op, coef, s, lsig0, lsig1);
+      redo_step(c, ch, op, coef, gscale, s, lsig0, lsig1);
       __syncthreads();
     }
   }
@@ -1609,7 +1652,7 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   }
 }
 
-template <bool kBf, bool kChain, bool kFold>
+template <bool kBf, bool kChain, bool kFold, bool kColl = false>
 __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, ChainIn ch, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms, int row0,
                                                     const float *__restrict__ e_obs, const float *__restrict__ e_act,
@@ -1617,8 +1660,8 @@ __global__ __launch_bounds__(GTB, 2) void k_mb_grad(ppo_cfg_t c, ChainIn ch, con
                                                     const float *__restrict__ e_ret, const float *__restrict__ e_adv,
                                                     float *e_mu, float *e_sigma, float *partials) {
   __shared__ GradSmem s;
-  mb_grad8w<kBf, kChain, kFold>(c, ch, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu, e_sigma,
-                                partials, s);
+  mb_grad8w<kBf, kChain, kFold, kColl>(c, ch, P, obs_rms, row0, e_obs, e_act, e_nlp, e_val, e_ret, e_adv, e_mu,
+                                       e_sigma, partials, s);
 }
 
 // k_reduce_partials: the per-workgroup partial rows (stride NPART_PAD floats, 16-B aligned)
@@ -2053,7 +2096,7 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        void *stream) {
   (void)val_rms;
   if (!cfg || !params || !obs_rms || !grad || !partials || !work) return 1;
-  if (cfg->minibatch % RB != 0) return 2;
+  if (cfg->minibatch % RB != 0 || ppo_partials_floats(cfg->minibatch) <= 0) return 2;   // no partial layout
   if (reinterpret_cast<uintptr_t>(params) & 15u) return 4;   // 16-byte weight staging loads
   hipStream_t s = (hipStream_t)stream;
   const int row0 = mb_index * cfg->minibatch;
@@ -2097,7 +2140,7 @@ static int fused_launch(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, con
                         float *kl_prev_out, void *stream) {
   if (!cfg || !obs_rms || !grad || !partials || !work || seq < 0) return 1;
   if (!banks_ok(banks)) return 4;
-  if (cfg->minibatch % RB != 0) return 2;
+  if (cfg->minibatch % RB != 0 || ppo_partials_floats(cfg->minibatch) <= 0) return 2;   // no partial layout
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
   if (dp) {
     if (dp->world < 1 || dp->world > PPO_DP_MAX || dp->rank < 0 || dp->rank >= dp->world || !dp->clock || !dp->err)
@@ -2163,6 +2206,64 @@ int ppo_minibatch_fused_dp(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, 
   if (!dp) return 5;
   return fused_launch(cfg, banks, dp, seq, obs_rms, update_obs_rms, mb_index, exp_obs, exp_act, exp_nlp, exp_val,
                       exp_ret, exp_adv, exp_mu, exp_sigma, grad, losses, partials, work, kl_prev_out, stream);
+}
+
+// Several ranks without the peer exchange (the RCCL fallback): two launches per minibatch and an in-stream SUM
+// all-reduce of grad[0, PPO_NPARAM] by the caller in between.  Minibatch seq's gradient kernel first takes
+// minibatch seq - 1's step in every workgroup (redo_step: the all-reduced gradient x grad_scale, k_apply's clip
+// norm of it) from bank (seq - 1) % 2 into bank seq % 2 and trains on the result; its reduction writes the plain
+// gradient sum (ppo_minibatch_grad's); ppo_minibatch_coll_finish takes the last step (k_apply).  The same bits as
+// ppo_minibatch_grad + all-reduce + ppo_minibatch_apply(grad_scale, norm_from_partials = 0).
+int ppo_minibatch_coll(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int seq, float grad_scale,
+                       double *obs_rms, int update_obs_rms, int mb_index, const float *exp_obs, const float *exp_act,
+                       const float *exp_nlp, const float *exp_val, const float *exp_ret, const float *exp_adv,
+                       float *exp_mu, float *exp_sigma, float *grad, float *losses, float *partials, double *work,
+                       float *kl_prev_out, void *stream) {
+  if (!cfg || !obs_rms || !grad || !partials || !work || seq < 0 || !(grad_scale > 0.f)) return 1;
+  if (!banks_ok(banks)) return 4;
+  if (cfg->minibatch % RB != 0 || ppo_partials_floats(cfg->minibatch) <= 0) return 2;   // no partial layout
+  if ((reinterpret_cast<uintptr_t>(partials) | reinterpret_cast<uintptr_t>(grad)) & 15u) return 3;
+  hipStream_t s = (hipStream_t)stream;
+  const int cur = seq & 1, prv = cur ^ 1, nblk = cfg->minibatch / RB, row0 = mb_index * cfg->minibatch;
+  if (update_obs_rms && cfg->normalize_input) {
+    hipLaunchKernelGGL(k_obs_stats, dim3(64), dim3(TB), 0, s, *cfg, exp_obs, row0, cfg->minibatch, work + 8, obs_rms,
+                       reinterpret_cast<unsigned *>(work + 7));
+    USV_CHECK_LAUNCH();
+  }
+  const float *P = banks->params[cur];
+  if (seq == 0) {
+    ChainIn ch{};
+    hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, false, false> : k_mb_grad<false, false, false>), dim3(nblk),
+                       dim3(GTB), 0, s, *cfg, ch, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val, exp_ret,
+                       exp_adv, exp_mu, exp_sigma, partials);
+  } else {
+    const ChainIn ch{banks->params[prv], banks->m[prv], banks->v[prv], banks->params[cur], banks->m[cur],
+                     banks->v[cur], grad, banks->opt + 8 * prv, banks->opt + 8 * cur, kl_prev_out, nullptr, 0,
+                     grad_scale};
+    hipLaunchKernelGGL((cfg->bf16_gemm ? k_mb_grad<true, true, false, true> : k_mb_grad<false, true, false, true>),
+                       dim3(nblk), dim3(GTB), 0, s, *cfg, ch, P, obs_rms, row0, exp_obs, exp_act, exp_nlp, exp_val,
+                       exp_ret, exp_adv, exp_mu, exp_sigma, partials);
+  }
+  USV_CHECK_LAUNCH();
+  hipLaunchKernelGGL((k_reduce_partials<false, false>), dim3(RED_BLOCKS), dim3(RD_TB), 0, s, partials, nblk, grad,
+                     losses, 1.0f / (float)cfg->minibatch, *cfg, AdamBanks{}, nullptr, ppo_dp_t{}, 0);
+  USV_CHECK_LAUNCH();
+  return 0;
+}
+
+int ppo_minibatch_coll_finish(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int count, const float *grad,
+                              float grad_scale, float *kl_out, void *stream) {
+  if (!cfg || !grad || count < 1 || !(grad_scale > 0.f)) return 1;
+  if (!banks_ok(banks)) return 4;
+  if (reinterpret_cast<uintptr_t>(grad) & 15u) return 2;
+  const int prv = (count - 1) & 1, cur = count & 1;
+  const AdamBanks a{banks->params[prv], banks->m[prv], banks->v[prv], banks->params[cur], banks->m[cur],
+                    banks->v[cur]};
+  hipLaunchKernelGGL((k_apply<false, false>), dim3((PPO_NPARAM + AP_TB - 1) / AP_TB), dim3(AP_TB), 0,
+                     (hipStream_t)stream, *cfg, a, grad, banks->opt + 8 * prv, banks->opt + 8 * cur, grad_scale,
+                     kl_out);
+  USV_CHECK_LAUNCH();
+  return 0;
 }
 
 long long ppo_dp_buffer_bytes(void) { return DP_BYTES; }
@@ -2255,11 +2356,10 @@ int ppo_minibatch_apply(const ppo_cfg_t *cfg, float *params, float *grad, float 
 
 // per-workgroup rows, the fold's group rows and its control lines (zero-initialised by the caller)
 int ppo_partials_floats(int minibatch) {
-  // the chunk-major rows (RED_BLOCKS x RD_P >= NPART_PAD floats per row) must stay below the fold control words
   static_assert(RED_BLOCKS * RD_P >= NPART_PAD, "chunk-major rows cover a partial row");
-  const int nblk = minibatch / RB;
-  if ((long long)nblk * RED_BLOCKS * RD_P > (long long)(nblk + FOLD_G) * NPART_PAD) return -1;
-  return (nblk + FOLD_G) * NPART_PAD + FOLD_G * FOLD_CTL_STRIDE;
+  if (minibatch < RB || minibatch % RB != 0) return -1;
+  const long long f = (long long)part_body_floats(minibatch / RB) + FOLD_G * FOLD_CTL_STRIDE;
+  return f > 0x7fffffffLL ? -1 : (int)f;
 }
 int ppo_grad_floats(void) { return PPO_NPARAM + 8 + RED_BLOCKS; }
 int ppo_meter_floats(int n_envs, int horizon) {

@@ -302,7 +302,10 @@ class A2CAgent:
         self._h_dp_err = None
         self._tail_staged = False
         self.dp_status = {"exchange": "none (one rank)", "selftest": "not run", "error": None}
-        self._dp = self._peer_exchange() if self.multi_gpu and self.rank_size > 1 else None
+        # the multi-rank update paths (also at world size 1 with USV_DP_RANK_PATHS=1: the one-GPU tests of the
+        # RCCL fallback, whose all-reduce over one rank is the identity)
+        self._dp_ranks = self.multi_gpu and (self.rank_size > 1 or os.getenv("USV_DP_RANK_PATHS", "0") == "1")
+        self._dp = self._peer_exchange() if self._dp_ranks else None
 
     def _peer_exchange(self):
         """Several ranks: the one-shot peer exchange of ppo_minibatch_fused_dp (dist_util.PeerExchange) unless
@@ -411,7 +414,7 @@ class A2CAgent:
     def _allreduce_grad(self) -> float:
         """trancate_gradients_and_step multi-GPU branch (a2c_common.py:309-323): flat SUM / world,
         with the minibatch KL in the same buffer (a2c_common.py:1218-1222)."""
-        if not self.multi_gpu or self.rank_size == 1:
+        if not self._dp_ranks:
             return 1.0
         return dist_util.allreduce_grad(self.grad[:NPARAM + 1])
 
@@ -429,8 +432,14 @@ class A2CAgent:
         """Two launches per minibatch (ppo_minibatch_fused; several ranks: ppo_minibatch_fused_dp with the
         peer exchange inside the reduction); USV_PPO_FUSED=0 keeps the three-launch split (grad, reduce,
         [torch.distributed all-reduce], apply), as does a multi-rank run without the peer exchange."""
-        dp_ok = not (self.multi_gpu and self.rank_size > 1) or getattr(self, "_dp", None) is not None
+        dp_ok = not self._dp_ranks or getattr(self, "_dp", None) is not None
         return dp_ok and os.environ.get("USV_PPO_FUSED", "1") != "0"
+
+    def _coll_update(self) -> bool:
+        """Several ranks without the peer exchange: the collective chain (ppo_minibatch_coll, two launches + the
+        all-reduce per minibatch) unless USV_PPO_FUSED=0 or USV_DP_COLL_CHAIN=0 (the three-launch split)."""
+        return (self._dp_ranks and getattr(self, "_dp", None) is None and os.environ.get("USV_PPO_FUSED", "1") != "0"
+                and os.environ.get("USV_DP_COLL_CHAIN", "1") != "0")
 
     def update_epoch_minibatches(self) -> None:
         """The mini-epoch / minibatch loop (a2c_common.py:1190-1245): per minibatch the gradient kernel
@@ -440,7 +449,7 @@ class A2CAgent:
         c = _capi
         cfg = c.byref(self.cfg)
         s = c.stream_ptr()
-        dp = self.multi_gpu and self.rank_size > 1
+        dp = self._dp_ranks
         k = 0
         seq = self.normalize_input and self.rms_seq.numel() > 1
         if seq:   # RunningMeanStd.train of mini-epoch 0, all minibatches in two launches
@@ -460,11 +469,26 @@ class A2CAgent:
                            c.ptr(self.kls[k - 1:k]) if k else None, s)
                     k += 1
             c.call("ppo_minibatch_finish", cfg, banks, k, c.ptr(self.grad), c.ptr(self.kls[k - 1:k]), s)
-            if k % 2:   # the chain ended in bank 1 / slot 1
-                self.model_params.copy_(self._bank1[0])
-                self.adam_m.copy_(self._bank1[1])
-                self.adam_v.copy_(self._bank1[2])
-                self.opt[:8].copy_(self.opt[8:])
+            self._bank_back(k)
+            return
+        if self._coll_update():
+            # the RCCL fallback on two launches: minibatch k's gradient kernel takes minibatch k-1's step from the
+            # all-reduced [grad, kl] in every workgroup; the in-stream all-reduce sits between the launches
+            banks = c.byref(self._adam_banks())
+            scale = 1.0 / dist_util.world()
+            for mini_ep in range(self.mini_epochs_num):
+                for i in range(self.num_minibatches):
+                    rms = self.rms_seq[2 * NIN * i:] if seq and mini_ep == 0 else self.obs_rms
+                    c.call("ppo_minibatch_coll", cfg, banks, k, float(scale), c.ptr(rms),
+                           int(mini_ep == 0 and not seq), i, c.ptr(self.exp_obs), c.ptr(self.exp_act),
+                           c.ptr(self.exp_nlp), c.ptr(self.exp_val), c.ptr(self.exp_ret), c.ptr(self.exp_adv),
+                           c.ptr(self.exp_mu), c.ptr(self.exp_sigma), c.ptr(self.grad), c.ptr(self.loss_log[k]),
+                           c.ptr(self.partials), c.ptr(self.work), c.ptr(self.kls[k - 1:k]) if k else None, s)
+                    self._allreduce_grad()
+                    k += 1
+            c.call("ppo_minibatch_coll_finish", cfg, banks, k, c.ptr(self.grad), float(scale),
+                   c.ptr(self.kls[k - 1:k]), s)
+            self._bank_back(k)
             return
         for mini_ep in range(self.mini_epochs_num):
             for i in range(self.num_minibatches):
@@ -482,17 +506,25 @@ class A2CAgent:
         if k % 2:   # the last minibatch wrote slot 1: the epoch ends with the state in slot 0
             self.opt[:8].copy_(self.opt[8:])
 
+    def _bank_back(self, k: int) -> None:
+        """A chain of k minibatches ended in bank k % 2: bank 1 / slot 1 is copied back to bank 0 / slot 0."""
+        if k % 2:
+            self.model_params.copy_(self._bank1[0])
+            self.adam_m.copy_(self._bank1[1])
+            self.adam_v.copy_(self._bank1[2])
+            self.opt[:8].copy_(self.opt[8:])
+
     def _update_capturable(self) -> bool:
-        """The minibatch update goes into a HIP graph on one GPU.  With several ranks, RCCL collectives inside
-        a captured graph are opt-in (USV_GRAPH_COLLECTIVES=1, nccl backend only: gloo's host-staged
-        collectives are not capturable); by default the multi-rank update with torch.distributed
-        collectives runs eagerly."""
+        """The minibatch update goes into a HIP graph: on one GPU, with the peer exchange (kernels only), and with
+        the RCCL all-reduces of the collective chain / split path on the nccl backend (USV_GRAPH_COLLECTIVES=0
+        keeps those eager; gloo's host-staged collectives are not capturable).  A capture that fails on any rank
+        sends every rank to the eager update (train_epoch, _ranks_agree)."""
         if getattr(self, "_graph_update_failed", False):
             return False
-        if not self.multi_gpu or self.rank_size == 1 or (self._dp is not None and self._fused_update()):
+        if not self._dp_ranks or (self._dp is not None and self._fused_update()):
             return True   # (the peer exchange is kernels only)
-        # the split path's torch.distributed all-reduces (no peer exchange, or USV_PPO_FUSED=0)
-        return dist_util.backend() == "nccl" and os.getenv("USV_GRAPH_COLLECTIVES", "0") == "1"
+        # the torch.distributed all-reduces (no peer exchange, or USV_PPO_FUSED=0)
+        return dist_util.backend() == "nccl" and os.getenv("USV_GRAPH_COLLECTIVES", "1") == "1"
 
     def _ranks_agree(self, ok: bool) -> bool:
         """All ranks succeeded (MIN over ranks; outside any capture), so no rank replays a graph while another
@@ -500,6 +532,29 @@ class A2CAgent:
         if not self.multi_gpu or self.rank_size == 1:
             return ok
         return dist_util.agree(ok, self.ppo_device)
+
+    def _update_from_graph(self) -> None:
+        """Replay the update graph, capturing it first.  The ranks agree on the capture (MIN over ranks, outside any
+        capture): if it failed on any rank (a collective the backend cannot capture), every rank runs this epoch's
+        update eagerly and stays eager, so no rank replays a graph while another issues eager collectives."""
+        if self._graph_update is not None:
+            self._graph_update.replay()
+            return
+        err = None
+        try:
+            self._graph_update = self._graph_capture(self.update_epoch_minibatches)
+        except RuntimeError as e:
+            err = e
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if not self._ranks_agree(err is None):   # eager from now on, on every rank
+            self._graph_update_failed = True
+            self._graph_update = None
+            if self.rank == 0:
+                print(f"update graph capture failed ({err or 'on another rank'}); the update runs eagerly")
+            self.update_epoch_minibatches()
+        else:
+            self._graph_update.replay()
 
     def _graph_capture(self, fn):
         g = torch.cuda.CUDAGraph()
@@ -546,23 +601,7 @@ class A2CAgent:
         self.curr_frames = batch["played_frames"]
         self.algo_observer.after_steps()
         if graphs and self._update_capturable():
-            if self._graph_update is None:
-                err = None
-                try:
-                    self._graph_update = self._graph_capture(self.update_epoch_minibatches)
-                except RuntimeError as e:   # a collective the backend cannot capture
-                    err = e
-                torch.cuda.synchronize()
-                if not self._ranks_agree(err is None):   # eager from now on, on every rank
-                    self._graph_update_failed = True
-                    self._graph_update = None
-                    if self.rank == 0:
-                        print(f"update graph capture failed ({err or 'on another rank'}); the update runs eagerly")
-                    self.update_epoch_minibatches()
-                else:
-                    self._graph_update.replay()
-            else:
-                self._graph_update.replay()
+            self._update_from_graph()
         else:
             self.update_epoch_minibatches()
         if pev is not None:

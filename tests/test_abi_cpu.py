@@ -110,3 +110,30 @@ def test_stale_root_needs_its_rows():
     assert lib.usv_reset(_capi.byref(cfg), _capi.byref(b), 0, 0, None, None) == 1
     assert lib.usv_env_step(_capi.byref(cfg), _capi.byref(b), ctypes.addressof(dummy), ctypes.addressof(dummy),
                             ctypes.c_float(0.0), 0, 0, None, None) == 1
+
+
+def test_partials_layout_for_every_minibatch_and_refused_sizes():
+    """ppo_partials_floats covers any positive multiple of 32 rows (the reference yaml's horizon x num_envs minibatch,
+    e.g. 65,536 or loopz-sized 76,800 rows, included): the fold control words follow the larger of the chunk-major
+    rows (RED_BLOCKS x 128 floats per 32-row block) and the row-major rows + group rows.  Sizes without a layout
+    are refused by the minibatch entry points with status 2 before any device work (argument checks only)."""
+    from omniisaacgymenvs_loop_amd import _capi
+    from omniisaacgymenvs_loop_amd._abi import DEFINES, PpoCfg
+    if not os.path.exists(_capi.LIB_PATH):
+        pytest.skip("libusv_hip.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_capi.LIB_PATH)
+    red_blocks = (DEFINES["PPO_NPARAM"] + 5 + 127) // 128
+    prev = 0
+    for mb in (32, 8192, 48576, 48608, 65536, 76800, 262144):
+        f = lib.ppo_partials_floats(mb)
+        assert f >= (mb // 32) * red_blocks * 128 + 8 * 64 and f > prev, (mb, f)
+        prev = f
+    for mb in (0, 16, 8200, 2 ** 31 - 32):
+        assert lib.ppo_partials_floats(mb) <= 0, mb
+    cfg = PpoCfg()
+    buf = ctypes.create_string_buffer(1 << 12)
+    p = ctypes.addressof(buf) + (-ctypes.addressof(buf) % 16)   # 16-byte aligned host scratch: never dereferenced
+    for mb in (8200, 2 ** 31 - 32):
+        cfg.minibatch = mb
+        args = [_capi.byref(cfg), p, p, p, 0, 0] + [p] * 9 + [None, p, p, None]   # .., grad, losses, partials, work, stream
+        assert _capi.lib().ppo_minibatch_grad(*args) == 2, mb

@@ -200,19 +200,81 @@ def test_peer_exchange_refuses_more_than_two_ranks_per_device(tmp_path, world, m
 
 
 def test_update_capturable_gates_on_the_path_that_runs(monkeypatch):
-    """Several ranks: the update graph is captured by default only when the peer exchange's kernels ARE the
-    update (fused chain); the split path's torch.distributed all-reduces stay behind USV_GRAPH_COLLECTIVES."""
+    """Several ranks: the update graph is captured by default with the peer exchange (kernels only) and, on the
+    nccl backend, with the RCCL all-reduces of the collective chain (USV_GRAPH_COLLECTIVES=0 keeps them eager; gloo
+    never captures them); the collective chain is the default path without the peer exchange (USV_DP_COLL_CHAIN=0
+    or USV_PPO_FUSED=0: the three-launch split)."""
     from types import SimpleNamespace
     from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
-    ns = SimpleNamespace(multi_gpu=True, rank_size=2, _dp=object())
+    ns = SimpleNamespace(multi_gpu=True, rank_size=2, _dp_ranks=True, _dp=object())
     ns._fused_update = lambda: A2CAgent._fused_update(ns)
-    monkeypatch.delenv("USV_GRAPH_COLLECTIVES", raising=False)
+    ns._coll_update = lambda: A2CAgent._coll_update(ns)
+    for k in ("USV_GRAPH_COLLECTIVES", "USV_DP_COLL_CHAIN"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("USV_DIST_BACKEND", "nccl")
     monkeypatch.setenv("USV_PPO_FUSED", "1")
-    assert A2CAgent._update_capturable(ns)
+    assert A2CAgent._update_capturable(ns) and ns._fused_update() and not ns._coll_update()
+    ns._dp = None                                   # no peer exchange: the collective chain, captured on nccl
+    assert not ns._fused_update() and ns._coll_update() and A2CAgent._update_capturable(ns)
+    monkeypatch.setenv("USV_GRAPH_COLLECTIVES", "0")
+    assert not A2CAgent._update_capturable(ns)
+    monkeypatch.delenv("USV_GRAPH_COLLECTIVES")
+    monkeypatch.setenv("USV_DIST_BACKEND", "gloo")
+    assert not A2CAgent._update_capturable(ns)
+    monkeypatch.setenv("USV_DIST_BACKEND", "nccl")
+    monkeypatch.setenv("USV_DP_COLL_CHAIN", "0")
+    assert not ns._coll_update()                    # the split path
+    monkeypatch.delenv("USV_DP_COLL_CHAIN")
     monkeypatch.setenv("USV_PPO_FUSED", "0")
-    assert not A2CAgent._update_capturable(ns)
-    ns._dp = None
+    assert not ns._coll_update() and not ns._fused_update()
+    ns._dp_ranks, ns.rank_size = False, 1
     monkeypatch.setenv("USV_PPO_FUSED", "1")
-    assert not A2CAgent._update_capturable(ns)
-    ns.rank_size = 1
-    assert A2CAgent._update_capturable(ns)
+    assert A2CAgent._update_capturable(ns) and ns._fused_update() and not ns._coll_update()
+
+
+def _capture_agree_worker(rank, world, port, out_dir, fail_ranks):
+    """One rank of A2CAgent._update_from_graph with a capture that raises on `fail_ranks` (a collective the backend
+    cannot capture): the ranks agree over gloo and every rank takes the eager update, this epoch and the next."""
+    from types import SimpleNamespace
+    from omniisaacgymenvs_loop_amd.rl_games.a2c_continuous import A2CAgent
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        log = []
+        ns = SimpleNamespace(rank=rank, rank_size=world, multi_gpu=True, ppo_device="cpu", _graph_update=None,
+                             _dp_ranks=True, _dp=None)
+
+        class G:
+            def replay(self):
+                log.append("replay")
+
+        def capture(fn):
+            if rank in fail_ranks:
+                raise RuntimeError("operation not permitted when stream is capturing")
+            return G()
+        ns._graph_capture = capture
+        ns.update_epoch_minibatches = lambda: log.append("eager")
+        ns._ranks_agree = lambda ok: A2CAgent._ranks_agree(ns, ok)
+        ns._fused_update = lambda: A2CAgent._fused_update(ns)
+        for _ in range(2):   # two epochs: capture (or fall back), then the steady state
+            if A2CAgent._update_capturable(ns):
+                A2CAgent._update_from_graph(ns)
+            else:
+                ns.update_epoch_minibatches()
+        np.savez(os.path.join(out_dir, f"cap{rank}.npz"), log=np.array(log), failed=getattr(ns, "_graph_update_failed",
+                                                                                             False))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_ranks", [(), (1,), (0, 1)])
+def test_graph_capture_agreement_chooses_one_path_on_every_rank(tmp_path, fail_ranks, monkeypatch):
+    """The update graph with RCCL collectives (the default on nccl): when the capture fails on any rank, every rank
+    runs the update eagerly (now and in later epochs); when it succeeds on all, every rank replays the graph.  gloo
+    carries the agreement here, as the nccl backend does on the GPUs."""
+    monkeypatch.setenv("USV_DIST_BACKEND", "nccl")   # the capture gate of the GPU runs (the agreement still uses gloo)
+    monkeypatch.delenv("USV_GRAPH_COLLECTIVES", raising=False)
+    mp.spawn(_capture_agree_worker, args=(2, _port(), str(tmp_path), fail_ranks), nprocs=2, join=True)
+    logs = [list(np.load(tmp_path / f"cap{r}.npz")["log"]) for r in range(2)]
+    want = ["eager", "eager"] if fail_ranks else ["replay", "replay"]
+    assert logs == [want, want], logs

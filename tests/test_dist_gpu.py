@@ -282,10 +282,38 @@ def _worker_rccl_one_rank(rank, port, out_dir):
         _load(plain, data, rows)
         plain.update_epoch_minibatches()
         torch.cuda.synchronize()
+        # the collective chain (ppo_minibatch_coll: two launches + the all-reduce per minibatch, the default
+        # fallback of several ranks) on the multi-rank paths at world 1, eager and captured, against the split
+        # path of several ranks (clip norm from the all-reduced gradient) without a collective
+        os.environ.update(USV_DP_RANK_PATHS="1", USV_DP_EXCHANGE="collective", USV_PPO_FUSED="1")
+        n0 = len(calls)
+        coll = with_allreduce(_agent(N, MB, True))
+        assert coll._dp is None and coll._coll_update() and coll._update_capturable()
+        _load(coll, data, rows)
+        coll.update_epoch_minibatches()
+        torch.cuda.synchronize()
+        n_coll = len(calls) - n0
+        collg = with_allreduce(_agent(N, MB, True))
+        _load(collg, data, rows)
+        collg._graph_capture(collg.update_epoch_minibatches).replay()
+        torch.cuda.synchronize()
+        n_collg = len(calls) - n0 - n_coll
+        os.environ["USV_PPO_FUSED"] = "0"
+        split = _agent(N, MB, True)           # split path, several-rank semantics, no collective at world 1
+        assert split._dp_ranks and not split._coll_update()
+        _load(split, data, rows)
+        split.update_epoch_minibatches()
+        torch.cuda.synchronize()
+        st = lambda ag: np.concatenate([ag.model_params.cpu().numpy(), ag.adam_m.cpu().numpy(),
+                                        ag.adam_v.cpu().numpy(), ag.opt[:8].cpu().numpy()])
         np.savez(os.path.join(out_dir, "rccl.npz"), eager=eager.model_params.cpu().numpy(),
                  graph=graph.model_params.cpu().numpy(), plain=plain.model_params.cpu().numpy(),
                  kl_eager=eager.kls.cpu().numpy(), kl_graph=graph.kls.cpu().numpy(), kl_plain=plain.kls.cpu().numpy(),
-                 n_eager=n_eager, n_capture=len(calls) - n_eager, minibatches=EPOCHS * N * H // MB)
+                 n_eager=n_eager, n_capture=n0 - n_eager, minibatches=EPOCHS * N * H // MB,
+                 coll=st(coll), collg=st(collg), split=st(split), kl_coll=coll.kls.cpu().numpy(),
+                 kl_collg=collg.kls.cpu().numpy(), kl_split=split.kls.cpu().numpy(),
+                 loss_coll=coll.loss_log.cpu().numpy(), loss_split=split.loss_log.cpu().numpy(),
+                 n_coll=n_coll, n_collg=n_collg)
     finally:
         dist.destroy_process_group()
 
@@ -304,3 +332,10 @@ def test_rccl_fallback_collective_on_one_rank(tmp_path):
     np.testing.assert_array_equal(r["kl_eager"], r["kl_plain"])
     np.testing.assert_array_equal(r["kl_graph"], r["kl_plain"])
     assert not np.array_equal(r["plain"], _agent(N, MB, False).model_params.cpu().numpy())   # the update moved them
+    # the collective chain: one all-reduce per minibatch, eager and captured, the split path's bits (parameters,
+    # Adam moments, optimiser scalars, KLs, losses)
+    assert int(r["n_coll"]) == int(r["n_collg"]) == int(r["minibatches"])
+    for k in ("coll", "collg"):
+        np.testing.assert_array_equal(r[k], r["split"], err_msg=k)
+        np.testing.assert_array_equal(r[f"kl_{k}"], r["kl_split"], err_msg=k)
+    np.testing.assert_array_equal(r["loss_coll"], r["loss_split"])

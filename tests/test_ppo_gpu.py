@@ -184,14 +184,16 @@ def test_minibatch_epoch_vs_reference(ppo):
         ET.record(tn, f"w:{k}", Pf[k], v)
 
 
-@pytest.mark.parametrize("entropy_coef,bf16", [(0.0, False), (0.01, False), (0.0, True)])
-def test_minibatch_gradient_vs_oracle_full_size(entropy_coef, bf16):
+@pytest.mark.parametrize("entropy_coef,bf16,rows", [(0.0, False, 8192), (0.01, False, 8192), (0.0, True, 8192),
+                                                    (0.0, False, 65536)])
+def test_minibatch_gradient_vs_oracle_full_size(entropy_coef, bf16, rows):
     """One 8192-row minibatch (BASELINE minibatch_size) vs the numpy oracle's gradient (with and without
     the entropy bonus of a2c_continuous.py:159); bf16: the bf16 GEMM mode (mixed_precision, BASELINE
     configs[2]) vs the oracle with the same bf16 operand rounding (1e-5 of the largest component) and,
-    recorded, vs fp32."""
-    N, H = 512, 16
-    ag = _agent(N, 8192, mini_epochs=1)
+    recorded, vs fp32.  65,536 rows: a minibatch of horizon_length x num_envs (the reference yaml's suggestion),
+    2,048 gradient workgroups whose chunk-major partial rows need more than the row-major footprint."""
+    N, H = rows // 16, 16
+    ag = _agent(N, rows, mini_epochs=1)
     ag.cfg.entropy_coef = entropy_coef
     ag.cfg.bf16_gemm = int(bf16)
     rng = np.random.default_rng(0)
@@ -221,13 +223,13 @@ def test_minibatch_gradient_vs_oracle_full_size(entropy_coef, bf16):
     orms.update(obs)
     np.testing.assert_allclose(ag.obs_rms.cpu().numpy()[:33], orms.mean, rtol=1e-6, atol=1e-9)
     g_ref, losses, kl, _, _ = PO.minibatch_grad(P, orms.norm(obs), act, nlp0, val, ret, adv, mu0 + 0.01, sig0,
-                                                PO.PPOConfig(minibatch=8192, entropy_coef=entropy_coef), lowp=bf16)
+                                                PO.PPOConfig(minibatch=rows, entropy_coef=entropy_coef), lowp=bf16)
     g = ag.grad.cpu().numpy()[:PO.NPARAM]
     scale = np.abs(g_ref).max()
-    tn = f"ppo_grad_full_ent{entropy_coef}" + ("_bf16" if bf16 else "")
+    tn = f"ppo_grad_full_ent{entropy_coef}" + ("_bf16" if bf16 else "") + ("" if rows == 8192 else f"_{rows}")
     if bf16:   # the bf16 mode's distance from the fp32 gradient (documented, not asserted)
         g32, _, _, _, _ = PO.minibatch_grad(P, orms.norm(obs), act, nlp0, val, ret, adv, mu0 + 0.01, sig0,
-                                            PO.PPOConfig(minibatch=8192, entropy_coef=entropy_coef))
+                                            PO.PPOConfig(minibatch=rows, entropy_coef=entropy_coef))
         ET.record(tn, "grad/max vs fp32", g / scale, g32 / scale)
     # 8192-row sums in different orders: each component within 1e-5 of the largest one.  bf16 mode: 5e-5 --
     # an operand whose fp32 value differs from the oracle's in the last bit can round to the neighbouring
