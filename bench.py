@@ -302,7 +302,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=HEADLINE_ENVS,
                     help="envs per GPU (default: BASELINE configs[4]'s per-GPU share, 131072 = 2^20 / 8)")
-    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--seeds", default="0,1,2,3,4",
+                    help="BASELINE.md's protocol: the headline (W warmup + K timed epochs) once per seed; `value` is "
+                         "the median, extra.seeds the per-seed values and min / max.  The first seed's run also "
+                         "carries the kernel timings, fps definitions, milestones and the sustained rate")
+    ap.add_argument("--seed", type=int, default=None, help="one seed only (same as --seeds <seed>)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches (no HIP graph capture)")
     ap.add_argument("--task", default="CaptureXY", choices=sorted(TASKS) + ["multitask"],
@@ -315,10 +319,12 @@ def main():
     ap.add_argument("--extra-steps", type=int, default=10,
                     help="one GPU: epochs of each of the configs[2] / configs[3] lines (extra.c3, extra.c4_pose, "
                          "extra.c4_track; 0 = skip)")
-    ap.add_argument("--milestone-seconds", type=float, default=30.0,
-                    help="one GPU: keep training after the measurements until rewards/step >= the last milestone "
-                         "or this many seconds (wall-clock to learning milestones; 0 = skip)")
+    ap.add_argument("--milestone-seconds", type=float, default=25.0,
+                    help="one GPU: keep training after the measurements for this many seconds: wall-clock to the "
+                         "learning milestones, and `sustained` = the mean rate over these epochs (0 = skip)")
     args = ap.parse_args()
+    seeds = [args.seed] if args.seed is not None else [int(x) for x in args.seeds.split(",") if x.strip()]
+    args.seed = seeds[0]
     import torch
     import torch.distributed as dist
     rank, world, local = _dist_setup(args.gpus)
@@ -478,13 +484,25 @@ def main():
     agent.obs, agent.dones = o_env, d_env   # the agent continues from the env's current state
     env_fps = args.envs * nenv / (time.perf_counter() - t1)
 
-    # wall-clock to learning milestones (one GPU): keep training until the last milestone or the budget
+    # wall-clock to learning milestones (one GPU), and the sustained rate: keep training for the budget; the mean
+    # env-steps/s over these epochs (resets grow as the policy learns, so late epochs cost more than the early ones
+    # the headline times)
+    sustained = None
     if world == 1 and args.milestone_seconds > 0:
+        torch.cuda.synchronize()
         t_m = time.perf_counter()
-        while miles[str(MILESTONES[-1])] is None and time.perf_counter() - t_m < args.milestone_seconds:
+        e_m = agent.epoch_num
+        while time.perf_counter() - t_m < args.milestone_seconds:
             agent.update_epoch()
             agent.train_epoch()
             note_reward()
+        torch.cuda.synchronize()
+        dt_m = time.perf_counter() - t_m
+        n_m = agent.epoch_num - e_m
+        sustained = {"value": args.envs * agent.horizon_length * n_m / dt_m, "unit": "env-steps/s",
+                     "epochs": [e_m + 1, agent.epoch_num], "seconds": dt_m,
+                     "ms_per_step": dt_m / max(n_m, 1) * 1e3,
+                     "method": "graph-replayed train epochs after the measurements, wall clock over all of them"}
 
     env_ms = env_timer.mean_ms()
     ppo_ms = ppo_timer.mean_ms()
@@ -552,6 +570,8 @@ def main():
                                          last100_mean_at_end=float(agent.game_rewards.get_mean())),
             "extra": dict(phase, **(dp_extra if world > 1 else {})),
         }
+        if sustained is not None:
+            out["sustained"] = sustained
         tf = os.path.join(ROOT, "profiles", f"env_step_traffic_{args.envs}.json")
         if not os.path.exists(tf) and args.envs == C2_ENVS:
             tf = os.path.join(ROOT, "profiles", "env_step_traffic.json")
@@ -563,6 +583,42 @@ def main():
                 out["roofline"]["traffic_read"] = tr.get("read_bytes_per_launch")
                 out["roofline"]["traffic_write"] = tr.get("write_bytes_per_launch")
                 out["roofline"]["traffic_source"] = tr.get("source")
+    # the other seeds of the protocol: the same build, W warmup and K timed epochs each (the first seed's run
+    # above is seed_values[0]); value = the median
+    seed_values = [value]
+    seed_ms = [elapsed / args.steps * 1e3]
+    if len(seeds) > 1:
+        if agent._dp is not None:
+            torch.cuda.synchronize()
+            agent._dp.release()
+        del agent, env, task
+        torch.cuda.empty_cache()
+        for sd in seeds[1:]:
+            env_s, task_s, agent_s = build(args.envs, local, world, sd, task_name, args.mixed_precision)
+            agent_s.use_graph = not args.no_graph
+            agent_s.obs = agent_s.env_reset()
+            for _ in range(max(args.warmup, 2)):
+                agent_s.update_epoch()
+                agent_s.train_epoch()
+            el_s = time_epochs(agent_s, args.steps, world, local)
+            seed_values.append(world * args.envs * agent_s.horizon_length * args.steps / el_s)
+            seed_ms.append(el_s / args.steps * 1e3)
+            if agent_s._dp is not None:
+                torch.cuda.synchronize()
+                agent_s._dp.release()
+            del agent_s, env_s, task_s
+            torch.cuda.empty_cache()
+        agent = env = task = None
+    med = sorted(range(len(seeds)), key=lambda i: seed_values[i])[(len(seeds) - 1) // 2]
+    if out is not None:
+        out["value"] = seed_values[med]
+        out["ms_per_step"] = seed_ms[med]
+        out["extra"]["seeds"] = {"seeds": seeds, "values": seed_values, "ms_per_step": seed_ms,
+                                 "median": seed_values[med], "min": min(seed_values), "max": max(seed_values),
+                                 "median_seed": seeds[med],
+                                 "note": "value / ms_per_step = the median seed's run (BASELINE.md protocol, seeds "
+                                         "0-4); the kernel timings, fps definitions, milestones and `sustained` "
+                                         f"come from seed {seeds[0]}'s run"}
     # secondary lines, same code path, graph-replayed epochs: BASELINE configs[1] (4096 envs/GPU) on any number
     # of ranks; on one GPU also configs[2] (65536 envs, bf16 GEMMs) and configs[3]'s per-GPU share of each task
     if args.envs != HEADLINE_ENVS or task_name != "CaptureXY" or args.mixed_precision:
@@ -581,7 +637,7 @@ def main():
                 ("c4_track", C4_ENVS, "TrackXYOVelocity", False, args.extra_steps,
                  f"USV_Virtual_TrackXYOVelocity num_envs={C4_ENVS}/GPU PPO-MLP fp32 (BASELINE configs[3]'s "
                  "per-GPU share, the TrackXYOVelocity ranks)")]
-    if any(st for *_, st, _ in secondary):
+    if any(st for *_, st, _ in secondary) and agent is not None:
         if agent._dp is not None:   # every rank: the headline agent's peer buffers, before the next agent maps its own
             torch.cuda.synchronize()
             agent._dp.release()

@@ -10,7 +10,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-B="$R/bench.py --steps 5 --warmup 2 --envs $ENVS --no-cpu-baseline --c2-steps 0 --extra-steps 0 --milestone-seconds 0"
+B="$R/bench.py --steps 5 --warmup 2 --envs $ENVS --seeds 0 --no-cpu-baseline --c2-steps 0 --extra-steps 0 --milestone-seconds 0"
 timeout -k 10 420 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT" -o trace -- python3 $B > "$OUT/trace.log" 2>&1
 echo "trace done"
 # the passes below count k_env_step alone: the plain sequential step (the overlapped one shares the GPU

@@ -233,3 +233,50 @@ def test_imitation_update_vs_reference(golden):
                             L.Config(im_coef=float(np.float32(0.7))), expert=d["expert_act"])
     bad_o = ~np.isclose(got - p0, pv - p0, rtol=1e-3, atol=2e-7)
     assert bad_o.mean() < 2e-3, int(bad_o.sum())
+
+
+def test_imitation_gradient_vs_oracle_each_step(golden):
+    """The imitation update on identical inputs at every step: the 16 minibatch gradients of the fixture's rollout
+    (loopz_update_expert.npz, in-order minibatches, (1 - rl_coeff) = 0.7 with the frozen expert's actions on the
+    stored observations) from the oracle's parameters before each step, against the oracle's gradient at 1e-5 of
+    its largest component (test_minibatch_vs_oracle's bar) -- no drift carried from step to step, no outliers
+    allowed.  The oracle then takes the clipped Adam step and both continue from its parameters."""
+    d = golden("loopz_update_expert.npz")
+    T, n = d["rew"].shape
+    ppo = _build(n, T, d, flat_expert=_Expert(d["expert_w"]))
+    ppo.update_rl_coeff(0.3)
+    st = ppo.storage
+    data = {"obs": d["obs"][:T], "actions": d["actions"], "logp": d["logp"], "values": d["values"],
+            "returns": d["returns"], "advantages": d["advantages"]}
+    for k, buf in (("obs", st.actor_obs), ("actions", st.actions), ("logp", st.actions_log_prob), ("values", st.values),
+                   ("returns", st.returns), ("advantages", st.advantages)):
+        buf.copy_(torch.tensor(np.ascontiguousarray(data[k]).reshape(buf.shape)))
+    ppo._bind_expert()
+    ex = ppo._expert_act.cpu().numpy().reshape(-1, 2)       # the kernel's expert actions, fed to the oracle too
+    np.testing.assert_allclose(ex, np.asarray(d["expert_act"]).reshape(-1, 2), rtol=1e-5, atol=1e-6)
+    cfg = L.Config(im_coef=float(np.float32(0.7)))
+    assert float(ppo.cfg.im_coef) == cfg.im_coef
+    flat = {k: np.asarray(v, np.float32).reshape((T * n,) + np.asarray(v).shape[2:]) for k, v in data.items()}
+    M = T * n // 4
+    pv = _params(d, "init")
+    adam = L.Adam.zeros(len(pv))
+    from omniisaacgymenvs_loop_amd import _capi
+    np_ = ppo.nparam
+    for k in range(16):
+        i = k % 4
+        sl = slice(i * M, (i + 1) * M)
+        ppo.params.copy_(torch.tensor(pv, device=DEV))
+        _capi.call("lz_minibatch", _capi.byref(ppo.cfg), _capi.ptr(ppo.params), _capi.ptr(ppo.adam_m),
+                   _capi.ptr(ppo.adam_v), _capi.ptr(ppo.opt), 0, i, _capi.ptr(st.actor_obs), _capi.ptr(st.actions),
+                   _capi.ptr(st.actions_log_prob), _capi.ptr(st.values), _capi.ptr(st.returns),
+                   _capi.ptr(st.advantages), _capi.ptr(ppo.partials), _capi.ptr(ppo.grad), _capi.stream_ptr())
+        torch.cuda.synchronize()
+        G, _, _, _ = L.minibatch_grad(L.unflatten(pv, OBS), flat["obs"][sl], flat["actions"][sl], flat["logp"][sl],
+                                      flat["values"][sl], flat["returns"][sl], flat["advantages"][sl], np.float32(1.0),
+                                      cfg, ex[sl])
+        g_ref = L.flatten(G, OBS)
+        scale = float(np.abs(g_ref).max())
+        ET.check("loopz_expert_grad_per_step", "grad/max", ppo.grad[:np_].cpu().numpy() / scale, g_ref / scale,
+                 1e-5, 1e-5, err_msg=f"step {k}")
+        gc, _ = L.clip_grad(G, OBS, cfg.max_grad_norm)
+        pv = adam.apply(pv, gc, cfg)
