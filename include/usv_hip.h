@@ -546,13 +546,6 @@ typedef struct ppo_cfg {
                                a2c_continuous.py:121): the rollout kernels stay fp32 -- BASELINE configs[2] */
   int   nan_probe;          /* 1: ppo_policy_step ORs USV_NAN_POLICY into *nan_flag on a non-finite mu / value */
   int32_t *nan_flag;        /* device int (nullable) */
-  int   exp_rec;            /* layout of the policy step's per-row experience outputs.  0: separate env-major
-                               arrays, act / mu / sigma [B][2] and nlp / val [B].  1: one 32-byte record per row,
-                               rec[B][8] = (mu0, mu1, sigma0, sigma1, act0, act1, nlp, val), passed as exp_mu = rec,
-                               exp_sigma = rec + 2, exp_act = rec + 4, exp_nlp = rec + 6, exp_val = rec + 7 with rec
-                               16-byte aligned (entry points check this: status 6).  A rollout step then writes one
-                               32-byte sector per row instead of five partial lines (the rows of one step are H
-                               records apart).  The env-major row order (swap_and_flatten01's) is the same. */
 } ppo_cfg_t;
 
 /* Rollout: obs RMS normalise (eval) -> MLP -> mu, value (denormalised),

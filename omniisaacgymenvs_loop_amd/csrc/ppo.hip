@@ -44,7 +44,6 @@ constexpr int P_LOSS = PPO_NPARAM;      // a, c, entropy, b, kl sums
 constexpr float kLog2Pi = 1.8378770664093453f;  // 0.5*log(2*pi)*2 (models.py:400)
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
@@ -397,17 +396,11 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
         vd = clampt(v, -5.0f, 5.0f);
         vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
       }
-      if (c.exp_rec) {   // the row's 32-byte record (ppo_cfg_t.exp_rec; exp_mu is its start, checked on the host)
-        f32x4v *rp = reinterpret_cast<f32x4v *>(exp_mu + slot * 8);
-        exp_st(rp, f32x4v{mu0, mu1, sg0, sg1});
-        exp_st(rp + 1, f32x4v{a0, a1, nlp, vd});
-      } else {
-        exp_st(&exp_act[slot * 2], a0); exp_st(&exp_act[slot * 2 + 1], a1);
-        exp_st(&exp_mu[slot * 2], mu0); exp_st(&exp_mu[slot * 2 + 1], mu1);
-        exp_st(&exp_sigma[slot * 2], sg0); exp_st(&exp_sigma[slot * 2 + 1], sg1);
-        exp_st(&exp_nlp[slot], nlp);
-        exp_st(&exp_val[slot], vd);
-      }
+      exp_st(&exp_act[slot * 2], a0); exp_st(&exp_act[slot * 2 + 1], a1);
+      exp_st(&exp_mu[slot * 2], mu0); exp_st(&exp_mu[slot * 2 + 1], mu1);
+      exp_st(&exp_sigma[slot * 2], sg0); exp_st(&exp_sigma[slot * 2 + 1], sg1);
+      exp_st(&exp_nlp[slot], nlp);
+      exp_st(&exp_val[slot], vd);
       exp_st(&exp_done[slot], (uint8_t)(dones_prev[e] != 0));
       // preprocess_actions: clamp(-1,1) then rescale to [low, high] = identity (a2c_common.py:1134-1144)
       actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
@@ -530,7 +523,6 @@ __global__ __launch_bounds__(TB) void k_gae(ppo_cfg_t c, const float *__restrict
                                             float *adv, double *work) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int H = c.horizon;
-  const int vs = c.exp_rec ? 8 : 1;   // row stride of val (ppo_cfg_t.exp_rec)
   double sv = 0, sv2 = 0, sr = 0, sr2 = 0, sa = 0, sa2 = 0;
   if (e < c.n_envs) {
     const size_t base = (size_t)e * H;
@@ -542,9 +534,9 @@ __global__ __launch_bounds__(TB) void k_gae(ppo_cfg_t c, const float *__restrict
         nv = last_val[e];
       } else {
         nnt = 1.0f - (float)done[base + t + 1];
-        nv = val[(base + t + 1) * vs];
+        nv = val[base + t + 1];
       }
-      const float v = val[(base + t) * vs];
+      const float v = val[base + t];
       const float delta = rew[base + t] + c.gamma * nv * nnt - v;
       lastgaelam = delta + c.gamma * c.tau * nnt * lastgaelam;
       const float R = lastgaelam + v;          // returns = advs + values (:763)
@@ -650,8 +642,7 @@ __global__ void k_prepare_apply(ppo_cfg_t c, const double *work, float *val, flo
   const size_t B = (size_t)c.n_envs * c.horizon;
   if (i >= B) return;
   if (c.normalize_value) {
-    const size_t vi = c.exp_rec ? i * 8 : i;   // val's row stride (ppo_cfg_t.exp_rec)
-    val[vi] = rms_norm(val[vi], work[0], work[1], c.rms_eps);
+    val[i] = rms_norm(val[i], work[0], work[1], c.rms_eps);
     ret[i] = rms_norm(ret[i], work[2], work[3], c.rms_eps);
   }
   if (c.normalize_advantage) {
@@ -845,6 +836,7 @@ constexpr int GTB = 512;          // threads per workgroup
 #ifndef USV_RD_NT
 #define USV_RD_NT 1   // non-temporal loads of the partial rows (A/B builds override it)
 #endif
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 constexpr int RD_TB = 512, RD_P = USV_RD_P;            // threads, slots per workgroup
 constexpr int RD_L = RD_P / 4;                          // lanes per row segment (float4 each)
 constexpr int RD_G = (RD_TB / RD_L);                    // row groups
@@ -1193,12 +1185,11 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
   RowIn ri;
   {
     const size_t row = (size_t)rb0 + (lane & (RB - 1));
-    const size_t r2 = row * (c.exp_rec ? 8 : 2), r1 = row * (c.exp_rec ? 8 : 1);   // ppo_cfg_t.exp_rec strides
-    ri.act0 = row_ld(&e_act[r2]); ri.act1 = row_ld(&e_act[r2 + 1]);
-    ri.nlp = row_ld(&e_nlp[r1]); ri.adv = row_ld(&e_adv[row]);
-    ri.val = row_ld(&e_val[r1]); ri.ret = row_ld(&e_ret[row]);
-    ri.mu0 = row_ld(&e_mu[r2]); ri.mu1 = row_ld(&e_mu[r2 + 1]);
-    ri.sg0 = row_ld(&e_sigma[r2]); ri.sg1 = row_ld(&e_sigma[r2 + 1]);
+    ri.act0 = row_ld(&e_act[row * 2]); ri.act1 = row_ld(&e_act[row * 2 + 1]);
+    ri.nlp = row_ld(&e_nlp[row]); ri.adv = row_ld(&e_adv[row]);
+    ri.val = row_ld(&e_val[row]); ri.ret = row_ld(&e_ret[row]);
+    ri.mu0 = row_ld(&e_mu[row * 2]); ri.mu1 = row_ld(&e_mu[row * 2 + 1]);
+    ri.sg0 = row_ld(&e_sigma[row * 2]); ri.sg1 = row_ld(&e_sigma[row * 2 + 1]);
   }
   // obs rows and the running statistics (always loaded; obs_rms is non-null, checked on the host)
   constexpr int NU = (RB * XG + GTB - 1) / GTB;
@@ -1429,9 +1420,8 @@ __device__ __forceinline__ void mb_grad8w(const ppo_cfg_t &c, const ChainIn &ch,
         const float om0 = ri.mu0, om1 = ri.mu1, os0 = ri.sg0, os1 = ri.sg1;
         const float kl0 = logf(os0 / sg0 + 1e-5f) + (sg0 * sg0 + (om0 - mu0) * (om0 - mu0)) / (2.0f * (os0 * os0 + 1e-5f)) - 0.5f;
         const float kl1 = logf(os1 / sg1 + 1e-5f) + (sg1 * sg1 + (om1 - mu1) * (om1 - mu1)) / (2.0f * (os1 * os1 + 1e-5f)) - 0.5f;
-        const size_t r2 = (size_t)row * (c.exp_rec ? 8 : 2);
-        e_mu[r2] = mu0; e_mu[r2 + 1] = mu1;
-        e_sigma[r2] = sg0; e_sigma[r2 + 1] = sg1;
+        e_mu[row * 2] = mu0; e_mu[row * 2 + 1] = mu1;
+        e_sigma[row * 2] = sg0; e_sigma[row * 2 + 1] = sg1;
         le = ent; lb = b_loss; lkl = kl0 + kl1;
       }
       le = wave_sum(le); lb = wave_sum(lb); lkl = wave_sum(lkl);
@@ -2016,17 +2006,6 @@ __global__ __launch_bounds__(AP_TB) void k_apply(ppo_cfg_t c, AdamBanks a, const
 
 }  // namespace
 
-// ppo_cfg_t.exp_rec = 1: the per-row arrays must be the views of one 16-byte aligned [B][8] record buffer
-// (NULL ones are not checked; ppo_prepare passes only val)
-static bool exp_layout_ok(const ppo_cfg_t *c, const float *act, const float *nlp, const float *val, const float *mu,
-                          const float *sigma) {
-  if (!c->exp_rec) return true;
-  const float *rec = mu ? mu : (val ? val - 7 : nullptr);
-  if (!rec || (reinterpret_cast<uintptr_t>(rec) & 15u)) return false;
-  return (!sigma || sigma == rec + 2) && (!act || act == rec + 4) && (!nlp || nlp == rec + 6) &&
-         (!val || val == rec + 7);
-}
-
 extern "C" {
 
 int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, const double *val_rms,
@@ -2035,7 +2014,6 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
                     float *actions_out, uint64_t seed, uint64_t step, const uint64_t *step_dev,
                     const float *eps_inject, void *stream) {
   if (!cfg || !params || !obs_rms || !obs || cfg->n_envs <= 0 || t < 0 || t >= cfg->horizon) return 1;
-  if (!exp_layout_ok(cfg, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma)) return 6;
   // USV_POLICY_GRID caps the persistent grid (A/B knob: fewer CUs for the policy kernel leaves the
   // rest to the side stream's field kernels in the overlapped step; results do not depend on it)
   const char *gcap = getenv("USV_POLICY_GRID");
@@ -2079,7 +2057,6 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
                 const float *last_obs, const int64_t *last_dones, const uint8_t *exp_done, float *exp_val,
                 const float *exp_rew, float *exp_ret, float *exp_adv, double *work, void *stream) {
   if (!cfg || !params || !work || cfg->n_envs <= 0) return 1;
-  if (!exp_layout_ok(cfg, nullptr, nullptr, exp_val, nullptr, nullptr)) return 6;
   hipStream_t s = (hipStream_t)stream;
   // last values (get_values :407-430) into work-adjacent scratch: reuse exp_ret's tail? use a dedicated slice
   float *last_val = reinterpret_cast<float *>(work + 8 + 8 * 4096);
@@ -2119,7 +2096,6 @@ int ppo_minibatch_grad(const ppo_cfg_t *cfg, const float *params, double *obs_rm
                        void *stream) {
   (void)val_rms;
   if (!cfg || !params || !obs_rms || !grad || !partials || !work) return 1;
-  if (!exp_layout_ok(cfg, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma)) return 6;
   if (cfg->minibatch % RB != 0 || ppo_partials_floats(cfg->minibatch) <= 0) return 2;   // no partial layout
   if (reinterpret_cast<uintptr_t>(params) & 15u) return 4;   // 16-byte weight staging loads
   hipStream_t s = (hipStream_t)stream;
@@ -2164,7 +2140,6 @@ static int fused_launch(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, con
                         float *kl_prev_out, void *stream) {
   if (!cfg || !obs_rms || !grad || !partials || !work || seq < 0) return 1;
   if (!banks_ok(banks)) return 4;
-  if (!exp_layout_ok(cfg, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma)) return 6;
   if (cfg->minibatch % RB != 0 || ppo_partials_floats(cfg->minibatch) <= 0) return 2;   // no partial layout
   if (reinterpret_cast<uintptr_t>(partials) & 15u) return 3;
   if (dp) {
@@ -2246,7 +2221,6 @@ int ppo_minibatch_coll(const ppo_cfg_t *cfg, const ppo_adam_banks_t *banks, int 
                        float *kl_prev_out, void *stream) {
   if (!cfg || !obs_rms || !grad || !partials || !work || seq < 0 || !(grad_scale > 0.f)) return 1;
   if (!banks_ok(banks)) return 4;
-  if (!exp_layout_ok(cfg, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma)) return 6;
   if (cfg->minibatch % RB != 0 || ppo_partials_floats(cfg->minibatch) <= 0) return 2;   // no partial layout
   if ((reinterpret_cast<uintptr_t>(partials) | reinterpret_cast<uintptr_t>(grad)) & 15u) return 3;
   hipStream_t s = (hipStream_t)stream;

@@ -267,23 +267,14 @@ class A2CAgent:
         self.work = torch.zeros(8 + 8 * 4096 + N // 2 + 64, **f64)
         B = N * H
         self.exp_obs = torch.zeros((B, NIN), **f32)
-        # the policy step's per-row outputs as one 32-byte record per row (ppo_cfg_t.exp_rec): the arrays are views
-        # of rec[B][8] = (mu, sigma, action, neglogp, value); USV_EXP_REC=0 keeps five separate arrays
-        self.cfg.exp_rec = int(os.environ.get("USV_EXP_REC", "1") != "0")
-        if self.cfg.exp_rec:
-            self._exp_rec = torch.zeros((B, 8), **f32)
-            self.exp_mu, self.exp_sigma = self._exp_rec[:, 0:2], self._exp_rec[:, 2:4]
-            self.exp_act, self.exp_nlp, self.exp_val = self._exp_rec[:, 4:6], self._exp_rec[:, 6], self._exp_rec[:, 7]
-        else:
-            self._exp_rec = None
-            self.exp_act = torch.zeros((B, NA), **f32)
-            self.exp_nlp = torch.zeros(B, **f32)
-            self.exp_val = torch.zeros(B, **f32)
-            self.exp_mu = torch.zeros((B, NA), **f32)
-            self.exp_sigma = torch.zeros((B, NA), **f32)
+        self.exp_act = torch.zeros((B, NA), **f32)
+        self.exp_nlp = torch.zeros(B, **f32)
+        self.exp_val = torch.zeros(B, **f32)
         self.exp_ret = torch.zeros(B, **f32)
         self.exp_adv = torch.zeros(B, **f32)
         self.exp_rew = torch.zeros(B, **f32)
+        self.exp_mu = torch.zeros((B, NA), **f32)
+        self.exp_sigma = torch.zeros((B, NA), **f32)
         self.exp_done = torch.zeros(B, device=dev, dtype=torch.uint8)
         self.actions = torch.zeros((N, NA), **f32)
         self.dones = torch.ones(N, device=dev, dtype=torch.int64)

@@ -137,28 +137,3 @@ def test_partials_layout_for_every_minibatch_and_refused_sizes():
         cfg.minibatch = mb
         args = [_capi.byref(cfg), p, p, p, 0, 0] + [p] * 9 + [None, p, p, None]   # .., grad, losses, partials, work, stream
         assert _capi.lib().ppo_minibatch_grad(*args) == 2, mb
-
-
-def test_experience_record_layout_is_checked():
-    """ppo_cfg_t.exp_rec = 1 (one 32-byte record per row): the entry points take the per-row arrays only as the views
-    rec + (mu 0, sigma 2, act 4, nlp 6, val 7) of a 16-byte aligned record buffer and refuse anything else with
-    status 6 before any device work (argument checks only: the pointers are never dereferenced here)."""
-    from omniisaacgymenvs_loop_amd import _capi
-    from omniisaacgymenvs_loop_amd._abi import PpoCfg
-    if not os.path.exists(_capi.LIB_PATH):
-        pytest.skip("libusv_hip.so not built (run __graft_entry__.build())")
-    lib = _capi.lib()
-    buf = ctypes.create_string_buffer(1 << 12)
-    rec = ctypes.addressof(buf) + (-ctypes.addressof(buf) % 16)
-    f = lambda k: rec + 4 * k                                     # noqa: E731
-    cfg = PpoCfg()
-    cfg.horizon, cfg.n_envs, cfg.minibatch, cfg.exp_rec = 16, 64, 8192, 1
-    good = dict(act=f(4), nlp=f(6), val=f(7), mu=f(0), sigma=f(2))
-    bad = [dict(good, act=f(2)), dict(good, sigma=f(4)), dict(good, nlp=f(7)),
-           {k: v + 4 for k, v in good.items()}]                   # consistent views of a misaligned record
-    for lay in bad:
-        assert lib.ppo_policy_step(_capi.byref(cfg), rec, rec, rec, rec, 0, rec, lay["act"], lay["nlp"], lay["val"],
-                                   lay["mu"], lay["sigma"], rec, rec, rec, 0, 0, None, None, None) == 6, lay
-        assert lib.ppo_minibatch_grad(_capi.byref(cfg), rec, rec, rec, 0, 0, rec, lay["act"], lay["nlp"], lay["val"],
-                                      rec, rec, lay["mu"], lay["sigma"], rec, None, rec, rec, None) == 6, lay
-    assert lib.ppo_prepare(_capi.byref(cfg), rec, rec, rec, rec, rec, rec, f(6), rec, rec, rec, rec, None) == 6

@@ -85,41 +85,6 @@ def test_policy_kernel_vs_reference_rollout(ppo):
     np.testing.assert_array_equal(rows(ag.exp_done), _swap(ppo["exp_dones"]))
 
 
-def test_experience_record_matches_separate_arrays(ppo, monkeypatch):
-    """ppo_cfg_t.exp_rec = 1 (the agent's default: mu / sigma / action / neglogp / value as one 32-byte record per
-    row) and exp_rec = 0 (five separate arrays) give the same bits through the rollout kernel, ppo_prepare and a
-    whole update (8 mini-epochs of the fused chain, mu / sigma written back)."""
-    from omniisaacgymenvs_loop_amd import _capi as c
-    H, N = ppo["exp_rewards"].shape[:2]
-    T = lambda a, **k: torch.tensor(np.ascontiguousarray(a), device=DEV, **k)
-    out = {}
-    for rec in ("1", "0"):
-        monkeypatch.setenv("USV_EXP_REC", rec)
-        ag = _agent(N, 128)
-        assert ag.cfg.exp_rec == int(rec) and (ag._exp_rec is not None) == (rec == "1")
-        ag.model_params.copy_(_flat_params(_params(ppo, "init")))
-        for t in range(H):
-            eps = (ppo["exp_actions"][t] - ppo["exp_mus"][t]) / ppo["exp_sigmas"][t]
-            c.call("ppo_policy_step", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms),
-                   c.ptr(ag.val_rms), c.ptr(T(ppo["env_obs"][t])), t, c.ptr(ag.exp_obs), c.ptr(ag.exp_act),
-                   c.ptr(ag.exp_nlp), c.ptr(ag.exp_val), c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.exp_done),
-                   c.ptr(T(ppo["exp_dones"][t].astype(np.int64))), c.ptr(ag.actions), 1, t, None, c.ptr(T(eps)),
-                   c.stream_ptr())
-        ag.exp_rew.copy_(T(_swap(ppo["exp_rewards"])[:, 0]))
-        ag.obs = {"obs": {"state": T(ppo["env_obs"][H])}}
-        ag.dones = T(ppo["env_dones"][H - 1].astype(np.int64))
-        ag.prepare_dataset()
-        snap = {k: getattr(ag, k).cpu().numpy().copy() for k in
-                ("exp_act", "exp_nlp", "exp_val", "exp_mu", "exp_sigma", "exp_ret", "exp_adv", "exp_done")}
-        ag.update_epoch_minibatches()
-        torch.cuda.synchronize()
-        snap.update({k + "_after": getattr(ag, k).cpu().numpy().copy() for k in ("exp_mu", "exp_sigma")})
-        snap.update({k: getattr(ag, k).cpu().numpy().copy() for k in ("model_params", "adam_m", "adam_v", "opt")})
-        out[rec] = snap
-    for k, v in out["0"].items():
-        np.testing.assert_array_equal(out["1"][k], v, err_msg=k)
-
-
 def _load_rollout(ag, ppo):
     H, N = ppo["exp_rewards"].shape[:2]
     T = lambda a, **k: torch.tensor(np.ascontiguousarray(a), device=DEV, **k)

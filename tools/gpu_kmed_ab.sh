@@ -10,7 +10,7 @@ for c in $CASES; do
   name=${c%%:*}; vars=${c#*:}
   for kv in ${vars//,/ }; do export "$kv"; done
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/$name -o t -- python3 $R/bench.py \
-    --steps ${STEPS:-3} --warmup 2 --seeds ${SEEDS:-0} --no-cpu-baseline --c2-steps 0 --milestone-seconds 0 > $O/$name.log 2>&1 || exit $?
+    --steps ${STEPS:-3} --warmup 2 --no-cpu-baseline --c2-steps 0 --milestone-seconds 0 > $O/$name.log 2>&1 || exit $?
   for kv in ${vars//,/ }; do unset "${kv%%=*}"; done
   python3 - "$O/$name" "$name" "${KERNELS:-k_field_stats}" <<'PY'
 import csv, glob, statistics, sys
