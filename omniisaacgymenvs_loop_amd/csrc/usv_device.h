@@ -95,26 +95,13 @@ __device__ __forceinline__ float usv_sin(float x) {
 // no fma) then gives R^T v = (C vx + S vy, -S vx + C vy); the integrator rotates the body-frame wrench with the same
 // R (its own definition, the PhysX step's), so one half-angle sincos per substep serves both
 struct QuatRot { float C, S, w, z; };
-// RN(2 / s) for s = w^2 + z^2 of a unit quaternion's rounded components (within a few ulp of 1) without the IEEE
-// division's ~15 instructions: t = 2 - s, q = 2 t, one Markstein correction fma(fma(-s, q, 2), t, q).  Equal to the
-// correctly rounded quotient for every float s in [1 - 4096 ulp, 1 + 4096 ulp] except s = 1 - 2^-24 (a quotient just
-// above a rounding midpoint), which is special-cased; outside that window the division runs (checked exhaustively:
-// tests/test_oracle_golden.py::test_two_over_s_fast_path_exhaustive)
-#ifndef USV_TWO_S_FAST
-#define USV_TWO_S_FAST 1
-#endif
-__device__ __forceinline__ float two_over_s(float s) {
-  if (!USV_TWO_S_FAST) return 2.0f / s;
-  const float t = 2.0f - s, q = t + t;
-  float r = fmaf(fmaf(-s, q, 2.0f), t, q);
-  r = (s == 0.99999994f) ? 2.00000024f : r;
-  if (!(fabsf(s - 1.0f) <= 2.44e-4f)) r = 2.0f / s;
-  return r;
-}
 __device__ __forceinline__ QuatRot usv_quat_rot(float yaw) {
   float z, w;
   usv_sincos(yaw * 0.5f, &z, &w);
-  const float two_s = two_over_s(w * w + z * z);   // (q * q).sum(-1) of (w, 0, 0, z); 2.0 / t == reciprocal * 2
+  // (q * q).sum(-1) of (w, 0, 0, z); torch's 2.0 / t is reciprocal * 2, the same bits as the IEEE quotient.  (A
+  // division-free RN(2 / s) on the window s lies in -- t = 2 - s, one Markstein fma correction -- measured 0.75 us
+  // SLOWER per env step in round 6, profiles/r06/r06e_two_s_ab.txt; not kept)
+  const float two_s = 2.0f / (w * w + z * z);
   return QuatRot{1.0f - two_s * (z * z), two_s * (z * w), w, z};
 }
 // exp, tanh and atan2 of the observation / reward formulas, by the same rule (oracle/usv_oracle.c restates them):

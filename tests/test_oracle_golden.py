@@ -370,45 +370,3 @@ def test_packaged_yaml_matches_fixture_config(golden):
             assert list(a) == list(b), name
         else:
             assert a == b, name
-
-
-def _rn32(q):
-    """The float32 nearest to the rational q (ties to even), exactly."""
-    from fractions import Fraction
-    f = np.float32(float(q))
-    cands = [f, np.nextafter(f, np.float32(np.inf)), np.nextafter(f, np.float32(-np.inf))]
-    return min(cands, key=lambda c: (abs(Fraction(float(c)) - q), int(np.float32(c).view(np.uint32)) & 1))
-
-
-def test_two_over_s_fast_path_exhaustive():
-    """csrc/usv_device.h:two_over_s -- the reference's two_s = 2 / (q * q).sum(-1) of quaternion_to_matrix without the
-    IEEE division -- restated with exact rational fma: equal to the correctly rounded 2 / s for every float s within
-    4096 ulp of 1 (the window its fast path takes; w^2 + z^2 of usv_sincos's components lies within a few ulp), the
-    one midpoint case s = 1 - 2^-24 special-cased as in the kernel."""
-    from fractions import Fraction as Fr
-    fma = lambda a, b, c: _rn32(Fr(float(a)) * Fr(float(b)) + Fr(float(c)))
-    s_vals, x = [np.float32(1.0)], np.float32(1.0)
-    for _ in range(4096):
-        x = np.nextafter(x, np.float32(0))
-        s_vals.append(x)
-    x = np.float32(1.0)
-    for _ in range(4096):
-        x = np.nextafter(x, np.float32(2))
-        s_vals.append(x)
-    inside = 0
-    for s in s_vals:
-        if not abs(float(s) - 1.0) <= float(np.float32(2.44e-4)):
-            continue
-        inside += 1
-        t = np.float32(np.float32(2.0) - s)
-        q = np.float32(t + t)
-        r = fma(fma(-s, q, np.float32(2.0)), t, q)
-        if s == np.float32(0.99999994):
-            r = np.float32(2.00000024)
-        assert r == _rn32(Fr(2) / Fr(float(s))), s
-    assert inside > 6000
-    # the stand-in's quaternions: s stays deep inside the window
-    yaw = np.linspace(-np.pi, np.pi, 200_001).astype(np.float32)
-    sn, cs = O.sincos(yaw * np.float32(0.5))
-    s = cs * cs + sn * sn
-    assert np.abs(s.astype(np.float64) - 1.0).max() < 1e-6
