@@ -22,6 +22,7 @@
 // in a fixed order.  clip + Adam + the adaptive LR run in k_apply.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "usv_device.h"
 
@@ -227,8 +228,9 @@ __device__ __forceinline__ void load_obs_tile3(const float *__restrict__ obs, in
     x[u] = obs[(size_t)(row0 + r) * NIN + kc];
   }
 }
+template <class S>
 __device__ __forceinline__ void put_obs_tile3(const float (&x)[NUO3], int tt, int row0, int nrows, bool normalize,
-                                              float eps, MlpSmem &s, float *exp_obs, int H, int t) {
+                                              float eps, S &s, float *exp_obs, int H, int t) {
 #pragma unroll
   for (int u = 0; u < NUO3; ++u) {
     const int q = tt + u * OT;
@@ -243,6 +245,9 @@ __device__ __forceinline__ void put_obs_tile3(const float (&x)[NUO3], int tt, in
     s.x[q] = v;
   }
 }
+
+template <class S>
+__device__ __forceinline__ void block_heads(S &s);
 
 // Forward of the RB rows staged in s.x (W1, biases, heads staged; W2 still in
 // registers on a launch's first tile, committed after layer 1); leaves h1, h2, out.
@@ -278,8 +283,14 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s, bool first_tile) {
     for (int r = 0; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + bj);
   }
   __syncthreads();
-  // ---- heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (8 threads per row, k = part + 8 kk: the 8
-  // threads of a row read 8 consecutive words, not 8 words 16 apart -- no 4-way bank conflicts) ----
+  block_heads(s);
+}
+
+// heads: mu = Wmu h2 + bmu, value = Wv h2 + bv (8 threads per row, k = part + 8 kk: the 8 threads of a row read 8
+// consecutive words, not 8 words 16 apart -- no 4-way bank conflicts)
+template <class S>
+__device__ __forceinline__ void block_heads(S &s) {
+  const int tid = threadIdx.x;
   {
     const int r = tid / 8, part = tid % 8;
     float a0 = 0.f, a1 = 0.f, av = 0.f;
@@ -306,13 +317,85 @@ __device__ void block_forward(const StagedW &wr, MlpSmem &s, bool first_tile) {
   __syncthreads();
 }
 
+// The policy step with its weights in registers: wave w keeps rows 32w..32w+31 of W1 and W2 as the B operands of
+// its matrix-core steps (lane (i, h) of step st holds W[32w + i][2 st + h]: 17 + 64 VGPRs) and the two biases, so
+// the workgroup needs 41 KB of LDS instead of 129 KB and three of them share a CU (3 waves per SIMD instead of
+// one).  The products see the same operands in the same order as block_forward's: the same bits.
+#ifndef USV_POL_WPC
+#define USV_POL_WPC 3
+#endif
+constexpr int POL_WPC = USV_POL_WPC;
+#ifndef USV_POL_L2B
+#define USV_POL_L2B 1   // layer 2 of the register-weight form: a scheduling fence every 16 steps
+#endif
+struct PolSmem {
+  float x[RB * XS];       // normalised obs
+  float h1[RB * HS];
+  float h2[RB * HS];
+  float out[RB * 4];      // mu0, mu1, value
+  float tail[TAIL + 1];   // params from b2 on (T_* offsets)
+  float om[NIN], od[NIN]; // (float)mean, sqrtf((float)var + eps) of the obs statistics
+  float zz[2][RB * 2];    // the N(0,1) draws of a tile's rows, one tile ahead
+};
+struct RegW {
+  float w1[17], w2[NH / 2], b1, b2, tlr[NTL];
+};
+__device__ __forceinline__ void regw_load(const float *__restrict__ P, RegW &r) {
+  const int tid = threadIdx.x, lane = tid & 63, i = lane & 31, h = lane >> 5, n = 32 * (tid >> 6) + i;
+#pragma unroll
+  for (int st = 0; st < 17; ++st) r.w1[st] = P[PPO_OFF_W1 + n * NIN + min(2 * st + h, NIN - 1)];
+  r.b1 = P[PPO_OFF_B1 + n];
+  r.b2 = P[PPO_OFF_B2 + n];
+#pragma unroll
+  for (int u = 0; u < NTL; ++u) r.tlr[u] = P[PPO_OFF_B2 + min(tid + u * TB, TAIL - 1)];
+#pragma unroll
+  for (int st = 0; st < NH / 2; ++st) r.w2[st] = P[PPO_OFF_W2 + n * NH + 2 * st + h];
+  __builtin_amdgcn_sched_barrier(0);
+  static_assert(2 * 16 + 1 == NIN, "k = 33 is layer 1's only zero column");
+  if (h) r.w1[16] = 0.f;
+}
+__device__ __forceinline__ void regw_store_tail(const RegW &r, PolSmem &s) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < NTL; ++u)
+    if (tid + u * TB < TAIL) s.tail[tid + u * TB] = r.tlr[u];
+}
+__device__ __forceinline__ void block_forward_rw(const RegW &wr, PolSmem &s) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
+  {
+    f32x16 acc = {};
+#pragma unroll
+    for (int st = 0; st < 17; ++st) acc = mfma32(s.x[i * XS + 2 * st + h], wr.w1[st], acc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + wr.b1);
+  }
+  __syncthreads();
+  {
+    f32x16 acc = {};
+#pragma unroll
+    for (int st = 0; st < NH / 2; ++st) {
+      acc = mfma32(s.h1[i * HS + 2 * st + h], wr.w2[st], acc);
+      // at most 16 operand reads in flight (a fully hoisted loop would hold 64 of them in registers)
+      if (USV_POL_L2B && st % 16 == 15) __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + wr.b2);
+  }
+  __syncthreads();
+  block_heads(s);
+}
+
 // ------------------------------------------------------------------ rollout
 // workgroups of the persistent forward kernels: one 32-row tile each up to 256
 // (one per CU at this LDS size), then tiles loop
 __host__ __device__ constexpr int policy_grid(int n) {
   return (n + RB - 1) / RB < 256 ? (n + RB - 1) / RB : 256;
 }
-__global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__restrict__ P,
+// kRW: the register-weight form (PolSmem / RegW above), grid up to 256 x POL_WPC workgroups; else the weights
+// staged in LDS once per workgroup, one workgroup per CU
+template <bool kRW>
+__global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_policy_step(ppo_cfg_t c, const float *__restrict__ P,
                                                     const double *__restrict__ obs_rms,
                                                     const double *__restrict__ val_rms, const float *__restrict__ obs,
                                                     int t, float *exp_obs, float *exp_act, float *exp_nlp,
@@ -320,7 +403,7 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
                                                     const int64_t *__restrict__ dones_prev, float *actions_out,
                                                     uint64_t seed, uint64_t step, const uint64_t *step_dev,
                                                     const float *eps_inject) {
-  __shared__ MlpSmem s;
+  __shared__ std::conditional_t<kRW, PolSmem, MlpSmem> s;
   USV_PHASE(pol, 0);
   const int n = c.n_envs, H = c.horizon;
   if (step_dev) step = *step_dev + (uint64_t)t;   // the rollout's first step + slot
@@ -328,8 +411,9 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   // Per tile: the forward on all four waves; then wave 0 samples the tile's actions, stores its
   // experience rows and draws the next tile's normals while waves 1-3 stage the next tile's obs
   // (loaded during the forward) -- one barrier per tile outside the forward
-  StagedW wr;
-  stage_load(P, wr);
+  std::conditional_t<kRW, RegW, StagedW> wr;
+  if constexpr (kRW) regw_load(P, wr);
+  else stage_load(P, wr);
   const int ntiles = (n + RB - 1) / RB;
   const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int tt = (int)threadIdx.x - 64;
@@ -366,7 +450,8 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
     put_obs_tile3(xo, tt, row0, min(RB, n - row0), normalize, c.rms_eps, s, exp_obs, H, t);
   }
   draw(blockIdx.x, 0);
-  stage_store_small(wr, s);
+  if constexpr (kRW) regw_store_tail(wr, s);
+  else stage_store_small(wr, s);
   __syncthreads();
   int buf = 0;
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -374,10 +459,15 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
   const int nrows = min(RB, n - row0);
   const int nt = tile + (int)gridDim.x;
   float xn[NUO3];   // the next tile's rows, in flight during the forward
-  if (w > 0 && nt < ntiles) load_obs_tile3(obs, n, nt, tt, xn);
+  // the obs path's slot indices recomputed per tile (opaque to the optimiser): hoisted out of the loop they held
+  // ~50 VGPRs through the forward, which the register-weight form cannot spare
+  int ttv = tt;
+  if constexpr (kRW) __asm__ volatile("" : "+v"(ttv));
+  if (w > 0 && nt < ntiles) load_obs_tile3(obs, n, nt, ttv, xn);
   USV_PHASE(pol, 1);   // (probe slots 1-4: the launch's last tile)
   USV_PHASE(pol, 2);
-  block_forward(wr, s, tile == (int)blockIdx.x);
+  if constexpr (kRW) block_forward_rw(wr, s);
+  else block_forward(wr, s, tile == (int)blockIdx.x);
   USV_PHASE(pol, 3);
   if (w == 0) {
     const int r = lane;
@@ -412,7 +502,7 @@ __global__ __launch_bounds__(TB) void k_policy_step(ppo_cfg_t c, const float *__
     }
     if (nt < ntiles) draw(nt, buf ^ 1);
   } else if (nt < ntiles) {   // s.x was last read by the forward's layer 1 (before its first barrier)
-    put_obs_tile3(xn, tt, nt * RB, min(RB, n - nt * RB), normalize, c.rms_eps, s, exp_obs, H, t);
+    put_obs_tile3(xn, ttv, nt * RB, min(RB, n - nt * RB), normalize, c.rms_eps, s, exp_obs, H, t);
   }
   __syncthreads();   // s.out / s.zz[buf] read above before the next tile's forward and draws rewrite them
   USV_PHASE(pol, 4);
@@ -2018,9 +2108,13 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
   // rest to the side stream's field kernels in the overlapped step; results do not depend on it)
   const char *gcap = getenv("USV_POLICY_GRID");
   const int grid_cap = gcap ? atoi(gcap) : 0;
-  int grid = policy_grid(cfg->n_envs);
+  // USV_POLICY_RW=0: the LDS-staged form (same results)
+  const char *rw = getenv("USV_POLICY_RW");
+  const bool reg_w = !(rw && atoi(rw) == 0);
+  const int ntiles = (cfg->n_envs + RB - 1) / RB;
+  int grid = reg_w ? (ntiles < 256 * POL_WPC ? ntiles : 256 * POL_WPC) : policy_grid(cfg->n_envs);
   if (grid_cap > 0 && grid_cap < grid) grid = grid_cap;
-  hipLaunchKernelGGL(k_policy_step, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
+  hipLaunchKernelGGL(reg_w ? k_policy_step<true> : k_policy_step<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
                      obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
                      actions_out, seed, step, step_dev, eps_inject);
   USV_CHECK_LAUNCH();

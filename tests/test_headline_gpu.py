@@ -1,8 +1,8 @@
 """Parity at the headline size (131,072 envs per GPU: BASELINE configs[4]'s 2^20 envs over 8 GPUs) for the
 code paths that only run above the sizes of the other parity tests:
 
-* the rollout kernels' persistent multi-tile loop (16 tiles per workgroup at 131,072 envs: next-tile obs
-  prefetch, next-tile normal draws by wave 0, W2 committed on the first tile only), with injected draws and
+* the rollout kernels' persistent multi-tile loop (5.3 tiles per workgroup at 131,072 envs in the register-weight
+  form, 16 in the LDS-staged one: next-tile obs prefetch, next-tile normal draws by wave 0), with injected draws and
   with the in-kernel Philox + Box-Muller sampler (models.py:372-386 Normal.sample), and ppo_value;
 * GAE + prepare_dataset over 131,072 x 16 rows (k_gae's 512 block partials, the k_prepare_finalize fold);
 * the potential field for ~1,300 resets in both launch shapes (3 rounds of the 512-workgroup sweep grid,
@@ -49,7 +49,7 @@ def _rand_agent(n, rng, mini_epochs=1, minibatch=8192):
 
 @pytest.mark.parametrize("inject", [True, False], ids=["eps_inject", "philox"])
 def test_policy_step_headline_multi_tile(inject):
-    """k_policy_step at 131,072 envs (256 workgroups x 16 tiles) vs the oracle forward: actions, mu, sigma,
+    """k_policy_step at 131,072 envs (768 workgroups x 5.3 tiles) vs the oracle forward: actions, mu, sigma,
     neglogp, denormalised value, raw obs rows and done flags of rollout slot t, the clamped env actions.
     philox: the in-kernel sampler (site 0x200, step from the device clock as in graph replay) vs its
     restatement PO.policy_normals."""
@@ -89,6 +89,37 @@ def test_policy_step_headline_multi_tile(inject):
     # the other slots of the experience rows are untouched
     other = np.arange(N) * H + (t + 1)
     assert float(np.abs(ag.exp_act.cpu().numpy()[other]).max()) == 0.0
+
+
+@pytest.mark.parametrize("n,grid_cap,inject", [(HEAD, 0, False), (HEAD, 0, True), (4128, 7, False), (100, 0, True)])
+def test_policy_step_register_weights_bit_identical(monkeypatch, n, grid_cap, inject):
+    """The register-weight policy kernel (k_policy_step<true>: W1 / W2 as the waves' matrix-core operands in VGPRs,
+    41 KB of LDS, three workgroups per CU) equals the LDS-staged one (USV_POLICY_RW=0) bit for bit: every experience
+    array and the env actions, at the headline size (768 workgroups, 5.3 tiles each), over a capped grid (4,128 rows on 7
+    workgroups: 19 tiles each, a ragged last tile) and for one partial tile."""
+    from omniisaacgymenvs_loop_amd import _capi as c
+    rng = np.random.default_rng(21)
+    ag, _, _, _ = _rand_agent(n, rng, minibatch=8192 if n % 512 == 0 else 16 * n)
+    obs = torch.tensor(rng.normal(0, 2, (n, 33)).astype(np.float32), device=DEV)
+    dprev = torch.tensor((rng.random(n) < 0.1).astype(np.int64), device=DEV)
+    eps = torch.tensor(rng.normal(0, 1, (n, 2)).astype(np.float32), device=DEV) if inject else None
+    step_dev = torch.tensor([2 ** 33 + 5], device=DEV, dtype=torch.int64)
+    monkeypatch.setenv("USV_POLICY_GRID", str(grid_cap))
+    out = {}
+    for rw in ("0", "1"):
+        monkeypatch.setenv("USV_POLICY_RW", rw)
+        for a in (ag.exp_obs, ag.exp_act, ag.exp_nlp, ag.exp_val, ag.exp_mu, ag.exp_sigma, ag.exp_done, ag.actions):
+            a.fill_(7)
+        for t in (0, 3):
+            c.call("ppo_policy_step", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms),
+                   c.ptr(obs), t, c.ptr(ag.exp_obs), c.ptr(ag.exp_act), c.ptr(ag.exp_nlp), c.ptr(ag.exp_val),
+                   c.ptr(ag.exp_mu), c.ptr(ag.exp_sigma), c.ptr(ag.exp_done), c.ptr(dprev), c.ptr(ag.actions), 99, 0,
+                   c.ptr(step_dev), c.ptr(eps), c.stream_ptr())
+        torch.cuda.synchronize()
+        out[rw] = [x.cpu().numpy().copy() for x in (ag.exp_obs, ag.exp_act, ag.exp_nlp, ag.exp_val, ag.exp_mu,
+                                                     ag.exp_sigma, ag.exp_done, ag.actions)]
+    for k, (a, b) in enumerate(zip(out["0"], out["1"])):
+        np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8), err_msg=str(k))
 
 
 def test_value_headline_multi_tile():
