@@ -319,10 +319,10 @@ __device__ __forceinline__ void block_heads(S &s) {
 
 // The policy step with its weights in registers: wave w keeps rows 32w..32w+31 of W1 and W2 as the B operands of
 // its matrix-core steps (lane (i, h) of step st holds W[32w + i][2 st + h]: 17 + 64 VGPRs) and the two biases, so
-// the workgroup needs 41 KB of LDS instead of 129 KB and three of them share a CU (3 waves per SIMD instead of
-// one).  The products see the same operands in the same order as block_forward's: the same bits.
+// the workgroup needs 41 KB of LDS instead of 129 KB and two of them share a CU (2 waves per SIMD instead of
+// one; USV_POL_WPC).  The products see the same operands in the same order as block_forward's: the same bits.
 #ifndef USV_POL_WPC
-#define USV_POL_WPC 3
+#define USV_POL_WPC 2
 #endif
 constexpr int POL_WPC = USV_POL_WPC;
 #ifndef USV_POL_L2B
@@ -360,7 +360,22 @@ __device__ __forceinline__ void regw_store_tail(const RegW &r, PolSmem &s) {
   for (int u = 0; u < NTL; ++u)
     if (tid + u * TB < TAIL) s.tail[tid + u * TB] = r.tlr[u];
 }
-__device__ __forceinline__ void block_forward_rw(const RegW &wr, PolSmem &s) {
+// probe build: per-phase wall-clock sums over a workgroup's tiles (wave 0's view), slots 5.. of g_probe_pol
+#ifdef USV_PHASE_PROBE
+struct PolAcc {
+  unsigned long long t, d[6];
+  __device__ void mark(int k) {
+    const unsigned long long q = wall_clock64();
+    d[k] += q - t;
+    t = q;
+  }
+};
+#else
+struct PolAcc {
+  __device__ void mark(int) {}
+};
+#endif
+__device__ __forceinline__ void block_forward_rw(const RegW &wr, PolSmem &s, PolAcc &pa) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int i = lane & 31, h = lane >> 5, n0 = 32 * w;
   {
@@ -371,6 +386,7 @@ __device__ __forceinline__ void block_forward_rw(const RegW &wr, PolSmem &s) {
     for (int r = 0; r < 16; ++r) s.h1[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + wr.b1);
   }
   __syncthreads();
+  pa.mark(1);
   {
     f32x16 acc = {};
 #pragma unroll
@@ -383,7 +399,9 @@ __device__ __forceinline__ void block_forward_rw(const RegW &wr, PolSmem &s) {
     for (int r = 0; r < 16; ++r) s.h2[crow(r, h) * HS + n0 + i] = fast_tanh(acc[r] + wr.b2);
   }
   __syncthreads();
+  pa.mark(2);
   block_heads(s);
+  pa.mark(3);
 }
 
 // ------------------------------------------------------------------ rollout
@@ -454,6 +472,10 @@ __global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_policy_step(ppo_cfg_t
   else stage_store_small(wr, s);
   __syncthreads();
   int buf = 0;
+  PolAcc pa{};
+#ifdef USV_PHASE_PROBE
+  pa.t = wall_clock64();
+#endif
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
   const int row0 = tile * RB;
   const int nrows = min(RB, n - row0);
@@ -466,7 +488,8 @@ __global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_policy_step(ppo_cfg_t
   if (w > 0 && nt < ntiles) load_obs_tile3(obs, n, nt, ttv, xn);
   USV_PHASE(pol, 1);   // (probe slots 1-4: the launch's last tile)
   USV_PHASE(pol, 2);
-  if constexpr (kRW) block_forward_rw(wr, s);
+  pa.mark(0);
+  if constexpr (kRW) block_forward_rw(wr, s, pa);
   else block_forward(wr, s, tile == (int)blockIdx.x);
   USV_PHASE(pol, 3);
   if (w == 0) {
@@ -506,8 +529,13 @@ __global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_policy_step(ppo_cfg_t
   }
   __syncthreads();   // s.out / s.zz[buf] read above before the next tile's forward and draws rewrite them
   USV_PHASE(pol, 4);
+  pa.mark(4);
   buf ^= 1;
   }
+#ifdef USV_PHASE_PROBE
+  if (threadIdx.x == 0 && blockIdx.x < 4096)
+    for (int k = 0; k < 5; ++k) g_probe_pol[blockIdx.x][5 + k] = pa.d[k];
+#endif
 }
 
 __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,

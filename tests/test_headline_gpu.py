@@ -1,7 +1,7 @@
 """Parity at the headline size (131,072 envs per GPU: BASELINE configs[4]'s 2^20 envs over 8 GPUs) for the
 code paths that only run above the sizes of the other parity tests:
 
-* the rollout kernels' persistent multi-tile loop (5.3 tiles per workgroup at 131,072 envs in the register-weight
+* the rollout kernels' persistent multi-tile loop (8 tiles per workgroup at 131,072 envs in the register-weight
   form, 16 in the LDS-staged one: next-tile obs prefetch, next-tile normal draws by wave 0), with injected draws and
   with the in-kernel Philox + Box-Muller sampler (models.py:372-386 Normal.sample), and ppo_value;
 * GAE + prepare_dataset over 131,072 x 16 rows (k_gae's 512 block partials, the k_prepare_finalize fold);
@@ -49,7 +49,7 @@ def _rand_agent(n, rng, mini_epochs=1, minibatch=8192):
 
 @pytest.mark.parametrize("inject", [True, False], ids=["eps_inject", "philox"])
 def test_policy_step_headline_multi_tile(inject):
-    """k_policy_step at 131,072 envs (768 workgroups x 5.3 tiles) vs the oracle forward: actions, mu, sigma,
+    """k_policy_step at 131,072 envs (512 workgroups x 8 tiles) vs the oracle forward: actions, mu, sigma,
     neglogp, denormalised value, raw obs rows and done flags of rollout slot t, the clamped env actions.
     philox: the in-kernel sampler (site 0x200, step from the device clock as in graph replay) vs its
     restatement PO.policy_normals."""
@@ -94,8 +94,8 @@ def test_policy_step_headline_multi_tile(inject):
 @pytest.mark.parametrize("n,grid_cap,inject", [(HEAD, 0, False), (HEAD, 0, True), (4128, 7, False), (100, 0, True)])
 def test_policy_step_register_weights_bit_identical(monkeypatch, n, grid_cap, inject):
     """The register-weight policy kernel (k_policy_step<true>: W1 / W2 as the waves' matrix-core operands in VGPRs,
-    41 KB of LDS, three workgroups per CU) equals the LDS-staged one (USV_POLICY_RW=0) bit for bit: every experience
-    array and the env actions, at the headline size (768 workgroups, 5.3 tiles each), over a capped grid (4,128 rows on 7
+    41 KB of LDS, two workgroups per CU) equals the LDS-staged one (USV_POLICY_RW=0) bit for bit: every experience
+    array and the env actions, at the headline size (512 workgroups, 8 tiles each), over a capped grid (4,128 rows on 7
     workgroups: 19 tiles each, a ragged last tile) and for one partial tile."""
     from omniisaacgymenvs_loop_amd import _capi as c
     rng = np.random.default_rng(21)

@@ -85,15 +85,22 @@ def main():
             print(f"  stamp {k} {what:22s} t = {d.mean():6.2f} us (max {d.max():6.2f})")
         print(f"  launch span (first start -> last end stamp): {(rb[:, 4].max() - rb[:, 0].min()) / 100:.2f} us")
     pp = read("pol")
-    b = pp[:256]
-    b = b[b[:, 0] > 0]
+    b = pp[pp[:, 0] > 0]
     ntiles = (agent.num_actors + 31) // 32
-    per = (ntiles + 255) // 256
-    print(f"k_policy_step (last launch, {per} tiles per workgroup; slots 1-4 are the last tile):")
+    per = ntiles / max(len(b), 1)
+    print(f"k_policy_step (last launch, {len(b)} workgroups, {per:.2f} tiles per workgroup; slots 1-4 are the last tile):")
     print(f"  last tile starts at t = {np.mean(b[:, 1] - b[:, 0]) / 100:7.2f} us (launch mean per tile "
           f"{np.mean(b[:, 4] - b[:, 0]) / 100 / per:6.2f} us)")
     for k, what in ((2, "obs staged"), (3, "forward done"), (4, "sampled + stored")):
         print(f"  slot {k} {what:18s} +{np.mean(b[:, k] - b[:, k - 1]) / 100:6.2f} us")
+    if np.any(b[:, 5:10] != 0):   # per-phase sums over the workgroup's tiles (wave 0's view)
+        tot = b[:, 5:10].sum(axis=1).mean()
+        for k, what in enumerate(("tile setup (obs prefetch issue)", "layer 1 + barrier", "layer 2 + barrier",
+                                  "heads + barrier", "epilogue / next obs + barrier")):
+            m = b[:, 5 + k].mean() / 100 / per
+            print(f"  per tile: {what:32s} {m:6.2f} us ({b[:, 5 + k].mean() / tot:5.1%})")
+        print(f"  launch span {(b[:, 4].max() - b[:, 0].min()) / 100:7.2f} us; start spread "
+              f"{(b[:, 0].max() - b[:, 0].min()) / 100:5.2f} us")
     cnt = int(task.ctl[0].item())
     print("reset count of the last step:", cnt)
     report("k_field_wave (last launch)", read("field"), min(cnt, 512), 4, extra_col=15)
