@@ -95,27 +95,13 @@ __device__ __forceinline__ float usv_sin(float x) {
 // no fma) then gives R^T v = (C vx + S vy, -S vx + C vy); the integrator rotates the body-frame wrench with the same
 // R (its own definition, the PhysX step's), so one half-angle sincos per substep serves both
 struct QuatRot { float C, S, w, z; };
-// RN(2 / s) without a division for s = w^2 + z^2 of usv_sincos's rounded components, which lies within a few ulp
-// of 1 (|s - 1| < 2^-20 for every argument: tests/test_oracle_golden.py::test_two_over_s_exact_on_the_window).  On
-// |s - 1| < 2^-13 the quotient is 2 - 2d + 2d^2 - .. (s = 1 + d): above 1 (d = k 2^-23) 4 - 2s is representable and
-// the rest is below half an ulp; below 1 (d = -k 2^-24) 2 + k 2^-23 lies on or at the midpoint below 2 + ceil(k / 2)
-// 2^-22 and the positive rest rounds it up.  Every operation is exact, branch-free; checked against the correctly
-// rounded quotient for every float on that window.  (Round 6 first tried a Markstein correction with an IEEE
-// fallback branch: 0.75 us SLOWER per env step, profiles/r06/r06e_two_s_ab.txt.)
-#ifndef USV_TWO_S_DIV
-#define USV_TWO_S_DIV 0   // 1: the IEEE division (A/B builds; the same bits on the window)
-#endif
-__host__ __device__ __forceinline__ float two_over_s(float s) {
-  if (USV_TWO_S_DIV) return 2.0f / s;
-  const float lo = 2.0f + ceilf((1.0f - s) * 8388608.0f) * 2.384185791015625e-7f;   // s < 1
-  const float hi = 4.0f - 2.0f * s;                                                   // s >= 1
-  return s < 1.0f ? lo : hi;
-}
 __device__ __forceinline__ QuatRot usv_quat_rot(float yaw) {
   float z, w;
   usv_sincos(yaw * 0.5f, &z, &w);
-  // (q * q).sum(-1) of (w, 0, 0, z); torch's 2.0 / t is reciprocal * 2, the same bits as the IEEE quotient
-  const float two_s = two_over_s(w * w + z * z);
+  // (q * q).sum(-1) of (w, 0, 0, z); torch's 2.0 / t is reciprocal * 2, the same bits as the IEEE quotient.  Round
+  // 6 measured two division-free forms of it (a Markstein correction with a fallback branch: +0.75 us per env step;
+  // an exact branch-free form on the window s lies in: +0.17 us; profiles/r06/r06e_two_s_ab.txt, r06h_two_s_ab.txt)
+  const float two_s = 2.0f / (w * w + z * z);
   return QuatRot{1.0f - two_s * (z * z), two_s * (z * w), w, z};
 }
 // exp, tanh and atan2 of the observation / reward formulas, by the same rule (oracle/usv_oracle.c restates them):

@@ -170,6 +170,30 @@ def test_prepare_headline_multi_block():
     assert vr[2] == vrms.count
 
 
+def test_gae_vector_form_bit_identical(monkeypatch):
+    """k_gae<16> (an env's 16 rows loaded and stored as 16-byte vectors) equals the runtime-horizon loop
+    (USV_GAE_VEC=0) bit for bit at 131,072 x 16 rows: normalised values, returns, advantages and the value RMS."""
+    rng = np.random.default_rng(14)
+    N = HEAD
+    ag, _, _, _ = _rand_agent(N, rng)
+    val0 = torch.tensor(rng.normal(0.5, 1.0, N * H).astype(np.float32), device=DEV)
+    ag.exp_rew.copy_(torch.tensor(rng.normal(0.0, 0.2, N * H).astype(np.float32), device=DEV))
+    ag.exp_done.copy_(torch.tensor((rng.random(N * H) < 0.05).astype(np.uint8), device=DEV))
+    ag.obs = {"obs": {"state": torch.tensor(rng.normal(0, 2, (N, 33)).astype(np.float32), device=DEV)}}
+    ag.dones = torch.tensor((rng.random(N) < 0.05).astype(np.int64), device=DEV)
+    rms0 = ag.val_rms.clone()
+    out = {}
+    for vec in ("1", "0"):
+        monkeypatch.setenv("USV_GAE_VEC", vec)
+        ag.exp_val.copy_(val0)
+        ag.val_rms.copy_(rms0)
+        ag.prepare_dataset()
+        torch.cuda.synchronize()
+        out[vec] = [x.cpu().numpy().copy() for x in (ag.exp_val, ag.exp_ret, ag.exp_adv, ag.val_rms)]
+    for a, b in zip(out["1"], out["0"]):
+        np.testing.assert_array_equal(a, b)
+
+
 @pytest.mark.parametrize("pack", ["0", "1"])
 def test_potential_field_1300_resets_vs_oracle(pack, monkeypatch):
     """~1,300 reset envs (the headline size's steady-state reset count) at 4,096 envs, whose launch geometry

@@ -371,44 +371,3 @@ def test_packaged_yaml_matches_fixture_config(golden):
         else:
             assert a == b, name
 
-
-def _rn32(q):
-    """The float32 nearest to the rational q (ties to even), exactly."""
-    from fractions import Fraction
-    f = np.float32(float(q))
-    cands = [f, np.nextafter(f, np.float32(np.inf)), np.nextafter(f, np.float32(-np.inf))]
-    return min(cands, key=lambda c: (abs(Fraction(float(c)) - q), int(np.float32(c).view(np.uint32)) & 1))
-
-
-def _two_over_s(s):
-    """csrc/usv_device.h:two_over_s, restated in float32 (every operation exact)."""
-    s = np.float32(s)
-    lo = np.float32(2.0) + np.float32(np.ceil(np.float32(np.float32(1.0) - s) * np.float32(8388608.0))) * \
-        np.float32(2.384185791015625e-7)
-    hi = np.float32(4.0) - np.float32(2.0) * s
-    return np.float32(lo if s < np.float32(1.0) else hi)
-
-
-def test_two_over_s_exact_on_the_window():
-    """The quaternion scale two_s = 2 / (w^2 + z^2) of quaternion_to_matrix (Hydrodynamics.py:209-217) without the
-    division (csrc/usv_device.h:two_over_s): equal to the correctly rounded quotient for EVERY float s with
-    |s - 1| < 2^-13 (exact rational arithmetic), and s = w^2 + z^2 of usv_sincos's components stays inside
-    |s - 1| < 2^-20 for every 61st float argument in [-4, 4] (yaw / 2 for |yaw| <= 2 pi plus margin: the
-    integrator's and the reset's range) and for all floats near the quadrant boundaries."""
-    from fractions import Fraction as Fr
-    n = 0
-    for direction in (np.float32(0.0), np.float32(2.0)):
-        x = np.float32(1.0)
-        while abs(float(x) - 1.0) < 2.0 ** -13:
-            assert _two_over_s(x) == _rn32(Fr(2) / Fr(float(x))), x
-            n += 1
-            x = np.nextafter(x, direction)
-    assert n > 3000
-    bits = np.arange(0, np.float32(4.0).view(np.int32), 61, dtype=np.int64).astype(np.int32)
-    xs = bits.view(np.float32)
-    near = np.concatenate([np.arange(-2 ** 16, 2 ** 16, dtype=np.int64) + np.float32(v).view(np.int32)
-                           for v in (np.pi / 4, np.pi / 2, 3 * np.pi / 4, np.pi)]).astype(np.int32).view(np.float32)
-    for x in (xs, -xs, near, -near):
-        z, w = O.sincos(np.ascontiguousarray(x, dtype=np.float32))
-        s = (w * w + z * z).astype(np.float32)
-        assert float(np.abs(s.astype(np.float64) - 1.0).max()) < 2.0 ** -20

@@ -7,7 +7,7 @@ O=$R/gpurun_out/r06h
 mkdir -p $O
 cd $R
 timeout -k 10 600 python3 -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_env_gpu.py \
-  tests/test_overlap_gpu.py > $O/pytest.log 2>&1 || exit $?
+  tests/test_overlap_gpu.py tests/test_headline_gpu.py tests/test_ppo_gpu.py > $O/pytest.log 2>&1 || exit $?
 tail -2 $O/pytest.log
 for rep in 1 2 3; do
   timeout -k 10 120 python3 tools/env_step_probe.py 131072 48 >> $O/ab_exact.txt 2>&1 || exit $?
