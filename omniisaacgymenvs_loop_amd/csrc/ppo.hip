@@ -339,6 +339,7 @@ struct PolSmem {
 };
 struct RegW {
   float w1[17], w2[NH / 2], b1, b2, tlr[NTL];
+  float hm0[NH / 8], hm1[NH / 8], hv[NH / 8];   // the heads' weights at k = tid % 8 + 8 kk (block_heads' k)
 };
 __device__ __forceinline__ void regw_load(const float *__restrict__ P, RegW &r) {
   const int tid = threadIdx.x, lane = tid & 63, i = lane & 31, h = lane >> 5, n = 32 * (tid >> 6) + i;
@@ -346,6 +347,13 @@ __device__ __forceinline__ void regw_load(const float *__restrict__ P, RegW &r) 
   for (int st = 0; st < 17; ++st) r.w1[st] = P[PPO_OFF_W1 + n * NIN + min(2 * st + h, NIN - 1)];
   r.b1 = P[PPO_OFF_B1 + n];
   r.b2 = P[PPO_OFF_B2 + n];
+#pragma unroll
+  for (int kk = 0; kk < NH / 8; ++kk) {
+    const int k = (tid & 7) + 8 * kk;
+    r.hm0[kk] = P[PPO_OFF_WMU + k];
+    r.hm1[kk] = P[PPO_OFF_WMU + NH + k];
+    r.hv[kk] = P[PPO_OFF_WV + k];
+  }
 #pragma unroll
   for (int u = 0; u < NTL; ++u) r.tlr[u] = P[PPO_OFF_B2 + min(tid + u * TB, TAIL - 1)];
 #pragma unroll
@@ -400,7 +408,29 @@ __device__ __forceinline__ void block_forward_rw(const RegW &wr, PolSmem &s, Pol
   }
   __syncthreads();
   pa.mark(2);
-  block_heads(s);
+  {   // block_heads with the head weights from registers (the same fmaf chains)
+    const int r = tid / 8, part = tid % 8;
+    float a0 = 0.f, a1 = 0.f, av = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < NH / 8; ++kk) {
+      const float hv = s.h2[r * HS + part + 8 * kk];
+      a0 = fmaf(wr.hm0[kk], hv, a0);
+      a1 = fmaf(wr.hm1[kk], hv, a1);
+      av = fmaf(wr.hv[kk], hv, av);
+    }
+#pragma unroll
+    for (int m = 1; m < 8; m <<= 1) {
+      a0 += __shfl_xor(a0, m, 64);
+      a1 += __shfl_xor(a1, m, 64);
+      av += __shfl_xor(av, m, 64);
+    }
+    if (part == 0) {
+      s.out[r * 4 + 0] = a0 + s.tail[T_BMU];
+      s.out[r * 4 + 1] = a1 + s.tail[T_BMU + 1];
+      s.out[r * 4 + 2] = av + s.tail[T_BV];
+    }
+  }
+  __syncthreads();
   pa.mark(3);
 }
 
@@ -438,22 +468,22 @@ __global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_policy_step(ppo_cfg_t
   const bool normalize = c.normalize_input != 0;
   if ((int)blockIdx.x >= ntiles) return;   // (the grid is at most ntiles; uniform)
   // N(0,1) draws of tile `tl`'s rows (wave 0, lane = row) into s.zz[buf]
+  // (lane 32 j + r of wave 0: row r's component j -- the two components' transcendentals in parallel)
   auto draw = [&](int tl, int buf) {
-    if (w == 0 && lane < RB) {
-      const int e = min(tl * RB + lane, n - 1);
-      float z0, z1;
+    if (w == 0) {
+      const int r = lane & (RB - 1), j = lane >> 5;
+      const int e = min(tl * RB + r, n - 1);
+      float zj;
       if (eps_inject) {
-        z0 = eps_inject[2 * e];
-        z1 = eps_inject[2 * e + 1];
-      } else {  // Normal.sample via Box-Muller on Philox(site 0x200)
+        zj = eps_inject[2 * e + j];
+      } else {  // Normal.sample via Box-Muller on Philox(site 0x200): z_j from (u[2 j], u[2 j + 1])
         float u[4];
         philox_u4(seed, (uint32_t)e, step, 0x200u, u);
-        const float rr0 = sqrtf(-2.0f * logf(1.0f - u[0])), rr1 = sqrtf(-2.0f * logf(1.0f - u[2]));
-        z0 = rr0 * cosf(USV_2PI_F * u[1]);
-        z1 = rr1 * cosf(USV_2PI_F * u[3]);
+        const float ua = j ? u[2] : u[0], ub = j ? u[3] : u[1];
+        const float rr = sqrtf(-2.0f * logf(1.0f - ua));
+        zj = rr * cosf(USV_2PI_F * ub);
       }
-      s.zz[buf][2 * lane] = z0;
-      s.zz[buf][2 * lane + 1] = z1;
+      s.zz[buf][2 * r + j] = zj;
     }
   };
   if (threadIdx.x < NIN) {
@@ -493,34 +523,39 @@ __global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_policy_step(ppo_cfg_t
   else block_forward(wr, s, tile == (int)blockIdx.x);
   USV_PHASE(pol, 3);
   if (w == 0) {
-    const int r = lane;
-    if (r < nrows) {
-      const int e = row0 + r;
-      const size_t slot = (size_t)e * H + t;
-      const float mu0 = s.out[r * 4], mu1 = s.out[r * 4 + 1], v = s.out[r * 4 + 2];
-      const float ls0 = mu0 * 0.f + P[PPO_OFF_SIGMA], ls1 = mu1 * 0.f + P[PPO_OFF_SIGMA + 1];
-      const float sg0 = expf(ls0), sg1 = expf(ls1);
-      const float z0 = s.zz[buf][2 * r], z1 = s.zz[buf][2 * r + 1];
-      const float a0 = mu0 + sg0 * z0, a1 = mu1 + sg1 * z1;
-      const float q0 = (a0 - mu0) / sg0, q1 = (a1 - mu1) / sg1;
-      const float nlp = 0.5f * (q0 * q0 + q1 * q1) + kLog2Pi + (ls0 + ls1);
-      float vd = v;
-      if (c.normalize_value) {  // denorm_value (running_mean_std.py:113-115)
-        vd = clampt(v, -5.0f, 5.0f);
-        vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
-      }
-      exp_st(&exp_act[slot * 2], a0); exp_st(&exp_act[slot * 2 + 1], a1);
-      exp_st(&exp_mu[slot * 2], mu0); exp_st(&exp_mu[slot * 2 + 1], mu1);
-      exp_st(&exp_sigma[slot * 2], sg0); exp_st(&exp_sigma[slot * 2 + 1], sg1);
-      exp_st(&exp_nlp[slot], nlp);
-      exp_st(&exp_val[slot], vd);
-      exp_st(&exp_done[slot], (uint8_t)(dones_prev[e] != 0));
+    // lane 32 j + r: row r's action component j; the neglogp's two terms meet by one cross-half exchange
+    const int r = lane & (RB - 1), j = lane >> 5;
+    const bool rowok = r < nrows;
+    const int e = row0 + (rowok ? r : 0);
+    const size_t slot = (size_t)e * H + t;
+    const float muj = s.out[r * 4 + j];
+    const float lsj = muj * 0.f + P[PPO_OFF_SIGMA + j];
+    const float sgj = expf(lsj);
+    const float aj = muj + sgj * s.zz[buf][2 * r + j];
+    const float qj = (aj - muj) / sgj;
+    const float qo = __shfl_xor(qj, 32, 64), lso = __shfl_xor(lsj, 32, 64);
+    const float q0 = j ? qo : qj, q1 = j ? qj : qo, ls0 = j ? lso : lsj, ls1 = j ? lsj : lso;
+    if (rowok) {
+      exp_st(&exp_act[slot * 2 + j], aj);
+      exp_st(&exp_mu[slot * 2 + j], muj);
+      exp_st(&exp_sigma[slot * 2 + j], sgj);
       // preprocess_actions: clamp(-1,1) then rescale to [low, high] = identity (a2c_common.py:1134-1144)
-      actions_out[2 * e] = clampt(a0, -1.0f, 1.0f);
-      actions_out[2 * e + 1] = clampt(a1, -1.0f, 1.0f);
+      actions_out[2 * e + j] = clampt(aj, -1.0f, 1.0f);
+      if (j == 0) {
+        const float nlp = 0.5f * (q0 * q0 + q1 * q1) + kLog2Pi + (ls0 + ls1);
+        float vd = s.out[r * 4 + 2];
+        if (c.normalize_value) {  // denorm_value (running_mean_std.py:113-115)
+          vd = clampt(vd, -5.0f, 5.0f);
+          vd = sqrtf((float)val_rms[1] + c.rms_eps) * vd + (float)val_rms[0];
+        }
+        exp_st(&exp_nlp[slot], nlp);
+        exp_st(&exp_val[slot], vd);
+        exp_st(&exp_done[slot], (uint8_t)(dones_prev[e] != 0));
+      }
     }
     if (c.nan_probe && c.nan_flag) {   // wave 0, uniform
-      const bool bad = r < nrows && (nonfinite(s.out[r * 4]) | nonfinite(s.out[r * 4 + 1]) | nonfinite(s.out[r * 4 + 2]));
+      const bool bad = lane < nrows && (nonfinite(s.out[lane * 4]) | nonfinite(s.out[lane * 4 + 1]) |
+                                        nonfinite(s.out[lane * 4 + 2]));
       nan_report(c.nan_flag, bad ? USV_NAN_POLICY : 0u);
     }
     if (nt < ntiles) draw(nt, buf ^ 1);
