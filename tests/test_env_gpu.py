@@ -333,14 +333,15 @@ def test_philox_mode_disturbances_matches_oracle():
         dp = _vs_oracle("philox_dist", task, E, obs, rew, dones, t, dp)
 
 
+@pytest.mark.parametrize("n,T,ep_len", [(4096, 40, 25), (65536, 9, 4)], ids=["4096", "65536"])
 @pytest.mark.parametrize("name", ["GoToPose", "TrackXYOVelocity"])
-def test_philox_mode_pose_tasks_match_oracle(golden, name):
-    """SURVEY A20 tasks at 4096 envs with in-kernel draws vs the oracle (TrackXYOVelocity's
-    all-env angular sum included)."""
+def test_philox_mode_pose_tasks_match_oracle(golden, name, n, T, ep_len):
+    """SURVEY A20 tasks with in-kernel draws vs the oracle (TrackXYOVelocity's all-env angular sum included): at
+    4096 envs over 40 steps, and at BASELINE configs[3]'s 65,536 envs per GPU over 9 steps with 4-step episodes
+    (two rounds of resets of every env)."""
     d = golden("episode_P.npz" if name == "GoToPose" else "episode_T.npz")
     task_cfg = json.loads(bytes(d["config_json"]).decode())
-    task_cfg["env"]["maxEpisodeLength"] = 25
-    n, T = 4096, 40
+    task_cfg["env"]["maxEpisodeLength"] = ep_len
     task = _task(task_cfg, n)
     E = _oracle_for(task.cfg, n, task_cfg)
     rng = np.random.default_rng(9)
