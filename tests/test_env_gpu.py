@@ -234,10 +234,11 @@ def _rew_diag(task, E, got, k=4):
     return "\n".join(out)
 
 
-@pytest.mark.parametrize("n,T", [(2048, 24), (1000, 12), (33, 12)])
+@pytest.mark.parametrize("n,T", [(2048, 24), (1000, 12), (33, 12), (1, 12)])
 def test_philox_mode_matches_oracle(n, T):
     """In-kernel Philox draws == the oracle's restatement of the same streams; also at ragged sizes (1000: a
-    partial last workgroup and wave; 33: one wave with a single lane past 32, the slab's smallest row stride)."""
+    partial last workgroup and wave; 33: one wave with a single lane past 32, the slab's smallest row stride; 1: a
+    single env, one active lane in every kernel)."""
     task_cfg = load_yaml(TEST_YAML)
     task = _task(task_cfg, n)
     E = _oracle_for(task.cfg, n, task_cfg)
