@@ -196,8 +196,9 @@ __device__ __forceinline__ void load_obs_tile(const float *__restrict__ obs, int
 }
 // normalised rows into s.x; with exp_obs, the raw rows also to the experience buffer (row
 // env * H + t, swap_and_flatten01 layout)
+template <class S>
 __device__ __forceinline__ void put_obs_tile(const float (&x)[NUO], const ObsCols &oc, int row0, int nrows,
-                                             bool normalize, float eps, MlpSmem &s, float *exp_obs, int H, int t) {
+                                             bool normalize, float eps, S &s, float *exp_obs, int H, int t) {
 #pragma unroll
   for (int u = 0; u < NUO; ++u) {
     const int q = threadIdx.x + u * TB;
@@ -573,12 +574,17 @@ __global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_policy_step(ppo_cfg_t
 #endif
 }
 
-__global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restrict__ P, const double *obs_rms,
-                                              const double *val_rms, const float *__restrict__ obs, float *values) {
-  __shared__ MlpSmem s;
+// kRW: the register-weight form of the policy step (RegW / PolSmem), up to 256 x POL_WPC workgroups
+template <bool kRW>
+__global__ __launch_bounds__(TB, kRW ? POL_WPC : 1) void k_value(ppo_cfg_t c, const float *__restrict__ P,
+                                                                 const double *obs_rms, const double *val_rms,
+                                                                 const float *__restrict__ obs, float *values) {
+  __shared__ std::conditional_t<kRW, PolSmem, MlpSmem> s;
   const int n = c.n_envs;
-  StagedW wr;
-  stage_load(P, wr);
+  std::conditional_t<kRW, RegW, StagedW> wr;
+  if constexpr (kRW) regw_load(P, wr);
+  else stage_load(P, wr);
+  PolAcc pa{};
   const int ntiles = (n + RB - 1) / RB;
   ObsCols oc;
   load_obs_cols(obs_rms, oc);
@@ -590,9 +596,13 @@ __global__ __launch_bounds__(TB) void k_value(ppo_cfg_t c, const float *__restri
     float xn[NUO];
     load_obs_tile(obs, n, min(tile + (int)gridDim.x, ntiles - 1), xn);
     put_obs_tile(xo, oc, row0, nrows, c.normalize_input != 0, c.rms_eps, s, nullptr, 0, 0);
-    if (tile == (int)blockIdx.x) stage_store_small(wr, s);
+    if (tile == (int)blockIdx.x) {
+      if constexpr (kRW) regw_store_tail(wr, s);
+      else stage_store_small(wr, s);
+    }
     __syncthreads();
-    block_forward(wr, s, tile == (int)blockIdx.x);
+    if constexpr (kRW) block_forward_rw(wr, s, pa);
+    else block_forward(wr, s, tile == (int)blockIdx.x);
     const int r = threadIdx.x;
     if (r < nrows) {
       float vd = s.out[r * 4 + 2];
@@ -2228,9 +2238,12 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
 int ppo_value(const ppo_cfg_t *cfg, const float *params, const double *obs_rms, const double *val_rms,
               const float *obs, float *values, void *stream) {
   if (!cfg || !params || !obs_rms || !obs || !values || cfg->n_envs <= 0) return 1;
-  const int grid = policy_grid(cfg->n_envs);
-  hipLaunchKernelGGL(k_value, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms, obs,
-                     values);
+  const char *rw = getenv("USV_POLICY_RW");   // 0: the LDS-staged form (same results)
+  const bool reg_w = !(rw && atoi(rw) == 0);
+  const int ntiles = (cfg->n_envs + RB - 1) / RB;
+  const int grid = reg_w ? (ntiles < 256 * POL_WPC ? ntiles : 256 * POL_WPC) : policy_grid(cfg->n_envs);
+  hipLaunchKernelGGL(reg_w ? k_value<true> : k_value<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg,
+                     params, obs_rms, val_rms, obs, values);
   USV_CHECK_LAUNCH();
   return 0;
 }

@@ -122,6 +122,24 @@ def test_policy_step_register_weights_bit_identical(monkeypatch, n, grid_cap, in
         np.testing.assert_array_equal(a.view(np.uint8), b.view(np.uint8), err_msg=str(k))
 
 
+@pytest.mark.parametrize("n", [HEAD, 4128, 100])
+def test_value_register_weights_bit_identical(monkeypatch, n):
+    """ppo_value's register-weight kernel (k_value<true>) equals the LDS-staged one (USV_POLICY_RW=0) bit for bit."""
+    from omniisaacgymenvs_loop_amd import _capi as c
+    rng = np.random.default_rng(22)
+    ag, _, _, _ = _rand_agent(n, rng, minibatch=8192 if n % 512 == 0 else 16 * n)
+    obs = torch.tensor(rng.normal(0, 2, (n, 33)).astype(np.float32), device=DEV)
+    out = {}
+    for rw in ("0", "1"):
+        monkeypatch.setenv("USV_POLICY_RW", rw)
+        v = torch.full((n,), 7.0, device=DEV)
+        c.call("ppo_value", c.byref(ag.cfg), c.ptr(ag.model_params), c.ptr(ag.obs_rms), c.ptr(ag.val_rms), c.ptr(obs),
+               c.ptr(v), c.stream_ptr())
+        torch.cuda.synchronize()
+        out[rw] = v.cpu().numpy()
+    np.testing.assert_array_equal(out["0"].view(np.uint32), out["1"].view(np.uint32))
+
+
 def test_value_headline_multi_tile():
     """k_value (ppo_value) at 131,072 envs vs the oracle's denormalised value."""
     from omniisaacgymenvs_loop_amd import _capi as c
