@@ -95,12 +95,13 @@ __device__ __forceinline__ bool occ_bit(const uint32_t *occ, int r, int cc) {
 // slot's scratch, where the result ends as k_field_wave leaves its raw cost, one block barrier per sweep; all waves of the block share the CU's L1, so plain
 // global loads see the other waves' stores after the barrier.
 constexpr int kRefSweeps = (G * 3) / 2;
+template <int NT>
 __device__ __forceinline__ void cost_sweeps_exact(const uint32_t *occ, int ix, int iy, float *A, float *B) {
   const int tid = threadIdx.x;
-  for (int q = tid; q < G2; q += kWaveThreads) A[q] = (q == iy * G + ix) ? 0.f : INFINITY;
+  for (int q = tid; q < G2; q += NT) A[q] = (q == iy * G + ix) ? 0.f : INFINITY;
   __syncthreads();
   for (int it = 0; it < kRefSweeps; ++it) {
-    for (int q = tid; q < G2; q += kWaveThreads) {
+    for (int q = tid; q < G2; q += NT) {
       const int r = q / G, cc = q % G;
       float m = A[q];
 #pragma unroll
@@ -445,9 +446,19 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
           Ft[i * USV_FIELD_TW + j] = __float_as_uint(h[i + 1][j + 1]) > kInfBits ? INFINITY : h[i + 1][j + 1];
     }
     if (tile_ok) lastc[tp] = -1000;   // ready for the next slot
+    if (exact) {   // (uniform) the reference's 225 literal sweeps for this env, over the tiles just stored
+      // (rare: never for the packaged spawn ranges; in the sweep kernel itself rather than a launch of its own,
+      // whose workgroups had to wait for CUs the concurrent policy step held: ~50 us on the field chain per step)
+      __syncthreads();
+      float *Fe = b.field + (size_t)e * FS;          // overwritten: the ping-pong buffer, then the cost tiles
+      float *scratch = b.sdf + (size_t)e * FS;      // the other ping-pong buffer
+      cost_sweeps_exact<NTHR>(occ, ix, iy, Fe, scratch);   // 225 (odd) sweeps: result in scratch
+      for (int q = tid; q < G2; q += NTHR) Fe[field_idx(q / G, q % G)] = scratch[q];
+      if (tid == 0) atomicAdd(&b.ctl[USV_CTL_FIELD_EXACT], 1);
+    }
     if (tid == 0) {
       b.slot_stats[(size_t)slot * kSlotStride + SS_ITERS] = (float)it;   // iterations (diagnostic)
-      b.slot_stats[(size_t)slot * kSlotStride + SS_EXACT] = exact ? 1.f : 0.f;   // k_field_exact redoes it
+      b.slot_stats[(size_t)slot * kSlotStride + SS_EXACT] = exact ? 1.f : 0.f;   // took the reference's sweeps
 #ifdef USV_PHASE_PROBE
       if (blockIdx.x < 4096) g_probe_field[blockIdx.x][15] = (unsigned long long)it;
 #endif
@@ -466,59 +477,6 @@ __global__ __launch_bounds__(kWaveThreads, USV_SWEEP_WAVES) void k_field_wave_pa
 constexpr int kHalfThreads = 512;
 __global__ __launch_bounds__(kHalfThreads) void k_field_wave_half(usv_cfg_t c, usv_bufs_t b) {
   field_wave_body<false, T, T / 2, kHalfThreads>(c, b);
-}
-
-// The reference's literal sweeps for the slots k_field_wave could not certify (SS_EXACT):
-// one workgroup per such slot, the occupancy bit map rebuilt from the slot's obstacles
-// exactly as k_field_wave builds it.  A separate launch keeps the sweep kernel's registers
-// untouched; with nothing flagged every workgroup exits after one round of flag loads (its
-// threads read the flags of all its slots at once: one load latency, not one per slot).
-__global__ __launch_bounds__(kWaveThreads) void k_field_exact(usv_cfg_t c, usv_bufs_t b) {
-  __shared__ uint32_t occ[G * kOccColWords];
-  __shared__ float so[2 * USV_NOBST];
-  __shared__ float slin[G];
-  const int n = b.n;
-  const int count = min(b.ctl[USV_CTL_RESET_COUNT], n);
-  const int tid = threadIdx.x;
-  bool any = false;
-  for (int slot = blockIdx.x + tid * gridDim.x; slot < count; slot += kWaveThreads * gridDim.x)
-    any |= b.slot_stats[(size_t)slot * kSlotStride + SS_EXACT] != 0.f;
-  if (!__syncthreads_or(any)) return;   // uniform per workgroup
-  for (int slot = blockIdx.x; slot < count; slot += gridDim.x) {
-    const float *st = b.slot_stats + (size_t)slot * kSlotStride;
-    if (st[SS_EXACT] == 0.f) continue;   // uniform per workgroup
-    const int e = b.reset_ids[slot];
-    if (tid < 2 * USV_NOBST) so[tid] = st[kSlotObst + tid];
-    if (tid < G) slin[tid] = grid_coord(b.grid_lin, c.map_size, tid);
-    for (int q = tid; q < G * kOccColWords; q += kWaveThreads) occ[q] = 0u;
-    __syncthreads();
-    const float half_m = (float)((double)c.map_size / 2);
-    const float cellf = (float)((double)c.map_size / G);
-    const int reach = (int)ceilf(c.obstacle_radius / cellf) + 2;
-    const int bw = 2 * reach + 1;
-    for (int q = tid; q < USV_NOBST * bw * bw; q += kWaveThreads) {
-      const int o = q / (bw * bw), k = q % (bw * bw);
-      const float ox = so[2 * o], oy = so[2 * o + 1];
-      const float ic = (ox + half_m) / cellf - 0.5f, jc = (oy + half_m) / cellf - 0.5f;
-      if (!(fabsf(ic) < 4.0f * G && fabsf(jc) < 4.0f * G)) continue;
-      const int cc = (int)floorf(ic) - reach + k % bw, r = (int)floorf(jc) - reach + k / bw;
-      if (cc < 0 || cc >= G || r < 0 || r >= G) continue;
-      const float dx = slin[cc] - ox, dy = slin[r] - oy;
-      if (sqrtf(fmaf(dy, dy, dx * dx)) - c.obstacle_radius <= 0.f)
-        atomicOr(&occ[cc * kOccColWords + (r >> 5)], 1u << (r & 31));
-    }
-    const float tx = b.field_old_tgt[e], ty = b.field_old_tgt[n + e];
-    int ix = (int)((tx + half_m) / cellf), iy = (int)((ty + half_m) / cellf);
-    ix = min(max(ix, 0), G - 1);
-    iy = min(max(iy, 0), G - 1);
-    __syncthreads();
-    float *Fe = b.field + (size_t)e * FS;          // overwritten: the ping-pong buffer, then the cost tiles
-    float *scratch = b.sdf + (size_t)e * FS;      // the other ping-pong buffer
-    cost_sweeps_exact(occ, ix, iy, Fe, scratch);  // row-major ping-pong, 225 (odd) sweeps: result in scratch
-    for (int q = tid; q < G2; q += kWaveThreads) Fe[field_idx(q / G, q % G)] = scratch[q];   // into the tiles
-    if (tid == 0) atomicAdd(&b.ctl[USV_CTL_FIELD_EXACT], 1);
-    __syncthreads();
-  }
 }
 
 // batch constants given every slot's statistics
@@ -970,8 +928,6 @@ int field_stages(const usv_cfg_t *cfg, const usv_bufs_t *b, int stage, hipStream
       hipLaunchKernelGGL(k_field_wave_pack, dim3(grid_w), dim3(kWaveThreads), 0, s, *cfg, *b);
     }
     USV_CHECK_LAUNCH();
-    hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
-    USV_CHECK_LAUNCH();
     const int grid_s = stats_grid(b->n);
     hipLaunchKernelGGL(k_field_stats, dim3(grid_s), dim3(256), 0, s, *cfg, *b);
     USV_CHECK_LAUNCH();
@@ -1022,8 +978,6 @@ extern "C" int usv_potential_field(const usv_cfg_t *cfg, const usv_bufs_t *b, vo
   if (pack) hipLaunchKernelGGL(k_field_wave_pack, dim3(b->n < kPackGrid ? b->n : kPackGrid), dim3(kWaveThreads), 0, s,
                               *cfg, *b);
   else hipLaunchKernelGGL(k_field_wave, dim3(grid_b), dim3(kWaveThreads), 0, s, *cfg, *b);
-  USV_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_field_exact, dim3(grid_b < 256 ? grid_b : 256), dim3(kWaveThreads), 0, s, *cfg, *b);
   USV_CHECK_LAUNCH();
   const int grid_s = stats_grid(b->n);
   hipLaunchKernelGGL(k_field_stats, dim3(grid_s), dim3(256), 0, s, *cfg, *b);

@@ -385,7 +385,10 @@ def test_philox_mode_scene_replay_matches_oracle():
     assert {5, 6, 0} <= seen          # start_index 5, cycling over 7 scenes
 
 
-def _run_field(task, ids, obst, tgt, lin=None):
+def _run_field(task, ids, obst, tgt, lin=None, stage=False):
+    """The fields of the reset envs `ids` (obstacles / targets given) by usv_potential_field, or with stage=True by
+    the overlapped step's usv_field_stage(2) (sweeps, statistics, batch fold, constants; USV_FIELD_HALF picks its
+    sweep kernel)."""
     from omniisaacgymenvs_loop_amd import _capi
     k = len(ids)
     ids_t = torch.tensor(ids, device=DEV, dtype=torch.int32)
@@ -398,7 +401,10 @@ def _run_field(task, ids, obst, tgt, lin=None):
     task.field_old_tgt[:, ids_t.long()] = torch.tensor(tgt.T, device=DEV)
     if lin is not None:
         task.set_grid_lin(torch.tensor(lin))
-    _capi.call("usv_potential_field", _capi.byref(task.cfg), _capi.byref(task._bufs), _capi.stream_ptr())
+    if stage:
+        _capi.call("usv_field_stage", _capi.byref(task.cfg), _capi.byref(task._bufs), 2, _capi.stream_ptr())
+    else:
+        _capi.call("usv_potential_field", _capi.byref(task.cfg), _capi.byref(task._bufs), _capi.stream_ptr())
     torch.cuda.synchronize()
     return task.field_rowmajor(ids_t.long()).cpu().numpy()
 
@@ -438,14 +444,17 @@ def test_potential_field_random_batches_vs_oracle(pack, monkeypatch):
         np.testing.assert_array_equal(f, ref)
 
 
-@pytest.mark.parametrize("pack", ["0", "1"])
-def test_potential_field_long_detour_takes_reference_sweeps(pack, monkeypatch):
+@pytest.mark.parametrize("route", ["field_plain", "field_pack", "stage_half", "stage_pack"])
+def test_potential_field_long_detour_takes_reference_sweeps(route, monkeypatch):
     """A wall of 16 obstacles across the diagonal from a corner target: finite costs reach 235 > 224,
     so the tile-sweep fixed point is not certified equal to the reference's 225 sweeps
-    (d_multi_gemini.py:171) and k_field_exact recomputes that env with them; the ordinary env of the
-    same batch keeps the fast path.  Both bit-exact against the oracle (which runs the 225 sweeps)."""
+    (d_multi_gemini.py:171) and the sweep kernel recomputes that env with them; the ordinary env of the
+    same batch keeps the fast path.  Both bit-exact against the oracle (which runs the 225 sweeps), in each of
+    the three sweep kernels (k_field_wave, k_field_wave_pack, k_field_wave_half: usv_potential_field and the
+    overlapped step's usv_field_stage)."""
     from omniisaacgymenvs_loop_amd._abi import DEFINES
-    monkeypatch.setenv("USV_FIELD_PACK", pack)
+    monkeypatch.setenv("USV_FIELD_PACK", "1" if route == "field_pack" else "0")
+    monkeypatch.setenv("USV_FIELD_HALF", "1" if route == "stage_half" else "0")
     task_cfg = load_yaml(TEST_YAML)
     task = _task(task_cfg, 16)
     k = np.arange(16) - 7.5
@@ -454,7 +463,7 @@ def test_potential_field_long_detour_takes_reference_sweeps(pack, monkeypatch):
     obst = np.stack([wall, rng.uniform(-12, 12, (16, 2))]).astype(np.float32)
     tgt = np.array([[-14.3, -14.3], [0.4, -0.3]], np.float32)
     ids = np.array([9, 2], np.int32)
-    f = _run_field(task, ids, obst, tgt)
+    f = _run_field(task, ids, obst, tgt, stage=route.startswith("stage"))
     ref, cost = O.potential_field(task.cfg, obst, tgt, want_cost=True)
     assert np.nanmax(np.where(np.isfinite(cost[0]), cost[0], np.nan)) > 224.0
     np.testing.assert_array_equal(f, ref)
