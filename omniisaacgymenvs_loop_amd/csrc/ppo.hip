@@ -2228,9 +2228,9 @@ int ppo_policy_step(const ppo_cfg_t *cfg, const float *params, const double *obs
   const int ntiles = (cfg->n_envs + RB - 1) / RB;
   int grid = reg_w ? (ntiles < 256 * POL_WPC ? ntiles : 256 * POL_WPC) : policy_grid(cfg->n_envs);
   if (grid_cap > 0 && grid_cap < grid) grid = grid_cap;
-  hipLaunchKernelGGL(reg_w ? k_policy_step<true> : k_policy_step<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream, *cfg, params, obs_rms, val_rms,
-                     obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma, exp_done, dones_prev,
-                     actions_out, seed, step, step_dev, eps_inject);
+  hipLaunchKernelGGL(reg_w ? k_policy_step<true> : k_policy_step<false>, dim3(grid), dim3(TB), 0, (hipStream_t)stream,
+                     *cfg, params, obs_rms, val_rms, obs, t, exp_obs, exp_act, exp_nlp, exp_val, exp_mu, exp_sigma,
+                     exp_done, dones_prev, actions_out, seed, step, step_dev, eps_inject);
   USV_CHECK_LAUNCH();
   return 0;
 }
@@ -2280,8 +2280,8 @@ int ppo_prepare(const ppo_cfg_t *cfg, const float *params, const double *obs_rms
                      ((reinterpret_cast<uintptr_t>(exp_val) | reinterpret_cast<uintptr_t>(exp_rew) |
                        reinterpret_cast<uintptr_t>(exp_ret) | reinterpret_cast<uintptr_t>(exp_adv) |
                        reinterpret_cast<uintptr_t>(exp_done)) & 15u) == 0;
-  hipLaunchKernelGGL(vec16 ? k_gae<16> : k_gae<0>, dim3(nblk), dim3(TB), 0, s, *cfg, last_val, last_dones, exp_done, exp_val, exp_rew,
-                     exp_ret, exp_adv, work);
+  hipLaunchKernelGGL(vec16 ? k_gae<16> : k_gae<0>, dim3(nblk), dim3(TB), 0, s, *cfg, last_val, last_dones, exp_done,
+                     exp_val, exp_rew, exp_ret, exp_adv, work);
   USV_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_prepare_finalize, dim3(1), dim3(FIN_TB), 0, s, *cfg, val_rms, work, nblk);
   USV_CHECK_LAUNCH();
