@@ -1,4 +1,4 @@
-"""World-size-2 gloo tests of the data-parallel PPO update (CPU, no GPU needed).
+"""World-size-2 (and 4) gloo tests of the data-parallel PPO update (CPU, no GPU needed).
 
 The multi-GPU path shards envs across ranks (independent per-rank env blocks,
 seeds offset by rank) and all-reduces the flat gradient + KL once per minibatch
@@ -102,6 +102,20 @@ def test_allreduced_gradient_equals_full_minibatch(two_ranks):
 
 def test_max_over_ranks(two_ranks):
     assert all(float(r["tmax"]) == 1.5 for r in two_ranks)
+
+
+def test_four_ranks_allreduced_gradient_equals_full_minibatch(tmp_path):
+    """The same at world size 4 (BASELINE configs[3] splits over 4 GPUs): rank 0's weights everywhere, scale 1/4,
+    identical averaged gradients on every rank equal to the 4 x 512-row minibatch's, the timing max over ranks."""
+    mp.spawn(_worker, args=(4, _port(), str(tmp_path)), nprocs=4, join=True)
+    rs = [np.load(tmp_path / f"r{r}.npz") for r in range(4)]
+    for r in rs:
+        np.testing.assert_array_equal(r["flat"], PO.flatten(_params(100)))
+        np.testing.assert_array_equal(r["g"], rs[0]["g"])
+        assert float(r["scale"]) == 0.25 and float(r["tmax"]) == 3.5
+    g_full, kl_full = _grad(_params(100), _data(4 * B), slice(0, 4 * B), 4 * B)
+    np.testing.assert_allclose(rs[0]["g"][:PO.NPARAM], g_full, rtol=2e-4, atol=2e-7)
+    np.testing.assert_allclose(rs[0]["g"][PO.NPARAM], kl_full, rtol=1e-5, atol=1e-7)
 
 
 class _FakeDpLib:
@@ -267,14 +281,14 @@ def _capture_agree_worker(rank, world, port, out_dir, fail_ranks):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail_ranks", [(), (1,), (0, 1)])
-def test_graph_capture_agreement_chooses_one_path_on_every_rank(tmp_path, fail_ranks, monkeypatch):
+@pytest.mark.parametrize("world,fail_ranks", [(2, ()), (2, (1,)), (2, (0, 1)), (4, ()), (4, (3,))])
+def test_graph_capture_agreement_chooses_one_path_on_every_rank(tmp_path, world, fail_ranks, monkeypatch):
     """The update graph with RCCL collectives (the default on nccl): when the capture fails on any rank, every rank
     runs the update eagerly (now and in later epochs); when it succeeds on all, every rank replays the graph.  gloo
-    carries the agreement here, as the nccl backend does on the GPUs."""
+    carries the agreement here, as the nccl backend does on the GPUs; 4 ranks rehearse BASELINE configs[3]'s split."""
     monkeypatch.setenv("USV_DIST_BACKEND", "nccl")   # the capture gate of the GPU runs (the agreement still uses gloo)
     monkeypatch.delenv("USV_GRAPH_COLLECTIVES", raising=False)
-    mp.spawn(_capture_agree_worker, args=(2, _port(), str(tmp_path), fail_ranks), nprocs=2, join=True)
-    logs = [list(np.load(tmp_path / f"cap{r}.npz")["log"]) for r in range(2)]
+    mp.spawn(_capture_agree_worker, args=(world, _port(), str(tmp_path), fail_ranks), nprocs=world, join=True)
+    logs = [list(np.load(tmp_path / f"cap{r}.npz")["log"]) for r in range(world)]
     want = ["eager", "eager"] if fail_ranks else ["replay", "replay"]
-    assert logs == [want, want], logs
+    assert logs == [want] * world, logs
