@@ -147,16 +147,25 @@ __device__ __forceinline__ void stage_store_w2(const StagedW &r, MlpSmem &s) {
   }
 }
 
-// tanh from one exp2 and one reciprocal (v_exp_f32 / v_rcp_f32): |error| < 2e-7
-// absolute (vs the library's correctly rounded tanhf; parity tolerances are
-// 5e-5); a 3-term series below |x| = 2^-7 keeps small arguments relative-accurate
+// tanh(x) = 1 - 2 / (exp(2x) + 1) from one exp2 and one reciprocal (v_exp_f32 / v_rcp_f32) and an fma: |error| <
+// 2e-7 absolute against float64 tanh over the whole range (exp2 overflows to +inf and gives 1, underflows to 0 and
+// gives -1; parity tolerances are 1e-5).  Round 5 used the odd form (1 - e) / (1 + e) of |x| with a 3-term series
+// below 2^-7 for relative accuracy at tiny arguments: ~8 more VALU operations per activation, on the forward's
+// critical path in the gradient and policy kernels, for an accuracy no consumer needs.
+#ifndef USV_TANH_ODD
+#define USV_TANH_ODD 0
+#endif
 __device__ __forceinline__ float fast_tanh(float x) {
-  const float ax = fabsf(x);
-  const float e = __builtin_amdgcn_exp2f(ax * -2.8853900817779268f);   // exp(-2|x|)
-  const float big = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
-  const float x2 = ax * ax;
-  const float small = ax * (1.0f - x2 * (0.33333334f - 0.13333334f * x2));
-  return copysignf(ax < 0.0078125f ? small : big, x);
+  if constexpr (USV_TANH_ODD != 0) {
+    const float ax = fabsf(x);
+    const float e = __builtin_amdgcn_exp2f(ax * -2.8853900817779268f);   // exp(-2|x|)
+    const float big = (1.0f - e) * __builtin_amdgcn_rcpf(1.0f + e);
+    const float x2 = ax * ax;
+    const float small = ax * (1.0f - x2 * (0.33333334f - 0.13333334f * x2));
+    return copysignf(ax < 0.0078125f ? small : big, x);
+  }
+  const float e = __builtin_amdgcn_exp2f(x * 2.8853900817779268f);        // exp(2x)
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
 }
 
 // The persistent forward kernels' obs path: a thread's slots q = tid + u TB of a tile's RB x XS
