@@ -8,6 +8,11 @@ two processes on one GPU (USV_RANKS_SHARE_DEVICE=0, gloo for the handle exchange
     goal counts exactly, as test_philox_mode_pose_tasks_match_oracle);
   - after two train epochs (eager, then graph-captured) both ranks hold bit-identical weights, LR and KLs;
   - the in-kernel peer exchange (ppo_minibatch_fused_dp) and the gloo all-reduce split give the same bits.
+The runs train with grad_norm = 1e6 (truncate_grads on, never binding): the two paths form the clip norm in
+different summation orders (the peer path from the reduction blocks' partial sums, the collective chain in
+k_apply's float4 order), so a minibatch whose norm passes the reference's grad_norm 1.0 is stepped with clip
+coefficients one ulp apart.  Random-init multi-task minibatches do pass 1.0, and the epoch-last norm the agent
+keeps cannot show which did -- the bit comparison is of the exchange, not of the norm's summation order.
 """
 import os
 import socket
@@ -54,7 +59,7 @@ def _worker(rank, world, port, out_dir, exchange):
         cfg = build_config({"num_envs": N, "seed": 42, "multi_gpu": True, "rl_device": "cuda:0",
                             "task": bench.TASKS[name][0]})
         cfg["train"]["params"]["config"].update(train_dir="/tmp/multitask_runs", print_stats=False,
-                                                minibatch_size=8192)
+                                                minibatch_size=8192, grad_norm=1e6)
         env = VecEnvRLGames(headless=True)
         task = initialize_task(cfg, env)
         assert task.seed == 42 + rank and task.cfg.task_kind == (1 if name == "GoToPose" else 2)
@@ -126,6 +131,6 @@ def test_multitask_ranks_share_one_policy(tmp_path_factory, exchange):
 def test_multitask_peer_exchange_equals_collective_path(tmp_path_factory):
     a = _run(tmp_path_factory, "peer")
     b = _run(tmp_path_factory, "collective")
-    assert float(b[0]["norm"]) < 1.0                                # grad_norm 1.0: no step clipped
+    assert float(b[0]["norm"]) < 1e6                                # no step clipped (see the module doc)
     for k in ("p", "m", "kls", "lr"):
         np.testing.assert_array_equal(a[0][k], b[0][k], err_msg=k)
