@@ -384,9 +384,16 @@ class USVVirtual:
         self.join_step()
         self._host_dirty = False
         bias, k = self._advance()
-        _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
+        # USV_FOLD_AFTER_FORK=1 (default): the overlapped step folds the episode extras (usv_reset_part 2) on this
+        # stream after the side stream has forked for the fields, instead of between the reset and the obstacle
+        # placement (the fold feeds nothing of the field chain, which bounds the step); 0: inside usv_reset
+        fold_late = overlapped and os.getenv("USV_FOLD_AFTER_FORK", "1") == "1"
+        if fold_late:
+            _capi.call("usv_reset_part", cfg, b, self.seed, k, _capi.ptr(u_reset), 1, s)
+        else:
+            _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
         if overlapped:
-            return self._step_overlapped(actions, bias, k, u_step)
+            return self._step_overlapped(actions, bias, k, u_step, fold_late=fold_late)
         if self._has_field:   # CaptureXY only (GoToPose / TrackXYOVelocity have no obstacles)
             _capi.call("usv_potential_field", cfg, b, s)
         substeps = self.cfg.substeps
@@ -400,7 +407,7 @@ class USVVirtual:
             self.cfg.substeps = substeps
         return self.obs_view, self.rew_buf, self.dones
 
-    def _step_overlapped(self, actions, bias, k, u_step, reset_on_side=False):
+    def _step_overlapped(self, actions, bias, k, u_step, reset_on_side=False, fold_late=False):
         """The rest of env_step with the reset envs' fields built on a side stream (usv_hip.h, the overlapped
         step): obstacle placement, then the step of every env (part 3) on this stream beside the sweeps /
         statistics / field kernels on the side stream, then the deferred reward of the reset envs there.
@@ -426,6 +433,8 @@ class USVVirtual:
             _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
             self._ev_fork.record(main)
             side.wait_event(self._ev_fork)
+            if fold_late:
+                _capi.call("usv_reset_part", cfg, b, self.seed, k, None, 2, main.cuda_stream)
         # USV_STATS_FIRST=1: the main stream (the next policy step) waits for the field statistics, which then
         # run alone instead of beside the policy kernel (A/B knob)
         stats_first = os.getenv("USV_STATS_FIRST", "0") == "1"

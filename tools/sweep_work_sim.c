@@ -1,0 +1,104 @@
+// CPU model of k_field_wave's sweep WORK (not only its iteration count): per iteration, the tiles the kernel's
+// dirty rule sweeps (a tile whose 3x3 tile neighbourhood changed in the previous iteration) and the waves that
+// issue (a wave runs an iteration if any tile of its quadrant is dirty).  Same maps as tools/sweep_sim.c.
+//   gcc -O2 -ffp-contract=off -o /tmp/sweep_work_sim tools/sweep_work_sim.c -lm && /tmp/sweep_work_sim 12
+#include <stdio.h>
+#include <stdlib.h>
+#include <math.h>
+#include <string.h>
+#define G 150
+#define T 10
+#define NT 15
+static float A[G][G], B[G][G];
+static int occ[G][G];
+static int lastc[NT + 2][NT + 2];
+static float relax(float h, float nb, float w) { float c = nb + w; return c < h ? c : h; }
+static int quad_of(int tr, int tc) { return (tr >= 8) * 2 + (tc >= 8); }
+int run(float (*init)[G], long *dirty_tiles, long *wave_its, long *hist) {
+  memcpy(A, init, sizeof(A));
+  for (int r = 0; r < NT + 2; ++r) for (int c = 0; c < NT + 2; ++c) lastc[r][c] = -1000;
+  for (int r = 1; r <= NT; ++r) for (int c = 1; c <= NT; ++c) lastc[r][c] = 0;
+  int it;
+  for (it = 0; it < 400; ++it) {
+    memcpy(B, A, sizeof(A));
+    int changed_any = 0, nd = 0, qact[4] = {0, 0, 0, 0};
+    static int newc[NT][NT];
+    for (int tr = 0; tr < NT; ++tr) for (int tc = 0; tc < NT; ++tc) {
+      newc[tr][tc] = 0;
+      int dirty = 0;
+      for (int dr = -1; dr <= 1; ++dr) for (int dc = -1; dc <= 1; ++dc) dirty |= lastc[tr + 1 + dr][tc + 1 + dc] >= it - 1;
+      if (!dirty) continue;
+      ++nd; qact[quad_of(tr, tc)] = 1;
+      float h[T + 2][T + 2];
+      for (int i = -1; i <= T; ++i) for (int j = -1; j <= T; ++j) {
+        int r = tr * T + i, c = tc * T + j;
+        float v = INFINITY;
+        if (r >= 0 && r < G && c >= 0 && c < G) v = (i >= 0 && i < T && j >= 0 && j < T) ? A[r][c] : B[r][c];
+        if (r >= 0 && r < G && c >= 0 && c < G && occ[r][c]) v = NAN;
+        h[i + 1][j + 1] = v;
+      }
+      int changed = 0;
+      for (int i = 1; i <= T; ++i) for (int j = 1; j <= T; ++j) {
+        if (isnan(h[i][j])) continue;
+        float m = h[i][j];
+        if (!isnan(h[i-1][j-1])) m = relax(m, h[i-1][j-1], 1.414f);
+        if (!isnan(h[i-1][j])) m = relax(m, h[i-1][j], 1.0f);
+        if (!isnan(h[i-1][j+1])) m = relax(m, h[i-1][j+1], 1.414f);
+        if (!isnan(h[i][j-1])) m = relax(m, h[i][j-1], 1.0f);
+        if (m != h[i][j]) changed = 1;
+        h[i][j] = m;
+      }
+      for (int i = T; i >= 1; --i) for (int j = T; j >= 1; --j) {
+        if (isnan(h[i][j])) continue;
+        float m = h[i][j];
+        if (!isnan(h[i+1][j+1])) m = relax(m, h[i+1][j+1], 1.414f);
+        if (!isnan(h[i+1][j])) m = relax(m, h[i+1][j], 1.0f);
+        if (!isnan(h[i+1][j-1])) m = relax(m, h[i+1][j-1], 1.414f);
+        if (!isnan(h[i][j+1])) m = relax(m, h[i][j+1], 1.0f);
+        if (m != h[i][j]) changed = 1;
+        h[i][j] = m;
+      }
+      for (int i = 0; i < T; ++i) for (int j = 0; j < T; ++j) if (!occ[tr*T+i][tc*T+j]) A[tr * T + i][tc * T + j] = h[i + 1][j + 1];
+      newc[tr][tc] = changed;
+      changed_any |= changed;
+    }
+    for (int tr = 0; tr < NT; ++tr) for (int tc = 0; tc < NT; ++tc) if (newc[tr][tc]) lastc[tr + 1][tc + 1] = it;
+    *dirty_tiles += nd;
+    *wave_its += qact[0] + qact[1] + qact[2] + qact[3];
+    if (hist && it < 40) hist[it] += nd;
+    if (!changed_any) break;
+  }
+  return it + 1;
+}
+int main(int argc, char **argv) {
+  int trials = argc > 1 ? atoi(argv[1]) : 20;
+  srand(7);
+  static float init[G][G];
+  long hist[40] = {0};
+  double s_it = 0, s_dt = 0, s_wi = 0;
+  for (int t = 0; t < trials; ++t) {
+    memset(occ, 0, sizeof(occ));
+    for (int r = 0; r < G; ++r) { occ[r][0] = occ[r][G-1] = 1; occ[0][r] = occ[G-1][r] = 1; }
+    for (int o = 0; o < 16; ++o) {
+      float ox = (rand() / (float)RAND_MAX) * 24 - 12, oy = (rand() / (float)RAND_MAX) * 24 - 12;
+      for (int r = 0; r < G; ++r) for (int c = 0; c < G; ++c) {
+        float x = -15 + 0.2f * (c + 0.5f), y = -15 + 0.2f * (r + 0.5f);
+        if (sqrtf((x-ox)*(x-ox)+(y-oy)*(y-oy)) <= 0.5f) occ[r][c] = 1;
+      }
+    }
+    int tx = 20 + rand() % 110, ty = 20 + rand() % 110;
+    occ[ty][tx] = 0;
+    for (int r = 0; r < G; ++r) for (int c = 0; c < G; ++c) init[r][c] = INFINITY;
+    init[ty][tx] = 0.f;
+    long dt = 0, wi = 0;
+    int n = run(init, &dt, &wi, hist);
+    printf("trial %d target (%d,%d): iterations %d, dirty tile-iterations %ld (%.1f per iteration of 225), "
+           "wave-iterations %ld (lane occupancy %.2f)\n", t, tx, ty, n, dt, (double)dt / n, wi, (double)dt / (64.0 * wi));
+    s_it += n; s_dt += dt; s_wi += wi;
+  }
+  printf("mean iterations %.1f, dirty tile-iterations %.0f, wave-iterations %.1f, lane occupancy %.3f\n",
+         s_it / trials, s_dt / trials, s_wi / trials, s_dt / (64.0 * s_wi));
+  printf("dirty tiles per iteration (mean over trials):");
+  for (int i = 0; i < 30; ++i) printf(" %.0f", (double)hist[i] / trials);
+  printf("\n");
+}
