@@ -48,14 +48,17 @@ class VecEnvRLGames:
         obs_dict = {"obs": {"state": obs}, "states": t.states_buf}
         return obs_dict, rew, dones, t.extras
 
-    def step_async(self, actions: torch.Tensor, chain: bool = False):
+    def step_async(self, actions: torch.Tensor, chain: bool = False, after_fork=None):
         """step() whose rewards are final only after join(): the reset envs' potential fields build on a side
         stream while the caller issues its next policy step (obs and dones are final on return).  chain=True
         when this call follows another step_async of the same rollout (one captured graph) with nothing but
-        the caller's own kernels in between: the step's reset then runs on the side stream too."""
+        the caller's own kernels in between: the step's reset then runs on the side stream too.  after_fork:
+        a callable issuing the caller's kernels that still read the previous step's rewards and dones; the step
+        runs it on the current stream after the reset, the obstacle placement and the fields' fork, before its
+        env kernels overwrite those buffers (off the field chain, which bounds the step)."""
         t = self._task
         a = actions if actions.device == torch.device(t.device) else actions.to(t.device)
-        obs, rew, dones = t.env_step(a, overlap=True, chain=chain)
+        obs, rew, dones = t.env_step(a, overlap=True, chain=chain, after_fork=after_fork)
         self.sim_frame_count += t.control_frequency_inv
         return {"obs": {"state": obs}, "states": t.states_buf}, rew, dones, t.extras
 

@@ -388,17 +388,32 @@ class A2CAgent:
                    c.ptr(self.dones), c.ptr(self.actions), self.seed + 7919 * self.rank, base + n,
                    c.ptr(self.step_dev), None, s)
 
+        def store(n, rewards, dones):
+            c.call("ppo_store_reward", cfg, c.ptr(rewards), c.ptr(dones), n, c.ptr(self.exp_rew),
+                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter_buf),
+                   c.ptr(self.step_dev), s)
+
+        # USV_STORE_DEFER=1 (default): store_reward(n) runs inside step n + 1 once its fields have forked (the
+        # env kernels that overwrite step n's rewards / dones follow it), so it leaves the field chain -- the
+        # step's critical path -- that otherwise runs join -> late reward -> store -> next reset; the last step's
+        # store follows its join.  0: right after each join
+        defer = os.getenv("USV_STORE_DEFER", "1") == "1"
+        pending = None
         policy(0)
         for n in range(self.horizon_length):
             t0 = time.time()
-            self.obs, rewards, self.dones, infos = self.vec_env.step_async(self.actions, chain=n > 0)
+            hook = (lambda p=pending: store(*p)) if pending is not None else None
+            self.obs, rewards, self.dones, infos = self.vec_env.step_async(self.actions, chain=n > 0,
+                                                                           after_fork=hook)
             step_time += time.time() - t0
             if n + 1 < self.horizon_length:
                 policy(n + 1)
             self.vec_env.join()
-            c.call("ppo_store_reward", cfg, c.ptr(rewards), c.ptr(self.dones), n, c.ptr(self.exp_rew),
-                   c.ptr(self.cur_rew), c.ptr(self.cur_shaped), c.ptr(self.cur_len), c.ptr(self.meter_buf),
-                   c.ptr(self.step_dev), s)
+            if defer and n + 1 < self.horizon_length:
+                pending = (n, rewards, self.dones)
+            else:
+                pending = None
+                store(n, rewards, self.dones)
             self.algo_observer.process_infos(infos, None)
         self._step_counter = base + self.horizon_length
         return {"played_frames": self.batch_size, "step_time": step_time}

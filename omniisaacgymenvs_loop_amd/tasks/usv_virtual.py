@@ -359,7 +359,7 @@ class USVVirtual:
 
     def env_step(self, actions: torch.Tensor, u_step: Optional[torch.Tensor] = None,
                  u_reset: Optional[torch.Tensor] = None, post_state: Optional[torch.Tensor] = None,
-                 overlap: bool = False, chain: bool = False):
+                 overlap: bool = False, chain: bool = False, after_fork=None):
         """pre_physics_step + 10 substeps + post_physics_step (USV_Virtual.py:1042-1652).
 
         Returns the device tensors (obs [n,33], rew [n], dones int64 [n]).  u_step / u_reset replay
@@ -368,11 +368,16 @@ class USVVirtual:
         the step then runs pre_physics_step and RLTask.post_physics_step (rl_task.py:283-303) on that
         state, as the reference does on whatever PhysX returned (parity of the post-physics path alone).
         overlap: the overlapped step (_step_overlapped); chain: this overlapped step directly follows one in the
-        same sequence of calls (a rollout, or one captured graph), so its reset may run on the side stream."""
+        same sequence of calls (a rollout, or one captured graph), so its reset may run on the side stream.
+        after_fork: a callable issuing work that reads the previous step's rew / dones, run on the current stream
+        before this step's env kernels write them (the default overlapped step: after the fields' fork)."""
         actions = self._f32(actions)
         s = _capi.stream_ptr()
         cfg, b = _capi.byref(self.cfg), _capi.byref(self._bufs)
         overlapped = overlap and self._has_field and post_state is None
+        if after_fork is not None and not overlapped:
+            after_fork()          # nothing forks: before any kernel of this step
+            after_fork = None
         if (overlapped and chain and self._side_tail_late and not self._host_dirty and u_step is None
                 and u_reset is None and os.getenv("USV_RESET_ON_SIDE", "0") == "1"):
             # (A/B knob, off: measured slower, DESIGN section 4) the previous overlapped step's side stream ends
@@ -380,6 +385,8 @@ class USVVirtual:
             # of its part 3 (final on this stream long before), not on this stream's later work (the next policy
             # step, the reward store), so they can run on the side stream right behind it
             bias, k = self._advance()
+            if after_fork is not None:
+                after_fork()
             return self._step_overlapped(actions, bias, k, u_step, reset_on_side=True)
         self.join_step()
         self._host_dirty = False
@@ -393,7 +400,7 @@ class USVVirtual:
         else:
             _capi.call("usv_reset", cfg, b, self.seed, k, _capi.ptr(u_reset), s)
         if overlapped:
-            return self._step_overlapped(actions, bias, k, u_step, fold_late=fold_late)
+            return self._step_overlapped(actions, bias, k, u_step, fold_late=fold_late, after_fork=after_fork)
         if self._has_field:   # CaptureXY only (GoToPose / TrackXYOVelocity have no obstacles)
             _capi.call("usv_potential_field", cfg, b, s)
         substeps = self.cfg.substeps
@@ -407,7 +414,7 @@ class USVVirtual:
             self.cfg.substeps = substeps
         return self.obs_view, self.rew_buf, self.dones
 
-    def _step_overlapped(self, actions, bias, k, u_step, reset_on_side=False, fold_late=False):
+    def _step_overlapped(self, actions, bias, k, u_step, reset_on_side=False, fold_late=False, after_fork=None):
         """The rest of env_step with the reset envs' fields built on a side stream (usv_hip.h, the overlapped
         step): obstacle placement, then the step of every env (part 3) on this stream beside the sweeps /
         statistics / field kernels on the side stream, then the deferred reward of the reset envs there.
@@ -433,6 +440,8 @@ class USVVirtual:
             _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
             self._ev_fork.record(main)
             side.wait_event(self._ev_fork)
+            if after_fork is not None:
+                after_fork()
             if fold_late:
                 _capi.call("usv_reset_part", cfg, b, self.seed, k, None, 2, main.cuda_stream)
         # USV_STATS_FIRST=1: the main stream (the next policy step) waits for the field statistics, which then

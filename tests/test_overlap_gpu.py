@@ -45,16 +45,21 @@ def test_overlapped_env_step_equals_plain_step(monkeypatch, n, half):
             np.testing.assert_array_equal(so[k], sp[k], err_msg=f"{k} step {t}")
 
 
-@pytest.mark.parametrize("reset_on_side,late_on_join", [("0", "0"), ("1", "0"), ("0", "1")])
-def test_overlapped_rollout_equals_sequential(monkeypatch, reset_on_side, late_on_join):
+@pytest.mark.parametrize("reset_on_side,late_on_join,store_defer,fold_late",
+                         [("0", "0", "1", "1"), ("1", "0", "1", "1"), ("0", "1", "1", "1"), ("0", "1", "0", "0")])
+def test_overlapped_rollout_equals_sequential(monkeypatch, reset_on_side, late_on_join, store_defer, fold_late):
     """A2CAgent.play_steps with the overlapped env step (policy n+1 beside step n's field kernels) vs the
     sequential loop: every experience buffer, the meters and the env state bit-identical after two epochs
     of rollouts (the first from the all-env reset); also with the chained steps' reset and obstacle placement
-    on the side stream (USV_RESET_ON_SIDE=1, usv_reset_part)."""
+    on the side stream (USV_RESET_ON_SIDE=1, usv_reset_part), and with step n's reward store inside step n + 1
+    after its fork (USV_STORE_DEFER, the default) or after each join, the episode-extras fold after the fork
+    (USV_FOLD_AFTER_FORK, the default) or inside usv_reset."""
     import os
     from tests.test_train_gpu import _agent_env
     monkeypatch.setenv("USV_RESET_ON_SIDE", reset_on_side)
     monkeypatch.setenv("USV_LATE_ON_JOIN", late_on_join)
+    monkeypatch.setenv("USV_STORE_DEFER", store_defer)
+    monkeypatch.setenv("USV_FOLD_AFTER_FORK", fold_late)
     runs = []
     for ov in ("0", "1"):
         os.environ["USV_STEP_OVERLAP"] = ov
