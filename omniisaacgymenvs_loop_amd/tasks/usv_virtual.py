@@ -427,6 +427,24 @@ class USVVirtual:
             self._side = torch.cuda.Stream(device=self._device, priority=int(os.getenv("USV_SIDE_PRIORITY", "0")))
             self._ev_fork, self._ev_early, self._ev_join = (torch.cuda.Event() for _ in range(3))
         side = self._side
+        # USV_STATS_FIRST=1: the main stream (the next policy step) waits for the field statistics, which then
+        # run alone instead of beside the policy kernel (A/B knob)
+        stats_first = os.getenv("USV_STATS_FIRST", "0") == "1"
+
+        def side_fields():
+            if stats_first:
+                if self._ev_stats is None:
+                    self._ev_stats = torch.cuda.Event()
+                _capi.call("usv_field_stage", cfg, b, 3, side.cuda_stream)
+                self._ev_stats.record(side)
+                _capi.call("usv_field_stage", cfg, b, 4, side.cuda_stream)
+            else:
+                _capi.call("usv_field_stage", cfg, b, 2, side.cuda_stream)
+
+        # USV_SIDE_FIRST=1 (default): the side stream's field kernels are captured right after the fork, before this
+        # stream's deferred store and extras fold (a captured graph's launch gives the placement's first dependent
+        # its queue, so the sweeps then follow the placement on one queue); 0: after them
+        side_first = os.getenv("USV_SIDE_FIRST", "1") == "1" and not reset_on_side
         if reset_on_side:
             # reset + obstacle placement on the side stream behind the previous step's deferred reward; this
             # stream waits for the placement, then folds the episode extras (so what it reads of them between
@@ -440,21 +458,14 @@ class USVVirtual:
             _capi.call("usv_field_stage", cfg, b, 1, main.cuda_stream)
             self._ev_fork.record(main)
             side.wait_event(self._ev_fork)
+            if side_first:
+                side_fields()
             if after_fork is not None:
                 after_fork()
             if fold_late:
                 _capi.call("usv_reset_part", cfg, b, self.seed, k, None, 2, main.cuda_stream)
-        # USV_STATS_FIRST=1: the main stream (the next policy step) waits for the field statistics, which then
-        # run alone instead of beside the policy kernel (A/B knob)
-        stats_first = os.getenv("USV_STATS_FIRST", "0") == "1"
-        if stats_first:
-            if self._ev_stats is None:
-                self._ev_stats = torch.cuda.Event()
-            _capi.call("usv_field_stage", cfg, b, 3, side.cuda_stream)
-            self._ev_stats.record(side)
-            _capi.call("usv_field_stage", cfg, b, 4, side.cuda_stream)
-        else:
-            _capi.call("usv_field_stage", cfg, b, 2, side.cuda_stream)
+        if not side_first:
+            side_fields()
         _capi.call("usv_env_step_part", cfg, b, _capi.ptr(actions), _capi.ptr(self.lut), ctypes.c_float(bias),
                    self.seed, k, _capi.ptr(u_step), 3, main.cuda_stream)
         if stats_first:
