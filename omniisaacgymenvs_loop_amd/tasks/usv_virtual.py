@@ -470,10 +470,13 @@ class USVVirtual:
                    self.seed, k, _capi.ptr(u_step), 3, main.cuda_stream)
         if stats_first:
             main.wait_event(self._ev_stats)
-        # USV_LATE_ON_JOIN=1 (default): the deferred reward runs on the joining stream right after its wait for the
-        # fields (one cross-stream wait per step fewer on the critical path: rollout -0.8% at 131072 envs, -1% at
-        # 4096, profiles/r04/r04z6_late_on_join_ab.txt); 0: on the side stream behind part 3
-        late_on_join = os.getenv("USV_LATE_ON_JOIN", "1") == "1"
+        # USV_LATE_ON_JOIN=1: the deferred reward runs on the joining stream right after its wait for the fields; 0: on
+        # the side stream behind part 3.  Unset: 0 from 32768 envs (the packed-sweep batches: with the round-6
+        # schedule the side queue then runs constants -> deferred reward -> next reset back to back, rollout -1.6% at
+        # 131072 envs, profiles/r06/r06zd_late_on_side_ab.txt), 1 below (-2% at 4096, r06ze_late_on_join_4096_ab.txt;
+        # round 4: profiles/r04/r04z6_late_on_join_ab.txt)
+        lj = os.getenv("USV_LATE_ON_JOIN", "")
+        late_on_join = lj == "1" if lj in ("0", "1") else self._num_envs < 32768
         if late_on_join:
             self._ev_join.record(side)
             self._late_pending = True
