@@ -287,6 +287,11 @@ __device__ __forceinline__ float field_value(const usv_cfg_t &c, const FieldNorm
 // lower-index obstacle; after USV_SPAWN_ITERS redraws the leftovers go to limbo
 // (999, 999).  Same uniforms as the per-env restatement (reset slots RU_OBST + 2o,
 // RU_RESAMPLE + 32 it + 2o (+1)).
+// USV_PLACE_SPLIT 1: the pair tests of a rejection iteration split over the four 16-lane groups (A/B: 0 = every
+// group runs all 15)
+#ifndef USV_PLACE_SPLIT
+#define USV_PLACE_SPLIT 1
+#endif
 __device__ __forceinline__ float2 place_obstacles(const usv_cfg_t &c, int ee, float sx, float sy, float tx, float ty,
                                                   uint64_t seed, uint64_t step, const float *__restrict__ inj) {
   static_assert(USV_NOBST == 16, "16-lane groups");
@@ -315,8 +320,24 @@ __device__ __forceinline__ float2 place_obstacles(const usv_cfg_t &c, int ee, fl
       const int it = 4 * r + qq;
       const float ds = tnorm2(ox - sx, oy - sy);
       const float dt = tnorm2(ox - tx, oy - ty);
-      bool bad = (ds < c.min_dist_safe) || (dt < c.min_dist_safe);
       const bool vo = ox < 900.f;
+#if USV_PLACE_SPLIT
+      // the four groups hold the same obstacles, so each checks a quarter of the lower-index ones: group q the
+      // obstacles 4q .. 4q + 3 (from its own lanes 16q + 4q + k), and the groups' verdicts meet in one ballot
+      // (obstacle o is bad iff bit o of some group is set) -- 4 dependent pair tests per iteration instead of 15
+      bool bad = q == 0 && ((ds < c.min_dist_safe) || (dt < c.min_dist_safe));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int i = 4 * q + k;
+        const float xi = __shfl(ox, gbase + i, 64), yi = __shfl(oy, gbase + i, 64);
+        const float ddx = xi - ox, ddy = yi - oy;
+        if (i < o && vo && (xi < 900.f) && (ddx * ddx + ddy * ddy) < sep2) bad = true;
+      }
+      const uint64_t bq = __ballot(bad);
+      const uint32_t inval = (uint32_t)((bq | (bq >> 16) | (bq >> 32) | (bq >> 48)) & 0xFFFFull);
+      bad = ((inval >> o) & 1u) != 0u;
+#else
+      bool bad = (ds < c.min_dist_safe) || (dt < c.min_dist_safe);
       // the four groups hold the same obstacles, so obstacle i is lane i's value: a scalar read of the lane
       // (v_readlane) instead of a per-lane LDS permute
 #pragma unroll
@@ -327,6 +348,7 @@ __device__ __forceinline__ float2 place_obstacles(const usv_cfg_t &c, int ee, fl
         if (i < o && vo && (xi < 900.f) && (ddx * ddx + ddy * ddy) < sep2) bad = true;
       }
       const uint32_t inval = (uint32_t)((__ballot(bad) >> gbase) & 0xFFFFull);   // same in every group
+#endif
       if (inval == 0) { done = true; break; }
       if (it == USV_SPAWN_ITERS) {  // leftovers to limbo (:1042-1048)
         if (bad) { ox = 999.0f; oy = 999.0f; }
