@@ -163,6 +163,9 @@ __global__ __launch_bounds__(kPlaceTB) void k_field_place(usv_cfg_t c, usv_bufs_
 #ifndef USV_SWEEP_CHG
 #define USV_SWEEP_CHG 2
 #endif
+#ifndef USV_SWEEP_FNOTE_EDGE
+#define USV_SWEEP_FNOTE_EDGE 1
+#endif
 #if USV_SWEEP_CHG == 2
 #define USV_SWEEP_NOTE(hb, m) (chg = __builtin_amdgcn_bitop3_b32(chg, (uint32_t)(hb), (uint32_t)(m), 0xF6))
 #elif USV_SWEEP_CHG
@@ -371,7 +374,12 @@ __device__ __forceinline__ void field_wave_body(const usv_cfg_t &c, const usv_bu
             m = min(m, __float_as_int(fabsf(h[i - 1][j]) + 1.0f));
             m = min(m, __float_as_int(fabsf(h[i - 1][j + 1]) + 1.414f));
             m = min(m, __float_as_int(fabsf(h[i][j - 1]) + 1.0f));
-            USV_SWEEP_NOTE(hb, m);
+            // USV_SWEEP_FNOTE_EDGE: the forward pass notes only the tile's edge cells (the halos its neighbours
+            // read).  The backward pass notes every cell, and a backward pass that lowers nothing leaves the tile
+            // at its fixed point under the current halos (after the forward pass every forward constraint holds;
+            // the unchanged backward pass keeps them and adds the backward ones), so an interior cell lowered by
+            // the forward pass alone needs no further sweep of this tile or of its neighbours
+            if (USV_SWEEP_FNOTE_EDGE == 0 || i == 1 || i == TH || j == 1 || j == TW) USV_SWEEP_NOTE(hb, m);
             h[i][j] = __int_as_float(m);
           }
 #pragma unroll
